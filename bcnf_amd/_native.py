@@ -1,0 +1,126 @@
+"""ctypes binding of the C-ABI in include/bcnf_amd.h (libbcnf_amd.so, built for gfx950).
+
+`import torch` happens first on purpose: torch ships its own libamdhip64.so.7; loading it before
+our library makes the dynamic linker resolve our DT_NEEDED libamdhip64.so.7 to torch's copy, so the
+HIP stream handles torch hands us belong to the same runtime.
+
+There is no fallback: if the library is missing every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede loading the HIP library)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libbcnf_amd.so")
+
+MAX_HIDDEN = 8
+
+OK, ERR_ARG, ERR_UNSUPPORTED, ERR_HIP = 0, 1, 2, 3
+
+# Every symbol include/bcnf_amd.h declares (checked by tests/test_native_abi.py).
+EXPORTS = (
+    "bcnf_stack_supported", "bcnf_param_count", "bcnf_packed_bytes", "bcnf_workspace_bytes",
+    "bcnf_slab_bytes", "bcnf_pack_params", "bcnf_stack_forward", "bcnf_stack_backward",
+    "bcnf_stack_inverse", "bcnf_status_string", "bcnf_last_hip_error",
+)
+
+
+class BcnfStackDesc(ctypes.Structure):
+    _fields_ = [
+        ("size", ctypes.c_int32),
+        ("n_conditions", ctypes.c_int32),
+        ("n_hidden", ctypes.c_int32),
+        ("hidden", ctypes.c_int32 * MAX_HIDDEN),
+        ("n_blocks", ctypes.c_int32),
+        ("act_norm", ctypes.c_int32),
+        ("two_way", ctypes.c_int32),
+        ("dropout", ctypes.c_float),
+    ]
+
+
+def make_desc(size, nested_sizes, n_blocks, n_conditions, dropout=0.0, act_norm=False, two_way=False):
+    d = BcnfStackDesc()
+    d.size = int(size)
+    d.n_conditions = int(n_conditions)
+    d.n_hidden = len(nested_sizes)
+    if len(nested_sizes) > MAX_HIDDEN:
+        raise ValueError(f"bcnf_amd supports at most {MAX_HIDDEN} nested layers, got {len(nested_sizes)}")
+    for i, hsz in enumerate(nested_sizes):
+        d.hidden[i] = int(hsz)
+    d.n_blocks = int(n_blocks)
+    d.act_norm = 1 if act_norm else 0
+    d.two_way = 1 if two_way else 0
+    d.dropout = float(dropout)
+    return d
+
+
+_lib = None
+_lock = threading.Lock()
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_pdesc = ctypes.POINTER(BcnfStackDesc)
+_pi64 = ctypes.POINTER(ctypes.c_int64)
+
+
+def _bind(lib):
+    sig = {
+        "bcnf_stack_supported": (_i32, [_pdesc]),
+        "bcnf_param_count": (_i32, [_pdesc, _pi64, _pi64]),
+        "bcnf_packed_bytes": (_i32, [_pdesc, _pi64]),
+        "bcnf_workspace_bytes": (_i32, [_pdesc, _i64, _i32, _pi64]),
+        "bcnf_slab_bytes": (_i32, [_pdesc, _i64, _pi64]),
+        "bcnf_pack_params": (_i32, [_pdesc, _vp, _vp, _vp, _vp]),
+        "bcnf_stack_forward": (_i32, [_pdesc, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
+        "bcnf_stack_backward": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+        "bcnf_stack_inverse": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp]),
+        "bcnf_status_string": (ctypes.c_char_p, [_i32]),
+        "bcnf_last_hip_error": (_i32, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def lib():
+    """The loaded HIP library. Raises if it has not been built (no silent fallback)."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise RuntimeError(
+                        f"bcnf_amd: HIP library {LIB_PATH} is missing. Build it with "
+                        "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950).")
+                handle = ctypes.CDLL(LIB_PATH)
+                _bind(handle)
+                _lib = handle
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != OK:
+        L = lib()
+        msg = L.bcnf_status_string(rc).decode()
+        extra = f" (hipError {L.bcnf_last_hip_error()})" if rc == ERR_HIP else ""
+        raise RuntimeError(f"bcnf_amd: {what} failed: {msg}{extra}")
+
+
+def ptr(t):
+    return ctypes.c_void_p(0) if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_handle(device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def query_i64(fn, *args) -> int:
+    out = ctypes.c_int64(0)
+    check(fn(*args, ctypes.byref(out)), fn.__name__)
+    return int(out.value)

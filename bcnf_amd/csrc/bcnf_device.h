@@ -1,0 +1,164 @@
+// Device-side building blocks for the fused CondRealNVP_v2 coupling stack (gfx950 / CDNA4).
+//
+// Execution layout ("row layout"): one sample per 16-lane DPP row, lane j of the row = neuron j.
+// A 64-wide wavefront therefore carries 4 samples and a 256-thread workgroup 16 samples. Every
+// dense layer of width <= 16 is a 16-step rotation: out_j = sum_r x[(j - r) & 15] * w_j[r], where the
+// rotated operand comes from `row_ror:r` DPP folded into `v_fmac_f32_dpp` (one VALU op per MAC step,
+// no LDS round trip), and w_j[r] is the lane's pre-rotated weight row staged in LDS by the pack kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define BCNF_WG 256
+#define BCNF_ROWS 16           // samples per workgroup
+#define BCNF_TSTRIDE 17        // padded row stride of the [16 samples][16] LDS tiles (bank spread)
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// Host-computed layout of one stack (passed by value to every kernel).
+struct BcnfLayout {
+  int D, Da, Db, C, Cp, NH, nb, act_norm;
+  int H[10];            // H[0] = Da (y-part width of layer 1), H[1..NH] hidden, H[NH+1] = 2*Db
+  int lin_w[10], lin_b[10], lin_in[10], lin_out[10];   // Linear l = 1..NH+1 inside a coupling
+  int an_size;          // 2*D if act_norm else 0
+  int blk_stride;       // canonical floats per (ActNorm + coupling) block
+  int n_trainable;
+  float p, keep_scale;
+  uint32_t thresh16;    // drop if u16 < thresh16
+  int RF, RB;           // per-lane record floats (forward/inverse, backward)
+  // record offsets (floats, per lane)
+  int rf_b1, rf_w1, rf_hid, rf_t, rf_s, rf_q;
+  int rb_w1t, rb_hid, rb_tt, rb_st, rb_qt;
+  // packed buffer offsets (floats)
+  long long pf_off, pb_off, pi_off, w1t_off, w1h_off, ldc_off, total;
+};
+
+__device__ __forceinline__ int coupling_base(const BcnfLayout& L, int k) {
+  return k * L.blk_stride + ((k < L.nb - 1) ? L.an_size : 0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Rotation dot product over a 16-lane row: acc + sum_r x[(j-r)&15] * w[r].
+// The 15 DPP steps sit in ONE asm statement: the leading `s_nop 1` covers the VALU-write -> DPP-read
+// hazard on x (2 wait states) for whatever the compiler scheduled right before, and no compiler
+// copy of x can land between two DPP reads.
+// ---------------------------------------------------------------------------------------------
+#define BCNF_DPP(R, A, X, W) "v_fmac_f32_dpp " A ", " X ", " W " row_ror:" #R " row_mask:0xf bank_mask:0xf\n\t"
+
+__device__ __forceinline__ float rot16(float x, const float* __restrict__ w, float acc) {
+  acc = fmaf(x, w[0], acc);
+  asm("s_nop 1\n\t"
+      BCNF_DPP(1, "%0", "%1", "%2") BCNF_DPP(2, "%0", "%1", "%3") BCNF_DPP(3, "%0", "%1", "%4")
+      BCNF_DPP(4, "%0", "%1", "%5") BCNF_DPP(5, "%0", "%1", "%6") BCNF_DPP(6, "%0", "%1", "%7")
+      BCNF_DPP(7, "%0", "%1", "%8") BCNF_DPP(8, "%0", "%1", "%9") BCNF_DPP(9, "%0", "%1", "%10")
+      BCNF_DPP(10, "%0", "%1", "%11") BCNF_DPP(11, "%0", "%1", "%12") BCNF_DPP(12, "%0", "%1", "%13")
+      BCNF_DPP(13, "%0", "%1", "%14") BCNF_DPP(14, "%0", "%1", "%15") BCNF_DPP(15, "%0", "%1", "%16")
+      : "+v"(acc)
+      : "v"(x), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]), "v"(w[6]), "v"(w[7]), "v"(w[8]),
+        "v"(w[9]), "v"(w[10]), "v"(w[11]), "v"(w[12]), "v"(w[13]), "v"(w[14]), "v"(w[15]));
+  return acc;
+}
+
+// Two independent rotation chains interleaved in one asm block (hides the fmac dependency latency).
+__device__ __forceinline__ void rot16x2(float x0, const float* __restrict__ w0, float& a0,
+                                        float x1, const float* __restrict__ w1, float& a1) {
+  a0 = fmaf(x0, w0[0], a0);
+  a1 = fmaf(x1, w1[0], a1);
+  asm("s_nop 1\n\t"
+      BCNF_DPP(1, "%0", "%2", "%4") BCNF_DPP(1, "%1", "%3", "%19")
+      BCNF_DPP(2, "%0", "%2", "%5") BCNF_DPP(2, "%1", "%3", "%20")
+      BCNF_DPP(3, "%0", "%2", "%6") BCNF_DPP(3, "%1", "%3", "%21")
+      BCNF_DPP(4, "%0", "%2", "%7") BCNF_DPP(4, "%1", "%3", "%22")
+      BCNF_DPP(5, "%0", "%2", "%8") BCNF_DPP(5, "%1", "%3", "%23")
+      BCNF_DPP(6, "%0", "%2", "%9") BCNF_DPP(6, "%1", "%3", "%24")
+      BCNF_DPP(7, "%0", "%2", "%10") BCNF_DPP(7, "%1", "%3", "%25")
+      BCNF_DPP(8, "%0", "%2", "%11") BCNF_DPP(8, "%1", "%3", "%26")
+      BCNF_DPP(9, "%0", "%2", "%12") BCNF_DPP(9, "%1", "%3", "%27")
+      BCNF_DPP(10, "%0", "%2", "%13") BCNF_DPP(10, "%1", "%3", "%28")
+      BCNF_DPP(11, "%0", "%2", "%14") BCNF_DPP(11, "%1", "%3", "%29")
+      BCNF_DPP(12, "%0", "%2", "%15") BCNF_DPP(12, "%1", "%3", "%30")
+      BCNF_DPP(13, "%0", "%2", "%16") BCNF_DPP(13, "%1", "%3", "%31")
+      BCNF_DPP(14, "%0", "%2", "%17") BCNF_DPP(14, "%1", "%3", "%32")
+      BCNF_DPP(15, "%0", "%2", "%18") BCNF_DPP(15, "%1", "%3", "%33")
+      : "+v"(a0), "+v"(a1)
+      : "v"(x0), "v"(x1),
+        "v"(w0[1]), "v"(w0[2]), "v"(w0[3]), "v"(w0[4]), "v"(w0[5]), "v"(w0[6]), "v"(w0[7]), "v"(w0[8]),
+        "v"(w0[9]), "v"(w0[10]), "v"(w0[11]), "v"(w0[12]), "v"(w0[13]), "v"(w0[14]), "v"(w0[15]),
+        "v"(w1[1]), "v"(w1[2]), "v"(w1[3]), "v"(w1[4]), "v"(w1[5]), "v"(w1[6]), "v"(w1[7]), "v"(w1[8]),
+        "v"(w1[9]), "v"(w1[10]), "v"(w1[11]), "v"(w1[12]), "v"(w1[13]), "v"(w1[14]), "v"(w1[15]));
+}
+
+// Sum over the 16 lanes of a row, result in every lane of the row.
+__device__ __forceinline__ float row_sum16(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xf, 0xf, true));  // row_ror:8
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xf, 0xf, true));  // row_ror:4
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x122, 0xf, 0xf, true));  // row_ror:2
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x121, 0xf, 0xf, true));  // row_ror:1
+  return v;
+}
+
+// Load 16 consecutive floats (16-B aligned LDS) into registers.
+__device__ __forceinline__ void ld16(float* __restrict__ w, const float* __restrict__ p) {
+  const floatx4* q = reinterpret_cast<const floatx4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const floatx4 v = q[i];
+    w[4 * i + 0] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Activations (exact-erf GELU as nn.GELU(approximate='none'), cnf.py:81 via LayerFactory).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float gelu_f(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+}
+// gelu'(x) = Phi(x) + x * phi(x)
+__device__ __forceinline__ float gelu_grad(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
+  const float pdf = expf(-0.5f * x * x) * 0.39894228040143267794f;
+  return cdf + x * pdf;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Philox4x32-10 counter-based RNG (Salmon et al. 2011) for in-register dropout masks.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += 0x9E3779B9u;
+    k.y += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// 8 keep-bits (bit l = keep decision for hidden layer l+1) for (sample, block, lane).
+__device__ __forceinline__ uint32_t dropout_bits(const BcnfLayout& L, uint64_t seed, uint64_t offset,
+                                                 long long sample, int block, int lane, uint32_t tag) {
+  uint4 ctr = make_uint4((uint32_t)sample, (uint32_t)((unsigned long long)sample >> 32) ^ ((uint32_t)block << 8) ^ tag,
+                         (uint32_t)lane, (uint32_t)offset);
+  uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32) ^ (uint32_t)(offset >> 32));
+  uint4 r = philox4x32_10(ctr, key);
+  const uint32_t t = L.thresh16;
+  uint32_t bits = 0;
+  bits |= ((r.x & 0xffffu) >= t) ? 1u : 0u;
+  bits |= ((r.x >> 16) >= t) ? 2u : 0u;
+  bits |= ((r.y & 0xffffu) >= t) ? 4u : 0u;
+  bits |= ((r.y >> 16) >= t) ? 8u : 0u;
+  bits |= ((r.z & 0xffffu) >= t) ? 16u : 0u;
+  bits |= ((r.z >> 16) >= t) ? 32u : 0u;
+  bits |= ((r.w & 0xffffu) >= t) ? 64u : 0u;
+  bits |= ((r.w >> 16) >= t) ? 128u : 0u;
+  return bits;
+}
+
+// ---------------------------------------------------------------------------------------------
+// fp32-in MFMA 16x16x4 (v_mfma_f32_16x16x4_f32; exact f32 fma chain).
+// Lane l: A[i = l&15][k = l>>4], B[k = l>>4][j = l&15], D[row = 4*(l>>4) + r][col = l&15].
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}

@@ -1,0 +1,329 @@
+"""Host runtime of the fused HIP coupling stack: flat parameter storage, packing, workspaces and the
+autograd boundary. PyTorch provides device memory, streams and autograd plumbing; all arithmetic of
+the coupling stack runs in libbcnf_amd.so (bcnf_amd/csrc/bcnf_stack.hip).
+
+Parameter storage
+-----------------
+The trainable coupling-stack parameters (ActNorm scale/bias + every nested-MLP Linear, in state_dict
+order, orthonormal matrices excluded) live in ONE contiguous fp32 buffer; every nn.Parameter of the
+reference module tree (`layers.0.scale`, `layers.1.nn_a.nn.0.weight`, ...) is a view into it, so
+state_dict / load_state_dict / optimizers keep working unchanged. The frozen orthonormal matrices
+live in a second buffer. `flat_param` is a leaf Parameter over the same storage: the autograd
+Function returns the whole flat gradient for it in a single AccumulateGrad. In "per_param" grad mode
+(the default, what the unchanged bcnf Trainer expects) a post-accumulate hook additionally exposes
+per-layer `.grad` tensors as views of that flat gradient.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from bcnf_amd import _native as N
+
+
+@dataclass
+class StackConfig:
+    size: int
+    nested_sizes: tuple
+    n_blocks: int
+    n_conditions: int
+    dropout: float
+    act_norm: bool
+    two_way: bool
+
+    def desc(self):
+        return N.make_desc(self.size, list(self.nested_sizes), self.n_blocks, self.n_conditions, self.dropout,
+                           self.act_norm, self.two_way)
+
+
+class FusedStack:
+    """Owns the flat parameter buffers of one coupling stack and drives the HIP kernels."""
+
+    def __init__(self, cfg: StackConfig, trainable: list, frozen: list, bind: bool = True):
+        self.cfg = cfg
+        self.bind = bind
+        self.desc = cfg.desc()
+        self._pdesc = ctypes.byref(self.desc)
+        self.trainable = list(trainable)   # canonical order (state_dict order, orthonormal excluded)
+        self.frozen = list(frozen)         # orthonormal matrices, block order
+        self.grad_mode = "per_param"
+        self._packed = None
+        self._pack_frozen = False
+        self._rng_state = None
+        self.seed = None
+        if bind:
+            self.flatten()
+        else:   # standalone layer: flat params are provided per call (see stack_forward(flat=...))
+            self.flat = None
+            self.qflat = None
+            self.flat_param = None
+
+    # ------------------------------------------------------------------ layout
+    @property
+    def supported(self) -> bool:
+        return bool(N.lib().bcnf_stack_supported(self._pdesc))
+
+    def counts(self):
+        a, b = ctypes.c_int64(0), ctypes.c_int64(0)
+        N.check(N.lib().bcnf_param_count(self._pdesc, ctypes.byref(a), ctypes.byref(b)), "bcnf_param_count")
+        return int(a.value), int(b.value)
+
+    def flatten(self):
+        """(Re)build the flat buffers on the parameters' current device and rebind every Parameter
+        to a view of them. Called at construction and after every Module._apply (to(), cuda(), ...)."""
+        params = self.trainable
+        dev = params[0].device
+        n = sum(p.numel() for p in params)
+        flat = torch.empty(n, dtype=torch.float32, device=dev)
+        off = 0
+        with torch.no_grad():
+            for p in params:
+                k = p.numel()
+                flat[off:off + k].copy_(p.detach().reshape(-1))
+                p.data = flat[off:off + k].view(p.shape)
+                off += k
+        nq = sum(q.numel() for q in self.frozen)
+        qflat = torch.empty(max(nq, 1), dtype=torch.float32, device=dev)
+        off = 0
+        with torch.no_grad():
+            for q in self.frozen:
+                k = q.numel()
+                qflat[off:off + k].copy_(q.detach().reshape(-1))
+                q.data = qflat[off:off + k].view(q.shape)
+                off += k
+        self.flat = flat
+        self.qflat = qflat
+        self.flat_param = torch.nn.Parameter(flat, requires_grad=True)
+        self.flat_param.register_post_accumulate_grad_hook(self._on_flat_grad)
+        self._offsets = []
+        off = 0
+        for p in params:
+            self._offsets.append((off, p.numel()))
+            off += p.numel()
+        self._packed = None
+        self._rng_state = None
+
+    def _on_flat_grad(self, fp):
+        if self.grad_mode != "per_param" or fp.grad is None:
+            return
+        g = fp.grad
+        for p, (off, k) in zip(self.trainable, self._offsets):
+            p.grad = g[off:off + k].view(p.shape)
+
+    def sync_grad_state(self):
+        """The Trainer zeroes per-layer grads (set_to_none); drop the stale flat grad with them."""
+        if self.bind and self.grad_mode == "per_param" and self.trainable[0].grad is None:
+            self.flat_param.grad = None
+
+    # ------------------------------------------------------------------ device helpers
+    def _check_inputs(self, x, h, what):
+        cfg = self.cfg
+        if x.dim() != 2 or x.shape[1] != cfg.size:
+            raise ValueError(f"bcnf_amd {what}: expected (N, {cfg.size}) input, got {tuple(x.shape)}")
+        if h.dim() != 2 or h.shape[1] != cfg.n_conditions:
+            raise ValueError(f"bcnf_amd {what}: expected features (N, {cfg.n_conditions}), got {tuple(h.shape)}")
+        self._check_device(x, h)
+
+    def _check_device(self, *tensors):
+        for t in tensors:
+            if t is None:
+                continue
+            if not t.is_cuda:
+                raise RuntimeError("bcnf_amd runs the coupling stack on the MI355X HIP kernels only; "
+                                   "move the model and inputs to a ROCm device (model.to('cuda')).")
+            if t.dtype != torch.float32:
+                raise TypeError(f"bcnf_amd coupling stack is fp32-only, got {t.dtype}")
+        if self.flat is None or self.flat.device.type != "cuda":
+            raise RuntimeError("bcnf_amd: model parameters are not on the GPU; call model.to('cuda') first.")
+
+    def packed(self, fresh: bool = False):
+        """Packed LDS-record buffer. Re-packed on every call unless inside `reuse_pack()` (parameters
+        change in place after each optimizer step; `.data`-rebound views do not share one reliable
+        version counter, so no staleness heuristics). Under HIP-graph capture the pack is a graph node."""
+        if fresh and not self._pack_frozen:
+            # private copy that a later forward cannot overwrite before this one's backward runs
+            nbytes = N.query_i64(N.lib().bcnf_packed_bytes, self._pdesc)
+            out = torch.empty(nbytes // 4, dtype=torch.float32, device=self.flat.device)
+            self._pack_into(out)
+            return out
+        if self._packed is None:
+            nbytes = N.query_i64(N.lib().bcnf_packed_bytes, self._pdesc)
+            self._packed = torch.empty(nbytes // 4, dtype=torch.float32, device=self.flat.device)
+        if not self._pack_frozen:
+            self._pack_into(self._packed)
+        return self._packed
+
+    def _pack_into(self, out):
+        rc = N.lib().bcnf_pack_params(self._pdesc, N.ptr(self.flat), N.ptr(self.qflat), N.ptr(out),
+                                      N.stream_handle(self.flat.device))
+        N.check(rc, "bcnf_pack_params")
+
+    class _Reuse:
+        def __init__(self, stack):
+            self.stack = stack
+
+        def __enter__(self):
+            self.stack.packed()
+            self.prev = self.stack._pack_frozen
+            self.stack._pack_frozen = True
+            return self.stack
+
+        def __exit__(self, *exc):
+            self.stack._pack_frozen = self.prev
+
+    def reuse_pack(self):
+        """Pack once and reuse it for every launch inside the block (e.g. all chunks of sample())."""
+        return FusedStack._Reuse(self)
+
+    def rng_state(self):
+        """Device-resident (seed, offset) for the in-kernel Philox dropout; the offset is bumped by a
+        device-side add after every training forward, so HIP-graph replays draw fresh masks."""
+        if self._rng_state is None:
+            seed = self.seed
+            if seed is None:
+                seed = (torch.cuda.initial_seed() * 0x9E3779B97F4A7C15 + id(self)) & ((1 << 62) - 1)
+            self._rng_state = torch.tensor([seed, 0], dtype=torch.int64, device=self.flat.device)
+        return self._rng_state
+
+    def set_seed(self, seed: int):
+        self.seed = int(seed)
+        self._rng_state = None
+
+    def workspace_bytes(self, batch: int, training: bool):
+        L = N.lib()
+        wb = N.query_i64(L.bcnf_workspace_bytes, self._pdesc, ctypes.c_int64(batch), ctypes.c_int32(int(training)))
+        sb = N.query_i64(L.bcnf_slab_bytes, self._pdesc, ctypes.c_int64(batch))
+        return wb, sb
+
+    # ------------------------------------------------------------------ launches
+    def launch_forward(self, y, h, training: bool, save: bool, want_logp: bool = False):
+        self._check_inputs(y, h, "forward")
+        if h.shape[0] != y.shape[0]:
+            raise ValueError(f"bcnf_amd forward: {y.shape[0]} samples but {h.shape[0]} feature rows")
+        B = y.shape[0]
+        dev = y.device
+        z = torch.empty_like(y)
+        ldj = torch.empty(B, dtype=torch.float32, device=dev)
+        logp = torch.empty(B, dtype=torch.float32, device=dev) if want_logp else None
+        drop = training and self.cfg.dropout > 0.0
+        rng = self.rng_state() if drop else None
+        ws = None
+        if save:
+            wb, _ = self.workspace_bytes(B, training)
+            ws = torch.empty(max(wb // 4, 1), dtype=torch.float32, device=dev)
+        pk = self.packed(fresh=save)
+        rc = N.lib().bcnf_stack_forward(self._pdesc, N.ptr(pk), N.ptr(y), N.ptr(h), ctypes.c_int64(B), N.ptr(z),
+                                        N.ptr(ldj), N.ptr(logp), ctypes.c_int32(int(training)), N.ptr(rng), N.ptr(ws),
+                                        N.stream_handle(dev))
+        N.check(rc, "bcnf_stack_forward")
+        if drop:
+            rng[1:2].add_(1)
+        return z, ldj, logp, (ws, pk)
+
+    def launch_backward(self, h, dz, dldj, training: bool, saved, want_dy: bool, want_dh: bool):
+        ws, pk = saved
+        B = h.shape[0]
+        dev = h.device
+        _, sb = self.workspace_bytes(B, training)
+        slab = torch.empty(max(sb // 4, 1), dtype=torch.float32, device=dev)
+        dparams = torch.empty_like(self.flat)
+        dh = torch.empty_like(h) if want_dh else None
+        dy = torch.empty((B, self.cfg.size), dtype=torch.float32, device=dev) if want_dy else None
+        rc = N.lib().bcnf_stack_backward(self._pdesc, N.ptr(pk), N.ptr(h), N.ptr(dz), N.ptr(dldj),
+                                         ctypes.c_int64(B), ctypes.c_int32(int(training)), N.ptr(ws), N.ptr(dy),
+                                         N.ptr(dh), N.ptr(dparams), N.ptr(slab), N.stream_handle(dev))
+        N.check(rc, "bcnf_stack_backward")
+        return dy, dh, dparams
+
+    def launch_inverse(self, z, h, cond_index=None, training: bool = False):
+        self._check_inputs(z, h, "inverse")
+        n = z.shape[0]
+        if cond_index is None and h.shape[0] != n:
+            raise ValueError(f"bcnf_amd inverse: {n} latents but {h.shape[0]} feature rows and no cond_index")
+        y = torch.empty_like(z)
+        drop = training and self.cfg.dropout > 0.0
+        rng = self.rng_state() if drop else None
+        if cond_index is not None:
+            cond_index = cond_index.to(device=z.device, dtype=torch.int64).contiguous()
+        rc = N.lib().bcnf_stack_inverse(self._pdesc, N.ptr(self.packed()), N.ptr(z), N.ptr(h), N.ptr(cond_index),
+                                        ctypes.c_int64(n), N.ptr(y), ctypes.c_int32(int(training)), N.ptr(rng),
+                                        N.stream_handle(z.device))
+        N.check(rc, "bcnf_stack_inverse")
+        if drop:
+            rng[1:2].add_(1)
+        return y
+
+
+class _StackForward(torch.autograd.Function):
+    """z, ldj = stack(y, h). Backward runs the fused HIP backward once and returns dL/dy, dL/dh and the
+    whole flat parameter gradient (one AccumulateGrad for `flat_param`)."""
+
+    @staticmethod
+    def forward(ctx, y, h, flat_param, stack: FusedStack, training: bool):
+        needs = ctx.needs_input_grad
+        save = any(needs[:3])
+        z, ldj, _, saved = stack.launch_forward(y, h, training, save=save)
+        ctx.stack = stack
+        ctx.training = training
+        ctx.saved = saved
+        ctx.save_for_backward(h)
+        return z, ldj
+
+    @staticmethod
+    def backward(ctx, dz, dldj):
+        (h,) = ctx.saved_tensors
+        stack = ctx.stack
+        if dz is not None:
+            dz = dz.contiguous()
+        if dldj is not None:
+            dldj = dldj.contiguous()
+        need_y, need_h, need_p = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        dy, dh, dparams = stack.launch_backward(h, dz, dldj, ctx.training, ctx.saved, want_dy=need_y, want_dh=need_h)
+        return dy, dh, (dparams if need_p else None), None, None
+
+
+class _StackInverse(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, h, stack: FusedStack, cond_index, training: bool):
+        return stack.launch_inverse(z, h, cond_index, training)
+
+    @staticmethod
+    def backward(ctx, dy):
+        raise NotImplementedError("bcnf_amd: CondRealNVP_v2.inverse is not differentiable (sampling path); "
+                                  "run it under torch.no_grad().")
+
+
+def _set_standalone_params(stack: FusedStack, flat, device):
+    stack.flat = flat.detach().contiguous()
+    if stack.qflat is None or stack.qflat.device != device:
+        stack.qflat = torch.zeros(1, dtype=torch.float32, device=device)
+
+
+def stack_forward(stack: FusedStack, y, h, training: bool, flat=None):
+    y = y.contiguous()
+    h = h.contiguous()
+    if flat is not None:
+        _set_standalone_params(stack, flat, y.device)
+        fp = flat
+        params_grad = flat.requires_grad
+    else:
+        stack.sync_grad_state()
+        params_grad = stack.trainable[0].requires_grad
+        fp = stack.flat_param
+    if torch.is_grad_enabled():
+        if params_grad or y.requires_grad or h.requires_grad:
+            return _StackForward.apply(y, h, fp if params_grad else fp.detach(), stack, training)
+    z, ldj, _, _ = stack.launch_forward(y, h, training, save=False)
+    return z, ldj
+
+
+def stack_inverse(stack: FusedStack, z, h, cond_index=None, training: bool = False, flat=None):
+    z = z.contiguous()
+    h = h.contiguous()
+    if flat is not None:
+        _set_standalone_params(stack, flat, z.device)
+    if torch.is_grad_enabled() and (z.requires_grad or h.requires_grad):
+        return _StackInverse.apply(z, h, stack, cond_index, training)
+    return stack.launch_inverse(z, h, cond_index, training)

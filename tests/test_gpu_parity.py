@@ -1,0 +1,288 @@
+"""GPU parity of the fused HIP coupling stack against the reference's own outputs (golden fixtures made
+by running psaegert/bcnf, tests/golden/make_golden.py) and against the CPU oracle (oracle/cnf_oracle.py).
+
+Tolerance (north star + SURVEY §8d): |got - ref| <= 1e-5 * |ref| + 1e-5 * max(1, max|ref|) for fp32
+values (log_prob, z, ldj, inverse-sampled parameters); orthonormal matrices and split indices bit-exact.
+Gradients (not covered by the north-star tolerance) are gated at rtol 1e-4 + 1e-4 * max(1, max|ref|).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import FC_SMALL_CFG, close, golden_sd, load_golden
+from oracle import cnf_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+FC_SMALL = FC_SMALL_CFG
+
+
+@pytest.fixture(scope="module")
+def model_g1(g1):
+    from bcnf_amd import CondRealNVP_v2
+    torch.manual_seed(0)
+    m = CondRealNVP_v2.from_config(FC_SMALL)
+    m.load_state_dict(golden_sd(g1))
+    m.to(DEV)
+    m.eval()
+    return m
+
+
+def t(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(DEV)
+
+
+def test_forward_matches_reference(model_g1, g1):
+    y, traj = t(g1["y"]), t(g1["traj"])
+    with torch.no_grad():
+        z, h = model_g1.forward(y, traj, log_det_J=True, return_features=True)
+    ok, err = close(z.cpu(), g1["z"])
+    assert ok, f"z max err {err}"
+    ok, err = close(model_g1.log_det_J.cpu(), g1["ldj"])
+    assert ok, f"ldj max err {err}"
+
+
+def test_log_prob_matches_reference(model_g1, g1):
+    y, traj = t(g1["y"]), t(g1["traj"])
+    with torch.no_grad():
+        lp = model_g1.log_prob(y, traj)
+    ref = -g1["nll"].astype(np.float64) - 0.5 * 19 * math.log(2 * math.pi)
+    ok, err = close(lp.cpu(), ref)
+    assert ok, f"log_prob max err {err}"
+
+
+def test_inverse_matches_reference(model_g1, g1):
+    traj = t(g1["traj"])
+    with torch.no_grad():
+        inv = model_g1.inverse(t(g1["zr"]), traj)
+    ok, err = close(inv.cpu(), g1["inv_zr"])
+    assert ok, f"inverse max err {err}"
+    # Round trip of the reference's z: ill-conditioned (|z| up to 46 through 31 perturbed ActNorms) —
+    # the reference's own fp32 result is ~2.6e-4 off the fp64 truth. Gate: at most 2x the reference's
+    # own error against the fp64 oracle (plus the 1e-5 relative floor).
+    with torch.no_grad():
+        rt = model_g1.inverse(t(g1["z"]), traj).cpu().double()
+    sd64 = {k: v.double() for k, v in golden_sd(g1).items()}
+    h64 = O.feature_forward(sd64, O.FC_SMALL_SPEC, torch.from_numpy(g1["traj"]).double())
+    truth = O.model_inverse(sd64, O.FC_SMALL_SPEC, torch.from_numpy(g1["z"]).double(), h64)
+    ref_err = (torch.from_numpy(g1["inv_z"]).double() - truth).abs().max().item()
+    our_err = (rt - truth).abs().max().item()
+    assert our_err <= 2.0 * ref_err + 1e-5 * max(1.0, truth.abs().max().item()), (our_err, ref_err)
+
+
+def test_eval_grads_match_reference(model_g1, g1):
+    from bcnf_amd import inn_nll_loss
+    m = model_g1
+    m.zero_grad(set_to_none=True)
+    y, traj = t(g1["y"]), t(g1["traj"])
+    z, h = m.forward(y, traj, log_det_J=True, return_features=True)
+    h.retain_grad()
+    loss = inn_nll_loss(z, m.log_det_J)
+    loss.backward()
+    assert abs(loss.item() - float(g1["loss"])) <= 1e-5 * abs(float(g1["loss"])) + 1e-5
+    ok, err = close(h.grad.cpu(), g1["dh"], rtol=1e-4, floor=1e-4)
+    assert ok, f"dL/dh max err {err}"
+    named = dict(m.named_parameters())
+    n_checked = 0
+    for k in g1.keys():
+        if not k.startswith("grad/"):
+            continue
+        name = k[5:]
+        ok, err = close(named[name].grad.cpu(), g1[k], rtol=1e-4, floor=1e-4)
+        assert ok, (name, err)
+        n_checked += 1
+    assert n_checked == 576
+    m.zero_grad(set_to_none=True)
+
+
+def test_adam_step_and_clip_match_reference(g1):
+    """Trainer._train_batch order (trainer.py:252-277): zero_grad, forward, NLL, backward, Adam.step,
+    clip_grad_norm_ after the step — with the unchanged per-parameter optimizer."""
+    from bcnf_amd import CondRealNVP_v2, inn_nll_loss
+    torch.manual_seed(0)
+    m = CondRealNVP_v2.from_config(FC_SMALL)
+    m.load_state_dict(golden_sd(g1))
+    m.to(DEV).eval()
+    opt = torch.optim.Adam(m.parameters(), lr=2e-4)
+    opt.zero_grad()
+    z, h = m.forward(t(g1["y"]), t(g1["traj"]), log_det_J=True, return_features=True)
+    inn_nll_loss(z, m.log_det_J).backward()
+    opt.step()
+    total = torch.nn.utils.clip_grad_norm_(m.parameters(), max_norm=1.0)
+    assert abs(total.item() - float(g1["clip_total_norm"])) <= 1e-4 * float(g1["clip_total_norm"])
+    named = dict(m.named_parameters())
+    for k in g1.keys():
+        if k.startswith("after/"):
+            name = k[6:]
+            ok, err = close(named[name].detach().cpu(), g1[k], rtol=1e-5, floor=1e-5)
+            assert ok, (name, err)
+
+
+def test_sample_matches_reference(model_g1):
+    d = load_golden("g3_sample.npz")
+    traj = torch.from_numpy(d["traj"])
+    torch.manual_seed(2024_03_25 + 4)
+    s = model_g1.sample(500, traj, outer=True, batch_size=100)
+    assert tuple(s.shape) == (500, 8, 19) and s.device.type == "cpu"
+    ok, err = close(s, d["sample"])
+    assert ok, f"sample max err {err}"
+    torch.manual_seed(2024_03_25 + 5)
+    s2 = model_g1.sample(250, traj, outer=True, batch_size=3, sample_batch_size=64)
+    ok, err = close(s2, d["sample2"])
+    assert ok, f"chunked sample max err {err}"
+
+
+def test_ballistic_trajectories_match_reference():
+    """Physical-magnitude conditions from the reference ODE simulator on the seeded init model."""
+    from bcnf_amd import CondRealNVP_v2
+    d = load_golden("g9_ballistic.npz")
+    torch.manual_seed(2024_03_25)
+    m = CondRealNVP_v2.from_config(FC_SMALL).to(DEV).eval()
+    with torch.no_grad():
+        z = m.forward(t(d["y"]), t(d["traj"]), log_det_J=True)
+        inv = m.inverse(z, t(d["traj"]))
+    assert close(z.cpu(), d["z"])[0]
+    assert close(m.log_det_J.cpu(), d["ldj"])[0]
+    assert close(inv.cpu(), d["inv"])[0]
+
+
+@pytest.mark.parametrize("B", [1, 15, 17, 33, 1000])
+def test_ragged_batches_vs_oracle(model_g1, g1, B):
+    sd = golden_sd(g1)
+    gen = torch.Generator().manual_seed(B)
+    y = torch.randn(B, 19, generator=gen)
+    traj = 3.0 * torch.randn(B, 30, 3, generator=gen)
+    h = O.feature_forward(sd, O.FC_SMALL_SPEC, traj)
+    zr, lr = O.model_forward(sd, O.FC_SMALL_SPEC, y, h)
+    zlat = torch.randn(B, 19, generator=gen)     # a latent draw (the sampling use case)
+    inv_r = O.model_inverse(sd, O.FC_SMALL_SPEC, zlat, h)
+    with torch.no_grad():
+        z = model_g1.forward(y.to(DEV), traj.to(DEV), log_det_J=True)
+        inv = model_g1.inverse(zlat.to(DEV), traj.to(DEV))
+    assert close(z.cpu(), zr)[0]
+    assert close(model_g1.log_det_J.cpu(), lr)[0]
+    ok, err = close(inv.cpu(), inv_r)
+    assert ok, err
+
+
+def test_empty_batch(model_g1):
+    """The reference's own FC feature net cannot view() an empty batch; the stack itself handles B=0."""
+    from bcnf_amd.fused import stack_forward, stack_inverse
+    with torch.no_grad():
+        z, ldj = stack_forward(model_g1.fused, torch.empty(0, 19, device=DEV), torch.empty(0, 80, device=DEV), False)
+        y = stack_inverse(model_g1.fused, torch.empty(0, 19, device=DEV), torch.empty(0, 80, device=DEV))
+    assert z.shape == (0, 19) and ldj.shape == (0,) and y.shape == (0, 19)
+
+
+@pytest.mark.parametrize("shape", [
+    dict(size=19, nested_sizes=[16] * 3, n_blocks=4, n_conditions=80, dropout=0.0, act_norm=True),
+    dict(size=7, nested_sizes=[12, 9], n_blocks=3, n_conditions=5, dropout=0.1, act_norm=False),
+    dict(size=32, nested_sizes=[16], n_blocks=2, n_conditions=200, dropout=0.0, act_norm=True),
+    dict(size=2, nested_sizes=[4] * 8, n_blocks=5, n_conditions=3, dropout=0.0, act_norm=True),
+])
+def test_other_shapes_vs_oracle(shape):
+    """Forward / inverse / eval grads for non-FC_small shapes (odd splits, no ActNorm, dropout stride 2/3,
+    padded C, 8 nested layers) against the oracle."""
+    from bcnf_amd import CondRealNVP_v2, inn_nll_loss
+    C = shape["n_conditions"]
+    torch.manual_seed(7)
+    fnets = [{"type": "ConcatenateCondition", "kwargs": {"input_size": None, "output_size": C}}]
+    cfg = {"global": {"parameter_selection": [f"p{i}" for i in range(shape["size"])]},
+           "model": {"kwargs": shape}, "feature_networks": fnets}
+    m = CondRealNVP_v2.from_config(cfg)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if n.endswith("scale"):
+                p.copy_(0.5 + torch.rand_like(p))
+            elif n.endswith("bias") and n.count(".") == 2:
+                p.copy_(0.1 * torch.randn_like(p))
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    spec = O.StackSpec(size=shape["size"], nested_sizes=shape["nested_sizes"], n_blocks=shape["n_blocks"],
+                       n_conditions=C, dropout=shape["dropout"], act_norm=shape["act_norm"])
+    m.to(DEV).eval()
+    B = 37
+    y = torch.randn(B, shape["size"])
+    c = torch.randn(B, C)
+    zr, lr = O.model_forward(sd, spec, y, c)
+    z = m.forward(y.to(DEV), c.to(DEV), log_det_J=True)
+    assert close(z.detach().cpu(), zr)[0]
+    assert close(m.log_det_J.detach().cpu(), lr)[0]
+    with torch.no_grad():
+        inv = m.inverse(zr.to(DEV), c.to(DEV))
+    assert close(inv.cpu(), y, rtol=1e-4, floor=1e-4)[0]
+    # eval-mode grads vs oracle autograd
+    sdg = {k: v.clone().requires_grad_(not k.endswith("orthonormal_matrix")) for k, v in sd.items()}
+    cg = c.clone().requires_grad_(True)
+    zo, lo = O.model_forward(sdg, spec, y, cg)
+    O.inn_nll_loss(zo, lo).backward()
+    m.zero_grad(set_to_none=True)
+    cd = c.to(DEV).requires_grad_(True)
+    zg = m.forward(y.to(DEV), cd, log_det_J=True)
+    inn_nll_loss(zg, m.log_det_J).backward()
+    assert close(cd.grad.cpu(), cg.grad, rtol=1e-4, floor=1e-4)[0]
+    for n, p in m.named_parameters():
+        if p.grad is None:
+            continue
+        ok, err = close(p.grad.cpu(), sdg[n].grad, rtol=1e-4, floor=1e-4)
+        assert ok, (n, err)
+
+
+def test_loaded_orthonormal_matrices_bit_exact(model_g1, g1):
+    """Q from a checkpoint reaches the device (flat frozen buffer) bit-for-bit."""
+    for i, layer in enumerate(model_g1.layers):
+        if hasattr(layer, "orthonormal_matrix"):
+            got = layer.orthonormal_matrix.detach().cpu().numpy()
+            assert got.tobytes() == g1[f"sd/layers.{i}.orthonormal_matrix"].tobytes()
+
+
+def test_training_dropout_statistics_and_consistency(g1):
+    """Train mode: Philox dropout keeps ~(1-p) of units, masks differ between steps, and the backward is
+    the exact gradient of the forward that drew them (central differences at a fixed RNG offset)."""
+    from bcnf_amd import CondRealNVP_v2, inn_nll_loss
+    torch.manual_seed(0)
+    m = CondRealNVP_v2.from_config(FC_SMALL)
+    m.load_state_dict(golden_sd(g1))
+    m.to(DEV).train()
+    m.fused.set_seed(1234)
+    y, traj = t(g1["y"]), t(g1["traj"])
+    with torch.no_grad():
+        z1 = m.forward(y, traj)
+        z2 = m.forward(y, traj)
+    assert not torch.allclose(z1, z2)   # fresh masks per call
+    # keep rate from the saved masks
+    st = m.fused
+    h = m.feature_network_stack(traj)
+    _, _, _, (ws, _) = st.launch_forward(y, h, True, save=True)
+    nb, B = 32, y.shape[0]
+    words = ws[nb * B * 32:].view(torch.int32)[: ((nb + 3) // 4) * B * 16].cpu().numpy().view(np.uint32)
+    bits = np.unpackbits(words.view(np.uint8)).reshape(-1, 4, 8)[:, :, 1:]  # 7 layers used of 8 bits/byte
+    keep = bits.mean()
+    assert abs(keep - (1 - 0.383)) < 0.01, keep
+
+    # gradient consistency at a fixed dropout offset: central difference along the gradient direction
+    def loss_at(offset):
+        st.rng_state()[1] = offset
+        zz = m.forward(y, traj, log_det_J=True)
+        return inn_nll_loss(zz, m.log_det_J)
+
+    m.zero_grad(set_to_none=True)
+    L0 = loss_at(77)
+    L0.backward()
+    g = torch.cat([p.grad.reshape(-1) for p in st.trainable])
+    gn = g.norm().item()
+    v = g / gn
+    eps = 1e-3 / max(1.0, gn / 100.0)
+    with torch.no_grad():
+        st.flat.add_(eps * v)
+        Lp = loss_at(77).double().item()
+        st.flat.add_(-2 * eps * v)
+        Lm = loss_at(77).double().item()
+        st.flat.add_(eps * v)
+    fd = (Lp - Lm) / (2 * eps)
+    assert abs(fd - gn) <= 2e-2 * gn, (fd, gn)
+    # a different offset draws different masks -> different loss
+    with torch.no_grad():
+        assert loss_at(78).item() != loss_at(77).item()
