@@ -25,7 +25,7 @@ OK, ERR_ARG, ERR_UNSUPPORTED, ERR_HIP = 0, 1, 2, 3
 EXPORTS = (
     "bcnf_stack_supported", "bcnf_param_count", "bcnf_packed_bytes", "bcnf_workspace_bytes",
     "bcnf_slab_bytes", "bcnf_pack_params", "bcnf_stack_forward", "bcnf_stack_backward",
-    "bcnf_stack_inverse", "bcnf_status_string", "bcnf_last_hip_error",
+    "bcnf_stack_inverse", "bcnf_grad_reduce", "bcnf_status_string", "bcnf_last_hip_error",
 )
 
 
@@ -79,6 +79,7 @@ def _bind(lib):
         "bcnf_stack_forward": (_i32, [_pdesc, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
         "bcnf_stack_backward": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
         "bcnf_stack_inverse": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp]),
+        "bcnf_grad_reduce": (_i32, [_pdesc, _vp, _i64, _vp, _vp]),
         "bcnf_status_string": (ctypes.c_char_p, [_i32]),
         "bcnf_last_hip_error": (_i32, []),
     }

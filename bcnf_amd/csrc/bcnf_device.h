@@ -46,17 +46,20 @@ __device__ __forceinline__ int coupling_base(const BcnfLayout& L, int k) {
 #define BCNF_DPP(R, A, X, W) "v_fmac_f32_dpp " A ", " X ", " W " row_ror:" #R " row_mask:0xf bank_mask:0xf\n\t"
 
 __device__ __forceinline__ float rot16(float x, const float* __restrict__ w, float acc) {
+  // two interleaved partial sums (even / odd rotations) halve the dependent fmac chain
+  float acc1;
   acc = fmaf(x, w[0], acc);
   asm("s_nop 1\n\t"
-      BCNF_DPP(1, "%0", "%1", "%2") BCNF_DPP(2, "%0", "%1", "%3") BCNF_DPP(3, "%0", "%1", "%4")
-      BCNF_DPP(4, "%0", "%1", "%5") BCNF_DPP(5, "%0", "%1", "%6") BCNF_DPP(6, "%0", "%1", "%7")
-      BCNF_DPP(7, "%0", "%1", "%8") BCNF_DPP(8, "%0", "%1", "%9") BCNF_DPP(9, "%0", "%1", "%10")
-      BCNF_DPP(10, "%0", "%1", "%11") BCNF_DPP(11, "%0", "%1", "%12") BCNF_DPP(12, "%0", "%1", "%13")
-      BCNF_DPP(13, "%0", "%1", "%14") BCNF_DPP(14, "%0", "%1", "%15") BCNF_DPP(15, "%0", "%1", "%16")
-      : "+v"(acc)
+      "v_mul_f32_dpp %1, %2, %3 row_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+      BCNF_DPP(2, "%0", "%2", "%4") BCNF_DPP(3, "%1", "%2", "%5") BCNF_DPP(4, "%0", "%2", "%6")
+      BCNF_DPP(5, "%1", "%2", "%7") BCNF_DPP(6, "%0", "%2", "%8") BCNF_DPP(7, "%1", "%2", "%9")
+      BCNF_DPP(8, "%0", "%2", "%10") BCNF_DPP(9, "%1", "%2", "%11") BCNF_DPP(10, "%0", "%2", "%12")
+      BCNF_DPP(11, "%1", "%2", "%13") BCNF_DPP(12, "%0", "%2", "%14") BCNF_DPP(13, "%1", "%2", "%15")
+      BCNF_DPP(14, "%0", "%2", "%16") BCNF_DPP(15, "%1", "%2", "%17")
+      : "+v"(acc), "=&v"(acc1)
       : "v"(x), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]), "v"(w[6]), "v"(w[7]), "v"(w[8]),
         "v"(w[9]), "v"(w[10]), "v"(w[11]), "v"(w[12]), "v"(w[13]), "v"(w[14]), "v"(w[15]));
-  return acc;
+  return acc + acc1;
 }
 
 // Two independent rotation chains interleaved in one asm block (hides the fmac dependency latency).
@@ -108,16 +111,58 @@ __device__ __forceinline__ void ld16(float* __restrict__ w, const float* __restr
 }
 
 // ---------------------------------------------------------------------------------------------
-// Activations (exact-erf GELU as nn.GELU(approximate='none'), cnf.py:81 via LayerFactory).
+// Branch-free fp32 erf / tanh (coefficients fitted and verified in emulated fp32 by
+// tools/fit_erf.py: erf <= 2.3 ulp / 1.1e-7 abs, tanh <= 1.3 ulp). Both regions are evaluated and
+// selected, so a GELU never splits the block body into divergent basic blocks (ocml's erff does).
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ float gelu_f(float x) {
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+__device__ __forceinline__ float erf_bf(float a) {
+  const float t = fabsf(a), s = a * a;
+  float p = 8.397787315e-05f;                       // |a| < 0.921875 : a * P(a^2)
+  p = fmaf(p, s, -8.149803616e-04f);
+  p = fmaf(p, s, 5.201715976e-03f);
+  p = fmaf(p, s, -2.685970254e-02f);
+  p = fmaf(p, s, 1.128370166e-01f);
+  p = fmaf(p, s, -3.761263490e-01f);
+  p = fmaf(p, s, 1.128379226e+00f);
+  const float ra = a * p;
+  float q = -8.156862918e-07f;                      // otherwise   : 1 - exp(-t Q(t))
+  q = fmaf(q, t, 3.048476174e-05f);
+  q = fmaf(q, t, -4.713801318e-04f);
+  q = fmaf(q, t, 4.200363066e-03f);
+  q = fmaf(q, t, -2.491468750e-02f);
+  q = fmaf(q, t, 1.075745374e-01f);
+  q = fmaf(q, t, 6.343348026e-01f);
+  q = fmaf(q, t, 1.128852129e+00f);
+  float rb = 1.0f - expf(-(q * t));
+  rb = (t >= 3.9375f) ? 1.0f : rb;
+  rb = copysignf(rb, a);
+  return (t < 0.921875f) ? ra : rb;
 }
-// gelu'(x) = Phi(x) + x * phi(x)
-__device__ __forceinline__ float gelu_grad(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
-  const float pdf = expf(-0.5f * x * x) * 0.39894228040143267794f;
-  return cdf + x * pdf;
+
+__device__ __forceinline__ float tanh_bf(float a) {
+  const float t = fabsf(a), s = a * a;
+  float p = 2.321433276e-03f;                       // |a| < 0.625 : a + a^3 P(a^2)
+  p = fmaf(p, s, -8.373901248e-03f);
+  p = fmaf(p, s, 2.178018540e-02f);
+  p = fmaf(p, s, -5.396108329e-02f);
+  p = fmaf(p, s, 1.333331466e-01f);
+  p = fmaf(p, s, -3.333333433e-01f);
+  const float rs = fmaf(a * s, p, a);
+  const float e = expf(2.0f * t);                   // otherwise   : 1 - 2 / (exp(2t) + 1)
+  float rl = 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
+  rl = copysignf(rl, a);
+  return (t < 0.625f) ? rs : rl;
+}
+
+// Exact-erf GELU as nn.GELU(approximate='none') (cnf.py:81 via LayerFactory).
+__device__ __forceinline__ float gelu_f(float x) {
+  return 0.5f * x * (1.0f + erf_bf(x * 0.70710678118654752440f));
+}
+// GELU and its derivative Phi(x) + x phi(x), sharing one erf.
+__device__ __forceinline__ void gelu_fg(float x, float& g, float& dg) {
+  const float cdf = 0.5f * (1.0f + erf_bf(x * 0.70710678118654752440f));
+  g = x * cdf;
+  dg = fmaf(x, expf(-0.5f * x * x) * 0.39894228040143267794f, cdf);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -15,6 +15,7 @@
 #include "../../include/bcnf_amd.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -23,7 +24,6 @@ namespace {
 
 constexpr int NT_EXTRA = 7;            // tiles: D_1..D_NH, D_T, D_S, A_0..A_NH, PA, GA, PB, GB
 constexpr int TILE = BCNF_ROWS * BCNF_TSTRIDE;   // 272 floats
-constexpr int MAXPF = 8;               // max float4 per thread for one staged record set
 
 // ------------------------------------------------------------------------------------------------
 // Host-side layout
@@ -90,11 +90,21 @@ int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
   L->pb_off = L->pf_off + nbl * 16 * L->RF;
   L->pi_off = L->pb_off + nbl * 16 * L->RB;
   L->w1t_off = L->pi_off + nbl * 16 * L->RF;
-  L->w1h_off = L->w1t_off + nbl * L->Cp * 16;
-  L->ldc_off = L->w1h_off + nbl * 16 * L->Cp;
+  L->w1h_off = L->w1t_off;                     // (single padded W1h^T copy serves HP, dh and dW1h)
+  L->ldc_off = L->w1t_off + nbl * (long long)L->Cp * 17;
   L->total = L->ldc_off + 4;
   return BCNF_OK;
 }
+
+size_t fwd_lds_bytes(const BcnfLayout& L) {   // rec ring 2, W1h^T ring 2, HP partials 2, features
+  return sizeof(float) * (size_t)(2 * 16 * L.RF + 2 * L.Cp * 17 + 2 * 1024 + 16 * (L.Cp + 1));
+}
+size_t bwd_lds_bytes(const BcnfLayout& L) {   // F/B rec rings 2, W1h^T ring 4, HP 2, tiles 2, features
+  const int NT = 2 * L.NH + NT_EXTRA;
+  return sizeof(float) * (size_t)(2 * 16 * L.RF + 2 * 16 * L.RB + 4 * L.Cp * 17 + 2 * 1024 + 2 * NT * TILE +
+                                  TILE + 8 * (2 * BCNF_MAX_HIDDEN + 8 + 16) + 16 * (L.Cp + 1));
+}
+constexpr size_t LDS_MAX = 160 * 1024;
 
 bool layout_supported(const BcnfLayout& L, const BcnfStackDesc* d) {
   if (d->two_way) return false;
@@ -103,7 +113,8 @@ bool layout_supported(const BcnfLayout& L, const BcnfStackDesc* d) {
   for (int l = 1; l <= L.NH; ++l)
     if (L.H[l] > 16) return false;
   if (L.C < 1 || L.Cp > 256) return false;
-  if (16 * (L.RF + L.RB) > MAXPF * 4 * BCNF_WG) return false;
+  if (16 * L.RF > 4 * 4 * BCNF_WG || 16 * L.RB > 4 * 4 * BCNF_WG || L.Cp * 17 > 5 * 4 * BCNF_WG) return false;
+  if (fwd_lds_bytes(L) > LDS_MAX || bwd_lds_bytes(L) > LDS_MAX) return false;
   return true;
 }
 
@@ -148,9 +159,12 @@ __device__ float rec_f(const BcnfLayout& L, const float* P, const float* Q, int 
     return (j < Db && src < L.H[NH]) ? cW(L, P, k, NH + 1, half * Db + j, src) : 0.f;
   }
   if (e >= L.rf_q && e < L.rf_q + 64) {
-    if (k >= L.nb - 1) return 0.f;
-    const float* q = Q + (long long)k * D * D;
     const int qi = (e - L.rf_q) / 16, r = (e - L.rf_q) % 16, src = (j - r) & 15;
+    if (k >= L.nb - 1) {   // last block has no mix: identity, so the kernels need no branch
+      if (r != 0) return 0.f;
+      return (qi == 0 && j < Da) || (qi == 3 && j < Db) ? 1.f : 0.f;
+    }
+    const float* q = Q + (long long)k * D * D;
     if (!inverse) {  // y_new = y @ Q   (cnf.py:335): [q0 QAA | q1 QBA | q2 QAB | q3 QBB]
       switch (qi) {
         case 0: return (j < Da && src < Da) ? q[src * D + j] : 0.f;
@@ -192,8 +206,8 @@ __device__ float rec_b(const BcnfLayout& L, const float* P, const float* Q, int 
 __global__ void k_pack(BcnfLayout L, const float* __restrict__ P, const float* __restrict__ Q, float* __restrict__ out) {
   const long long n_pf = (long long)L.nb * 16 * L.RF;
   const long long n_pb = (long long)L.nb * 16 * L.RB;
-  const long long n_w = (long long)L.nb * L.Cp * 16;
-  const long long total = 2 * n_pf + n_pb + 2 * n_w;
+  const long long n_w = (long long)L.nb * L.Cp * 17;
+  const long long total = 2 * n_pf + n_pb + n_w;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
     float v;
     long long o;
@@ -211,16 +225,11 @@ __global__ void k_pack(BcnfLayout L, const float* __restrict__ P, const float* _
       const int e = (int)(ii % L.RF), j = (int)((ii / L.RF) % 16), k = (int)(ii / (16LL * L.RF));
       v = rec_f(L, P, Q, k, j, e, true);
       o = L.pi_off + ii;
-    } else if (i < 2 * n_pf + n_pb + n_w) {           // W1hT [k][c][j]
+    } else {                                          // W1h^T [k][c][17] (column 16 = pad)
       const long long ii = i - 2 * n_pf - n_pb;
-      const int j = (int)(ii % 16), c = (int)((ii / 16) % L.Cp), k = (int)(ii / (16LL * L.Cp));
-      v = (j < L.H[1] && c < L.C) ? cW(L, P, k, 1, j, L.Da + c) : 0.f;
+      const int j = (int)(ii % 17), c = (int)((ii / 17) % L.Cp), k = (int)(ii / (17LL * L.Cp));
+      v = (j < 16 && j < L.H[1] && c < L.C) ? cW(L, P, k, 1, j, L.Da + c) : 0.f;
       o = L.w1t_off + ii;
-    } else {                                          // W1h [k][j][c]
-      const long long ii = i - 2 * n_pf - n_pb - n_w;
-      const int c = (int)(ii % L.Cp), j = (int)((ii / L.Cp) % 16), k = (int)(ii / (16LL * L.Cp));
-      v = (j < L.H[1] && c < L.C) ? cW(L, P, k, 1, j, L.Da + c) : 0.f;
-      o = L.w1h_off + ii;
     }
     out[o] = v;
   }
@@ -249,29 +258,35 @@ __global__ void k_ldc(BcnfLayout L, const float* __restrict__ P, float* __restri
 // ------------------------------------------------------------------------------------------------
 // Shared pieces of the stack kernels
 // ------------------------------------------------------------------------------------------------
-// Cooperative copy of n floats (multiple of 4) global -> registers (phase 1) -> LDS (phase 2).
-// Named members (no array) so the staging registers never become a scratch alloca.
+// Cooperative copy of n floats (multiple of 4) global -> registers (phase 1) -> LDS (phase 2), so the
+// global latency of the NEXT block's data hides under the current block's compute.
+template <int N>
 struct Stage {
-  floatx4 r0, r1, r2, r3, r4, r5, r6, r7;   // ext_vector (not HIP's float4 struct: that copies via memcpy)
+  floatx4 r[N];
   __device__ __forceinline__ void load(const float* __restrict__ g, int n) {
     const floatx4* g4 = reinterpret_cast<const floatx4*>(g);
     const int n4 = n >> 2, t = (int)threadIdx.x;
-#define BCNF_LD(I) { const int idx = t + (I) * BCNF_WG; r##I = g4[idx < n4 ? idx : 0]; }
-    BCNF_LD(0) BCNF_LD(1) BCNF_LD(2) BCNF_LD(3) BCNF_LD(4) BCNF_LD(5) BCNF_LD(6) BCNF_LD(7)
-#undef BCNF_LD
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int idx = t + i * BCNF_WG;
+      r[i] = g4[idx < n4 ? idx : 0];   // unconditional (clamped) so r[] stays in VGPRs
+    }
   }
   __device__ __forceinline__ void store(float* __restrict__ s, int n) const {
     floatx4* s4 = reinterpret_cast<floatx4*>(s);
     const int n4 = n >> 2, t = (int)threadIdx.x;
-#define BCNF_ST(I) { const int idx = t + (I) * BCNF_WG; if (idx < n4) s4[idx] = r##I; }
-    BCNF_ST(0) BCNF_ST(1) BCNF_ST(2) BCNF_ST(3) BCNF_ST(4) BCNF_ST(5) BCNF_ST(6) BCNF_ST(7)
-#undef BCNF_ST
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int idx = t + i * BCNF_WG;
+      if (idx < n4) s4[idx] = r[i];
+    }
   }
 };
-static_assert(MAXPF == 8, "Stage holds 8 float4 per thread");
+constexpr int STAGE_REC = 4;   // 16 * RF floats  <= 4 float4 per thread (RF <= 256)
+constexpr int STAGE_W1T = 5;   // Cp * 17 floats  <= 5 float4 per thread (Cp <= 256)
 
 // Stage the workgroup's 16 feature rows h[row] (optionally gathered via cond_index) into
-// ht[16][Cp+1], zero-padded to Cp columns.
+// ht[16][Cp+1], zero-padded to Cp columns. Rows past the batch repeat the last row.
 __device__ __forceinline__ void stage_features(const BcnfLayout& L, const float* __restrict__ h,
                                                const int64_t* __restrict__ cond_index, long long n_rows,
                                                float* __restrict__ ht) {
@@ -285,16 +300,27 @@ __device__ __forceinline__ void stage_features(const BcnfLayout& L, const float*
   }
 }
 
-// Per-wave K-quarter of HP_k = H (16 x Cp) @ W1h_k^T (Cp x 16) on fp32 MFMA; partial tile to hpbuf[wave].
-__device__ __forceinline__ void hp_quarter(const BcnfLayout& L, const float* __restrict__ w1t,
-                                           const float* __restrict__ ht, float* __restrict__ hpbuf, int blk) {
+// Per-wave K-quarter of HP_k = H (16 x Cp) @ W1h_k^T (Cp x 16) on fp32 MFMA from LDS; the partial
+// tile goes to hpbuf[wave] and the consumer sums the four quarters.
+__device__ __forceinline__ void hp_quarter(const BcnfLayout& L, const float* __restrict__ wt,
+                                           const float* __restrict__ ht, float* __restrict__ hpbuf) {
   const int wave = threadIdx.x >> 6, l64 = threadIdx.x & 63, q = l64 >> 4, r = l64 & 15;
   const int nsteps = L.Cp >> 2;
   const int t0 = (wave * nsteps) >> 2, t1 = ((wave + 1) * nsteps) >> 2;
-  const float* wb = w1t + (long long)blk * L.Cp * 16;
   const int hs = L.Cp + 1;
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int t = t0; t < t1; ++t) acc = mfma4(ht[r * hs + 4 * t + q], wb[(4 * t + q) * 16 + r], acc);
+  int t = t0;
+  for (; t + 4 <= t1; t += 4) {        // all operand reads of 4 steps before their MFMAs
+    float a[4], bv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a[u] = ht[r * hs + 4 * (t + u) + q];
+      bv[u] = wt[(4 * (t + u) + q) * 17 + r];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = mfma4(a[u], bv[u], acc);
+  }
+  for (; t < t1; ++t) acc = mfma4(ht[r * hs + 4 * t + q], wt[(4 * t + q) * 17 + r], acc);
   float* o = hpbuf + wave * 256;
 #pragma unroll
   for (int i = 0; i < 4; ++i) o[(4 * q + i) * 16 + r] = acc[i];
@@ -305,33 +331,70 @@ __device__ __forceinline__ float hp_sum(const float* __restrict__ hpbuf, int s, 
   return (p[0] + p[256]) + (p[512] + p[768]);
 }
 
-// Nested MLP forward on the row layout (cnf.py:98-107). Input x (layer-1 y-part operand), returns
-// t, s' (pre-tanh). Optionally keeps activations / masked GELU derivatives for the backward.
+// Compile-time mirror of the forward / backward record layouts of make_layout (checked on the host).
+template <int NH>
+struct RecF {
+  static constexpr int B1 = 4, W1 = 8, HID = 24, T = 24 + 17 * (NH - 1), S = T + 17;
+  static constexpr int Q = (S + 17 + 3) & ~3, MLP_END = (S + 17 + 3) & ~3, USED = Q + 64;
+};
+template <int NH>
+struct RecB {
+  static constexpr int W1T = 0, HID = 16, TT = 16 + 16 * (NH - 1), ST = TT + 16, QT = ST + 16, USED = QT + 64;
+};
+
+// Burst-load floats [lo, hi) of this lane's LDS record into registers (compile-time indices, so the
+// array lives in VGPRs): one LDS wait per block instead of one per layer.
+template <int LO, int HI>
+__device__ __forceinline__ void ld_rec(float* __restrict__ rr, const float* __restrict__ R) {
+  static_assert(LO % 4 == 0 && HI % 4 == 0, "record slices are 16-B aligned");
+  const floatx4* R4 = reinterpret_cast<const floatx4*>(R + LO);
+#pragma unroll
+  for (int i = 0; i < (HI - LO) / 4; ++i) {
+    const floatx4 v = R4[i];
+    rr[LO + 4 * i + 0] = v.x;
+    rr[LO + 4 * i + 1] = v.y;
+    rr[LO + 4 * i + 2] = v.z;
+    rr[LO + 4 * i + 3] = v.w;
+  }
+}
+
+// Nested MLP forward on the row layout (cnf.py:98-107) from a register-resident forward record.
+// Input x (layer-1 y-part operand); returns t and s' (pre-tanh). KEEP: also the (masked) activations
+// and masked GELU derivatives for the backward.
 template <int NH, bool KEEP>
-__device__ __forceinline__ void mlp_forward(const BcnfLayout& L, const float* __restrict__ R, float x, float hp,
+__device__ __forceinline__ void mlp_forward(const BcnfLayout& L, const float* __restrict__ rr, float x, float hp,
                                             uint32_t bits, bool drop, float& T, float& Sp,
                                             float* act, float* gd) {
-  float w[16];
-  ld16(w, R + L.rf_w1);
-  float pre = rot16(x, w, R[L.rf_b1] + hp);
-  float m = drop ? ((bits & 1u) ? L.keep_scale : 0.f) : 1.f;
-  float a = gelu_f(pre) * m;
-  if (KEEP) { act[0] = a; gd[0] = gelu_grad(pre) * m; }
+  using F = RecF<NH>;
+  float a = x;
 #pragma unroll
-  for (int l = 2; l <= NH; ++l) {
-    const float* Rl = R + L.rf_hid + 17 * (l - 2);
-    ld16(w, Rl);
-    pre = rot16(a, w, Rl[16]);
-    m = drop ? (((bits >> (l - 1)) & 1u) ? L.keep_scale : 0.f) : 1.f;
-    a = gelu_f(pre) * m;
-    if (KEEP) { act[l - 1] = a; gd[l - 1] = gelu_grad(pre) * m; }
+  for (int l = 1; l <= NH; ++l) {
+    const float* w = (l == 1) ? rr + F::W1 : rr + F::HID + 17 * (l - 2);
+    const float bias = (l == 1) ? rr[F::B1] + hp : w[16];
+    const float pre = rot16(a, w, bias);
+    const float m = drop ? (((bits >> (l - 1)) & 1u) ? L.keep_scale : 0.f) : 1.f;
+    if (KEEP) {
+      float g, dg;
+      gelu_fg(pre, g, dg);
+      a = g * m;
+      act[l - 1] = a;
+      gd[l - 1] = dg * m;
+    } else {
+      a = gelu_f(pre) * m;
+    }
   }
-  float wt[16], ws[16];
-  ld16(wt, R + L.rf_t);
-  ld16(ws, R + L.rf_s);
-  T = R[L.rf_t + 16];
-  Sp = R[L.rf_s + 16];
-  rot16x2(a, wt, T, a, ws, Sp);
+  T = rr[F::T + 16];
+  Sp = rr[F::S + 16];
+  rot16x2(a, rr + F::T, T, a, rr + F::S, Sp);
+}
+
+// Row-layout orthonormal mix: (na, nb) = (a, b) @ M with the four pre-rotated quadrants at rq
+// (register-resident): [a->a | b->a | a->b | b->b].
+__device__ __forceinline__ void mix(const float* __restrict__ rq, float a, float b, float& na, float& nbv) {
+  na = 0.f;
+  nbv = 0.f;
+  rot16x2(a, rq, na, a, rq + 32, nbv);
+  rot16x2(b, rq + 16, na, b, rq + 48, nbv);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -344,90 +407,88 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
                                                      float* __restrict__ logp, const uint64_t* __restrict__ rng,
                                                      float* __restrict__ ysave, uint32_t* __restrict__ msave) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int RFL = 16 * L.RF;
+  const int RFL = 16 * L.RF, WTL = L.Cp * 17;
   float* rec = smem;                    // [2][16*RF]
-  float* hpb = rec + 2 * RFL;           // [2][4][256]
+  float* wt = rec + 2 * RFL;            // [2][Cp*17]   W1h^T ring, staged two blocks ahead
+  float* hpb = wt + 2 * WTL;            // [2][4][256]
   float* ht = hpb + 2 * 1024;           // [16][Cp+1]
   const int tid = threadIdx.x, j = tid & 15, s = tid >> 4;
   const long long b = (long long)blockIdx.x * 16 + s;
-  const bool valid = b < B;
-  const long long bc = valid ? b : B - 1;
+  const long long bc = b < B ? b : B - 1;           // rows past the batch replay the last sample
   const int D = L.D, Da = L.Da, Db = L.Db, nb = L.nb;
+  const float* pf = pk + L.pf_off;
+  const float* pw = pk + L.w1t_off;
 
-  stage_features(L, h, nullptr, B, ht);
-  {
-    Stage st;
-    st.load(pk + L.pf_off, RFL);
-    st.store(rec, RFL);
-  }
-  __syncthreads();
-  hp_quarter(L, pk + L.w1t_off, ht, hpb, 0);
-  __syncthreads();
-
+  // every global input the loop reads is loaded before the prologue barrier, so the loop's only
+  // outstanding VMEM ops are its own (unconditional) prefetches and the waitcnt pass never has to
+  // drain them early
   float ya = (j < Da) ? y[bc * D + j] : 0.f;
   float yb = (j < Db) ? y[bc * D + Da + j] : 0.f;
-  float ldj = 0.f;
   uint64_t seed = 0, off = 0;
   if (DROP) { seed = rng[0]; off = rng[1]; }
+  const float ldc = pk[L.ldc_off];
+  stage_features(L, h, nullptr, B, ht);
+  {
+    Stage<STAGE_REC> sr;
+    sr.load(pf, RFL);
+    sr.store(rec, RFL);
+    Stage<STAGE_W1T> sw;
+    sw.load(pw, WTL);
+    sw.store(wt, WTL);
+    sw.load(pw + (long long)(nb > 1 ? 1 : 0) * WTL, WTL);
+    sw.store(wt + WTL, WTL);
+  }
+  __syncthreads();
+  hp_quarter(L, wt, ht, hpb);
+  __syncthreads();
+
+  float ldj = 0.f;
   uint32_t mword = 0;
 
   for (int k = 0; k < nb; ++k) {
     const int cur = k & 1;
-    Stage st;
-    if (k + 1 < nb) {
-      st.load(pk + L.pf_off + (long long)(k + 1) * RFL, RFL);
-      hp_quarter(L, pk + L.w1t_off, ht, hpb + (cur ^ 1) * 1024, k + 1);
-    }
-    const float* R = rec + cur * RFL + j * L.RF;
-    if (SAVE && valid) {
-      float* ys = ysave + ((long long)k * B + b) * 32;
+    const int k1 = k + 1 < nb ? k + 1 : nb - 1, k2 = k + 2 < nb ? k + 2 : nb - 1;   // clamped: no branches
+    Stage<STAGE_REC> sr;
+    Stage<STAGE_W1T> sw;
+    sr.load(pf + (long long)k1 * RFL, RFL);
+    sw.load(pw + (long long)k2 * WTL, WTL);
+    hp_quarter(L, wt + (cur ^ 1) * WTL, ht, hpb + (cur ^ 1) * 1024);
+
+    float rr[RecF<NH>::USED];
+    ld_rec<0, RecF<NH>::USED>(rr, rec + cur * RFL + j * L.RF);
+    if (SAVE) {
+      float* ys = ysave + ((long long)k * B + bc) * 32;
       ys[j] = ya;
       ys[16 + j] = yb;
     }
-    const floatx4 an = *reinterpret_cast<const floatx4*>(R);
-    const float xa = fmaf(an.x, ya, an.y);           // ActNorm (cnf.py:349)
-    const float xb = fmaf(an.z, yb, an.w);
+    const float xa = fmaf(rr[0], ya, rr[1]);          // ActNorm (cnf.py:349)
+    const float xb = fmaf(rr[2], yb, rr[3]);
     uint32_t bits = 0xffu;
-    if (DROP) bits = dropout_bits(L, seed, off, b, k, j, 0u);
+    if (DROP) bits = dropout_bits(L, seed, off, bc, k, j, 0u);
+    float T, Sp;
+    mlp_forward<NH, false>(L, rr, xa, hp_sum(hpb + cur * 1024, s, j), bits, DROP, T, Sp, nullptr, nullptr);
+    const float S = tanh_bf(Sp);                      // cnf.py:107
+    const float zb = fmaf(expf(S), xb, T);            // cnf.py:179
+    ldj += S;                                          // cnf.py:190
+    mix(rr + RecF<NH>::Q, xa, zb, ya, yb);             // y @ Q (cnf.py:335); identity after the last block
     if (SAVE && DROP) {
       mword |= bits << (8 * (k & 3));
       if ((k & 3) == 3 || k == nb - 1) {
-        if (valid) msave[((long long)(k >> 2) * B + b) * 16 + j] = mword;
+        msave[((long long)(k >> 2) * B + bc) * 16 + j] = mword;
         mword = 0;
       }
     }
-    float T, Sp;
-    mlp_forward<NH, false>(L, R, xa, hp_sum(hpb + cur * 1024, s, j), bits, DROP, T, Sp, nullptr, nullptr);
-    const float S = tanhf(Sp);                        // cnf.py:107
-    const float zb = fmaf(expf(S), xb, T);            // cnf.py:179
-    ldj += S;                                          // cnf.py:190
-    if (k < nb - 1) {                                  // orthonormal mix y @ Q (cnf.py:335)
-      float q0[16], q1[16];
-      float na = 0.f, nbv = 0.f;
-      ld16(q0, R + L.rf_q);
-      ld16(q1, R + L.rf_q + 32);
-      rot16x2(xa, q0, na, xa, q1, nbv);
-      ld16(q0, R + L.rf_q + 16);
-      ld16(q1, R + L.rf_q + 48);
-      rot16x2(zb, q0, na, zb, q1, nbv);
-      ya = na;
-      yb = nbv;
-    } else {
-      ya = xa;
-      yb = zb;
-    }
-    if (k + 1 < nb) st.store(rec + (cur ^ 1) * RFL, RFL);
+    sr.store(rec + (cur ^ 1) * RFL, RFL);      // past the end these refill a buffer nobody reads
+    sw.store(wt + cur * WTL, WTL);
     __syncthreads();
   }
-  const float ltot = row_sum16(ldj) + pk[L.ldc_off];
-  if (valid) {
-    if (j < Da) z[b * D + j] = ya;
-    if (j < Db) z[b * D + Da + j] = yb;
-    if (j == 0 && ldj_out) ldj_out[b] = ltot;
-  }
+  const float ltot = row_sum16(ldj) + ldc;
+  if (j < Da) z[bc * D + j] = ya;
+  if (j < Db) z[bc * D + Da + j] = yb;
+  if (j == 0 && ldj_out) ldj_out[bc] = ltot;
   if (logp) {
     const float q2 = row_sum16(ya * ya + yb * yb);
-    if (valid && j == 0) logp[b] = -(0.5f * q2 - ltot) - 0.5f * (float)D * 1.8378770664093454836f;
+    if (j == 0) logp[bc] = -(0.5f * q2 - ltot) - 0.5f * (float)D * 1.8378770664093454836f;
   }
 }
 
@@ -440,71 +501,64 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse(BcnfLayout L, const float* 
                                                      const int64_t* __restrict__ cond_index, long long N,
                                                      float* __restrict__ yout, const uint64_t* __restrict__ rng) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int RFL = 16 * L.RF;
+  const int RFL = 16 * L.RF, WTL = L.Cp * 17;
   float* rec = smem;
-  float* hpb = rec + 2 * RFL;
+  float* wt = rec + 2 * RFL;
+  float* hpb = wt + 2 * WTL;
   float* ht = hpb + 2 * 1024;
   const int tid = threadIdx.x, j = tid & 15, s = tid >> 4;
   const long long b = (long long)blockIdx.x * 16 + s;
-  const bool valid = b < N;
-  const long long bc = valid ? b : N - 1;
+  const long long bc = b < N ? b : N - 1;
   const int D = L.D, Da = L.Da, Db = L.Db, nb = L.nb;
-
-  stage_features(L, h, cond_index, N, ht);
-  const int klast = nb - 1;
-  {
-    Stage st;
-    st.load(pk + L.pi_off + (long long)klast * RFL, RFL);
-    st.store(rec + (klast & 1) * RFL, RFL);
-  }
-  __syncthreads();
-  hp_quarter(L, pk + L.w1t_off, ht, hpb + (klast & 1) * 1024, klast);
-  __syncthreads();
+  const float* pi = pk + L.pi_off;
+  const float* pw = pk + L.w1t_off;
 
   float ya = (j < Da) ? zin[bc * D + j] : 0.f;
   float yb = (j < Db) ? zin[bc * D + Da + j] : 0.f;
   uint64_t seed = 0, off = 0;
   if (DROP) { seed = rng[0]; off = rng[1]; }
+  stage_features(L, h, cond_index, N, ht);
+  const int kl = nb - 1;
+  {
+    Stage<STAGE_REC> sr;
+    sr.load(pi + (long long)kl * RFL, RFL);
+    sr.store(rec + (kl & 1) * RFL, RFL);
+    Stage<STAGE_W1T> sw;
+    sw.load(pw + (long long)kl * WTL, WTL);
+    sw.store(wt + (kl & 1) * WTL, WTL);
+    const int km = kl >= 1 ? kl - 1 : 0;
+    sw.load(pw + (long long)km * WTL, WTL);
+    sw.store(wt + (km & 1) * WTL, WTL);
+  }
+  __syncthreads();
+  hp_quarter(L, wt + (kl & 1) * WTL, ht, hpb + (kl & 1) * 1024);
+  __syncthreads();
 
-  for (int k = klast; k >= 0; --k) {
+  for (int k = kl; k >= 0; --k) {
     const int cur = k & 1;
-    Stage st;
-    if (k >= 1) {
-      st.load(pk + L.pi_off + (long long)(k - 1) * RFL, RFL);
-      hp_quarter(L, pk + L.w1t_off, ht, hpb + (cur ^ 1) * 1024, k - 1);
-    }
-    const float* R = rec + cur * RFL + j * L.RF;
+    const int k1 = k >= 1 ? k - 1 : 0, k2 = k >= 2 ? k - 2 : 0;   // clamped: no branches
+    Stage<STAGE_REC> sr;
+    Stage<STAGE_W1T> sw;
+    sr.load(pi + (long long)k1 * RFL, RFL);
+    sw.load(pw + (long long)k2 * WTL, WTL);
+    hp_quarter(L, wt + (cur ^ 1) * WTL, ht, hpb + (cur ^ 1) * 1024);
+    float rr[RecF<NH>::USED];
+    ld_rec<0, RecF<NH>::USED>(rr, rec + cur * RFL + j * L.RF);
     float za, zb;
-    if (k < nb - 1) {                                  // z @ Q^T (cnf.py:339)
-      float q0[16], q1[16];
-      za = 0.f;
-      zb = 0.f;
-      ld16(q0, R + L.rf_q);
-      ld16(q1, R + L.rf_q + 32);
-      rot16x2(ya, q0, za, ya, q1, zb);
-      ld16(q0, R + L.rf_q + 16);
-      ld16(q1, R + L.rf_q + 48);
-      rot16x2(yb, q0, za, yb, q1, zb);
-    } else {
-      za = ya;
-      zb = yb;
-    }
+    mix(rr + RecF<NH>::Q, ya, yb, za, zb);             // z @ Q^T (cnf.py:339); identity for the last block
     uint32_t bits = 0xffu;
-    if (DROP) bits = dropout_bits(L, seed, off, b, k, j, 0x40000000u);
+    if (DROP) bits = dropout_bits(L, seed, off, bc, k, j, 0x40000000u);
     float T, Sp;
-    mlp_forward<NH, false>(L, R, za, hp_sum(hpb + cur * 1024, s, j), bits, DROP, T, Sp, nullptr, nullptr);
-    const float S = tanhf(Sp);
-    yb = (zb - T) * expf(-S);                          // cnf.py:205
-    ya = za;
-    const floatx4 an = *reinterpret_cast<const floatx4*>(R);   // ActNorm inverse (cnf.py:353-354)
-    if (L.act_norm && k < nb - 1) {
-      ya = (j < Da) ? (ya - an.y) / an.x : 0.f;
-      yb = (j < Db) ? (yb - an.w) / an.z : 0.f;
-    }
-    if (k >= 1) st.store(rec + (cur ^ 1) * RFL, RFL);
+    mlp_forward<NH, false>(L, rr, za, hp_sum(hpb + cur * 1024, s, j), bits, DROP, T, Sp, nullptr, nullptr);
+    const float S = tanh_bf(Sp);
+    const float ybn = (zb - T) * expf(-S);             // cnf.py:205
+    ya = (j < Da) ? (za - rr[1]) / rr[0] : 0.f;        // ActNorm inverse (cnf.py:353-354); identity where none
+    yb = (j < Db) ? (ybn - rr[3]) / rr[2] : 0.f;
+    sr.store(rec + (cur ^ 1) * RFL, RFL);
+    sw.store(wt + cur * WTL, WTL);
     __syncthreads();
   }
-  if (valid) {
+  if (b < N) {
     if (j < Da) yout[b * D + j] = ya;
     if (j < Db) yout[b * D + Da + j] = yb;
   }
@@ -526,100 +580,124 @@ struct BwdTiles {   // tile indices inside one tile buffer
   __device__ __forceinline__ int count() const { return 2 * NH + NT_EXTRA; }
 };
 
-// dW-style chain: out[j][n] = sum_s Dt[s][j] * Bt[s][n] over the 16 samples; B may be ones.
-__device__ __forceinline__ floatx4 chain_tt(const float* __restrict__ Dt, const float* __restrict__ Bt, int q, int r) {
-  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int sidx = (4 * t + q) * BCNF_TSTRIDE + r;
-    acc = mfma4(Dt[sidx], Bt ? Bt[sidx] : 1.0f, acc);
+// One gradient "chain" = 4 fp32 MFMAs over the workgroup's 16 samples:
+//   out[j][n] = sum_s A[s][j] * B[s][n],  A a [16][17] tile, B a [16][b_stride] LDS region (ones for
+//   bias / ActNorm sums, the feature tile for the W1 condition part), written to the workgroup's slab at
+//   base + j * row_stride + n for j < nrows, n < ncols. Built once per workgroup (no runtime indexing of
+//   the kernel-argument struct inside the loop, and no per-type branches).
+struct ChainDesc {
+  int a_off;       // A tile offset (floats) inside the tile buffer
+  int b_off;       // B offset: inside the tile buffer, or (flag B_ABS) inside smem
+  int b_stride;
+  int out_rel;     // slab offset relative to the block base (k * blk_stride)
+  int row_stride;
+  int nrows;
+  int ncols;
+  int flags;       // 1: coupling-relative (add an_size for blocks with ActNorm) 2: ActNorm chain 4: B_ABS
+};
+constexpr int CH_COUPLING = 1, CH_ACTNORM = 2, CH_BABS = 4;
+constexpr int MAX_CHAINS = 2 * BCNF_MAX_HIDDEN + 8 + 16;
+
+template <int NH>
+__device__ void build_chains(const BcnfLayout& L, ChainDesc* cd, int ones_abs, int ht_abs) {
+  const BwdTiles TI{NH};
+  const int NC16 = L.Cp >> 4;
+  const int n_chains = 2 * NH + 8 + NC16;
+  for (int c = threadIdx.x; c < n_chains; c += BCNF_WG) {
+    ChainDesc d;
+    d.b_stride = BCNF_TSTRIDE;
+    d.flags = CH_COUPLING;
+    if (c < NH + 2) {                                   // weight gradients of Linear l / output t, s rows
+      const int l = (c < NH) ? c + 1 : NH + 1;
+      d.a_off = TILE * ((c < NH) ? TI.D(l) : (c == NH ? TI.DT() : TI.DS()));
+      d.b_off = TILE * ((c < NH) ? TI.A(l - 1) : TI.A(NH));
+      const int row0 = (c == NH + 1) ? L.Db : 0;
+      d.out_rel = L.lin_w[l] + row0 * L.lin_in[l];
+      d.row_stride = L.lin_in[l];
+      d.nrows = (c < NH) ? L.H[l] : L.Db;
+      d.ncols = (l == 1) ? L.Da : L.H[l - 1];
+    } else if (c < 2 * NH + 4) {                        // bias gradients (B = ones)
+      const int cc = c - (NH + 2);
+      const int l = (cc < NH) ? cc + 1 : NH + 1;
+      d.a_off = TILE * ((cc < NH) ? TI.D(l) : (cc == NH ? TI.DT() : TI.DS()));
+      d.b_off = ones_abs;
+      d.flags |= CH_BABS;
+      d.out_rel = L.lin_b[l] + ((cc == NH + 1) ? L.Db : 0);
+      d.row_stride = 1;
+      d.nrows = (cc < NH) ? L.H[l] : L.Db;
+      d.ncols = 1;
+    } else if (c < 2 * NH + 8) {                        // ActNorm scale / bias (B = ones)
+      const int a = c - (2 * NH + 4);                   // 0: scale_a 1: bias_a 2: scale_b 3: bias_b
+      d.a_off = TILE * ((a == 0) ? TI.PA() : (a == 1 ? TI.GA() : (a == 2 ? TI.PB() : TI.GB())));
+      d.b_off = ones_abs;
+      d.flags = CH_ACTNORM | CH_BABS;
+      d.out_rel = ((a & 1) ? L.D : 0) + ((a < 2) ? 0 : L.Da);
+      d.row_stride = 1;
+      d.nrows = (a < 2) ? L.Da : L.Db;
+      d.ncols = 1;
+    } else {                                            // W1 condition part: B = feature tile columns
+      const int n = c - (2 * NH + 8);
+      d.a_off = TILE * TI.D(1);
+      d.b_off = ht_abs + 16 * n;
+      d.b_stride = L.Cp + 1;
+      d.flags |= CH_BABS;
+      d.out_rel = L.lin_w[1] + L.Da + 16 * n;
+      d.row_stride = L.lin_in[1];
+      d.nrows = L.H[1];
+      d.ncols = min(16, L.C - 16 * n);
+    }
+    cd[c] = d;
   }
-  return acc;
 }
 
 template <int NH>
-__device__ __forceinline__ void bwd_mfma_phase(const BcnfLayout& L, const float* __restrict__ pk, const float* __restrict__ T,
-                                               const float* __restrict__ ht, float* __restrict__ slab, int m,
+__device__ __forceinline__ void bwd_mfma_phase(const BcnfLayout& L, const float* __restrict__ smem,
+                                               const float* __restrict__ T, const ChainDesc* __restrict__ cd,
+                                               const float* __restrict__ wtm, float* __restrict__ slab, int m,
                                                floatx4* dhacc) {
   const BwdTiles TI{NH};
   const int wave = threadIdx.x >> 6, l64 = threadIdx.x & 63, q = l64 >> 4, r = l64 & 15;
   const int NC16 = L.Cp >> 4;
-  const int cb = coupling_base(L, m);
-  const bool has_an = L.act_norm && m < L.nb - 1;
   const int n_chains = 2 * NH + 8 + NC16;
+  const int blk = m * L.blk_stride;
+  const bool has_an = L.act_norm && m < L.nb - 1;
+  const int cpl = has_an ? L.an_size : 0;
   for (int c = wave; c < n_chains; c += 4) {
-    if (c < NH + 2) {                      // weight gradients of Linear l (or output t / s rows)
-      const int l = (c < NH) ? c + 1 : NH + 1;
-      const int dtile = (c < NH) ? TI.D(l) : (c == NH ? TI.DT() : TI.DS());
-      const int atile = (c < NH) ? TI.A(l - 1) : TI.A(NH);
-      const floatx4 acc = chain_tt(T + dtile * TILE, T + atile * TILE, q, r);
-      const int in_eff = (l == 1) ? L.Da : L.H[l - 1];
-      const int out_l = (c < NH) ? L.H[l] : L.Db;
-      const int row0 = (c == NH + 1) ? L.Db : 0;
-      if (r < in_eff) {
+    const ChainDesc d = cd[c];
+    const float* A = T + d.a_off;
+    const float* Bm = ((d.flags & CH_BABS) ? smem : T) + d.b_off;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    float a[4], bv[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int jr = 4 * q + i;
-          if (jr < out_l) slab[cb + L.lin_w[l] + (row0 + jr) * L.lin_in[l] + r] = acc[i];
-        }
-      }
-    } else if (c < 2 * NH + 4) {           // bias gradients
-      const int cc = c - (NH + 2);
-      const int l = (cc < NH) ? cc + 1 : NH + 1;
-      const int dtile = (cc < NH) ? TI.D(l) : (cc == NH ? TI.DT() : TI.DS());
-      const floatx4 acc = chain_tt(T + dtile * TILE, nullptr, q, r);
-      const int out_l = (cc < NH) ? L.H[l] : L.Db;
-      const int row0 = (cc == NH + 1) ? L.Db : 0;
-      if (r == 0) {
+    for (int t = 0; t < 4; ++t) {
+      a[t] = A[(4 * t + q) * BCNF_TSTRIDE + r];
+      bv[t] = Bm[(4 * t + q) * d.b_stride + r];
+    }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int jr = 4 * q + i;
-          if (jr < out_l) slab[cb + L.lin_b[l] + row0 + jr] = acc[i];
-        }
-      }
-    } else if (c < 2 * NH + 8) {           // ActNorm scale / bias
-      if (!has_an) continue;
-      const int a = c - (2 * NH + 4);      // 0: scale_a 1: bias_a 2: scale_b 3: bias_b
-      const int tile = (a == 0) ? TI.PA() : (a == 1 ? TI.GA() : (a == 2 ? TI.PB() : TI.GB()));
-      const floatx4 acc = chain_tt(T + tile * TILE, nullptr, q, r);
-      const int cnt = (a < 2) ? L.Da : L.Db;
-      const int base = m * L.blk_stride + ((a & 1) ? L.D : 0) + ((a < 2) ? 0 : L.Da);
-      if (r == 0) {
+    for (int t = 0; t < 4; ++t) acc = mfma4(a[t], bv[t], acc);
+    const int nrows = ((d.flags & CH_ACTNORM) && !has_an) ? 0 : d.nrows;
+    const int base = blk + d.out_rel + ((d.flags & CH_COUPLING) ? cpl : 0);
+    if (r < d.ncols) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int jr = 4 * q + i;
-          if (jr < cnt) slab[base + jr] = acc[i];
-        }
-      }
-    } else {                               // W1 condition part: dW1h[j][c] = sum_s D1[s][j] h[s][c]
-      const int n = c - (2 * NH + 8);
-      const float* Dt = T + TI.D(1) * TILE;
-      const int hs = L.Cp + 1;
-      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-        acc = mfma4(Dt[(4 * t + q) * BCNF_TSTRIDE + r], ht[(4 * t + q) * hs + 16 * n + r], acc);
-      const int col = 16 * n + r;
-      if (col < L.C) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int jr = 4 * q + i;
-          if (jr < L.H[1]) slab[cb + L.lin_w[1] + jr * L.lin_in[1] + L.Da + col] = acc[i];
-        }
-      }
+      for (int i = 0; i < 4; ++i)
+        if (4 * q + i < nrows) slab[base + (4 * q + i) * d.row_stride + r] = acc[i];
     }
   }
   // dh[s][c] += sum_j D1[s][j] W1h_m[j][c]   (wave w owns column tiles n = w, w+4, ...)
   const float* D1 = T + TI.D(1) * TILE;
-  const float* w1h = pk + L.w1h_off + (long long)m * 16 * L.Cp;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int n = wave + 4 * u;
     if (n < NC16) {
       floatx4 acc = dhacc[u];
+      float a[4], bv[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-        acc = mfma4(D1[r * BCNF_TSTRIDE + 4 * t + q], w1h[(4 * t + q) * L.Cp + 16 * n + r], acc);
+      for (int t = 0; t < 4; ++t) {
+        a[t] = D1[r * BCNF_TSTRIDE + 4 * t + q];
+        bv[t] = wtm[(16 * n + r) * 17 + 4 * t + q];
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc = mfma4(a[t], bv[t], acc);
       dhacc[u] = acc;
     }
   }
@@ -634,93 +712,109 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
                                                       float* __restrict__ slab_all, long long slab_stride) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const BwdTiles TI{NH};
-  const int RFL = 16 * L.RF, RBL = 16 * L.RB;
+  const int RFL = 16 * L.RF, RBL = 16 * L.RB, WTL = L.Cp * 17;
   const int NT = TI.count();
   float* recF = smem;                   // [2][16*RF]
   float* recB = recF + 2 * RFL;         // [2][16*RB]
-  float* hpb = recB + 2 * RBL;          // [2][4][256]
+  float* wt = recB + 2 * RBL;           // [4][Cp*17]  W1h^T ring: block k-1 (HP), k+1 (dh) live at step k
+  float* hpb = wt + 4 * WTL;            // [2][4][256]
   float* tiles = hpb + 2 * 1024;        // [2][NT][272]
-  float* ht = tiles + 2 * NT * TILE;    // [16][Cp+1]
+  float* ones = tiles + 2 * NT * TILE;  // [272] ones (B operand of the bias / ActNorm sums)
+  ChainDesc* cd = reinterpret_cast<ChainDesc*>(ones + TILE);   // [MAX_CHAINS]
+  float* ht = ones + TILE + MAX_CHAINS * 8;                      // [16][Cp+1]
   const int tid = threadIdx.x, j = tid & 15, s = tid >> 4;
   const int wave = tid >> 6, l64 = tid & 63, q = l64 >> 4, r = l64 & 15;
+  for (int i = tid; i < TILE; i += BCNF_WG) ones[i] = 1.0f;
+  build_chains<NH>(L, cd, (int)(ones - smem), (int)(ht - smem));
   const long long b = (long long)blockIdx.x * 16 + s;
   const bool valid = b < B;
   const long long bc = valid ? b : B - 1;
   const int D = L.D, Da = L.Da, Db = L.Db, nb = L.nb;
   float* slab = slab_all + (long long)blockIdx.x * slab_stride;
   const bool drop = msave != nullptr;
-
-  stage_features(L, h, nullptr, B, ht);
-  {
-    Stage st;
-    const int kl = nb - 1;
-    st.load(pk + L.pf_off + (long long)kl * RFL, RFL);
-    st.store(recF + (kl & 1) * RFL, RFL);
-    st.load(pk + L.pb_off + (long long)kl * RBL, RBL);
-    st.store(recB + (kl & 1) * RBL, RBL);
-  }
-  __syncthreads();
-  hp_quarter(L, pk + L.w1t_off, ht, hpb + ((nb - 1) & 1) * 1024, nb - 1);
-  __syncthreads();
+  const float* pf = pk + L.pf_off;
+  const float* pbk = pk + L.pb_off;
+  const float* pw = pk + L.w1t_off;
 
   float gya = 0.f, gyb = 0.f, dl = 0.f;
-  if (valid) {
+  if (valid) {                                      // padded rows carry zero gradient
     if (dz) {
       gya = (j < Da) ? dz[b * D + j] : 0.f;
       gyb = (j < Db) ? dz[b * D + Da + j] : 0.f;
     }
     if (dldj) dl = dldj[b];
   }
+  // saved input / dropout masks of the block about to be processed (prefetched one block ahead)
+  float ya_n, yb_n;
+  uint32_t mw_n = 0xffffffffu;
+  {
+    const float* ys = ysave + ((long long)(nb - 1) * B + bc) * 32;
+    ya_n = ys[j];
+    yb_n = ys[16 + j];
+    if (drop) mw_n = msave[((long long)((nb - 1) >> 2) * B + bc) * 16 + j];
+  }
+  stage_features(L, h, nullptr, B, ht);
+  {
+    const int kl = nb - 1;
+    Stage<STAGE_REC> sr;
+    sr.load(pf + (long long)kl * RFL, RFL);
+    sr.store(recF + (kl & 1) * RFL, RFL);
+    sr.load(pbk + (long long)kl * RBL, RBL);
+    sr.store(recB + (kl & 1) * RBL, RBL);
+    Stage<STAGE_W1T> sw;
+    sw.load(pw + (long long)kl * WTL, WTL);
+    sw.store(wt + (kl & 3) * WTL, WTL);
+    const int km = kl >= 1 ? kl - 1 : 0;
+    sw.load(pw + (long long)km * WTL, WTL);
+    sw.store(wt + (km & 3) * WTL, WTL);
+  }
+  __syncthreads();
+  hp_quarter(L, wt + ((nb - 1) & 3) * WTL, ht, hpb + ((nb - 1) & 1) * 1024);
+  __syncthreads();
+
   floatx4 dhacc[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) dhacc[u] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   for (int k = nb - 1; k >= 0; --k) {
     const int cur = k & 1;
-    // (a) prefetch
-    const float* ys = ysave + ((long long)k * B + bc) * 32;
-    const float ya = ys[j], yb = ys[16 + j];
-    uint32_t mword = 0xffffffffu;
-    if (drop) mword = msave[((long long)(k >> 2) * B + bc) * 16 + j];
-    Stage stF, stB;
-    if (k >= 1) {
-      stF.load(pk + L.pf_off + (long long)(k - 1) * RFL, RFL);
+    const int k1 = k >= 1 ? k - 1 : 0, k2 = k >= 2 ? k - 2 : 0;   // clamped: no branches
+    const float ya = ya_n, yb = yb_n;
+    const uint32_t mword = mw_n;
+    // (a) prefetch: next records, W1h^T two blocks ahead, next block's saved input / masks
+    Stage<STAGE_REC> sF, sB;
+    Stage<STAGE_W1T> sw;
+    sF.load(pf + (long long)k1 * RFL, RFL);
+    sB.load(pbk + (long long)k1 * RBL, RBL);
+    sw.load(pw + (long long)k2 * WTL, WTL);
+    {
+      const float* ys = ysave + ((long long)k1 * B + bc) * 32;
+      ya_n = ys[j];
+      yb_n = ys[16 + j];
+      if (drop) mw_n = msave[((long long)(k1 >> 2) * B + bc) * 16 + j];
     }
-    // (b) MFMA phase: gradients of block k+1 from its tiles, HP of block k-1
-    if (k + 1 < nb) bwd_mfma_phase<NH>(L, pk, tiles + ((k + 1) & 1) * NT * TILE, ht, slab, k + 1, dhacc);
-    if (k >= 1) {
-      stB.load(pk + L.pb_off + (long long)(k - 1) * RBL, RBL);
-      hp_quarter(L, pk + L.w1t_off, ht, hpb + (cur ^ 1) * 1024, k - 1);
-    }
-    // (c) VALU phase for block k
-    const float* RF_ = recF + cur * RFL + j * L.RF;
-    const float* RB_ = recB + cur * RBL + j * L.RB;
+    // (b) MFMA phase: parameter gradients + dh of block k+1, HP of block k-1
+    if (k + 1 < nb)
+      bwd_mfma_phase<NH>(L, smem, tiles + ((k + 1) & 1) * NT * TILE, cd, wt + ((k + 1) & 3) * WTL, slab, k + 1,
+                         dhacc);
+    hp_quarter(L, wt + (k1 & 3) * WTL, ht, hpb + (cur ^ 1) * 1024);
+    // (c) VALU phase: recompute block k, then back-propagate through it
     float* Tt = tiles + cur * NT * TILE;
     const int tix = s * BCNF_TSTRIDE + j;
-    const floatx4 an = *reinterpret_cast<const floatx4*>(RF_);
-    const float xa = fmaf(an.x, ya, an.y);
-    const float xb = fmaf(an.z, yb, an.w);
+    using RBk = RecB<NH>;
+    float rf[RecF<NH>::MLP_END], rb[RBk::USED];
+    ld_rec<0, RecF<NH>::MLP_END>(rf, recF + cur * RFL + j * L.RF);   // recompute part (no forward mix)
+    ld_rec<0, RBk::USED>(rb, recB + cur * RBL + j * L.RB);
+    const float xa = fmaf(rf[0], ya, rf[1]);
+    const float xb = fmaf(rf[2], yb, rf[3]);
     const uint32_t bits = (mword >> (8 * (k & 3))) & 0xffu;
     float act[NH], gd[NH];
     float T, Sp;
-    mlp_forward<NH, true>(L, RF_, xa, hp_sum(hpb + cur * 1024, s, j), bits, drop, T, Sp, act, gd);
-    const float S = tanhf(Sp);
+    mlp_forward<NH, true>(L, rf, xa, hp_sum(hpb + cur * 1024, s, j), bits, drop, T, Sp, act, gd);
+    const float S = tanh_bf(Sp);
     const float e = expf(S);
     float gza, gzb;
-    if (k < nb - 1) {                                  // grad through y @ Q: g @ Q^T
-      float q0[16], q1[16];
-      gza = 0.f;
-      gzb = 0.f;
-      ld16(q0, RB_ + L.rb_qt);
-      ld16(q1, RB_ + L.rb_qt + 32);
-      rot16x2(gya, q0, gza, gya, q1, gzb);
-      ld16(q0, RB_ + L.rb_qt + 16);
-      ld16(q1, RB_ + L.rb_qt + 48);
-      rot16x2(gyb, q0, gza, gyb, q1, gzb);
-    } else {
-      gza = gya;
-      gzb = gyb;
-    }
+    mix(rb + RBk::QT, gya, gyb, gza, gzb);            // g @ Q^T (identity for the last block)
     const float dT = gzb;                              // z_b = exp(s) y_b + t
     const float dS = (j < Db) ? fmaf(gzb * e, xb, dl) : 0.f;
     const float dSp = dS * (1.f - S * S);
@@ -728,52 +822,37 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
     Tt[TI.DT() * TILE + tix] = dT;
     Tt[TI.DS() * TILE + tix] = dSp;
     Tt[TI.A(NH) * TILE + tix] = act[NH - 1];
-    float da, da2;
-    {
-      float w0[16], w1[16];
-      da = 0.f;
-      da2 = 0.f;
-      ld16(w0, RB_ + L.rb_tt);
-      ld16(w1, RB_ + L.rb_st);
-      rot16x2(dT, w0, da, dSp, w1, da2);
-    }
+    float da = 0.f, da2 = 0.f;
+    rot16x2(dT, rb + RBk::TT, da, dSp, rb + RBk::ST, da2);
     da += da2;
 #pragma unroll
     for (int l = NH; l >= 2; --l) {
       const float dpre = da * gd[l - 1];
       Tt[TI.D(l) * TILE + tix] = dpre;
       Tt[TI.A(l - 1) * TILE + tix] = act[l - 2];
-      float w[16];
-      ld16(w, RB_ + L.rb_hid + 16 * (l - 2));
-      da = rot16(dpre, w, 0.f);
+      da = rot16(dpre, rb + RBk::HID + 16 * (l - 2), 0.f);
     }
     const float dpre1 = da * gd[0];
     Tt[TI.D(1) * TILE + tix] = dpre1;
     Tt[TI.A(0) * TILE + tix] = xa;
-    float dxa;
-    {
-      float w[16];
-      ld16(w, RB_ + L.rb_w1t);
-      dxa = rot16(dpre1, w, gza);
-    }
-    if (L.act_norm && k < nb - 1) {
-      const float inv_a = (j < Da) ? 1.f / an.x : 0.f;
-      const float inv_b = (j < Db) ? 1.f / an.z : 0.f;
+    const float dxa = rot16(dpre1, rb + RBk::W1T, gza);
+    {   // ActNorm tiles (consumed only for blocks that have an ActNorm)
+      const float inv_a = (j < Da) ? __builtin_amdgcn_rcpf(rf[0]) : 0.f;
+      const float inv_b = (j < Db) ? __builtin_amdgcn_rcpf(rf[2]) : 0.f;
       Tt[TI.PA() * TILE + tix] = fmaf(dxa, ya, dl * inv_a);
       Tt[TI.GA() * TILE + tix] = dxa;
       Tt[TI.PB() * TILE + tix] = fmaf(dxb, yb, dl * inv_b);
       Tt[TI.GB() * TILE + tix] = dxb;
     }
-    gya = an.x * dxa;
-    gyb = an.z * dxb;
-    // (d) commit prefetched records
-    if (k >= 1) {
-      stF.store(recF + (cur ^ 1) * RFL, RFL);
-      stB.store(recB + (cur ^ 1) * RBL, RBL);
-    }
+    gya = rf[0] * dxa;
+    gyb = rf[2] * dxb;
+    // (d) commit prefetched records (past the end they refill buffers nobody reads)
+    sF.store(recF + (cur ^ 1) * RFL, RFL);
+    sB.store(recB + (cur ^ 1) * RBL, RBL);
+    if (k >= 2) sw.store(wt + (k2 & 3) * WTL, WTL);
     __syncthreads();
   }
-  bwd_mfma_phase<NH>(L, pk, tiles, ht, slab, 0, dhacc);
+  bwd_mfma_phase<NH>(L, smem, tiles, cd, wt, slab, 0, dhacc);
   if (dy && valid) {
     if (j < Da) dy[b * D + j] = gya;
     if (j < Db) dy[b * D + Da + j] = gyb;
@@ -839,13 +918,7 @@ int check_launch() {
   return BCNF_OK;
 }
 
-size_t fwd_lds_bytes(const BcnfLayout& L) {
-  return sizeof(float) * (size_t)(2 * 16 * L.RF + 2 * 1024 + 16 * (L.Cp + 1));
-}
-size_t bwd_lds_bytes(const BcnfLayout& L) {
-  const int NT = 2 * L.NH + NT_EXTRA;
-  return sizeof(float) * (size_t)(2 * 16 * L.RF + 2 * 16 * L.RB + 2 * 1024 + 2 * NT * TILE + 16 * (L.Cp + 1));
-}
+
 
 // Raise a kernel's dynamic-LDS limit once (cached per kernel; safe to call under stream capture
 // after the first eager call has set it).
@@ -854,9 +927,20 @@ const void* g_attr_fn[256];
 size_t g_attr_lds[256];
 int g_attr_n = 0;
 
+// Optional occupancy shaping (env BCNF_LDS_MIN_KB): pad the dynamic LDS request so at most
+// floor(160 / pad) workgroups share a CU. Read once.
+size_t lds_floor_bytes() {
+  static size_t v = [] {
+    const char* e = getenv("BCNF_LDS_MIN_KB");
+    return e ? (size_t)atoi(e) * 1024 : (size_t)0;
+  }();
+  return v;
+}
+
 template <typename K>
-int launch_lds(K kernel, size_t lds) {
-  if (lds > 160 * 1024) return BCNF_ERR_UNSUPPORTED;
+int launch_lds(K kernel, size_t& lds) {
+  if (lds < lds_floor_bytes()) lds = lds_floor_bytes();
+  if (lds > LDS_MAX) return BCNF_ERR_UNSUPPORTED;
   const void* fn = reinterpret_cast<const void*>(kernel);
   std::lock_guard<std::mutex> lk(g_attr_mu);
   for (int i = 0; i < g_attr_n; ++i)
@@ -878,11 +962,20 @@ int launch_lds(K kernel, size_t lds) {
 }
 
 template <int NH>
+bool layout_matches(const BcnfLayout& L) {
+  return L.rf_b1 == RecF<NH>::B1 && L.rf_w1 == RecF<NH>::W1 && L.rf_hid == RecF<NH>::HID && L.rf_t == RecF<NH>::T &&
+         L.rf_s == RecF<NH>::S && L.rf_q == RecF<NH>::Q && L.RF >= RecF<NH>::USED && L.rb_w1t == RecB<NH>::W1T &&
+         L.rb_hid == RecB<NH>::HID && L.rb_tt == RecB<NH>::TT && L.rb_st == RecB<NH>::ST && L.rb_qt == RecB<NH>::QT &&
+         L.RB >= RecB<NH>::USED;
+}
+
+template <int NH>
 int fwd_dispatch(const BcnfLayout& L, const float* pk, const float* y, const float* h, long long B, float* z,
                  float* ldj, float* logp, bool drop, const uint64_t* rng, float* ysave, uint32_t* msave,
                  hipStream_t st) {
+  if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
   const dim3 grid((unsigned)((B + 15) / 16));
-  const size_t lds = fwd_lds_bytes(L);
+  size_t lds = fwd_lds_bytes(L);
   const bool save = ysave != nullptr;
   int rc;
 #define BCNF_FWD(DR, SV)                                                                                    \
@@ -902,8 +995,9 @@ int fwd_dispatch(const BcnfLayout& L, const float* pk, const float* y, const flo
 template <int NH>
 int inv_dispatch(const BcnfLayout& L, const float* pk, const float* zin, const float* h, const int64_t* ci,
                  long long N, float* y, bool drop, const uint64_t* rng, hipStream_t st) {
+  if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
   const dim3 grid((unsigned)((N + 15) / 16));
-  const size_t lds = fwd_lds_bytes(L);
+  size_t lds = fwd_lds_bytes(L);
   int rc;
   if (drop) {
     rc = launch_lds(k_inverse<NH, true>, lds);
@@ -921,8 +1015,9 @@ template <int NH>
 int bwd_dispatch(const BcnfLayout& L, const float* pk, const float* h, const float* dz, const float* dldj,
                  long long B, const float* ysave, const uint32_t* msave, float* dy, float* dh, float* slab,
                  long long stride, hipStream_t st) {
+  if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
   const dim3 grid((unsigned)((B + 15) / 16));
-  const size_t lds = bwd_lds_bytes(L);
+  size_t lds = bwd_lds_bytes(L);
   const int rc = launch_lds(k_backward<NH>, lds);
   if (rc) return rc;
   hipLaunchKernelGGL((k_backward<NH>), grid, dim3(BCNF_WG), lds, st, L, pk, h, dz, dldj, B, ysave, msave, dy,
@@ -1030,10 +1125,11 @@ int bcnf_stack_backward(const BcnfStackDesc* desc, const void* packed, const flo
   int rc = make_layout(desc, &L);
   if (rc) return rc;
   if (!layout_supported(L, desc)) return BCNF_ERR_UNSUPPORTED;
-  if (batch < 0 || !packed || !h || !workspace || !dparams || !slab) return BCNF_ERR_ARG;
+  if (batch < 0 || !packed || !h || !workspace || !slab) return BCNF_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   if (batch == 0) {
-    if (hipMemsetAsync(dparams, 0, sizeof(float) * (size_t)L.n_trainable, st) != hipSuccess) return BCNF_ERR_HIP;
+    if (dparams && hipMemsetAsync(dparams, 0, sizeof(float) * (size_t)L.n_trainable, st) != hipSuccess)
+      return BCNF_ERR_HIP;
     return BCNF_OK;
   }
   // `training` must match the forward call that filled the workspace: it says whether dropout masks
@@ -1050,10 +1146,19 @@ int bcnf_stack_backward(const BcnfStackDesc* desc, const void* packed, const flo
     default: return BCNF_ERR_UNSUPPORTED;
   }
   if (rc) return rc;
+  if (!dparams) return BCNF_OK;   // caller reduces with bcnf_grad_reduce
+  return bcnf_grad_reduce(desc, slab, batch, dparams, stream);
+}
+
+int bcnf_grad_reduce(const BcnfStackDesc* desc, const void* slab, int64_t batch, float* dparams, void* stream) {
+  BcnfLayout L;
+  const int rc = make_layout(desc, &L);
+  if (rc) return rc;
+  if (!slab || !dparams || batch < 1) return BCNF_ERR_ARG;
   const long long P = L.n_trainable;
   const unsigned nblk = (unsigned)((P / 4 + BCNF_WG) / BCNF_WG);
-  hipLaunchKernelGGL(k_reduce, dim3(nblk), dim3(BCNF_WG), 0, st, (const float*)slab, stride,
-                     (int)((batch + 15) / 16), P, dparams);
+  hipLaunchKernelGGL(k_reduce, dim3(nblk), dim3(BCNF_WG), 0, (hipStream_t)stream, (const float*)slab,
+                     slab_stride_of(L), (int)((batch + 15) / 16), P, dparams);
   return check_launch();
 }
 

@@ -53,6 +53,7 @@ class FusedStack:
         self._pack_frozen = False
         self._rng_state = None
         self.seed = None
+        self.timers = None       # dict -> per-kernel HIP-event pairs (bench.py kernel timing phase)
         if bind:
             self.flatten()
         else:   # standalone layer: flat params are provided per call (see stack_forward(flat=...))
@@ -214,10 +215,18 @@ class FusedStack:
             wb, _ = self.workspace_bytes(B, training)
             ws = torch.empty(max(wb // 4, 1), dtype=torch.float32, device=dev)
         pk = self.packed(fresh=save)
+        tm = self.timers
+        if tm is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         rc = N.lib().bcnf_stack_forward(self._pdesc, N.ptr(pk), N.ptr(y), N.ptr(h), ctypes.c_int64(B), N.ptr(z),
                                         N.ptr(ldj), N.ptr(logp), ctypes.c_int32(int(training)), N.ptr(rng), N.ptr(ws),
                                         N.stream_handle(dev))
         N.check(rc, "bcnf_stack_forward")
+        if tm is not None:
+            e1.record()
+            tm.setdefault("k_forward", []).append((e0, e1))
         if drop:
             rng[1:2].add_(1)
         return z, ldj, logp, (ws, pk)
@@ -231,10 +240,25 @@ class FusedStack:
         dparams = torch.empty_like(self.flat)
         dh = torch.empty_like(h) if want_dh else None
         dy = torch.empty((B, self.cfg.size), dtype=torch.float32, device=dev) if want_dy else None
+        stream = N.stream_handle(dev)
+        tm = self.timers
+        if tm is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e2 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         rc = N.lib().bcnf_stack_backward(self._pdesc, N.ptr(pk), N.ptr(h), N.ptr(dz), N.ptr(dldj),
                                          ctypes.c_int64(B), ctypes.c_int32(int(training)), N.ptr(ws), N.ptr(dy),
-                                         N.ptr(dh), N.ptr(dparams), N.ptr(slab), N.stream_handle(dev))
+                                         N.ptr(dh), None, N.ptr(slab), stream)
         N.check(rc, "bcnf_stack_backward")
+        if tm is not None:
+            e1.record()
+        N.check(N.lib().bcnf_grad_reduce(self._pdesc, N.ptr(slab), ctypes.c_int64(B), N.ptr(dparams), stream),
+                "bcnf_grad_reduce")
+        if tm is not None:
+            e2.record()
+            tm.setdefault("k_backward", []).append((e0, e1))
+            tm.setdefault("k_reduce", []).append((e1, e2))
         return dy, dh, dparams
 
     def launch_inverse(self, z, h, cond_index=None, training: bool = False):

@@ -1,0 +1,220 @@
+"""Benchmark: NLL-training samples/s of CondRealNVP_v2 trajectory_FC_small (B=4096 per GPU) on MI355X.
+
+One step = bcnf.train.Trainer._train_batch semantics (src/bcnf/train/trainer.py:244-277): zero_grad,
+forward(log_det_J, return_features) [FC feature net in PyTorch-ROCm + fused HIP coupling stack], NLL,
+backward [fused HIP backward + deterministic reduce + feature-net autograd], (N>1: RCCL all-reduce of the
+flat gradient), Adam step, clip_grad_norm_ after the step, one host sync for the logged losses.
+Synthetic ballistic trajectories (bcnf_amd/data.py), device-resident, pre-shuffled; dropout active.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]    (N>1: launched by torch.distributed.run)
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import math
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "NLL-training samples/sec + log_prob max-abs-err vs ref, trajectory_FC_small"
+FC_SMALL = {
+    "global": {"parameter_selection": ['x0_x', 'x0_y', 'x0_z', 'v0_x', 'v0_y', 'v0_z', 'g', 'w_x', 'w_y', 'w_z',
+                                       'b', 'm', 'a_x', 'a_y', 'a_z', 'r', 'A', 'Cd', 'rho']},
+    "model": {"kwargs": {"size": 19, "nested_sizes": [16] * 7, "n_conditions": 80, "n_blocks": 32,
+                         "dropout": 0.383, "act_norm": True}},
+    "feature_networks": [
+        {"type": "ConcatenateCondition", "kwargs": {"input_size": None, "output_size": 90}},
+        {"type": "FullyConnected", "kwargs": {"sizes": [90, 80], "dropout": 0.244}},
+    ],
+}
+# Algorithmic work per sample (recompute excluded). MAC counts for FC_small:
+#   forward flow  = 32 * (90*16 + 6*16*16 + 16*18) + 31 * 19*19 = 115,639 MAC
+#   backward flow = dX (115,639) + dW of every Linear (32 * 3,264 = 104,448)      = 220,087 MAC
+FWD_FLOP_PER_SAMPLE = 2 * 115_639
+BWD_FLOP_PER_SAMPLE = 2 * 220_087
+# Minimal HBM bytes per sample of the fused kernels (inputs + outputs + saved block inputs / masks):
+#   forward (train): y 76 + h 320 + z 76 + ldj 4 + ysave 32*128 + masks 8*64        = 5,164 B
+#   backward       : h 320 + dz 76 + dldj 4 + ysave 4,096 + masks 512 + dh 320 + slab share = 5,328 B + slab
+PEAK_FP32_TFLOPS = 157.3       # MI355X fp32 (vector = MFMA f32), MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=4096, help="samples per GPU (weak scaling)")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=12)
+    ap.add_argument("--kernel-iters", type=int, default=20)
+    return ap.parse_args()
+
+
+def init_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def log_prob_error(model, device):
+    """log_prob max-abs-err vs the reference's own outputs (golden fixture produced by running psaegert/bcnf)."""
+    path = os.path.join(ROOT, "tests", "golden", "g1_fc_small.npz")
+    if not os.path.exists(path):
+        return None, None
+    g1 = np.load(path)
+    sd = {k[3:]: torch.from_numpy(np.ascontiguousarray(g1[k])) for k in g1.keys() if k.startswith("sd/")}
+    from bcnf_amd import CondRealNVP_v2
+    torch.manual_seed(0)
+    m = CondRealNVP_v2.from_config(FC_SMALL)
+    m.load_state_dict(sd)
+    m.to(device).eval()
+    with torch.no_grad():
+        lp = m.log_prob(torch.from_numpy(g1["y"]).to(device), torch.from_numpy(g1["traj"]).to(device)).double().cpu()
+    ref = -torch.from_numpy(g1["nll"]).double() - 0.5 * 19 * math.log(2 * math.pi)
+    err = (lp - ref).abs()
+    return float(err.max()), float((err / ref.abs().clamp_min(1.0)).max())
+
+
+def cpu_baseline(args):
+    """The CPU oracle (PyTorch-eager restatement of the reference, pinned to its outputs) timed on this host's
+    cores: same FC_small step at the same batch, bounded sample."""
+    from oracle import cnf_oracle as O
+    from bcnf_amd.data import simulate
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(2024_03_25)
+    from bcnf_amd import CondRealNVP_v2
+    m = CondRealNVP_v2.from_config(FC_SMALL)
+    sd = {k: v.detach().clone().requires_grad_(not k.endswith("orthonormal_matrix")) for k, v in m.state_dict().items()}
+    opt = torch.optim.Adam([v for v in sd.values() if v.requires_grad], lr=2e-4)
+    y, traj = simulate(args.batch, seed=7)
+    y = torch.from_numpy(y)
+    traj = torch.from_numpy(traj)
+    y = (y - y.mean(0)) / (y.std(0) + 1e-6)
+    traj = (traj - traj.mean((0, 1))) / (traj.std((0, 1)) + 1e-6)
+    times = []
+    for i in range(3 + args.cpu_steps):
+        t0 = time.perf_counter()
+        O.train_step_cpu(sd, O.FC_SMALL_SPEC, y, traj, opt, training=True)
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times[3:])
+    return {"value": round(args.batch / med, 1), "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/cnf_oracle.train_step_cpu (PyTorch-eager CPU restatement pinned to the reference), "
+                      f"FC_small B={args.batch}, dropout on, median of {args.cpu_steps} steps after 3 warmup, "
+                      f"{threads} threads, {med * 1e3:.1f} ms/step"}
+
+
+def kernel_timing(model, data, args):
+    """Average device time of each fused kernel, measured with HIP events on the launch stream over
+    `kernel_iters` eager training forward/backward passes."""
+    from bcnf_amd import inn_nll_loss
+    st = model.fused
+    st.timers = {}
+    for _ in range(args.kernel_iters):
+        idx = data.next_indices()
+        y, traj = data.y[idx], data.traj[idx]
+        model.zero_grad(set_to_none=True)
+        z = model(y, traj, log_det_J=True)
+        inn_nll_loss(z, model.log_det_J).backward()
+    torch.cuda.synchronize()
+    out = {}
+    for name, pairs in st.timers.items():
+        ms = [a.elapsed_time(b) for a, b in pairs[2:]]   # drop the first launches (code-object load)
+        out[name] = sum(ms) / len(ms) * 1e3               # microseconds
+    st.timers = None
+    return out
+
+
+def main():
+    args = parse()
+    world, rank, local = init_dist(args)
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    from bcnf_amd import CondRealNVP_v2
+    from bcnf_amd.data import DeviceBatches
+    from bcnf_amd.train import TrainStep
+
+    torch.manual_seed(2024_03_25)
+    model = CondRealNVP_v2.from_config(FC_SMALL).to(device)
+    model.train()
+    model.fused.set_seed(2024_03_25 + 7919 * rank)
+    data = DeviceBatches(65536, args.batch, device, seed=2024_03_25 + rank)
+    step = TrainStep(model, lr=2e-4, capture=not args.no_graph)
+    step.broadcast_parameters()
+
+    for _ in range(args.warmup):
+        idx = data.next_indices()
+        step.step(data.y[idx], data.traj[idx])
+    batches = [data.next_indices() for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    losses = None
+    for idx in batches:
+        losses = step.step(data.y[idx], data.traj[idx])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ms_per_step = dt / args.steps * 1e3
+    value = world * args.batch * args.steps / dt
+
+    kern = kernel_timing(model, data, args) if rank == 0 else {}
+    if rank == 0:
+        B = args.batch
+        dom = max(("k_forward", "k_backward"), key=lambda k: kern.get(k, 0.0))
+        flop = (FWD_FLOP_PER_SAMPLE if dom == "k_forward" else BWD_FLOP_PER_SAMPLE) * B
+        us = kern.get(dom, float("nan"))
+        achieved = flop / (us * 1e-6) / 1e12
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get(dom)
+        lp_abs, lp_rel = log_prob_error(model, device)
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic ballistic trajectories (bcnf_amd/data.py RK4 restatement of physics.py), device-resident",
+            "config": {"workload": "trajectory_FC_small NLL training step (configs[1])", "batch_per_gpu": B,
+                       "global_batch": B * world, "parallelism": f"dp{world}", "hip_graph": not args.no_graph,
+                       "n_blocks": 32, "nested_sizes": [16] * 7, "n_conditions": 80, "dropout": 0.383},
+            "log_prob_max_abs_err": lp_abs, "log_prob_max_rel_err": lp_rel,
+            "last_loss": losses[0] if losses else None,
+            "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+                         "avg_us": round(us, 2), "flop_per_launch": flop,
+                         "note": "fp32 VALU (DPP rotations) + fp32 MFMA; peak is the fp32 vector = MFMA-f32 rate"},
+            "kernels_us": {k: round(v, 2) for k, v in kern.items()},
+        }
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

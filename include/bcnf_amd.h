@@ -82,13 +82,18 @@ int bcnf_stack_forward(const BcnfStackDesc* desc, const void* packed, const floa
                        int64_t batch, float* z, float* ldj, float* log_prob, int32_t training,
                        const uint64_t* rng_state, void* workspace, void* stream);
 
-/* Backward: given dz (B x D) and dldj (B) (either may be NULL = zeros), writes dparams
- * (canonical flat, n_trainable floats, overwritten), dh (B x C, overwritten, nullable) and
- * dy (B x D, nullable). `training` and `workspace` must be those of the forward call.
- * slab: bcnf_slab_bytes of scratch. Launches the fused backward and the deterministic slab sum. */
+/* Backward: given dz (B x D) and dldj (B) (either may be NULL = zeros), writes dh (B x C,
+ * overwritten, nullable), dy (B x D, nullable) and the per-workgroup gradient slabs into `slab`
+ * (bcnf_slab_bytes). With dparams != NULL it then reduces the slabs into dparams (canonical flat,
+ * n_trainable floats, overwritten); with dparams == NULL the caller runs bcnf_grad_reduce.
+ * `training` and `workspace` must be those of the forward call. */
 int bcnf_stack_backward(const BcnfStackDesc* desc, const void* packed, const float* h, const float* dz,
                         const float* dldj, int64_t batch, int32_t training, const void* workspace, float* dy,
                         float* dh, float* dparams, void* slab, void* stream);
+
+/* Deterministic (fixed-order) sum of the slabs of a backward over `batch` samples into dparams.
+ * Replaces autograd's implicit batch reduction of the parameter gradients. */
+int bcnf_grad_reduce(const BcnfStackDesc* desc, const void* slab, int64_t batch, float* dparams, void* stream);
 
 /* Inverse of the whole stack: y (N x D) from z (N x D). Row r uses feature row
  * cond_index[r] of h when cond_index != NULL (h then has any number of rows), else row r. */

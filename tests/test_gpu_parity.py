@@ -180,7 +180,7 @@ def test_empty_batch(model_g1):
 @pytest.mark.parametrize("shape", [
     dict(size=19, nested_sizes=[16] * 3, n_blocks=4, n_conditions=80, dropout=0.0, act_norm=True),
     dict(size=7, nested_sizes=[12, 9], n_blocks=3, n_conditions=5, dropout=0.1, act_norm=False),
-    dict(size=32, nested_sizes=[16], n_blocks=2, n_conditions=200, dropout=0.0, act_norm=True),
+    dict(size=32, nested_sizes=[16], n_blocks=2, n_conditions=120, dropout=0.0, act_norm=True),
     dict(size=2, nested_sizes=[4] * 8, n_blocks=5, n_conditions=3, dropout=0.0, act_norm=True),
 ])
 def test_other_shapes_vs_oracle(shape):
