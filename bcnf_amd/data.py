@@ -3,7 +3,8 @@ simulator so benchmarks run on realistic conditions without the offline-unavaila
 
 * ODE: ballistic_ODE (src/bcnf/simulation/physics.py:7-50):
       dv/dt = g - g rho (4/3) pi r^3 / m - (0.5 b / m) (v^2 v/|v| - w^2 w/|w|) + a
-  integrated with classical RK4 on the reference's time grid t = arange(0, T, dt) (physics.py:144),
+  integrated with classical RK4 (16 sub-steps per frame) on the reference's time grid t = arange(0, T, dt)
+  (physics.py:144),
   positions x_i = x_{i-1} + v_i dt (physics.py:150-152), no impact break (configs use break_on_impact False).
 * Priors: configs/data/config.yaml (polar x0/v0/w in the xy-plane, gamma g / rho / r / Cd, m).
 * y: the 19 parameters of trajectory_FC_small's `parameter_selection`, in that order.
@@ -32,7 +33,7 @@ def _dvdt(v, g, w, b, m, rho, r, a):
     return g - buoy - drag + a
 
 
-def simulate(n: int, seed: int = 2024_03_25, T: float = 2.0, dt: float = 0.067):
+def simulate(n: int, seed: int = 2024_03_25, T: float = 2.0, dt: float = 0.067, substeps: int = 16):
     """Return (y (n, 19) float32, trajectories (n, len(arange(0,T,dt)), 3) float32)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     x0x, x0y = _polar(rng, n, 20.0)
@@ -63,12 +64,13 @@ def simulate(n: int, seed: int = 2024_03_25, T: float = 2.0, dt: float = 0.067):
     traj[:, 0] = x
     f = lambda vv: _dvdt(vv, g, w, bb, mm, rr, rh, a)  # noqa: E731
     for i in range(1, steps):
-        h = t[i] - t[i - 1]
-        k1 = f(v)
-        k2 = f(v + 0.5 * h * k1)
-        k3 = f(v + 0.5 * h * k2)
-        k4 = f(v + h * k3)
-        v = v + (h / 6.0) * (k1 + 2 * k2 + 2 * k3 + k4)
+        h = (t[i] - t[i - 1]) / substeps     # odeint is adaptive; fixed RK4 needs sub-steps for
+        for _ in range(substeps):            # the stiff light-and-draggy tail of the priors
+            k1 = f(v)
+            k2 = f(v + 0.5 * h * k1)
+            k3 = f(v + 0.5 * h * k2)
+            k4 = f(v + h * k3)
+            v = v + (h / 6.0) * (k1 + 2 * k2 + 2 * k3 + k4)
         x = x + v * dt
         traj[:, i] = x
     y = np.stack([x0x, x0y, x0z, v0x, v0y, v0z, gz, wx, wy, wz, b, m, zeros, zeros, zeros, r, A, cd, rho], 1)

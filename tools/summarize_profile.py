@@ -1,0 +1,59 @@
+"""Turn a tools/profile_round.sh output dir into committed summaries under profiles/:
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --stats kernel summary (the bench command)
+  profiles/<tag>_pmc_traffic.csv    per-kernel HBM bytes per launch from FETCH_SIZE / WRITE_SIZE
+  profiles/pmc_traffic.json         {kernel: bytes_per_launch} read by bench.py (roofline.traffic)
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch; on gfx950 FETCH_SIZE reports half the bytes of a wide
+coalesced stream (MI355X_MICROARCH.md §HBM), so traffic = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024."""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+src = os.path.join(root, "gpurun_out", f"prof_{tag}")
+dst = os.path.join(root, "profiles")
+os.makedirs(dst, exist_ok=True)
+
+stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
+if stats:
+    shutil.copy(stats[0], os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    print("kernel stats:", stats[0])
+
+
+def short(name):
+    for k in ("k_forward", "k_backward", "k_inverse", "k_reduce", "k_pack", "k_ldc"):
+        if k in name:
+            return k
+    return None
+
+
+def per_kernel(counter_glob, counter):
+    out = {}
+    for f in glob.glob(os.path.join(src, counter_glob, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            if k and r["Counter_Name"] == counter:
+                out.setdefault(k, []).append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in out.items()}
+
+
+fetch = per_kernel("fetch", "FETCH_SIZE")
+write = per_kernel("write", "WRITE_SIZE")
+rows, traffic = [], {}
+for k in sorted(set(fetch) | set(write)):
+    fb = 2.0 * fetch.get(k, 0.0) * 1024
+    wb = write.get(k, 0.0) * 1024
+    traffic[k] = round(fb + wb)
+    rows.append({"kernel": k, "FETCH_SIZE_KiB": round(fetch.get(k, 0.0), 1), "WRITE_SIZE_KiB": round(write.get(k, 0.0), 1),
+                 "hbm_bytes_per_launch": round(fb + wb)})
+if rows:
+    with open(os.path.join(dst, f"{tag}_pmc_traffic.csv"), "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
+        w.writeheader()
+        w.writerows(rows)
+    with open(os.path.join(dst, "pmc_traffic.json"), "w") as f:
+        json.dump(traffic, f, indent=1)
+print(json.dumps(rows, indent=1))
