@@ -26,7 +26,10 @@ EXPORTS = (
     "bcnf_stack_supported", "bcnf_param_count", "bcnf_packed_bytes", "bcnf_workspace_bytes",
     "bcnf_slab_bytes", "bcnf_pack_params", "bcnf_stack_forward", "bcnf_stack_backward",
     "bcnf_stack_inverse", "bcnf_grad_reduce", "bcnf_status_string", "bcnf_last_hip_error",
+    "bcnf_nll_forward", "bcnf_nll_backward", "bcnf_grad_partials", "bcnf_adam_step", "bcnf_grad_sumsq",
+    "bcnf_clip_grad_norm", "bcnf_linear_forward", "bcnf_linear_work_bytes", "bcnf_linear_backward",
 )
+MAX_TENSORS = 16
 
 
 class BcnfStackDesc(ctypes.Structure):
@@ -80,6 +83,16 @@ def _bind(lib):
         "bcnf_stack_backward": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
         "bcnf_stack_inverse": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp]),
         "bcnf_grad_reduce": (_i32, [_pdesc, _vp, _i64, _vp, _vp]),
+        "bcnf_nll_forward": (_i32, [_pdesc, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp]),
+        "bcnf_nll_backward": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+        "bcnf_grad_partials": (_i64, [_i64]),
+        "bcnf_adam_step": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double,
+                                  ctypes.c_double, ctypes.c_double, ctypes.c_double, _vp, _vp, _vp]),
+        "bcnf_grad_sumsq": (_i32, [_i32, _vp, _vp, _vp, _vp]),
+        "bcnf_clip_grad_norm": (_i32, [_i32, _vp, _vp, _vp, ctypes.c_float, _vp, _vp]),
+        "bcnf_linear_forward": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp]),
+        "bcnf_linear_work_bytes": (_i64, [_i64, _i32, _i32]),
+        "bcnf_linear_backward": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
         "bcnf_status_string": (ctypes.c_char_p, [_i32]),
         "bcnf_last_hip_error": (_i32, []),
     }
@@ -119,6 +132,21 @@ def ptr(t):
 
 def stream_handle(device) -> ctypes.c_void_p:
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr_array(tensors):
+    """ctypes array of device pointers (None -> NULL) for the multi-tensor entry points."""
+    arr = (ctypes.c_void_p * len(tensors))()
+    for i, t in enumerate(tensors):
+        arr[i] = None if t is None else t.data_ptr()
+    return arr
+
+
+def i64_array(values):
+    arr = (ctypes.c_int64 * len(values))()
+    for i, v in enumerate(values):
+        arr[i] = int(v)
+    return arr
 
 
 def query_i64(fn, *args) -> int:

@@ -25,7 +25,7 @@ import torch.nn as nn
 
 from bcnf_amd.factories import FeatureNetworkFactory, LayerFactory
 from bcnf_amd.feature_network import FeatureNetwork, FeatureNetworkStack
-from bcnf_amd.fused import FusedStack, StackConfig, stack_forward, stack_inverse
+from bcnf_amd.fused import FusedStack, StackConfig, stack_forward, stack_inverse, stack_nll
 from bcnf_amd.utils import ParameterIndexMapping, log_prob_from_latent
 
 
@@ -381,6 +381,18 @@ class CondRealNVP_v2(ConditionalInvertibleLayer):
         if return_features:
             return z, condition
         return z
+
+    def nll_loss(self, y: torch.Tensor, *conditions: torch.Tensor) -> torch.Tensor:
+        """The Trainer's training loss in one fused pass (trainer.py:260-266 with hybrid_weight = 0):
+        returns vals = [loss, nll, mse] where loss = nll = inn_nll_loss(z, log_det_J) and mse = 0.
+        `vals` is differentiable (backprop loss via vals[0] or with cotangent [1, 0, 0]); the feature
+        network runs through autograd as usual, the coupling stack and the loss through the fused
+        kernels with no dz / dldj tensors in between."""
+        self._check_supported()
+        condition = self._features(conditions)
+        if y.dim() == 1:
+            y = y.unsqueeze(0)
+        return stack_nll(self._fused, y, condition, self.training)
 
     def log_prob(self, y: torch.Tensor, *conditions: torch.Tensor) -> torch.Tensor:
         """log p(y | conditions) = -0.5 |z|^2 + log|det J| - D/2 log(2 pi). The reference has no such

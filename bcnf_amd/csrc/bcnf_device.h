@@ -15,6 +15,20 @@
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
+// Last HIP error seen by any entry point of the library (bcnf_last_hip_error), shared by all
+// translation units.
+namespace bcnf_rt {
+extern thread_local int last_hip;
+inline int launched() {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    last_hip = (int)e;
+    return 3;   // BCNF_ERR_HIP
+  }
+  return 0;
+}
+}  // namespace bcnf_rt
+
 // Host-computed layout of one stack (passed by value to every kernel).
 struct BcnfLayout {
   int D, Da, Db, C, Cp, NH, nb, act_norm;

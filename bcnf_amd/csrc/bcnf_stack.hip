@@ -1,8 +1,8 @@
 // bcnf_amd: fused CondRealNVP_v2 coupling stack for MI355X (gfx950 / CDNA4).
 //
 // Kernels (all fp32):
-//   k_pack      canonical nn.Module parameters -> per-lane LDS records (rotation-ready weight rows)
-//   k_ldc       ActNorm log|det| constant  sum_k sum_i log|scale_k,i|            (cnf.py:350)
+//   k_pack      canonical nn.Module parameters -> per-lane LDS records (rotation-ready weight rows),
+//               plus the ActNorm log|det| constant  sum_k sum_i log|scale_k,i|   (cnf.py:350)
 //   k_forward   whole-stack forward, one launch: ActNorm -> nested MLP (GELU, dropout) -> affine
 //               coupling -> log-det -> orthonormal mix, for all n_blocks   (cnf.py:476-488)
 //   k_inverse   whole-stack inverse, one launch                              (cnf.py:499-506)
@@ -19,6 +19,10 @@
 #include <string.h>
 
 #include <mutex>
+
+namespace bcnf_rt {
+thread_local int last_hip = 0;
+}
 
 namespace {
 
@@ -203,56 +207,62 @@ __device__ float rec_b(const BcnfLayout& L, const float* P, const float* Q, int 
   return 0.f;
 }
 
-__global__ void k_pack(BcnfLayout L, const float* __restrict__ P, const float* __restrict__ Q, float* __restrict__ out) {
-  const long long n_pf = (long long)L.nb * 16 * L.RF;
-  const long long n_pb = (long long)L.nb * 16 * L.RB;
-  const long long n_w = (long long)L.nb * L.Cp * 17;
-  const long long total = 2 * n_pf + n_pb + n_w;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+// Grid: PACK_WG record workgroups (grid-stride over every packed float) + 1 workgroup that computes
+// the ActNorm log|det| constant  sum_k sum_i log|scale_k,i|  (cnf.py:350) in a fixed order.
+constexpr int PACK_WG = 512;
+
+__global__ __launch_bounds__(BCNF_WG) void k_pack(BcnfLayout L, const float* __restrict__ P,
+                                                  const float* __restrict__ Q, float* __restrict__ out) {
+  if (blockIdx.x == PACK_WG) {
+    __shared__ float part[BCNF_WG];
+    float acc = 0.f;
+    if (L.act_norm) {
+      const int n = (L.nb - 1) * L.D;
+      for (int i = threadIdx.x; i < n; i += BCNF_WG) {
+        const int k = i / L.D, d = i - k * L.D;
+        acc += logf(fabsf(P[k * L.blk_stride + d]));
+      }
+    }
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = BCNF_WG / 2; s > 0; s >>= 1) {
+      if ((int)threadIdx.x < s) part[threadIdx.x] += part[threadIdx.x + s];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) out[L.ldc_off] = part[0];
+    return;
+  }
+  // every packed section is < 2^31 floats (layout_supported bounds the shapes), so 32-bit index math
+  const int n_pf = L.nb * 16 * L.RF;
+  const int n_pb = L.nb * 16 * L.RB;
+  const int n_w = L.nb * L.Cp * 17;
+  const int total = 2 * n_pf + n_pb + n_w;
+  for (int i = blockIdx.x * BCNF_WG + threadIdx.x; i < total; i += PACK_WG * BCNF_WG) {
     float v;
     long long o;
     if (i < n_pf) {                                   // PF
-      const int e = (int)(i % L.RF), j = (int)((i / L.RF) % 16), k = (int)(i / (16LL * L.RF));
-      v = rec_f(L, P, Q, k, j, e, false);
+      const int kj = i / L.RF, e = i - kj * L.RF;
+      v = rec_f(L, P, Q, kj >> 4, kj & 15, e, false);
       o = L.pf_off + i;
     } else if (i < n_pf + n_pb) {                     // PB
-      const long long ii = i - n_pf;
-      const int e = (int)(ii % L.RB), j = (int)((ii / L.RB) % 16), k = (int)(ii / (16LL * L.RB));
-      v = rec_b(L, P, Q, k, j, e);
+      const int ii = i - n_pf;
+      const int kj = ii / L.RB, e = ii - kj * L.RB;
+      v = rec_b(L, P, Q, kj >> 4, kj & 15, e);
       o = L.pb_off + ii;
     } else if (i < 2 * n_pf + n_pb) {                 // PI
-      const long long ii = i - n_pf - n_pb;
-      const int e = (int)(ii % L.RF), j = (int)((ii / L.RF) % 16), k = (int)(ii / (16LL * L.RF));
-      v = rec_f(L, P, Q, k, j, e, true);
+      const int ii = i - n_pf - n_pb;
+      const int kj = ii / L.RF, e = ii - kj * L.RF;
+      v = rec_f(L, P, Q, kj >> 4, kj & 15, e, true);
       o = L.pi_off + ii;
     } else {                                          // W1h^T [k][c][17] (column 16 = pad)
-      const long long ii = i - 2 * n_pf - n_pb;
-      const int j = (int)(ii % 17), c = (int)((ii / 17) % L.Cp), k = (int)(ii / (17LL * L.Cp));
+      const int ii = i - 2 * n_pf - n_pb;
+      const int kc = ii / 17, j = ii - kc * 17;
+      const int k = kc / L.Cp, c = kc - k * L.Cp;
       v = (j < 16 && j < L.H[1] && c < L.C) ? cW(L, P, k, 1, j, L.Da + c) : 0.f;
       o = L.w1t_off + ii;
     }
     out[o] = v;
   }
-}
-
-// sum over ActNorm layers of sum_i log|scale_i| (cnf.py:350); one workgroup, fixed order.
-__global__ void k_ldc(BcnfLayout L, const float* __restrict__ P, float* __restrict__ out) {
-  __shared__ float part[BCNF_WG];
-  float acc = 0.f;
-  if (L.act_norm) {
-    const int n = (L.nb - 1) * L.D;
-    for (int i = threadIdx.x; i < n; i += BCNF_WG) {
-      const int k = i / L.D, d = i - k * L.D;
-      acc += logf(fabsf(P[k * L.blk_stride + d]));
-    }
-  }
-  part[threadIdx.x] = acc;
-  __syncthreads();
-  for (int s = BCNF_WG / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) part[threadIdx.x] += part[threadIdx.x + s];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) out[L.ldc_off] = part[0];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -404,8 +414,10 @@ template <int NH, bool DROP, bool SAVE>
 __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* __restrict__ pk,
                                                      const float* __restrict__ y, const float* __restrict__ h,
                                                      long long B, float* __restrict__ z, float* __restrict__ ldj_out,
-                                                     float* __restrict__ logp, const uint64_t* __restrict__ rng,
-                                                     float* __restrict__ ysave, uint32_t* __restrict__ msave) {
+                                                     float* __restrict__ logp, const uint64_t* rng,
+                                                     float* __restrict__ ysave, uint32_t* __restrict__ msave,
+                                                     float* __restrict__ nll_part, unsigned* __restrict__ sync,
+                                                     float* __restrict__ loss_out, uint64_t* rng_w) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int RFL = 16 * L.RF, WTL = L.Cp * 17;
   float* rec = smem;                    // [2][16*RF]
@@ -489,6 +501,42 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
   if (logp) {
     const float q2 = row_sum16(ya * ya + yb * yb);
     if (j == 0) logp[bc] = -(0.5f * q2 - ltot) - 0.5f * (float)D * 1.8378770664093454836f;
+  }
+  if (nll_part) {   // inn_nll_loss(z, ldj) = mean_b(0.5 |z_b|^2 - ldj_b)   (utils.py:40-46)
+    const float q2 = row_sum16(ya * ya + yb * yb);
+    float* red = hpb;                                  // free after the loop's last barrier
+    if (j == 0) red[s] = (b < B) ? 0.5f * q2 - ltot : 0.f;
+    __syncthreads();
+    if (tid == 0) {
+      float acc = 0.f;
+      for (int i = 0; i < 16; ++i) acc += red[i];
+      nll_part[blockIdx.x] = acc;
+      __threadfence();                                 // release the partial before counting in
+      const unsigned prev = atomicAdd(sync, 1u);
+      red[16] = (prev == gridDim.x - 1) ? 1.f : 0.f;
+    }
+    __syncthreads();
+    if (red[16] != 0.f) {                              // last workgroup: all partials are visible
+      __threadfence();
+      float acc = 0.f;
+      for (int i = tid; i < (int)gridDim.x; i += BCNF_WG)
+        acc += __hip_atomic_load(nll_part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      float* r2 = hpb + 32;
+      r2[tid] = acc;
+      __syncthreads();
+      for (int w = BCNF_WG / 2; w > 0; w >>= 1) {
+        if (tid < w) r2[tid] += r2[tid + w];
+        __syncthreads();
+      }
+      if (tid == 0) {
+        const float nll = r2[0] / (float)B;
+        loss_out[0] = nll;                             // (nll + mse * 0) / (1 + 0)   (trainer.py:264)
+        loss_out[1] = nll;
+        loss_out[2] = 0.f;
+        if (rng_w) rng_w[1] += 1;                      // every workgroup has read the offset
+        *sync = 0u;
+      }
+    }
   }
 }
 
@@ -706,7 +754,8 @@ __device__ __forceinline__ void bwd_mfma_phase(const BcnfLayout& L, const float*
 template <int NH>
 __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float* __restrict__ pk,
                                                       const float* __restrict__ h, const float* __restrict__ dz,
-                                                      const float* __restrict__ dldj, long long B,
+                                                      const float* __restrict__ dldj, const float* __restrict__ dloss,
+                                                      int nll, long long B,
                                                       const float* __restrict__ ysave, const uint32_t* __restrict__ msave,
                                                       float* __restrict__ dy, float* __restrict__ dh,
                                                       float* __restrict__ slab_all, long long slab_stride) {
@@ -738,11 +787,18 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
 
   float gya = 0.f, gyb = 0.f, dl = 0.f;
   if (valid) {                                      // padded rows carry zero gradient
-    if (dz) {
-      gya = (j < Da) ? dz[b * D + j] : 0.f;
-      gyb = (j < Db) ? dz[b * D + Da + j] : 0.f;
+    if (nll) {    // d/dz, d/dldj of mean_b(0.5 |z_b|^2 - ldj_b); dz holds z here
+      const float sc = (dloss ? dloss[0] + dloss[1] : 1.f) / (float)B;   // d loss/d nll = d nll/d nll = 1
+      gya = (j < Da) ? dz[b * D + j] * sc : 0.f;
+      gyb = (j < Db) ? dz[b * D + Da + j] * sc : 0.f;
+      dl = -sc;
+    } else {
+      if (dz) {
+        gya = (j < Da) ? dz[b * D + j] : 0.f;
+        gyb = (j < Db) ? dz[b * D + Da + j] : 0.f;
+      }
+      if (dldj) dl = dldj[b];
     }
-    if (dldj) dl = dldj[b];
   }
   // saved input / dropout masks of the block about to be processed (prefetched one block ahead)
   float ya_n, yb_n;
@@ -907,16 +963,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_reduce(const float* __restrict__ sl
 // ------------------------------------------------------------------------------------------------
 // Launch helpers
 // ------------------------------------------------------------------------------------------------
-thread_local int g_last_hip = 0;
-
-int check_launch() {
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) {
-    g_last_hip = (int)e;
-    return BCNF_ERR_HIP;
-  }
-  return BCNF_OK;
-}
+int check_launch() { return bcnf_rt::launched(); }
 
 
 
@@ -947,7 +994,7 @@ int launch_lds(K kernel, size_t& lds) {
     if (g_attr_fn[i] == fn && g_attr_lds[i] >= lds) return BCNF_OK;
   const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) {
-    g_last_hip = (int)e;
+    bcnf_rt::last_hip = (int)e;
     return BCNF_ERR_HIP;
   }
   int slot = -1;
@@ -969,10 +1016,17 @@ bool layout_matches(const BcnfLayout& L) {
          L.RB >= RecB<NH>::USED;
 }
 
+struct NllOut {
+  float* part = nullptr;
+  unsigned* sync = nullptr;
+  float* loss = nullptr;
+  uint64_t* rng_w = nullptr;
+};
+
 template <int NH>
 int fwd_dispatch(const BcnfLayout& L, const float* pk, const float* y, const float* h, long long B, float* z,
                  float* ldj, float* logp, bool drop, const uint64_t* rng, float* ysave, uint32_t* msave,
-                 hipStream_t st) {
+                 const NllOut& no, hipStream_t st) {
   if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
   const dim3 grid((unsigned)((B + 15) / 16));
   size_t lds = fwd_lds_bytes(L);
@@ -982,7 +1036,7 @@ int fwd_dispatch(const BcnfLayout& L, const float* pk, const float* y, const flo
   rc = launch_lds(k_forward<NH, DR, SV>, lds);                                                    \
   if (rc) return rc;                                                                                        \
   hipLaunchKernelGGL((k_forward<NH, DR, SV>), grid, dim3(BCNF_WG), lds, st, L, pk, y, h, B, z, ldj, logp,   \
-                     rng, ysave, msave);
+                     rng, ysave, msave, no.part, no.sync, no.loss, no.rng_w);
   if (drop) {
     if (save) { BCNF_FWD(true, true) } else { BCNF_FWD(true, false) }
   } else {
@@ -1013,19 +1067,68 @@ int inv_dispatch(const BcnfLayout& L, const float* pk, const float* zin, const f
 
 template <int NH>
 int bwd_dispatch(const BcnfLayout& L, const float* pk, const float* h, const float* dz, const float* dldj,
-                 long long B, const float* ysave, const uint32_t* msave, float* dy, float* dh, float* slab,
-                 long long stride, hipStream_t st) {
+                 const float* dloss, int nll, long long B, const float* ysave, const uint32_t* msave, float* dy,
+                 float* dh, float* slab, long long stride, hipStream_t st) {
   if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
   const dim3 grid((unsigned)((B + 15) / 16));
   size_t lds = bwd_lds_bytes(L);
   const int rc = launch_lds(k_backward<NH>, lds);
   if (rc) return rc;
-  hipLaunchKernelGGL((k_backward<NH>), grid, dim3(BCNF_WG), lds, st, L, pk, h, dz, dldj, B, ysave, msave, dy,
-                     dh, slab, stride);
+  hipLaunchKernelGGL((k_backward<NH>), grid, dim3(BCNF_WG), lds, st, L, pk, h, dz, dldj, dloss, nll, B, ysave,
+                     msave, dy, dh, slab, stride);
   return check_launch();
 }
 
 long long slab_stride_of(const BcnfLayout& L) { return ((long long)L.n_trainable + 3) & ~3LL; }
+
+// Workspace: [saved block inputs nb*B*32][dropout masks ceil(nb/4)*B*16 u32, if dropout][loss partials]
+long long ws_mask_off(const BcnfLayout& L, long long B) { return (long long)L.nb * B * 32; }
+long long ws_part_off(const BcnfLayout& L, long long B, bool drop) {
+  return ws_mask_off(L, B) + (drop ? (long long)((L.nb + 3) / 4) * B * 16 : 0);
+}
+long long ws_floats(const BcnfLayout& L, long long B, bool drop) {
+  return ws_part_off(L, B, drop) + (((B + 15) / 16 + 3) & ~3LL);
+}
+
+int forward_impl(const BcnfStackDesc* desc, const void* packed, const float* y, const float* h, int64_t batch,
+                 float* z, float* ldj, float* log_prob, int32_t training, const uint64_t* rng_state, void* workspace,
+                 bool nll, unsigned* sync, float* loss_out, void* stream) {
+  BcnfLayout L;
+  const int rc = make_layout(desc, &L);
+  if (rc) return rc;
+  if (!layout_supported(L, desc)) return BCNF_ERR_UNSUPPORTED;
+  if (batch < 0) return BCNF_ERR_ARG;
+  if (batch == 0) return nll ? BCNF_ERR_ARG : BCNF_OK;      // the mean over an empty batch is undefined
+  if (!packed || !y || !h || !z) return BCNF_ERR_ARG;
+  if (nll && (!workspace || !sync || !loss_out)) return BCNF_ERR_ARG;
+  const bool drop = training && L.p > 0.f;
+  if (drop && !rng_state) return BCNF_ERR_ARG;
+  float* ysave = nullptr;
+  uint32_t* msave = nullptr;
+  NllOut no;
+  if (workspace) {
+    ysave = (float*)workspace;
+    if (drop) msave = (uint32_t*)(ysave + ws_mask_off(L, batch));
+    if (nll) {
+      no.part = ysave + ws_part_off(L, batch, drop);
+      no.sync = sync;
+      no.loss = loss_out;
+      no.rng_w = drop ? const_cast<uint64_t*>(rng_state) : nullptr;
+    }
+  }
+  const float* pk = (const float*)packed;
+  hipStream_t st = (hipStream_t)stream;
+  switch (L.NH) {
+#define BCNF_CASE(N) case N: return fwd_dispatch<N>(L, pk, y, h, batch, z, ldj, log_prob, drop, rng_state, ysave, msave, no, st);
+    BCNF_CASE(1) BCNF_CASE(2) BCNF_CASE(3) BCNF_CASE(4) BCNF_CASE(5) BCNF_CASE(6) BCNF_CASE(7) BCNF_CASE(8)
+#undef BCNF_CASE
+    default: return BCNF_ERR_UNSUPPORTED;
+  }
+}
+
+int backward_impl(const BcnfStackDesc* desc, const void* packed, const float* h, const float* dz, const float* dldj,
+                  const float* dloss, int nll, int64_t batch, int32_t training, const void* workspace, float* dy,
+                  float* dh, float* dparams, void* slab, void* stream);
 
 }  // namespace
 
@@ -1063,9 +1166,7 @@ int bcnf_workspace_bytes(const BcnfStackDesc* desc, int64_t batch, int32_t train
   const int rc = make_layout(desc, &L);
   if (rc) return rc;
   if (!bytes || batch < 0) return BCNF_ERR_ARG;
-  int64_t n = (int64_t)L.nb * batch * 32 * 4;
-  if (training && L.p > 0.f) n += (int64_t)((L.nb + 3) / 4) * batch * 16 * 4;
-  *bytes = n;
+  *bytes = ws_floats(L, batch, training && L.p > 0.f) * 4;
   return BCNF_OK;
 }
 
@@ -1085,69 +1186,37 @@ int bcnf_pack_params(const BcnfStackDesc* desc, const float* params, const float
   if (!layout_supported(L, desc)) return BCNF_ERR_UNSUPPORTED;
   if (!params || !packed || (L.nb > 1 && !qmats)) return BCNF_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_pack, dim3(512), dim3(BCNF_WG), 0, st, L, params, qmats, (float*)packed);
-  if ((rc = check_launch())) return rc;
-  hipLaunchKernelGGL(k_ldc, dim3(1), dim3(BCNF_WG), 0, st, L, params, (float*)packed);
+  hipLaunchKernelGGL(k_pack, dim3(PACK_WG + 1), dim3(BCNF_WG), 0, st, L, params, qmats, (float*)packed);
   return check_launch();
 }
 
 int bcnf_stack_forward(const BcnfStackDesc* desc, const void* packed, const float* y, const float* h, int64_t batch,
                        float* z, float* ldj, float* log_prob, int32_t training, const uint64_t* rng_state,
                        void* workspace, void* stream) {
-  BcnfLayout L;
-  const int rc = make_layout(desc, &L);
-  if (rc) return rc;
-  if (!layout_supported(L, desc)) return BCNF_ERR_UNSUPPORTED;
-  if (batch == 0) return BCNF_OK;
-  if (batch < 0 || !packed || !y || !h || !z) return BCNF_ERR_ARG;
-  const bool drop = training && L.p > 0.f;
-  if (drop && !rng_state) return BCNF_ERR_ARG;
-  float* ysave = nullptr;
-  uint32_t* msave = nullptr;
-  if (workspace) {
-    ysave = (float*)workspace;
-    if (drop) msave = (uint32_t*)(ysave + (long long)L.nb * batch * 32);
-  }
-  const float* pk = (const float*)packed;
-  hipStream_t st = (hipStream_t)stream;
-  switch (L.NH) {
-#define BCNF_CASE(N) case N: return fwd_dispatch<N>(L, pk, y, h, batch, z, ldj, log_prob, drop, rng_state, ysave, msave, st);
-    BCNF_CASE(1) BCNF_CASE(2) BCNF_CASE(3) BCNF_CASE(4) BCNF_CASE(5) BCNF_CASE(6) BCNF_CASE(7) BCNF_CASE(8)
-#undef BCNF_CASE
-    default: return BCNF_ERR_UNSUPPORTED;
-  }
+  return forward_impl(desc, packed, y, h, batch, z, ldj, log_prob, training, rng_state, workspace, false, nullptr,
+                      nullptr, stream);
+}
+
+int bcnf_nll_forward(const BcnfStackDesc* desc, const void* packed, const float* y, const float* h, int64_t batch,
+                     float* z, float* ldj, int32_t training, uint64_t* rng_state, void* workspace, uint32_t* sync,
+                     float* loss_out, void* stream) {
+  return forward_impl(desc, packed, y, h, batch, z, ldj, nullptr, training, rng_state, workspace, true,
+                      (unsigned*)sync, loss_out, stream);
 }
 
 int bcnf_stack_backward(const BcnfStackDesc* desc, const void* packed, const float* h, const float* dz,
                         const float* dldj, int64_t batch, int32_t training, const void* workspace, float* dy,
                         float* dh, float* dparams, void* slab, void* stream) {
-  BcnfLayout L;
-  int rc = make_layout(desc, &L);
-  if (rc) return rc;
-  if (!layout_supported(L, desc)) return BCNF_ERR_UNSUPPORTED;
-  if (batch < 0 || !packed || !h || !workspace || !slab) return BCNF_ERR_ARG;
-  hipStream_t st = (hipStream_t)stream;
-  if (batch == 0) {
-    if (dparams && hipMemsetAsync(dparams, 0, sizeof(float) * (size_t)L.n_trainable, st) != hipSuccess)
-      return BCNF_ERR_HIP;
-    return BCNF_OK;
-  }
-  // `training` must match the forward call that filled the workspace: it says whether dropout masks
-  // were saved behind the block inputs.
-  const float* ysave = (const float*)workspace;
-  const uint32_t* msave = nullptr;
-  if (training && L.p > 0.f) msave = (const uint32_t*)(ysave + (long long)L.nb * batch * 32);
-  const float* pk = (const float*)packed;
-  const long long stride = slab_stride_of(L);
-  switch (L.NH) {
-#define BCNF_CASE(N) case N: rc = bwd_dispatch<N>(L, pk, h, dz, dldj, batch, ysave, msave, dy, dh, (float*)slab, stride, st); break;
-    BCNF_CASE(1) BCNF_CASE(2) BCNF_CASE(3) BCNF_CASE(4) BCNF_CASE(5) BCNF_CASE(6) BCNF_CASE(7) BCNF_CASE(8)
-#undef BCNF_CASE
-    default: return BCNF_ERR_UNSUPPORTED;
-  }
-  if (rc) return rc;
-  if (!dparams) return BCNF_OK;   // caller reduces with bcnf_grad_reduce
-  return bcnf_grad_reduce(desc, slab, batch, dparams, stream);
+  return backward_impl(desc, packed, h, dz, dldj, nullptr, 0, batch, training, workspace, dy, dh, dparams, slab,
+                       stream);
+}
+
+int bcnf_nll_backward(const BcnfStackDesc* desc, const void* packed, const float* h, const float* z,
+                      const float* dloss, int64_t batch, int32_t training, const void* workspace, float* dy,
+                      float* dh, float* dparams, void* slab, void* stream) {
+  if (!z && batch > 0) return BCNF_ERR_ARG;
+  return backward_impl(desc, packed, h, z, nullptr, dloss, 1, batch, training, workspace, dy, dh, dparams, slab,
+                       stream);
 }
 
 int bcnf_grad_reduce(const BcnfStackDesc* desc, const void* slab, int64_t batch, float* dparams, void* stream) {
@@ -1193,6 +1262,43 @@ const char* bcnf_status_string(int status) {
   }
 }
 
-int bcnf_last_hip_error(void) { return g_last_hip; }
+int bcnf_last_hip_error(void) { return bcnf_rt::last_hip; }
 
 }  // extern "C"
+
+namespace {
+
+int backward_impl(const BcnfStackDesc* desc, const void* packed, const float* h, const float* dz, const float* dldj,
+                  const float* dloss, int nll, int64_t batch, int32_t training, const void* workspace, float* dy,
+                  float* dh, float* dparams, void* slab, void* stream) {
+  BcnfLayout L;
+  int rc = make_layout(desc, &L);
+  if (rc) return rc;
+  if (!layout_supported(L, desc)) return BCNF_ERR_UNSUPPORTED;
+  if (batch < 0 || !packed || !h || !workspace || !slab) return BCNF_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  if (batch == 0) {
+    if (dparams && hipMemsetAsync(dparams, 0, sizeof(float) * (size_t)L.n_trainable, st) != hipSuccess)
+      return BCNF_ERR_HIP;
+    return BCNF_OK;
+  }
+  // `training` must match the forward call that filled the workspace: it says whether dropout masks
+  // were saved behind the block inputs.
+  const float* ysave = (const float*)workspace;
+  const uint32_t* msave = nullptr;
+  if (training && L.p > 0.f) msave = (const uint32_t*)(ysave + ws_mask_off(L, batch));
+  const float* pk = (const float*)packed;
+  const long long stride = slab_stride_of(L);
+  switch (L.NH) {
+#define BCNF_CASE(N) case N: rc = bwd_dispatch<N>(L, pk, h, dz, dldj, dloss, nll, batch, ysave, msave, dy, dh, (float*)slab, stride, st); break;
+    BCNF_CASE(1) BCNF_CASE(2) BCNF_CASE(3) BCNF_CASE(4) BCNF_CASE(5) BCNF_CASE(6) BCNF_CASE(7) BCNF_CASE(8)
+#undef BCNF_CASE
+    default: return BCNF_ERR_UNSUPPORTED;
+  }
+  if (rc) return rc;
+  if (!dparams) return BCNF_OK;   // caller reduces with bcnf_grad_reduce
+  return bcnf_grad_reduce(desc, slab, batch, dparams, stream);
+}
+
+}  // namespace
+

@@ -1,0 +1,390 @@
+// bcnf_amd: the training-step kernels around the coupling stack (gfx950 / CDNA4).
+//
+//   k_adam     multi-tensor Adam over the flat parameter buffers (torch.optim.Adam semantics,
+//              trainer.py:136 / :270), fused with the per-workgroup sum of squared gradients that
+//              clip_grad_norm_ needs (trainer.py:272) and with the device-side step counter bump
+//   k_sumsq    per-workgroup sum of squared gradients (standalone clip)
+//   k_clip     total norm from the partials (fixed order) + in-place gradient scaling
+//   k_gemm     small fp32 MFMA GEMM C = A * op(B) (+ bias) for the feature network's nn.Linear
+//              (feature_network.py:114-145): forward and dL/dx
+//   k_gemm_wt  split-K dL/dW = dY^T X and dL/db = sum dY partials; k_wt_reduce sums them (fixed order)
+//
+// Every reduction has a fixed order, so results are bit-reproducible run to run.
+#include "bcnf_device.h"
+#include "../../include/bcnf_amd.h"
+
+#include <math.h>
+
+namespace {
+
+constexpr int EPT = 4;                          // elements per thread in the elementwise kernels
+constexpr int CHUNK = BCNF_WG * EPT;            // elements per workgroup
+
+struct TList {
+  float* p[BCNF_MAX_TENSORS];
+  float* g[BCNF_MAX_TENSORS];
+  float* m[BCNF_MAX_TENSORS];
+  float* v[BCNF_MAX_TENSORS];
+  long long start[BCNF_MAX_TENSORS + 1];        // prefix offsets of the concatenated index space
+  int n;
+};
+
+__device__ __forceinline__ int find_tensor(const TList& T, long long i) {
+  int t = 0;
+#pragma unroll 1
+  while (t + 1 < T.n && i >= T.start[t + 1]) ++t;
+  return t;
+}
+
+// Fixed-order workgroup sum: every thread contributes `v`; thread 0 gets the total.
+__device__ __forceinline__ float wg_sum(float v, float* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+#pragma unroll
+  for (int s = BCNF_WG / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  return red[0];
+}
+
+// torch.optim.Adam (amsgrad=False, maximize=False), per element (torch/optim/adam.py _single_tensor_adam):
+//   g += wd * p;  m = lerp(m, g, 1-b1);  v = b2 v + (1-b2) g g;
+//   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+// Hyper-parameters arrive as doubles (Python floats) and every scalar is derived in double, then
+// rounded once, as torch does (1 - beta2 in fp32 from 0.999f would be off by 1e-5 relative).
+__global__ __launch_bounds__(BCNF_WG) void k_adam(TList T, float* __restrict__ step, double lr, double b1d,
+                                                  double b2d, double epsd, double wdd, float* __restrict__ part,
+                                                  unsigned* __restrict__ sync) {
+  __shared__ float red[BCNF_WG];
+  __shared__ int last;
+  const float st = step[0] + 1.0f;
+  const double bc1 = 1.0 - pow(b1d, (double)st);
+  const double bc2 = 1.0 - pow(b2d, (double)st);
+  const float step_size = (float)(lr / bc1);
+  const float bc2s = (float)sqrt(bc2);
+  const float omb1 = (float)(1.0 - b1d), omb2 = (float)(1.0 - b2d);
+  const float b2 = (float)b2d, eps = (float)epsd, wd = (float)wdd;
+  const long long total = T.start[T.n];
+  float ss = 0.f;
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const long long i = (long long)blockIdx.x * CHUNK + e * BCNF_WG + threadIdx.x;
+    if (i < total) {
+      const int t = find_tensor(T, i);
+      const long long o = i - T.start[t];
+      float g = T.g[t][o];
+      float p = T.p[t][o];
+      ss = fmaf(g, g, ss);
+      if (wd != 0.f) g = fmaf(wd, p, g);
+      float m = T.m[t][o];
+      m = m + omb1 * (g - m);                       // lerp, |weight| < 0.5 branch
+      const float v = T.v[t][o] * b2 + omb2 * (g * g);
+      const float denom = sqrtf(v) / bc2s + eps;
+      p = p + (-step_size) * (m / denom);
+      T.m[t][o] = m;
+      T.v[t][o] = v;
+      T.p[t][o] = p;
+    }
+  }
+  const float s = wg_sum(ss, red);
+  if (threadIdx.x == 0) {
+    if (part) part[blockIdx.x] = s;
+    __threadfence();
+    const unsigned prev = atomicAdd(sync, 1u);
+    last = (prev == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {   // every workgroup has read step[0]: publish the increment
+    step[0] = st;
+    *sync = 0u;
+  }
+}
+
+__global__ __launch_bounds__(BCNF_WG) void k_sumsq(TList T, float* __restrict__ part) {
+  __shared__ float red[BCNF_WG];
+  const long long total = T.start[T.n];
+  float ss = 0.f;
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const long long i = (long long)blockIdx.x * CHUNK + e * BCNF_WG + threadIdx.x;
+    if (i < total) {
+      const int t = find_tensor(T, i);
+      const float g = T.g[t][i - T.start[t]];
+      ss = fmaf(g, g, ss);
+    }
+  }
+  const float s = wg_sum(ss, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// torch.nn.utils.clip_grad_norm_: coef = min(max_norm / (||g||_2 + 1e-6), 1); g *= coef.
+__global__ __launch_bounds__(BCNF_WG) void k_clip(TList T, const float* __restrict__ part, int nparts, float max_norm,
+                                                  float* __restrict__ norm_out) {
+  __shared__ float red[BCNF_WG];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += BCNF_WG) acc += part[i];
+  const float tot = sqrtf(wg_sum(acc, red));
+  const float coef = fminf(max_norm / (tot + 1e-6f), 1.0f);
+  const long long total = T.start[T.n];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const long long i = (long long)blockIdx.x * CHUNK + e * BCNF_WG + threadIdx.x;
+    if (i < total) {
+      const int t = find_tensor(T, i);
+      T.g[t][i - T.start[t]] *= coef;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && norm_out) norm_out[0] = tot;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Small GEMMs for nn.Linear. One wave = one 16x16 output tile, v_mfma_f32_16x16x4f32 over the
+// reduction; lane l supplies A[l&15][l>>4] and B[l>>4][l&15] and owns D[4(l>>4)+i][l&15].
+// C[M][Nc] = A[M][K] * op(B) + bias; op(B)[k][n] = TB ? B[n*ldb + k] : B[k*ldb + n].
+// ------------------------------------------------------------------------------------------------
+template <bool TB>
+__global__ __launch_bounds__(BCNF_WG) void k_gemm(const float* __restrict__ A, int lda, const float* __restrict__ Bm,
+                                                  int ldb, const float* __restrict__ bias, float* __restrict__ C,
+                                                  int ldc, long long M, int Nc, int K) {
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lq = l >> 4;
+  const long long row0 = ((long long)blockIdx.x * 4 + wave) * 16;
+  const int col0 = blockIdx.y * 16;
+  if (row0 >= M) return;
+  const long long ar = row0 + lr < M ? row0 + lr : M - 1;     // clamped rows: loaded, never stored
+  const int bc = col0 + lr < Nc ? col0 + lr : Nc - 1;
+  const float* a = A + ar * lda;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  int k0 = 0;
+  for (; k0 + 16 <= K; k0 += 16) {              // 4 MFMA steps, loads issued first
+    float av[4], bv[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int k = k0 + 4 * t + lq;
+      av[t] = a[k];
+      bv[t] = TB ? Bm[(long long)bc * ldb + k] : Bm[(long long)k * ldb + bc];
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc = mfma4(av[t], bv[t], acc);
+  }
+  for (; k0 < K; k0 += 4) {
+    const int k = k0 + lq;
+    const int kc = k < K ? k : K - 1;
+    float av = a[kc];
+    float bv = TB ? Bm[(long long)bc * ldb + kc] : Bm[(long long)kc * ldb + bc];
+    av = k < K ? av : 0.f;
+    bv = k < K ? bv : 0.f;
+    acc = mfma4(av, bv, acc);
+  }
+  const int col = col0 + lr;
+  if (col < Nc) {
+    const float bb = bias ? bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long long r = row0 + 4 * lq + i;
+      if (r < M) C[r * ldc + col] = acc[i] + bb;
+    }
+  }
+}
+
+// Split-K weight gradient: work[s][n][k] = sum_{m in split s} dY[m][n] X[m][k],
+// bwork[s][n] = sum_{m in split s} dY[m][n]. grid = (tiles_n * tiles_k / 4 rounded up, splits).
+__global__ __launch_bounds__(BCNF_WG) void k_gemm_wt(const float* __restrict__ X, const float* __restrict__ dY,
+                                                     long long M, int N, int K, int rows_per_split,
+                                                     float* __restrict__ work, float* __restrict__ bwork) {
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lq = l >> 4;
+  const int tiles_k = (K + 15) / 16, tiles_n = (N + 15) / 16;
+  const int tile = blockIdx.x * 4 + wave;
+  if (tile >= tiles_n * tiles_k) return;
+  const int n0 = (tile / tiles_k) * 16, k0 = (tile % tiles_k) * 16;
+  const int s = blockIdx.y;
+  const long long m_begin = (long long)s * rows_per_split;
+  long long m_end = m_begin + rows_per_split;
+  if (m_end > M) m_end = M;
+  const int n = n0 + lr < N ? n0 + lr : N - 1;
+  const int k = k0 + lr < K ? k0 + lr : K - 1;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+  long long m0 = m_begin;
+  for (; m0 + 16 <= m_end; m0 += 16) {
+    float av[4], bv[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const long long m = m0 + 4 * t + lq;
+      av[t] = dY[m * N + n];
+      bv[t] = X[m * K + k];
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      bsum += av[t];
+      acc = mfma4(av[t], bv[t], acc);
+    }
+  }
+  for (; m0 < m_end; m0 += 4) {
+    const long long m = m0 + lq;
+    const long long mc = m < m_end ? m : m_end - 1;
+    float av = dY[mc * N + n];          // A[n][m] = dY[m][n]
+    float bv = X[mc * K + k];           // B[m][k] = X[m][k]
+    av = m < m_end ? av : 0.f;
+    bv = m < m_end ? bv : 0.f;
+    bsum += av;
+    acc = mfma4(av, bv, acc);
+  }
+  float* w = work + (long long)s * N * K;
+  const int kk = k0 + lr;
+  if (kk < K) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int nn = n0 + 4 * lq + i;
+      if (nn < N) w[(long long)nn * K + kk] = acc[i];
+    }
+  }
+  if (k0 == 0 && bwork) {             // dY column sums of this split: fold the 4 lane quarters
+    bsum += __shfl_xor(bsum, 16);
+    bsum += __shfl_xor(bsum, 32);
+    if (lq == 0 && n0 + lr < N) bwork[(long long)s * N + n0 + lr] = bsum;
+  }
+}
+
+__global__ __launch_bounds__(BCNF_WG) void k_wt_reduce(const float* __restrict__ work, const float* __restrict__ bwork,
+                                                       int splits, int N, int K, float* __restrict__ dW,
+                                                       float* __restrict__ db) {
+  const long long NK = (long long)N * K;
+  const long long i = (long long)blockIdx.x * BCNF_WG + threadIdx.x;
+  if (i < NK) {
+    float acc = 0.f;
+    for (int s = 0; s < splits; ++s) acc += work[(long long)s * NK + i];
+    dW[i] = acc;
+  } else if (db && i < NK + N) {
+    const int n = (int)(i - NK);
+    float acc = 0.f;
+    for (int s = 0; s < splits; ++s) acc += bwork[(long long)s * N + n];
+    db[n] = acc;
+  }
+}
+
+using bcnf_rt::launched;
+
+int make_tlist(int n, float* const* p, float* const* g, float* const* m, float* const* v, const int64_t* numel,
+               TList* T) {
+  if (n < 1 || n > BCNF_MAX_TENSORS || !g || !numel) return BCNF_ERR_ARG;
+  T->n = n;
+  T->start[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    if (numel[i] < 0 || !g[i]) return BCNF_ERR_ARG;
+    T->p[i] = p ? p[i] : nullptr;
+    T->g[i] = g[i];
+    T->m[i] = m ? m[i] : nullptr;
+    T->v[i] = v ? v[i] : nullptr;
+    T->start[i + 1] = T->start[i] + numel[i];
+  }
+  return BCNF_OK;
+}
+
+int split_rows(long long M) {        // rows per split-K chunk of the weight gradient (multiple of 4)
+  long long r = (M + 63) / 64;
+  if (r < 64) r = 64;
+  return (int)((r + 3) & ~3LL);
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t bcnf_grad_partials(int64_t total_numel) { return total_numel <= 0 ? 1 : (total_numel + CHUNK - 1) / CHUNK; }
+
+int bcnf_adam_step(int32_t n_tensors, float* const* params, float* const* grads, float* const* exp_avg,
+                   float* const* exp_avg_sq, const int64_t* numel, float* step, double lr, double beta1,
+                   double beta2, double eps, double weight_decay, float* grad_partials, uint32_t* sync,
+                   void* stream) {
+  TList T;
+  int rc = make_tlist(n_tensors, params, grads, exp_avg, exp_avg_sq, numel, &T);
+  if (rc) return rc;
+  if (!params || !exp_avg || !exp_avg_sq || !step || !sync) return BCNF_ERR_ARG;
+  for (int i = 0; i < n_tensors; ++i)
+    if (!T.p[i] || !T.m[i] || !T.v[i]) return BCNF_ERR_ARG;
+  const long long total = T.start[T.n];
+  const unsigned nwg = (unsigned)bcnf_grad_partials(total);
+  hipLaunchKernelGGL(k_adam, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, step, lr, beta1, beta2, eps,
+                     weight_decay, grad_partials, (unsigned*)sync);
+  return launched();
+}
+
+int bcnf_grad_sumsq(int32_t n_tensors, float* const* grads, const int64_t* numel, float* grad_partials, void* stream) {
+  TList T;
+  int rc = make_tlist(n_tensors, nullptr, grads, nullptr, nullptr, numel, &T);
+  if (rc) return rc;
+  if (!grad_partials) return BCNF_ERR_ARG;
+  const unsigned nwg = (unsigned)bcnf_grad_partials(T.start[T.n]);
+  hipLaunchKernelGGL(k_sumsq, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, grad_partials);
+  return launched();
+}
+
+int bcnf_clip_grad_norm(int32_t n_tensors, float* const* grads, const int64_t* numel, const float* grad_partials,
+                        float max_norm, float* total_norm, void* stream) {
+  TList T;
+  int rc = make_tlist(n_tensors, nullptr, grads, nullptr, nullptr, numel, &T);
+  if (rc) return rc;
+  if (!grad_partials) return BCNF_ERR_ARG;
+  const long long np = bcnf_grad_partials(T.start[T.n]);
+  hipLaunchKernelGGL(k_clip, dim3((unsigned)np), dim3(BCNF_WG), 0, (hipStream_t)stream, T, grad_partials, (int)np,
+                     max_norm, total_norm);
+  return launched();
+}
+
+int bcnf_linear_forward(const float* x, const float* weight, const float* bias, int64_t rows, int32_t in_features,
+                        int32_t out_features, float* y, void* stream) {
+  if (rows < 0 || in_features < 1 || out_features < 1) return BCNF_ERR_ARG;
+  if (rows == 0) return BCNF_OK;
+  if (!x || !weight || !y) return BCNF_ERR_ARG;
+  const dim3 grid((unsigned)((rows + 63) / 64), (unsigned)((out_features + 15) / 16));
+  hipLaunchKernelGGL(k_gemm<true>, grid, dim3(BCNF_WG), 0, (hipStream_t)stream, x, in_features, weight, in_features,
+                     bias, y, out_features, (long long)rows, out_features, in_features);
+  return launched();
+}
+
+int64_t bcnf_linear_work_bytes(int64_t rows, int32_t in_features, int32_t out_features) {
+  if (rows <= 0) return 0;
+  const long long splits = (rows + split_rows(rows) - 1) / split_rows(rows);
+  return (int64_t)splits * ((int64_t)out_features * in_features + out_features) * 4;
+}
+
+int bcnf_linear_backward(const float* x, const float* weight, const float* dy, int64_t rows, int32_t in_features,
+                         int32_t out_features, float* dx, float* dweight, float* dbias, void* work, void* stream) {
+  if (rows < 0 || in_features < 1 || out_features < 1) return BCNF_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const int K = in_features, N = out_features;
+  if (rows == 0) {
+    if (dweight && hipMemsetAsync(dweight, 0, sizeof(float) * (size_t)N * K, st) != hipSuccess) return BCNF_ERR_HIP;
+    if (dbias && hipMemsetAsync(dbias, 0, sizeof(float) * (size_t)N, st) != hipSuccess) return BCNF_ERR_HIP;
+    return BCNF_OK;
+  }
+  if (!dy) return BCNF_ERR_ARG;
+  if (dx) {   // dX[m][k] = sum_n dY[m][n] W[n][k]
+    if (!weight) return BCNF_ERR_ARG;
+    const dim3 grid((unsigned)((rows + 63) / 64), (unsigned)((K + 15) / 16));
+    hipLaunchKernelGGL(k_gemm<false>, grid, dim3(BCNF_WG), 0, st, dy, N, weight, K, (const float*)nullptr, dx, K,
+                       (long long)rows, K, N);
+    int rc = launched();
+    if (rc) return rc;
+  }
+  if (dweight || dbias) {
+    if (!x || !work || !dweight) return BCNF_ERR_ARG;
+    const int rps = split_rows(rows);
+    const int splits = (int)((rows + rps - 1) / rps);
+    const int tiles = ((N + 15) / 16) * ((K + 15) / 16);
+    float* w = (float*)work;
+    float* bw = w + (long long)splits * N * K;
+    hipLaunchKernelGGL(k_gemm_wt, dim3((unsigned)((tiles + 3) / 4), (unsigned)splits), dim3(BCNF_WG), 0, st, x, dy,
+                       (long long)rows, N, K, rps, w, dbias ? bw : nullptr);
+    int rc = launched();
+    if (rc) return rc;
+    const long long outs = (long long)N * K + (dbias ? N : 0);
+    hipLaunchKernelGGL(k_wt_reduce, dim3((unsigned)((outs + BCNF_WG - 1) / BCNF_WG)), dim3(BCNF_WG), 0, st, w, bw,
+                       splits, N, K, dweight, dbias);
+    return launched();
+  }
+  return BCNF_OK;
+}
+
+}  // extern "C"

@@ -18,6 +18,52 @@ import torch
 from torch import nn
 
 
+class _LinearFn(torch.autograd.Function):
+    """y = x W^T + b on the HIP GEMM kernels (bcnf_linear_forward / bcnf_linear_backward)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        from bcnf_amd import _native as N
+        rows, k = x.shape
+        n = weight.shape[0]
+        y = torch.empty((rows, n), dtype=torch.float32, device=x.device)
+        N.check(N.lib().bcnf_linear_forward(N.ptr(x), N.ptr(weight), N.ptr(bias), rows, k, n, N.ptr(y),
+                                            N.stream_handle(x.device)), "bcnf_linear_forward")
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from bcnf_amd import _native as N
+        x, weight = ctx.saved_tensors
+        dy = dy.contiguous()
+        rows, k = x.shape
+        n = weight.shape[0]
+        need_x, need_w, need_b = ctx.needs_input_grad
+        dx = torch.empty_like(x) if need_x else None
+        dw = torch.empty_like(weight) if (need_w or need_b) else None
+        db = torch.empty(n, dtype=torch.float32, device=x.device) if (need_b and ctx.has_bias) else None
+        work = None
+        if dw is not None:
+            wb = int(N.lib().bcnf_linear_work_bytes(rows, k, n))
+            work = torch.empty(max(wb // 4, 1), dtype=torch.float32, device=x.device)
+        N.check(N.lib().bcnf_linear_backward(N.ptr(x), N.ptr(weight), N.ptr(dy), rows, k, n, N.ptr(dx), N.ptr(dw),
+                                             N.ptr(db), N.ptr(work), N.stream_handle(x.device)),
+                "bcnf_linear_backward")
+        return dx, (dw if need_w else None), db
+
+
+class HIPLinear(nn.Linear):
+    """nn.Linear (same parameters / state_dict keys) whose fp32 GPU forward and backward run on the
+    library's MFMA GEMM kernels; other devices / dtypes use torch's own linear."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and self.weight.dtype == torch.float32:
+            return _LinearFn.apply(x.contiguous(), self.weight, self.bias)
+        return super().forward(x)
+
+
 class FeatureNetwork(nn.Module):
     input_size: int
     output_size: int
@@ -53,13 +99,13 @@ class FullyConnectedFeatureNetwork(FeatureNetwork):
             self.nn.append(nn.Identity())
             return
         for a, b in zip(sizes[:-2], sizes[1:-1]):
-            self.nn.append(nn.Linear(a, b))
+            self.nn.append(HIPLinear(a, b))
             if batch_norm:
                 self.nn.append(nn.BatchNorm1d(b))
             self.nn.append(activation())
             if dropout > 0.0:
                 self.nn.append(nn.Dropout(dropout))
-        self.nn.append(nn.Linear(sizes[-2], sizes[-1]))
+        self.nn.append(HIPLinear(sizes[-2], sizes[-1]))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return self.nn(x.view(x.size(0), -1))

@@ -261,6 +261,74 @@ class FusedStack:
             tm.setdefault("k_reduce", []).append((e1, e2))
         return dy, dh, dparams
 
+    def sync_word(self):
+        """One zero-initialised uint32 of device memory for the kernels' last-workgroup handshake."""
+        if getattr(self, "_sync", None) is None or self._sync.device != self.flat.device:
+            self._sync = torch.zeros(1, dtype=torch.int32, device=self.flat.device)
+        return self._sync
+
+    def launch_nll_forward(self, y, h, training: bool):
+        """Stack forward fused with inn_nll_loss (trainer.py:260-266): returns z, ldj, vals=[loss, nll, mse]
+        and the saved state for launch_nll_backward. The kernel itself advances the dropout RNG offset."""
+        self._check_inputs(y, h, "forward")
+        if h.shape[0] != y.shape[0]:
+            raise ValueError(f"bcnf_amd forward: {y.shape[0]} samples but {h.shape[0]} feature rows")
+        B = y.shape[0]
+        if B == 0:
+            raise ValueError("bcnf_amd: the NLL of an empty batch is undefined")
+        dev = y.device
+        z = torch.empty_like(y)
+        ldj = torch.empty(B, dtype=torch.float32, device=dev)
+        vals = torch.empty(3, dtype=torch.float32, device=dev)
+        drop = training and self.cfg.dropout > 0.0
+        rng = self.rng_state() if drop else None
+        wb, _ = self.workspace_bytes(B, training)
+        ws = torch.empty(max(wb // 4, 1), dtype=torch.float32, device=dev)
+        pk = self.packed(fresh=True)
+        tm = self.timers
+        if tm is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        rc = N.lib().bcnf_nll_forward(self._pdesc, N.ptr(pk), N.ptr(y), N.ptr(h), ctypes.c_int64(B), N.ptr(z),
+                                      N.ptr(ldj), ctypes.c_int32(int(training)), N.ptr(rng), N.ptr(ws),
+                                      N.ptr(self.sync_word()), N.ptr(vals), N.stream_handle(dev))
+        N.check(rc, "bcnf_nll_forward")
+        if tm is not None:
+            e1.record()
+            tm.setdefault("k_forward", []).append((e0, e1))
+        return z, ldj, vals, (ws, pk)
+
+    def launch_nll_backward(self, h, z, dvals, training: bool, saved, want_dy: bool, want_dh: bool):
+        ws, pk = saved
+        B = h.shape[0]
+        dev = h.device
+        _, sb = self.workspace_bytes(B, training)
+        slab = torch.empty(max(sb // 4, 1), dtype=torch.float32, device=dev)
+        dparams = torch.empty_like(self.flat)
+        dh = torch.empty_like(h) if want_dh else None
+        dy = torch.empty((B, self.cfg.size), dtype=torch.float32, device=dev) if want_dy else None
+        stream = N.stream_handle(dev)
+        tm = self.timers
+        if tm is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e2 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        rc = N.lib().bcnf_nll_backward(self._pdesc, N.ptr(pk), N.ptr(h), N.ptr(z), N.ptr(dvals), ctypes.c_int64(B),
+                                       ctypes.c_int32(int(training)), N.ptr(ws), N.ptr(dy), N.ptr(dh), None,
+                                       N.ptr(slab), stream)
+        N.check(rc, "bcnf_nll_backward")
+        if tm is not None:
+            e1.record()
+        N.check(N.lib().bcnf_grad_reduce(self._pdesc, N.ptr(slab), ctypes.c_int64(B), N.ptr(dparams), stream),
+                "bcnf_grad_reduce")
+        if tm is not None:
+            e2.record()
+            tm.setdefault("k_backward", []).append((e0, e1))
+            tm.setdefault("k_reduce", []).append((e1, e2))
+        return dy, dh, dparams
+
     def launch_inverse(self, z, h, cond_index=None, training: bool = False):
         self._check_inputs(z, h, "inverse")
         n = z.shape[0]
@@ -306,6 +374,40 @@ class _StackForward(torch.autograd.Function):
         need_y, need_h, need_p = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
         dy, dh, dparams = stack.launch_backward(h, dz, dldj, ctx.training, ctx.saved, want_dy=need_y, want_dh=need_h)
         return dy, dh, (dparams if need_p else None), None, None
+
+
+class _StackNLL(torch.autograd.Function):
+    """vals = [loss, nll, mse] of inn_nll_loss(stack(y, h)) in one fused launch; backward is the fused NLL
+    backward (no dz / dldj tensors, no elementwise loss kernels)."""
+
+    @staticmethod
+    def forward(ctx, y, h, flat_param, stack: FusedStack, training: bool):
+        z, _, vals, saved = stack.launch_nll_forward(y, h, training)
+        ctx.stack = stack
+        ctx.training = training
+        ctx.saved = saved
+        ctx.save_for_backward(h, z)
+        return vals
+
+    @staticmethod
+    def backward(ctx, dvals):
+        h, z = ctx.saved_tensors
+        need_y, need_h, need_p = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        dy, dh, dparams = ctx.stack.launch_nll_backward(h, z, dvals.contiguous(), ctx.training, ctx.saved,
+                                                        want_dy=need_y, want_dh=need_h)
+        return dy, dh, (dparams if need_p else None), None, None
+
+
+def stack_nll(stack: FusedStack, y, h, training: bool):
+    """[loss, nll, mse] (mse = 0, hybrid_weight = 0) of the Trainer's loss on the fused stack."""
+    y = y.contiguous()
+    h = h.contiguous()
+    stack.sync_grad_state()
+    params_grad = stack.trainable[0].requires_grad
+    fp = stack.flat_param
+    if torch.is_grad_enabled() and (params_grad or y.requires_grad or h.requires_grad):
+        return _StackNLL.apply(y, h, fp if params_grad else fp.detach(), stack, training)
+    return stack.launch_nll_forward(y, h, training)[2]
 
 
 class _StackInverse(torch.autograd.Function):

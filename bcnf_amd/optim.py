@@ -1,0 +1,125 @@
+"""Optimizer step and gradient clipping of the bcnf Trainer on the library's HIP kernels.
+
+The Trainer builds `torch.optim.Adam(model.parameters(), lr=...)` (src/bcnf/train/trainer.py:136) and,
+after every `optimizer.step()`, calls `torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)`
+(trainer.py:270-272). With the coupling stack held in one flat buffer (CondRealNVP_v2.flat_parameters())
+torch's multi-tensor kernels see a handful of large tensors and parallelise poorly (one workgroup per
+64 K-element chunk); `FusedAdam` runs the whole update as ONE launch over the concatenated index space
+and emits the per-workgroup sums of squared gradients in the same pass, so the clip that follows is a
+single further launch (`clip_grad_norm_after_step`).
+
+Semantics are torch.optim.Adam's (amsgrad = maximize = False, optional L2 weight decay) with the step
+count kept on the device (as Adam(capturable=True) does), so the step is HIP-graph capturable.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from bcnf_amd import _native as N
+
+
+def _groups(tensors, limit=N.MAX_TENSORS):
+    for i in range(0, len(tensors), limit):
+        yield tensors[i:i + limit]
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0):
+        if lr < 0.0 or eps < 0.0 or weight_decay < 0.0:
+            raise ValueError("invalid Adam hyper-parameter")
+        super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay))
+        self._partials = None      # per-workgroup sum(g^2) of the last step, consumed by the clip
+        self._partials_for = None
+        self._sync = None
+
+    def _state(self, p):
+        st = self.state[p]
+        if len(st) == 0:
+            st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        return st
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        L = N.lib()
+        all_grads = []
+        for group in self.param_groups:
+            params = [p for p in group["params"] if p.grad is not None]
+            if not params:
+                continue
+            for p in params:
+                if not p.is_cuda or p.dtype != torch.float32 or not p.is_contiguous() or not p.grad.is_contiguous():
+                    raise RuntimeError("bcnf_amd FusedAdam: parameters and grads must be contiguous fp32 GPU tensors")
+            b1, b2 = group["betas"]
+            dev = params[0].device
+            if self._sync is None or self._sync.device != dev:
+                self._sync = torch.zeros(1, dtype=torch.int32, device=dev)
+            for chunk in _groups(params):
+                states = [self._state(p) for p in chunk]
+                step = states[0]["step"]
+                for st in states[1:]:                  # one shared device step per launch
+                    if st["step"] is not step:
+                        st["step"] = step
+                grads = [p.grad for p in chunk]
+                numel = N.i64_array([p.numel() for p in chunk])
+                total = sum(p.numel() for p in chunk)
+                part = torch.empty(int(L.bcnf_grad_partials(total)), dtype=torch.float32, device=dev)
+                rc = L.bcnf_adam_step(len(chunk), N.ptr_array(chunk), N.ptr_array(grads),
+                                      N.ptr_array([s["exp_avg"] for s in states]),
+                                      N.ptr_array([s["exp_avg_sq"] for s in states]), numel, N.ptr(step),
+                                      ctypes.c_double(group["lr"]), ctypes.c_double(b1), ctypes.c_double(b2),
+                                      ctypes.c_double(group["eps"]), ctypes.c_double(group["weight_decay"]),
+                                      N.ptr(part), N.ptr(self._sync), N.stream_handle(dev))
+                N.check(rc, "bcnf_adam_step")
+                all_grads.append((chunk, grads, numel, part))
+        self._partials = all_grads
+        self._partials_for = [p for chunk, _, _, _ in all_grads for p in chunk]
+        return loss
+
+    @torch.no_grad()
+    def clip_grad_norm_after_step(self, max_norm: float = 1.0):
+        """clip_grad_norm_(params, max_norm) for exactly the gradients the last step() consumed (unchanged
+        since), reusing that step's squared-gradient partials. Returns the pre-clip total norm (device)."""
+        if not self._partials:
+            raise RuntimeError("bcnf_amd FusedAdam: clip_grad_norm_after_step() needs a preceding step()")
+        if len(self._partials) != 1:   # several launches: recompute the norm over all of them
+            return clip_grad_norm_(self._partials_for, max_norm)
+        _, grads, numel, part = self._partials[0]
+        dev = grads[0].device
+        norm = torch.empty((), dtype=torch.float32, device=dev)
+        rc = N.lib().bcnf_clip_grad_norm(len(grads), N.ptr_array(grads), numel, N.ptr(part),
+                                         ctypes.c_float(max_norm), N.ptr(norm), N.stream_handle(dev))
+        N.check(rc, "bcnf_clip_grad_norm")
+        return norm
+
+
+@torch.no_grad()
+def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0):
+    """torch.nn.utils.clip_grad_norm_ (2-norm) on the HIP kernels. Returns the total norm (device scalar)."""
+    if norm_type != 2.0:
+        raise NotImplementedError("bcnf_amd clip_grad_norm_: only the 2-norm (the Trainer's) is implemented")
+    if isinstance(parameters, torch.Tensor):
+        parameters = [parameters]
+    grads = [p.grad for p in parameters if p.grad is not None]
+    if not grads:
+        return torch.zeros(())
+    if len(grads) > N.MAX_TENSORS:
+        raise NotImplementedError(f"bcnf_amd clip_grad_norm_: at most {N.MAX_TENSORS} tensors per call")
+    L = N.lib()
+    dev = grads[0].device
+    numel = N.i64_array([g.numel() for g in grads])
+    total = sum(g.numel() for g in grads)
+    part = torch.empty(int(L.bcnf_grad_partials(total)), dtype=torch.float32, device=dev)
+    stream = N.stream_handle(dev)
+    N.check(L.bcnf_grad_sumsq(len(grads), N.ptr_array(grads), numel, N.ptr(part), stream), "bcnf_grad_sumsq")
+    norm = torch.empty((), dtype=torch.float32, device=dev)
+    N.check(L.bcnf_clip_grad_norm(len(grads), N.ptr_array(grads), numel, N.ptr(part), ctypes.c_float(max_norm),
+                                  N.ptr(norm), stream), "bcnf_clip_grad_norm")
+    return norm

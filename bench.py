@@ -1,9 +1,10 @@
 """Benchmark: NLL-training samples/s of CondRealNVP_v2 trajectory_FC_small (B=4096 per GPU) on MI355X.
 
-One step = bcnf.train.Trainer._train_batch semantics (src/bcnf/train/trainer.py:244-277): zero_grad,
-forward(log_det_J, return_features) [FC feature net in PyTorch-ROCm + fused HIP coupling stack], NLL,
-backward [fused HIP backward + deterministic reduce + feature-net autograd], (N>1: RCCL all-reduce of the
-flat gradient), Adam step, clip_grad_norm_ after the step, one host sync for the logged losses.
+One step = bcnf.train.Trainer._train_batch semantics (src/bcnf/train/trainer.py:244-277): batch gather
+from the device-resident pool, zero_grad, forward [FC feature net Linear on the HIP GEMM + fused coupling
+stack with the NLL in the same launch], backward [fused NLL backward + deterministic slab reduce + Linear
+weight-gradient GEMM], (N>1: RCCL all-reduce of the gradients), Adam step (one fused launch), clip_grad_norm_
+after the step, one host sync for the three logged losses. The step is one HIP-graph replay.
 Synthetic ballistic trajectories (bcnf_amd/data.py), device-resident, pre-shuffled; dropout active.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]    (N>1: launched by torch.distributed.run)
@@ -122,15 +123,15 @@ def cpu_baseline(args):
 def kernel_timing(model, data, args):
     """Average device time of each fused kernel, measured with HIP events on the launch stream over
     `kernel_iters` eager training forward/backward passes."""
-    from bcnf_amd import inn_nll_loss
     st = model.fused
     st.timers = {}
+    cot = torch.tensor([1.0, 0.0, 0.0], device=data.y.device)
     for _ in range(args.kernel_iters):
         idx = data.next_indices()
         y, traj = data.y[idx], data.traj[idx]
         model.zero_grad(set_to_none=True)
-        z = model(y, traj, log_det_J=True)
-        inn_nll_loss(z, model.log_det_J).backward()
+        st.flat_param.grad = None
+        torch.autograd.backward(model.nll_loss(y, traj), cot)
     torch.cuda.synchronize()
     out = {}
     for name, pairs in st.timers.items():
@@ -156,10 +157,10 @@ def main():
     data = DeviceBatches(65536, args.batch, device, seed=2024_03_25 + rank)
     step = TrainStep(model, lr=2e-4, capture=not args.no_graph)
     step.broadcast_parameters()
+    step.set_pool(data.y, data.traj)
 
     for _ in range(args.warmup):
-        idx = data.next_indices()
-        step.step(data.y[idx], data.traj[idx])
+        step.step_indexed(data.next_indices())
     batches = [data.next_indices() for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
@@ -167,7 +168,7 @@ def main():
     t0 = time.perf_counter()
     losses = None
     for idx in batches:
-        losses = step.step(data.y[idx], data.traj[idx])
+        losses = step.step_indexed(idx)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -22,6 +22,14 @@
  *                           conditions (cnf.py:577-582) without materialising the tiled features
  *   bcnf_pack_params     <- (no reference counterpart) re-lays the nn.Module parameters into the
  *                           kernels' LDS-record layout; call after every parameter update
+ *   bcnf_nll_forward     <- Trainer._train_batch forward + loss, trainer.py:260-266: the stack forward
+ *                           fused with inn_nll_loss(z, log_det_J) (utils.py:40-46, reduction 'mean')
+ *   bcnf_nll_backward    <- loss.backward() of that loss through the stack (trainer.py:268)
+ *   bcnf_adam_step       <- optimizer.step() of torch.optim.Adam built by the Trainer (trainer.py:136,270)
+ *   bcnf_clip_grad_norm  <- torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)
+ *                           (trainer.py:272, after the step)
+ *   bcnf_linear_forward / bcnf_linear_backward
+ *                        <- nn.Linear of FullyConnectedFeatureNetwork (feature_network.py:114-145)
  */
 #ifndef BCNF_AMD_H
 #define BCNF_AMD_H
@@ -33,6 +41,7 @@ extern "C" {
 #endif
 
 #define BCNF_MAX_HIDDEN 8
+#define BCNF_MAX_TENSORS 16
 
 enum {
   BCNF_OK = 0,
@@ -63,7 +72,8 @@ int bcnf_param_count(const BcnfStackDesc* desc, int64_t* n_trainable, int64_t* n
 /* Bytes of the packed-parameter buffer written by bcnf_pack_params. */
 int bcnf_packed_bytes(const BcnfStackDesc* desc, int64_t* bytes);
 
-/* Bytes of the forward->backward workspace (saved block inputs + dropout masks) for a batch. */
+/* Bytes of the forward->backward workspace (saved block inputs + dropout masks + per-workgroup
+ * loss partials) for a batch. */
 int bcnf_workspace_bytes(const BcnfStackDesc* desc, int64_t batch, int32_t training, int64_t* bytes);
 
 /* Bytes of the per-workgroup gradient slab used by bcnf_stack_backward for a batch. */
@@ -100,6 +110,60 @@ int bcnf_grad_reduce(const BcnfStackDesc* desc, const void* slab, int64_t batch,
 int bcnf_stack_inverse(const BcnfStackDesc* desc, const void* packed, const float* z, const float* h,
                        const int64_t* cond_index, int64_t n_rows, float* y, int32_t training,
                        const uint64_t* rng_state, void* stream);
+
+/* ---- NLL training pass (forward + inn_nll_loss + backward without any host round trip) ---------
+ * bcnf_nll_forward = bcnf_stack_forward (workspace required) plus, in the same launch,
+ *   loss_out[0] = loss = (nll + 0 * mse) / (1 + 0), loss_out[1] = nll = mean_b(0.5 |z_b|^2 - ldj_b),
+ *   loss_out[2] = mse = 0            (the Trainer's three logged values with hybrid_weight == 0)
+ * The last workgroup to finish reduces the per-workgroup partials in a fixed order and, when dropout
+ * is active, advances rng_state[1] by one (so graph replays draw fresh masks). `sync` is one uint32 of
+ * device memory that must be zero before the first call; every call leaves it zero. */
+int bcnf_nll_forward(const BcnfStackDesc* desc, const void* packed, const float* y, const float* h, int64_t batch,
+                     float* z, float* ldj, int32_t training, uint64_t* rng_state, void* workspace, uint32_t* sync,
+                     float* loss_out, void* stream);
+
+/* Backward through loss_out w.r.t. y, h and the stack parameters: dz = z * g / B, dldj = -g / B with
+ * g = dloss[0] + dloss[1], dloss being the device cotangent of loss_out[0..2] (NULL means d loss = 1,
+ * i.e. loss.backward(); mse carries no gradient). z is the forward's output. Otherwise as
+ * bcnf_stack_backward. */
+int bcnf_nll_backward(const BcnfStackDesc* desc, const void* packed, const float* h, const float* z,
+                      const float* dloss, int64_t batch, int32_t training, const void* workspace, float* dy,
+                      float* dh, float* dparams, void* slab, void* stream);
+
+/* ---- Optimizer ------------------------------------------------------------------------------------
+ * Tensors are passed as arrays of n_tensors (<= BCNF_MAX_TENSORS) device pointers + element counts and
+ * treated as one concatenated index space. bcnf_grad_partials(total) = number of per-workgroup partial
+ * sums of squared gradients the kernels below write / read. */
+int64_t bcnf_grad_partials(int64_t total_numel);
+
+/* One torch.optim.Adam step (amsgrad = maximize = False) over every tensor; hyper-parameters are
+ * doubles (derived scalars such as 1 - beta2 are formed in double and rounded once, as torch does);
+ * `step` is the device-side
+ * float step count (incremented by the call, as Adam(capturable=True) keeps it). With grad_partials !=
+ * NULL it also writes the per-workgroup sums of squared gradients for bcnf_clip_grad_norm. `sync`: one
+ * zero-initialised uint32 of device memory (left zero). */
+int bcnf_adam_step(int32_t n_tensors, float* const* params, float* const* grads, float* const* exp_avg,
+                   float* const* exp_avg_sq, const int64_t* numel, float* step, double lr, double beta1,
+                   double beta2, double eps, double weight_decay, float* grad_partials, uint32_t* sync,
+                   void* stream);
+
+/* Per-workgroup sums of squared gradients (when no bcnf_adam_step produced them). */
+int bcnf_grad_sumsq(int32_t n_tensors, float* const* grads, const int64_t* numel, float* grad_partials, void* stream);
+
+/* clip_grad_norm_(max_norm, norm_type=2): total = sqrt(sum partials); g *= min(max_norm/(total+1e-6), 1).
+ * total_norm (device float, nullable) receives the pre-clip norm. */
+int bcnf_clip_grad_norm(int32_t n_tensors, float* const* grads, const int64_t* numel, const float* grad_partials,
+                        float max_norm, float* total_norm, void* stream);
+
+/* ---- nn.Linear (row-major, weight out_features x in_features) ------------------------------------ */
+int bcnf_linear_forward(const float* x, const float* weight, const float* bias, int64_t rows, int32_t in_features,
+                        int32_t out_features, float* y, void* stream);
+/* Scratch bytes bcnf_linear_backward needs for its split-K weight gradient. */
+int64_t bcnf_linear_work_bytes(int64_t rows, int32_t in_features, int32_t out_features);
+/* dx (nullable) = dy W; dweight = dy^T x and dbias (nullable) = column sums of dy, both overwritten
+ * (fixed-order split-K reduction through `work`). dweight may be NULL only when dbias is NULL too. */
+int bcnf_linear_backward(const float* x, const float* weight, const float* dy, int64_t rows, int32_t in_features,
+                         int32_t out_features, float* dx, float* dweight, float* dbias, void* work, void* stream);
 
 const char* bcnf_status_string(int status);
 int bcnf_last_hip_error(void);

@@ -14,7 +14,7 @@ HEADER = os.path.join(ROOT, "include", "bcnf_amd.h")
 
 def header_functions():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(bcnf_\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t|const char\*)\s+(bcnf_\w+)\s*\(", src, flags=re.M)))
 
 
 def test_library_exports_every_header_symbol():
@@ -43,7 +43,7 @@ def test_layout_queries_match_module_tree():
     assert m.fused.supported
     d = m.fused.desc
     ws = N.query_i64(N.lib().bcnf_workspace_bytes, ctypes.byref(d), ctypes.c_int64(4096), ctypes.c_int32(1))
-    assert ws == 32 * 4096 * 32 * 4 + 8 * 4096 * 16 * 4
+    assert ws == 32 * 4096 * 32 * 4 + 8 * 4096 * 16 * 4 + 256 * 4   # inputs, masks, loss partials
     sb = N.query_i64(N.lib().bcnf_slab_bytes, ctypes.byref(d), ctypes.c_int64(4096))
     assert sb == 256 * ((109786 + 3) // 4 * 4) * 4
 
