@@ -15,7 +15,7 @@ import threading
 import torch  # noqa: F401  (must precede loading the HIP library)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libbcnf_amd.so")
+LIB_PATH = os.environ.get("BCNF_AMD_LIB") or os.path.join(_HERE, "libbcnf_amd.so")   # override: A/B experiments
 
 MAX_HIDDEN = 8
 

@@ -20,6 +20,13 @@
 
 #include <mutex>
 
+// Experiment switches for A/B timing only (tools/exp_variants.sh builds separate libraries; results of a
+// nonzero BCNF_EXP are NOT valid): 1 = records read by row 0 only, 2 = no slab stores, 4 = no MFMA
+// gradient phase, 8 = no dropout RNG in the forward.
+#ifndef BCNF_EXP
+#define BCNF_EXP 0
+#endif
+
 namespace bcnf_rt {
 thread_local int last_hip = 0;
 }
@@ -70,6 +77,7 @@ int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
   L->an_size = L->act_norm ? 2 * L->D : 0;
   L->blk_stride = L->an_size + off;
   L->n_trainable = (L->nb - 1) * L->blk_stride + off;
+  L->blk_pad = (L->blk_stride + 3) & ~3;
   L->p = d->dropout;
   L->keep_scale = (d->dropout > 0.f) ? (1.0f / (1.0f - d->dropout)) : 1.0f;
   double t = (double)d->dropout * 65536.0;
@@ -106,8 +114,12 @@ size_t fwd_lds_bytes(const BcnfLayout& L) {   // rec ring 2, W1h^T ring 2, HP pa
 size_t bwd_lds_bytes(const BcnfLayout& L) {   // F/B rec rings 2, W1h^T ring 4, HP 2, tiles 2, features
   const int NT = 2 * L.NH + NT_EXTRA;
   return sizeof(float) * (size_t)(2 * 16 * L.RF + 2 * 16 * L.RB + 4 * L.Cp * 17 + 2 * 1024 + 2 * NT * TILE +
-                                  TILE + 8 * (2 * BCNF_MAX_HIDDEN + 8 + 16) + 16 * (L.Cp + 1));
+                                  8 * (2 * (BCNF_MAX_HIDDEN + 2) + 4 + 1) + 16 * (L.Cp + 1) + L.blk_pad + 64);
 }
+// float4 stores per thread that copy one block's gradient partials from LDS to the slab (fixed count:
+// the compiler's vmcnt bookkeeping then never has to over-wait on them)
+constexpr int COPY4_MAX = 8;
+int copy4_of(const BcnfLayout& L) { return (L.blk_pad / 4 + BCNF_WG - 1) / BCNF_WG <= 4 ? 4 : 8; }
 constexpr size_t LDS_MAX = 160 * 1024;
 
 bool layout_supported(const BcnfLayout& L, const BcnfStackDesc* d) {
@@ -119,6 +131,7 @@ bool layout_supported(const BcnfLayout& L, const BcnfStackDesc* d) {
   if (L.C < 1 || L.Cp > 256) return false;
   if (16 * L.RF > 4 * 4 * BCNF_WG || 16 * L.RB > 4 * 4 * BCNF_WG || L.Cp * 17 > 5 * 4 * BCNF_WG) return false;
   if (fwd_lds_bytes(L) > LDS_MAX || bwd_lds_bytes(L) > LDS_MAX) return false;
+  if (L.blk_pad / 4 > COPY4_MAX * BCNF_WG) return false;
   return true;
 }
 
@@ -368,6 +381,17 @@ __device__ __forceinline__ void ld_rec(float* __restrict__ rr, const float* __re
   }
 }
 
+template <int LO, int HI>
+__device__ __forceinline__ void ld_rec_exp(float* __restrict__ rr, const float* __restrict__ R) {
+  if (BCNF_EXP & 1) {
+#pragma unroll
+    for (int i = LO; i < HI; ++i) rr[i] = 0.f;
+    if ((threadIdx.x & 48) == 0) ld_rec<LO, HI>(rr, R);
+  } else {
+    ld_rec<LO, HI>(rr, R);
+  }
+}
+
 // Nested MLP forward on the row layout (cnf.py:98-107) from a register-resident forward record.
 // Input x (layer-1 y-part operand); returns t and s' (pre-tanh). KEEP: also the (masked) activations
 // and masked GELU derivatives for the backward.
@@ -467,7 +491,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
     hp_quarter(L, wt + (cur ^ 1) * WTL, ht, hpb + (cur ^ 1) * 1024);
 
     float rr[RecF<NH>::USED];
-    ld_rec<0, RecF<NH>::USED>(rr, rec + cur * RFL + j * L.RF);
+    ld_rec_exp<0, RecF<NH>::USED>(rr, rec + cur * RFL + j * L.RF);
     if (SAVE) {
       float* ys = ysave + ((long long)k * B + bc) * 32;
       ys[j] = ya;
@@ -476,7 +500,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
     const float xa = fmaf(rr[0], ya, rr[1]);          // ActNorm (cnf.py:349)
     const float xb = fmaf(rr[2], yb, rr[3]);
     uint32_t bits = 0xffu;
-    if (DROP) bits = dropout_bits(L, seed, off, bc, k, j, 0u);
+    if (DROP && !(BCNF_EXP & 8)) bits = dropout_bits(L, seed, off, bc, k, j, 0u);
     float T, Sp;
     mlp_forward<NH, false>(L, rr, xa, hp_sum(hpb + cur * 1024, s, j), bits, DROP, T, Sp, nullptr, nullptr);
     const float S = tanh_bf(Sp);                      // cnf.py:107
@@ -628,130 +652,231 @@ struct BwdTiles {   // tile indices inside one tile buffer
   __device__ __forceinline__ int count() const { return 2 * NH + NT_EXTRA; }
 };
 
-// One gradient "chain" = 4 fp32 MFMAs over the workgroup's 16 samples:
-//   out[j][n] = sum_s A[s][j] * B[s][n],  A a [16][17] tile, B a [16][b_stride] LDS region (ones for
-//   bias / ActNorm sums, the feature tile for the W1 condition part), written to the workgroup's slab at
-//   base + j * row_stride + n for j < nrows, n < ncols. Built once per workgroup (no runtime indexing of
-//   the kernel-argument struct inside the loop, and no per-type branches).
-struct ChainDesc {
-  int a_off;       // A tile offset (floats) inside the tile buffer
-  int b_off;       // B offset: inside the tile buffer, or (flag B_ABS) inside smem
-  int b_stride;
-  int out_rel;     // slab offset relative to the block base (k * blk_stride)
-  int row_stride;
-  int nrows;
-  int ncols;
-  int flags;       // 1: coupling-relative (add an_size for blocks with ActNorm) 2: ActNorm chain 4: B_ABS
+// Gradient jobs of one block, built once per workgroup into LDS:
+//   W jobs   (NH + 2): dW of every Linear (the last one as its t and s row halves): 4 fp32 MFMAs over the
+//            workgroup's 16 samples, out[j][i] = sum_s delta[s][j] * act[s][i] ([16][17] LDS tiles)
+//   sum jobs (NH + 2 + 4): bias and ActNorm gradients = column sums of a tile over the 16 samples (VALU +
+//            two cross-row permlane swaps; no MFMA against a ones tile)
+//   cond job (1): geometry of the W1 condition part (MFMA against the feature tile, column tiles of 16)
+struct GradDesc {
+  int a_tile;   // float offset of the delta tile in the tile buffer
+  int b_tile;   // W jobs: offset of the activation tile; cond job: smem offset of the feature tile
+  int out;      // block-relative output offset of element (0, 0), coupling offset excluded
+  int rs;       // output row stride
+  int nrows;    // valid rows (W, cond) / valid elements (sum jobs)
+  int ncols;    // valid columns
+  int flags;    // 1: coupling-relative (add the ActNorm size for blocks that have one), 2: ActNorm job
+  int pad;
 };
-constexpr int CH_COUPLING = 1, CH_ACTNORM = 2, CH_BABS = 4;
-constexpr int MAX_CHAINS = 2 * BCNF_MAX_HIDDEN + 8 + 16;
+constexpr int GD_COUPLING = 1, GD_ACTNORM = 2;
+constexpr int MAX_JOBS = 2 * (BCNF_MAX_HIDDEN + 2) + 4 + 1;
 
 template <int NH>
-__device__ void build_chains(const BcnfLayout& L, ChainDesc* cd, int ones_abs, int ht_abs) {
+__device__ void build_jobs(const BcnfLayout& L, GradDesc* gd, int ht_abs) {
   const BwdTiles TI{NH};
-  const int NC16 = L.Cp >> 4;
-  const int n_chains = 2 * NH + 8 + NC16;
-  for (int c = threadIdx.x; c < n_chains; c += BCNF_WG) {
-    ChainDesc d;
-    d.b_stride = BCNF_TSTRIDE;
-    d.flags = CH_COUPLING;
-    if (c < NH + 2) {                                   // weight gradients of Linear l / output t, s rows
+  constexpr int NW = NH + 2, NS = NH + 6;
+  for (int c = threadIdx.x; c < NW + NS + 1; c += BCNF_WG) {
+    GradDesc d;
+    d.pad = 0;
+    d.flags = GD_COUPLING;
+    d.b_tile = 0;
+    d.rs = 1;
+    d.ncols = 16;
+    if (c < NW) {                                         // dW of Linear l (t rows, s rows for l = NH + 1)
       const int l = (c < NH) ? c + 1 : NH + 1;
-      d.a_off = TILE * ((c < NH) ? TI.D(l) : (c == NH ? TI.DT() : TI.DS()));
-      d.b_off = TILE * ((c < NH) ? TI.A(l - 1) : TI.A(NH));
+      d.a_tile = TILE * ((c < NH) ? TI.D(l) : (c == NH ? TI.DT() : TI.DS()));
+      d.b_tile = TILE * ((c < NH) ? TI.A(l - 1) : TI.A(NH));
       const int row0 = (c == NH + 1) ? L.Db : 0;
-      d.out_rel = L.lin_w[l] + row0 * L.lin_in[l];
-      d.row_stride = L.lin_in[l];
+      d.out = L.lin_w[l] + row0 * L.lin_in[l];
+      d.rs = L.lin_in[l];
       d.nrows = (c < NH) ? L.H[l] : L.Db;
       d.ncols = (l == 1) ? L.Da : L.H[l - 1];
-    } else if (c < 2 * NH + 4) {                        // bias gradients (B = ones)
-      const int cc = c - (NH + 2);
+    } else if (c < NW + NH + 2) {                         // bias of Linear l (t half, s half)
+      const int cc = c - NW;
       const int l = (cc < NH) ? cc + 1 : NH + 1;
-      d.a_off = TILE * ((cc < NH) ? TI.D(l) : (cc == NH ? TI.DT() : TI.DS()));
-      d.b_off = ones_abs;
-      d.flags |= CH_BABS;
-      d.out_rel = L.lin_b[l] + ((cc == NH + 1) ? L.Db : 0);
-      d.row_stride = 1;
+      d.a_tile = TILE * ((cc < NH) ? TI.D(l) : (cc == NH ? TI.DT() : TI.DS()));
+      d.out = L.lin_b[l] + ((cc == NH + 1) ? L.Db : 0);
       d.nrows = (cc < NH) ? L.H[l] : L.Db;
-      d.ncols = 1;
-    } else if (c < 2 * NH + 8) {                        // ActNorm scale / bias (B = ones)
-      const int a = c - (2 * NH + 4);                   // 0: scale_a 1: bias_a 2: scale_b 3: bias_b
-      d.a_off = TILE * ((a == 0) ? TI.PA() : (a == 1 ? TI.GA() : (a == 2 ? TI.PB() : TI.GB())));
-      d.b_off = ones_abs;
-      d.flags = CH_ACTNORM | CH_BABS;
-      d.out_rel = ((a & 1) ? L.D : 0) + ((a < 2) ? 0 : L.Da);
-      d.row_stride = 1;
+    } else if (c < NW + NS) {                             // ActNorm scale_a, bias_a, scale_b, bias_b
+      const int a = c - (NW + NH + 2);
+      d.a_tile = TILE * ((a == 0) ? TI.PA() : (a == 1 ? TI.GA() : (a == 2 ? TI.PB() : TI.GB())));
+      d.flags = GD_ACTNORM;
+      d.out = ((a & 1) ? L.D : 0) + ((a < 2) ? 0 : L.Da);
       d.nrows = (a < 2) ? L.Da : L.Db;
-      d.ncols = 1;
-    } else {                                            // W1 condition part: B = feature tile columns
-      const int n = c - (2 * NH + 8);
-      d.a_off = TILE * TI.D(1);
-      d.b_off = ht_abs + 16 * n;
-      d.b_stride = L.Cp + 1;
-      d.flags |= CH_BABS;
-      d.out_rel = L.lin_w[1] + L.Da + 16 * n;
-      d.row_stride = L.lin_in[1];
+    } else {                                              // W1 condition part
+      d.a_tile = TILE * TI.D(1);
+      d.b_tile = ht_abs;
+      d.out = L.lin_w[1] + L.Da;
+      d.rs = L.lin_in[1];
       d.nrows = L.H[1];
-      d.ncols = min(16, L.C - 16 * n);
     }
-    cd[c] = d;
+    gd[c] = d;
   }
 }
 
+// Sum of v over the 4 rows (16-lane groups) of the wave, returned in every lane (gfx950 permlane swaps:
+// the two results of each swap are the row pairs, so adding them is the pairwise sum whatever the order).
+__device__ __forceinline__ float sum_rows4(float v) {
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  const auto p2 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(p2[0]) + __uint_as_float(p2[1]);
+}
+
+// MFMA phase of one block: every parameter gradient of block m into the LDS gradient block `gbuf`, and
+// the block's dh contribution into dhacc. Masked-off lanes store into a private dummy slot
+// (gbuf[blk_pad + lane]) so no store needs an exec-mask branch.
 template <int NH>
 __device__ __forceinline__ void bwd_mfma_phase(const BcnfLayout& L, const float* __restrict__ smem,
-                                               const float* __restrict__ T, const ChainDesc* __restrict__ cd,
-                                               const float* __restrict__ wtm, float* __restrict__ slab, int m,
+                                               const float* __restrict__ T, const GradDesc* __restrict__ gd,
+                                               const float* __restrict__ wtm, float* __restrict__ gbuf, int m,
                                                floatx4* dhacc) {
   const BwdTiles TI{NH};
-  const int wave = threadIdx.x >> 6, l64 = threadIdx.x & 63, q = l64 >> 4, r = l64 & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l64 = threadIdx.x & 63, q = l64 >> 4, r = l64 & 15;
   const int NC16 = L.Cp >> 4;
-  const int n_chains = 2 * NH + 8 + NC16;
-  const int blk = m * L.blk_stride;
+  constexpr int NW = NH + 2, NS = NH + 6;
+  constexpr int UW = (NW + 3) / 4, US = (NS + 3) / 4;
   const bool has_an = L.act_norm && m < L.nb - 1;
   const int cpl = has_an ? L.an_size : 0;
-  for (int c = wave; c < n_chains; c += 4) {
-    const ChainDesc d = cd[c];
-    const float* A = T + d.a_off;
-    const float* Bm = ((d.flags & CH_BABS) ? smem : T) + d.b_off;
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    float a[4], bv[4];
+  float* dummy = gbuf + L.blk_pad + l64;
+  // ---- weight gradients (MFMA), all operand reads first, independent chains interleaved
+  {
+    GradDesc d[UW];
+    float a[UW][4], bv[UW][4];
+    floatx4 acc[UW];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      a[t] = A[(4 * t + q) * BCNF_TSTRIDE + r];
-      bv[t] = Bm[(4 * t + q) * d.b_stride + r];
+    for (int u = 0; u < UW; ++u) {
+      const int c = wave + 4 * u;
+      d[u] = gd[c < NW ? c : NW - 1];
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc = mfma4(a[t], bv[t], acc);
-    const int nrows = ((d.flags & CH_ACTNORM) && !has_an) ? 0 : d.nrows;
-    const int base = blk + d.out_rel + ((d.flags & CH_COUPLING) ? cpl : 0);
-    if (r < d.ncols) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (4 * q + i < nrows) slab[base + (4 * q + i) * d.row_stride + r] = acc[i];
-    }
-  }
-  // dh[s][c] += sum_j D1[s][j] W1h_m[j][c]   (wave w owns column tiles n = w, w+4, ...)
-  const float* D1 = T + TI.D(1) * TILE;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int n = wave + 4 * u;
-    if (n < NC16) {
-      floatx4 acc = dhacc[u];
-      float a[4], bv[4];
+    for (int u = 0; u < UW; ++u) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        a[t] = D1[r * BCNF_TSTRIDE + 4 * t + q];
-        bv[t] = wtm[(16 * n + r) * 17 + 4 * t + q];
+        a[u][t] = T[d[u].a_tile + (4 * t + q) * BCNF_TSTRIDE + r];
+        bv[u][t] = T[d[u].b_tile + (4 * t + q) * BCNF_TSTRIDE + r];
       }
+      acc[u] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc = mfma4(a[t], bv[t], acc);
-      dhacc[u] = acc;
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int u = 0; u < UW; ++u) acc[u] = mfma4(a[u][t], bv[u][t], acc[u]);
+#pragma unroll
+    for (int u = 0; u < UW; ++u) {
+      if (wave + 4 * u >= NW) continue;                   // wave-uniform
+      const int base = d[u].out + cpl + __mul24(4 * q, d[u].rs) + r;
+      const bool colok = r < d[u].ncols;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool ok = colok && (4 * q + i < d[u].nrows) && !(BCNF_EXP & 2);
+        *(ok ? gbuf + base + i * d[u].rs : dummy) = acc[u][i];
+      }
+    }
+  }
+  // ---- bias / ActNorm gradients: column sums over the 16 samples (VALU)
+  {
+    GradDesc e[US];
+    float v[US][4];
+#pragma unroll
+    for (int u = 0; u < US; ++u) {
+      const int c = wave + 4 * u;
+      e[u] = gd[NW + (c < NS ? c : NS - 1)];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) v[u][t] = T[e[u].a_tile + (4 * t + q) * BCNF_TSTRIDE + r];
+    }
+#pragma unroll
+    for (int u = 0; u < US; ++u) {
+      if (wave + 4 * u >= NS) continue;                   // wave-uniform
+      const float tot = sum_rows4((v[u][0] + v[u][1]) + (v[u][2] + v[u][3]));
+      const bool live = !(e[u].flags & GD_ACTNORM) || has_an;
+      const bool ok = live && q == 0 && r < e[u].nrows && !(BCNF_EXP & 2);
+      *(ok ? gbuf + e[u].out + ((e[u].flags & GD_COUPLING) ? cpl : 0) + r : dummy) = tot;
+    }
+  }
+  // ---- W1 condition part (column tiles n = wave, wave + 4, ...) and dh[s][c] += sum_j D1[s][j] W1h_m[j][c]
+  const GradDesc dc = gd[NW + NS];
+  const float* D1 = T + TI.D(1) * TILE;
+  float d1a[4], d1t[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    d1a[t] = D1[(4 * t + q) * BCNF_TSTRIDE + r];         // A[s][j] for dW (K = samples)
+    d1t[t] = D1[r * BCNF_TSTRIDE + 4 * t + q];           // A[s][j] transposed for dh (K = neurons)
+  }
+  const int hs = L.Cp + 1;
+  const float* hb = smem + dc.b_tile;
+  const int base_c = dc.out + cpl + __mul24(4 * q, dc.rs) + r;
+#pragma unroll
+  for (int u = 0; u < 4; u += 2) {
+    const int n0 = wave + 4 * u, n1 = n0 + 4;
+    if (n0 >= NC16) break;                               // wave-uniform
+    const bool two = n1 < NC16;
+    const int n1c = two ? n1 : n0;
+    float b0[4], b1[4], w0[4], w1[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      b0[t] = hb[(4 * t + q) * hs + 16 * n0 + r];
+      b1[t] = hb[(4 * t + q) * hs + 16 * n1c + r];
+      w0[t] = wtm[(16 * n0 + r) * 17 + 4 * t + q];
+      w1[t] = wtm[(16 * n1c + r) * 17 + 4 * t + q];
+    }
+    floatx4 g0 = {0.f, 0.f, 0.f, 0.f}, g1 = {0.f, 0.f, 0.f, 0.f};
+    floatx4 h0 = dhacc[u], h1 = dhacc[u + 1];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      g0 = mfma4(d1a[t], b0[t], g0);
+      h0 = mfma4(d1t[t], w0[t], h0);
+      g1 = mfma4(d1a[t], b1[t], g1);
+      h1 = mfma4(d1t[t], w1[t], h1);     // without a second tile this accumulates into an unused slot
+    }
+    dhacc[u] = h0;
+    dhacc[u + 1] = h1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool rowok = (4 * q + i < dc.nrows) && !(BCNF_EXP & 2);
+      const bool ok0 = rowok && 16 * n0 + r < L.C;
+      const bool ok1 = rowok && two && 16 * n1 + r < L.C;
+      *(ok0 ? gbuf + base_c + 16 * n0 + i * dc.rs : dummy) = g0[i];
+      *(ok1 ? gbuf + base_c + 16 * n1 + i * dc.rs : dummy) = g1[i];
     }
   }
 }
 
-template <int NH>
+// LDS gradient block (bwd_mfma_phase output) -> slab block m: CP4 unconditional float4 stores per thread
+// (indices clamped; duplicates rewrite the same value), fully coalesced.
+__device__ float g_exp_sink;
+// BCNF_EXP & 128: per-phase cycle counts of the backward loop (wave 0 of workgroup 0)
+__device__ unsigned long long g_phase[16];
+#define PH(i)                                                                          \
+  if (BCNF_EXP & 128) {                                                                \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();                        \
+    if (blockIdx.x == 0 && threadIdx.x == 0) ph_acc[i] += _t - ph_t;                   \
+    ph_t = _t;                                                                         \
+  }
+template <int CP4>
+__device__ __forceinline__ void copy_out(const BcnfLayout& L, const float* __restrict__ gbuf,
+                                         float* __restrict__ slab, int m, float& sink) {
+  const int n4 = L.blk_pad >> 2;
+  const floatx4* g4 = reinterpret_cast<const floatx4*>(gbuf);
+  floatx4* s4 = reinterpret_cast<floatx4*>(slab + ((BCNF_EXP & 16) ? 0LL : (long long)m * L.blk_pad));
+  floatx4 v[CP4];
+#pragma unroll
+  for (int u = 0; u < CP4; ++u) {
+    const int i = (int)threadIdx.x + u * BCNF_WG;
+    v[u] = g4[i < n4 ? i : n4 - 1];
+  }
+#pragma unroll
+  for (int u = 0; u < CP4; ++u) {
+    const int i = (int)threadIdx.x + u * BCNF_WG;
+    if (BCNF_EXP & 64)
+      sink += v[u].x + v[u].y + v[u].z + v[u].w;
+    else if (!(BCNF_EXP & 2))
+      s4[i < n4 ? i : n4 - 1] = v[u];
+  }
+}
+
+template <int NH, int CP4>
 __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float* __restrict__ pk,
                                                       const float* __restrict__ h, const float* __restrict__ dz,
                                                       const float* __restrict__ dldj, const float* __restrict__ dloss,
@@ -768,18 +893,20 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
   float* wt = recB + 2 * RBL;           // [4][Cp*17]  W1h^T ring: block k-1 (HP), k+1 (dh) live at step k
   float* hpb = wt + 4 * WTL;            // [2][4][256]
   float* tiles = hpb + 2 * 1024;        // [2][NT][272]
-  float* ones = tiles + 2 * NT * TILE;  // [272] ones (B operand of the bias / ActNorm sums)
-  ChainDesc* cd = reinterpret_cast<ChainDesc*>(ones + TILE);   // [MAX_CHAINS]
-  float* ht = ones + TILE + MAX_CHAINS * 8;                      // [16][Cp+1]
+  GradDesc* cd = reinterpret_cast<GradDesc*>(tiles + 2 * NT * TILE);   // [MAX_JOBS]
+  float* ht = tiles + 2 * NT * TILE + MAX_JOBS * 8;                      // [16][Cp+1]
+  float* gbuf = ht + 16 * (L.Cp + 1);                            // [blk_pad + 64] block gradient + dummies
+  float exp_sink = 0.f;
+  unsigned long long ph_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long ph_t = (BCNF_EXP & 128) ? __builtin_amdgcn_s_memtime() : 0ULL;
   const int tid = threadIdx.x, j = tid & 15, s = tid >> 4;
   const int wave = tid >> 6, l64 = tid & 63, q = l64 >> 4, r = l64 & 15;
-  for (int i = tid; i < TILE; i += BCNF_WG) ones[i] = 1.0f;
-  build_chains<NH>(L, cd, (int)(ones - smem), (int)(ht - smem));
+  build_jobs<NH>(L, cd, (int)(ht - smem));
   const long long b = (long long)blockIdx.x * 16 + s;
   const bool valid = b < B;
   const long long bc = valid ? b : B - 1;
   const int D = L.D, Da = L.Da, Db = L.Db, nb = L.nb;
-  float* slab = slab_all + (long long)blockIdx.x * slab_stride;
+  float* slab = slab_all + ((BCNF_EXP & 32) ? 0LL : (long long)blockIdx.x * slab_stride);
   const bool drop = msave != nullptr;
   const float* pf = pk + L.pf_off;
   const float* pbk = pk + L.pb_off;
@@ -837,6 +964,13 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
     const int k1 = k >= 1 ? k - 1 : 0, k2 = k >= 2 ? k - 2 : 0;   // clamped: no branches
     const float ya = ya_n, yb = yb_n;
     const uint32_t mword = mw_n;
+    // (0) gradient block k+2 (MFMA phase of the previous iteration) LDS -> slab, before any load of
+    // this iteration is issued; then the MFMA phase below may overwrite the LDS block
+    if (k + 2 < nb) {
+      copy_out<CP4>(L, gbuf, slab, k + 2, exp_sink);
+      __syncthreads();
+    }
+    PH(0)
     // (a) prefetch: next records, W1h^T two blocks ahead, next block's saved input / masks
     Stage<STAGE_REC> sF, sB;
     Stage<STAGE_W1T> sw;
@@ -849,24 +983,29 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
       yb_n = ys[16 + j];
       if (drop) mw_n = msave[((long long)(k1 >> 2) * B + bc) * 16 + j];
     }
+    PH(1)
     // (b) MFMA phase: parameter gradients + dh of block k+1, HP of block k-1
-    if (k + 1 < nb)
-      bwd_mfma_phase<NH>(L, smem, tiles + ((k + 1) & 1) * NT * TILE, cd, wt + ((k + 1) & 3) * WTL, slab, k + 1,
+    if (k + 1 < nb && !(BCNF_EXP & 4))
+      bwd_mfma_phase<NH>(L, smem, tiles + ((k + 1) & 1) * NT * TILE, cd, wt + ((k + 1) & 3) * WTL, gbuf, k + 1,
                          dhacc);
+    PH(2)
     hp_quarter(L, wt + (k1 & 3) * WTL, ht, hpb + (cur ^ 1) * 1024);
+    PH(3)
     // (c) VALU phase: recompute block k, then back-propagate through it
     float* Tt = tiles + cur * NT * TILE;
     const int tix = s * BCNF_TSTRIDE + j;
     using RBk = RecB<NH>;
     float rf[RecF<NH>::MLP_END], rb[RBk::USED];
-    ld_rec<0, RecF<NH>::MLP_END>(rf, recF + cur * RFL + j * L.RF);   // recompute part (no forward mix)
-    ld_rec<0, RBk::USED>(rb, recB + cur * RBL + j * L.RB);
+    ld_rec_exp<0, RecF<NH>::MLP_END>(rf, recF + cur * RFL + j * L.RF);   // recompute part (no forward mix)
+    ld_rec_exp<0, RBk::USED>(rb, recB + cur * RBL + j * L.RB);
     const float xa = fmaf(rf[0], ya, rf[1]);
     const float xb = fmaf(rf[2], yb, rf[3]);
     const uint32_t bits = (mword >> (8 * (k & 3))) & 0xffu;
     float act[NH], gd[NH];
     float T, Sp;
+    PH(4)
     mlp_forward<NH, true>(L, rf, xa, hp_sum(hpb + cur * 1024, s, j), bits, drop, T, Sp, act, gd);
+    PH(5)
     const float S = tanh_bf(Sp);
     const float e = expf(S);
     float gza, gzb;
@@ -902,13 +1041,25 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
     }
     gya = rf[0] * dxa;
     gyb = rf[2] * dxb;
+    PH(6)
     // (d) commit prefetched records (past the end they refill buffers nobody reads)
     sF.store(recF + (cur ^ 1) * RFL, RFL);
     sB.store(recB + (cur ^ 1) * RBL, RBL);
     if (k >= 2) sw.store(wt + (k2 & 3) * WTL, WTL);
+    PH(7)
+    __syncthreads();
+    PH(8)
+  }
+  if ((BCNF_EXP & 128) && blockIdx.x == 0 && threadIdx.x == 0)
+    for (int i = 0; i < 10; ++i) g_phase[i] = ph_acc[i];
+  if (nb >= 2) {                                   // block 1 (MFMA phase of the last iteration)
+    copy_out<CP4>(L, gbuf, slab, 1, exp_sink);
     __syncthreads();
   }
-  bwd_mfma_phase<NH>(L, smem, tiles, cd, wt, slab, 0, dhacc);
+  bwd_mfma_phase<NH>(L, smem, tiles, cd, wt, gbuf, 0, dhacc);
+  __syncthreads();
+  copy_out<CP4>(L, gbuf, slab, 0, exp_sink);
+  if ((BCNF_EXP & 64) && exp_sink == 1234.5f) g_exp_sink = exp_sink;
   if (dy && valid) {
     if (j < Da) dy[b * D + j] = gya;
     if (j < Db) dy[b * D + Da + j] = gyb;
@@ -930,34 +1081,36 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
   }
 }
 
-// Deterministic sum of the per-workgroup gradient slabs (fixed order over workgroups).
-__global__ __launch_bounds__(BCNF_WG) void k_reduce(const float* __restrict__ slab, long long stride, int nwg,
-                                                    long long P, float* __restrict__ out) {
-  const long long p = ((long long)blockIdx.x * BCNF_WG + threadIdx.x) * 4;
-  if (p >= P) return;
+// Deterministic sum of the per-workgroup gradient slabs (fixed order over workgroups). The slab holds
+// block m's canonical parameters [m * blk_stride, m * blk_stride + size_m) at [m * blk_pad, ...).
+__global__ __launch_bounds__(BCNF_WG) void k_reduce(BcnfLayout L, const float* __restrict__ slab, long long stride,
+                                                    int nwg, float* __restrict__ out) {
+  const long long i = ((long long)blockIdx.x * BCNF_WG + threadIdx.x) * 4;
+  if (i >= stride) return;
+  const int m = (int)(i / L.blk_pad), o = (int)(i - (long long)m * L.blk_pad);
+  const int size_m = (m < L.nb - 1) ? L.blk_stride : L.blk_stride - L.an_size;
+  if (o >= size_m) return;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   int w = 0;
   for (; w + 4 <= nwg; w += 4) {
-    const float4 v0 = *reinterpret_cast<const float4*>(slab + (long long)(w + 0) * stride + p);
-    const float4 v1 = *reinterpret_cast<const float4*>(slab + (long long)(w + 1) * stride + p);
-    const float4 v2 = *reinterpret_cast<const float4*>(slab + (long long)(w + 2) * stride + p);
-    const float4 v3 = *reinterpret_cast<const float4*>(slab + (long long)(w + 3) * stride + p);
+    const float4 v0 = *reinterpret_cast<const float4*>(slab + (long long)(w + 0) * stride + i);
+    const float4 v1 = *reinterpret_cast<const float4*>(slab + (long long)(w + 1) * stride + i);
+    const float4 v2 = *reinterpret_cast<const float4*>(slab + (long long)(w + 2) * stride + i);
+    const float4 v3 = *reinterpret_cast<const float4*>(slab + (long long)(w + 3) * stride + i);
     acc.x += v0.x; acc.y += v0.y; acc.z += v0.z; acc.w += v0.w;
     acc.x += v1.x; acc.y += v1.y; acc.z += v1.z; acc.w += v1.w;
     acc.x += v2.x; acc.y += v2.y; acc.z += v2.z; acc.w += v2.w;
     acc.x += v3.x; acc.y += v3.y; acc.z += v3.z; acc.w += v3.w;
   }
   for (; w < nwg; ++w) {
-    const float4 v = *reinterpret_cast<const float4*>(slab + (long long)w * stride + p);
+    const float4 v = *reinterpret_cast<const float4*>(slab + (long long)w * stride + i);
     acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
   }
-  if (p + 3 < P) {
-    *reinterpret_cast<float4*>(out + p) = acc;
-  } else {
-    out[p] = acc.x;
-    if (p + 1 < P) out[p + 1] = acc.y;
-    if (p + 2 < P) out[p + 2] = acc.z;
-  }
+  float* dst = out + (long long)m * L.blk_stride + o;
+  dst[0] = acc.x;
+  if (o + 1 < size_m) dst[1] = acc.y;
+  if (o + 2 < size_m) dst[2] = acc.z;
+  if (o + 3 < size_m) dst[3] = acc.w;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1072,14 +1225,18 @@ int bwd_dispatch(const BcnfLayout& L, const float* pk, const float* h, const flo
   if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
   const dim3 grid((unsigned)((B + 15) / 16));
   size_t lds = bwd_lds_bytes(L);
-  const int rc = launch_lds(k_backward<NH>, lds);
-  if (rc) return rc;
-  hipLaunchKernelGGL((k_backward<NH>), grid, dim3(BCNF_WG), lds, st, L, pk, h, dz, dldj, dloss, nll, B, ysave,
-                     msave, dy, dh, slab, stride);
+  int rc;
+#define BCNF_BWD(CP)                                                                                      \
+  rc = launch_lds(k_backward<NH, CP>, lds);                                                               \
+  if (rc) return rc;                                                                                      \
+  hipLaunchKernelGGL((k_backward<NH, CP>), grid, dim3(BCNF_WG), lds, st, L, pk, h, dz, dldj, dloss, nll, B, \
+                     ysave, msave, dy, dh, slab, stride);
+  if (copy4_of(L) == 4) { BCNF_BWD(4) } else { BCNF_BWD(8) }
+#undef BCNF_BWD
   return check_launch();
 }
 
-long long slab_stride_of(const BcnfLayout& L) { return ((long long)L.n_trainable + 3) & ~3LL; }
+long long slab_stride_of(const BcnfLayout& L) { return (long long)L.nb * L.blk_pad; }
 
 // Workspace: [saved block inputs nb*B*32][dropout masks ceil(nb/4)*B*16 u32, if dropout][loss partials]
 long long ws_mask_off(const BcnfLayout& L, long long B) { return (long long)L.nb * B * 32; }
@@ -1224,10 +1381,10 @@ int bcnf_grad_reduce(const BcnfStackDesc* desc, const void* slab, int64_t batch,
   const int rc = make_layout(desc, &L);
   if (rc) return rc;
   if (!slab || !dparams || batch < 1) return BCNF_ERR_ARG;
-  const long long P = L.n_trainable;
-  const unsigned nblk = (unsigned)((P / 4 + BCNF_WG) / BCNF_WG);
-  hipLaunchKernelGGL(k_reduce, dim3(nblk), dim3(BCNF_WG), 0, (hipStream_t)stream, (const float*)slab,
-                     slab_stride_of(L), (int)((batch + 15) / 16), P, dparams);
+  const long long S = slab_stride_of(L);
+  const unsigned nblk = (unsigned)((S / 4 + BCNF_WG - 1) / BCNF_WG);
+  hipLaunchKernelGGL(k_reduce, dim3(nblk), dim3(BCNF_WG), 0, (hipStream_t)stream, L, (const float*)slab, S,
+                     (int)((batch + 15) / 16), dparams);
   return check_launch();
 }
 
@@ -1263,6 +1420,12 @@ const char* bcnf_status_string(int status) {
 }
 
 int bcnf_last_hip_error(void) { return bcnf_rt::last_hip; }
+
+#if BCNF_EXP & 128
+int bcnf_debug_phases(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(g_phase)) == hipSuccess ? 0 : 3;
+}
+#endif
 
 }  // extern "C"
 

@@ -58,11 +58,14 @@ __global__ __launch_bounds__(BCNF_WG) void k_adam(TList T, float* __restrict__ s
                                                   unsigned* __restrict__ sync) {
   __shared__ float red[BCNF_WG];
   __shared__ int last;
+  __shared__ float sc[2];
   const float st = step[0] + 1.0f;
-  const double bc1 = 1.0 - pow(b1d, (double)st);
-  const double bc2 = 1.0 - pow(b2d, (double)st);
-  const float step_size = (float)(lr / bc1);
-  const float bc2s = (float)sqrt(bc2);
+  if (threadIdx.x == 0) {                          // double pow once per workgroup, not per thread
+    sc[0] = (float)(lr / (1.0 - pow(b1d, (double)st)));
+    sc[1] = (float)sqrt(1.0 - pow(b2d, (double)st));
+  }
+  __syncthreads();
+  const float step_size = sc[0], bc2s = sc[1];
   const float omb1 = (float)(1.0 - b1d), omb2 = (float)(1.0 - b2d);
   const float b2 = (float)b2d, eps = (float)epsd, wd = (float)wdd;
   const long long total = T.start[T.n];
@@ -156,16 +159,16 @@ __global__ __launch_bounds__(BCNF_WG) void k_gemm(const float* __restrict__ A, i
   const float* a = A + ar * lda;
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
   int k0 = 0;
-  for (; k0 + 16 <= K; k0 += 16) {              // 4 MFMA steps, loads issued first
-    float av[4], bv[4];
+  for (; k0 + 32 <= K; k0 += 32) {              // 8 MFMA steps, all 16 loads issued first
+    float av[8], bv[8];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < 8; ++t) {
       const int k = k0 + 4 * t + lq;
       av[t] = a[k];
       bv[t] = TB ? Bm[(long long)bc * ldb + k] : Bm[(long long)k * ldb + bc];
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc = mfma4(av[t], bv[t], acc);
+    for (int t = 0; t < 8; ++t) acc = mfma4(av[t], bv[t], acc);
   }
   for (; k0 < K; k0 += 4) {
     const int k = k0 + lq;
@@ -206,16 +209,16 @@ __global__ __launch_bounds__(BCNF_WG) void k_gemm_wt(const float* __restrict__ X
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;
   long long m0 = m_begin;
-  for (; m0 + 16 <= m_end; m0 += 16) {
-    float av[4], bv[4];
+  for (; m0 + 32 <= m_end; m0 += 32) {
+    float av[8], bv[8];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < 8; ++t) {
       const long long m = m0 + 4 * t + lq;
       av[t] = dY[m * N + n];
       bv[t] = X[m * K + k];
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < 8; ++t) {
       bsum += av[t];
       acc = mfma4(av[t], bv[t], acc);
     }
@@ -251,16 +254,31 @@ __global__ __launch_bounds__(BCNF_WG) void k_wt_reduce(const float* __restrict__
                                                        float* __restrict__ db) {
   const long long NK = (long long)N * K;
   const long long i = (long long)blockIdx.x * BCNF_WG + threadIdx.x;
+  const float* src;
+  long long stride;
+  float* dst;
   if (i < NK) {
-    float acc = 0.f;
-    for (int s = 0; s < splits; ++s) acc += work[(long long)s * NK + i];
-    dW[i] = acc;
+    src = work + i;
+    stride = NK;
+    dst = dW + i;
   } else if (db && i < NK + N) {
-    const int n = (int)(i - NK);
-    float acc = 0.f;
-    for (int s = 0; s < splits; ++s) acc += bwork[(long long)s * N + n];
-    db[n] = acc;
+    src = bwork + (i - NK);
+    stride = N;
+    dst = db + (i - NK);
+  } else {
+    return;
   }
+  float acc = 0.f;
+  int s = 0;
+  for (; s + 8 <= splits; s += 8) {              // 8 loads in flight, summed in split order
+    float v[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = src[(long long)(s + t) * stride];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc += v[t];
+  }
+  for (; s < splits; ++s) acc += src[(long long)s * stride];
+  *dst = acc;
 }
 
 using bcnf_rt::launched;
@@ -281,10 +299,10 @@ int make_tlist(int n, float* const* p, float* const* g, float* const* m, float* 
   return BCNF_OK;
 }
 
-int split_rows(long long M) {        // rows per split-K chunk of the weight gradient (multiple of 4)
-  long long r = (M + 63) / 64;
-  if (r < 64) r = 64;
-  return (int)((r + 3) & ~3LL);
+int split_rows(long long M) {        // rows per split-K chunk of the weight gradient: <= 32 splits
+  long long r = (M + 31) / 32;
+  if (r < 128) r = 128;
+  return (int)((r + 31) & ~31LL);
 }
 
 }  // namespace

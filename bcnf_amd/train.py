@@ -137,6 +137,9 @@ class TrainStep:
             self._restore(snap)
         torch.cuda.current_stream().wait_stream(s)
         self.opt.zero_grad(set_to_none=True)
+        # the three logged values land in pinned host memory as the graph's last node: the host reads
+        # them after one stream sync instead of issuing a separate device-to-host copy per step
+        self._host_vals = torch.empty(3, dtype=torch.float32, pin_memory=True)
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1):
             if indexed:
@@ -144,17 +147,25 @@ class TrainStep:
             vals = self._forward_backward(sy, st)
             if self.world == 1:
                 self._update()
+                self._host_vals.copy_(vals, non_blocking=True)
         g2 = None
         if self.world > 1:
             g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g2):
                 self._update()
+                self._host_vals.copy_(vals, non_blocking=True)
         self._graphs = (g1, g2, vals)
 
     def step(self, y, traj):
         """One training step; returns (loss, nll, mse) as Python floats (the Trainer's three .item())."""
         vals = self.step_async(y, traj)
-        return tuple(vals.tolist())
+        if not self.capture:
+            return tuple(vals.tolist())
+        return self._host_values()
+
+    def _host_values(self):
+        torch.cuda.current_stream().synchronize()
+        return tuple(self._host_vals.tolist())
 
     def step_async(self, y, traj):
         if not self.capture:
@@ -184,7 +195,8 @@ class TrainStep:
             py, pt = self._pool
             self._build_graphs(py.index_select(0, idx), pt.index_select(0, idx), idx=idx)
         self._static[2].copy_(idx, non_blocking=True)
-        return tuple(self._replay().tolist())
+        self._replay()
+        return self._host_values()
 
     def _replay(self):
         g1, g2, vals = self._graphs

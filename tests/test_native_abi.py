@@ -45,7 +45,7 @@ def test_layout_queries_match_module_tree():
     ws = N.query_i64(N.lib().bcnf_workspace_bytes, ctypes.byref(d), ctypes.c_int64(4096), ctypes.c_int32(1))
     assert ws == 32 * 4096 * 32 * 4 + 8 * 4096 * 16 * 4 + 256 * 4   # inputs, masks, loss partials
     sb = N.query_i64(N.lib().bcnf_slab_bytes, ctypes.byref(d), ctypes.c_int64(4096))
-    assert sb == 256 * ((109786 + 3) // 4 * 4) * 4
+    assert sb == 256 * 32 * 3432 * 4          # per workgroup: nb blocks of blk_stride (3430) padded to 4
 
 
 def test_unsupported_shapes_are_rejected():

@@ -46,5 +46,24 @@ def main():
         print(f"{k:14s} median {v[len(v)//2]:8.1f} us   min {v[0]:8.1f} us")
 
 
+
+
+def phases():
+    """Per-phase cycles of the backward loop (experiment build with BCNF_EXP & 128)."""
+    import ctypes
+    from bcnf_amd import _native as N
+    L = N.lib()
+    if not hasattr(L, "bcnf_debug_phases"):
+        return
+    buf = (ctypes.c_ulonglong * 16)()
+    L.bcnf_debug_phases(buf)
+    names = ["copy_out+bar", "prefetch issue", "mfma phase", "hp_quarter", "ld_rec+setup", "mlp recompute",
+             "backprop", "commit", "end barrier"]
+    tot = sum(buf[i] for i in range(9))
+    for i, n in enumerate(names):
+        print(f"  {n:16s} {buf[i]:10d} cycles  {100.0 * buf[i] / max(tot, 1):5.1f}%")
+
+
 if __name__ == "__main__":
     main()
+    phases()

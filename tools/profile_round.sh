@@ -1,5 +1,6 @@
 # Usage (on the GPU box): bash tools/profile_round.sh r01
 # 1) rocprofv3 --kernel-trace --stats of the bench command  2) FETCH_SIZE pass  3) WRITE_SIZE pass
+# (counters in their own passes, never combined with runtime / sys traces)
 set -e
 TAG=${1:-r01}
 cd $GRAFT_REPO_ROOT
