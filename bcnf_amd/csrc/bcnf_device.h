@@ -36,7 +36,8 @@ struct BcnfLayout {
   int lin_w[10], lin_b[10], lin_in[10], lin_out[10];   // Linear l = 1..NH+1 inside a coupling
   int an_size;          // 2*D if act_norm else 0
   int blk_stride;       // canonical floats per (ActNorm + coupling) block
-  int blk_pad;          // blk_stride rounded up to 4: per-block stride of the gradient slab
+  int cblk;             // slab floats per block: blk_stride without the W1 condition columns (H1 x C)
+  int blk_pad;          // cblk rounded up to 4: per-block stride of the gradient slab
   int n_trainable;
   float p, keep_scale;
   uint32_t thresh16;    // drop if u16 < thresh16

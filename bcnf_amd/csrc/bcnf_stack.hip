@@ -33,7 +33,8 @@ thread_local int last_hip = 0;
 
 namespace {
 
-constexpr int NT_EXTRA = 7;            // tiles: D_1..D_NH, D_T, D_S, A_0..A_NH, PA, GA, PB, GB
+constexpr int NT_EXTRA = 7;
+constexpr int NC16_MAX = 16;           // C <= 256: register-resident column tiles of k_hp / k_dh / k_dw1h            // tiles: D_1..D_NH, D_T, D_S, A_0..A_NH, PA, GA, PB, GB
 constexpr int TILE = BCNF_ROWS * BCNF_TSTRIDE;   // 272 floats
 
 // ------------------------------------------------------------------------------------------------
@@ -77,7 +78,8 @@ int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
   L->an_size = L->act_norm ? 2 * L->D : 0;
   L->blk_stride = L->an_size + off;
   L->n_trainable = (L->nb - 1) * L->blk_stride + off;
-  L->blk_pad = (L->blk_stride + 3) & ~3;
+  L->cblk = L->blk_stride - L->H[1] * L->C;
+  L->blk_pad = (L->cblk + 3) & ~3;
   L->p = d->dropout;
   L->keep_scale = (d->dropout > 0.f) ? (1.0f / (1.0f - d->dropout)) : 1.0f;
   double t = (double)d->dropout * 65536.0;
@@ -108,16 +110,15 @@ int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
   return BCNF_OK;
 }
 
-size_t fwd_lds_bytes(const BcnfLayout& L) {   // rec ring 2, W1h^T ring 2, HP partials 2, features
-  return sizeof(float) * (size_t)(2 * 16 * L.RF + 2 * L.Cp * 17 + 2 * 1024 + 16 * (L.Cp + 1));
+size_t fwd_lds_bytes(const BcnfLayout& L) {   // forward / inverse record ring (2 blocks)
+  return sizeof(float) * (size_t)(2 * 16 * L.RF);
 }
-size_t bwd_lds_bytes(const BcnfLayout& L) {   // F/B rec rings 2, W1h^T ring 4, HP 2, tiles 2, features
+size_t bwd_lds_bytes(const BcnfLayout& L) {   // F/B record rings, gradient tiles (2), job table, gradient block
   const int NT = 2 * L.NH + NT_EXTRA;
-  return sizeof(float) * (size_t)(2 * 16 * L.RF + 2 * 16 * L.RB + 4 * L.Cp * 17 + 2 * 1024 + 2 * NT * TILE +
-                                  8 * (2 * (BCNF_MAX_HIDDEN + 2) + 4 + 1) + 16 * (L.Cp + 1) + L.blk_pad + 64);
+  return sizeof(float) * (size_t)(2 * 16 * L.RF + 2 * 16 * L.RB + 2 * NT * TILE + 8 * (2 * (BCNF_MAX_HIDDEN + 2) + 4) +
+                                  L.blk_pad + 64);
 }
-// float4 stores per thread that copy one block's gradient partials from LDS to the slab (fixed count:
-// the compiler's vmcnt bookkeeping then never has to over-wait on them)
+// float4 stores per thread that copy one block's gradient partials from LDS to the slab (fixed count)
 constexpr int COPY4_MAX = 8;
 int copy4_of(const BcnfLayout& L) { return (L.blk_pad / 4 + BCNF_WG - 1) / BCNF_WG <= 4 ? 4 : 8; }
 constexpr size_t LDS_MAX = 160 * 1024;
@@ -128,8 +129,8 @@ bool layout_supported(const BcnfLayout& L, const BcnfStackDesc* d) {
   if (L.Da > 16 || L.Db > 16) return false;
   for (int l = 1; l <= L.NH; ++l)
     if (L.H[l] > 16) return false;
-  if (L.C < 1 || L.Cp > 256) return false;
-  if (16 * L.RF > 4 * 4 * BCNF_WG || 16 * L.RB > 4 * 4 * BCNF_WG || L.Cp * 17 > 5 * 4 * BCNF_WG) return false;
+  if (L.C < 1 || L.Cp > 16 * NC16_MAX) return false;
+  if (16 * L.RF > 4 * 4 * BCNF_WG || 16 * L.RB > 4 * 4 * BCNF_WG) return false;
   if (fwd_lds_bytes(L) > LDS_MAX || bwd_lds_bytes(L) > LDS_MAX) return false;
   if (L.blk_pad / 4 > COPY4_MAX * BCNF_WG) return false;
   return true;
@@ -306,52 +307,173 @@ struct Stage {
   }
 };
 constexpr int STAGE_REC = 4;   // 16 * RF floats  <= 4 float4 per thread (RF <= 256)
-constexpr int STAGE_W1T = 5;   // Cp * 17 floats  <= 5 float4 per thread (Cp <= 256)
 
-// Stage the workgroup's 16 feature rows h[row] (optionally gathered via cond_index) into
-// ht[16][Cp+1], zero-padded to Cp columns. Rows past the batch repeat the last row.
-__device__ __forceinline__ void stage_features(const BcnfLayout& L, const float* __restrict__ h,
-                                               const int64_t* __restrict__ cond_index, long long n_rows,
-                                               float* __restrict__ ht) {
-  const int Cp = L.Cp, hs = Cp + 1;
-  for (int i = threadIdx.x; i < 16 * Cp; i += BCNF_WG) {
-    const int ss = i / Cp, c = i - ss * Cp;
-    long long bb = (long long)blockIdx.x * 16 + ss;
-    if (bb > n_rows - 1) bb = n_rows - 1;
-    const long long src = cond_index ? (long long)cond_index[bb] : bb;
-    ht[ss * hs + c] = (c < L.C) ? h[src * L.C + c] : 0.f;
+// ------------------------------------------------------------------------------------------------
+// Condition projection, hoisted out of the stack kernels (one fp32 MFMA GEMM per direction):
+//   HP[k][r][j] = sum_c h[r][c] W1_k[j][Da + c] + b1_k[j]     (the y-independent part of Linear 1)
+//   dh[b][c]   = sum_k sum_j D1[k][b][j] W1_k[j][Da + c]      (dL/dh, all blocks)
+//   dW1_k[j][Da + c] = sum_b D1[k][b][j] h[b][c]               (split-K, then fixed-order reduce)
+// W1h^T comes from the packed buffer ([k][Cp][17], zero-padded); D1 = dL/d pre-activation of Linear 1.
+// MFMA lane roles: A[l&15][l>>4], B[l>>4][l&15], D[4(l>>4)+i][l&15].
+// ------------------------------------------------------------------------------------------------
+// Shape of the three GEMMs: one workgroup per 16-row slice; a wave keeps its A fragment in registers and
+// reuses it for every output column tile; the 4 waves split the reduction dimension and their partial
+// tiles are summed through LDS in a fixed order (deterministic).
+
+// HP[k][r][j] for 16 rows r; wave w computes blocks k = w, w + 4, ... The A fragment (the 16 h rows,
+// Cp/4 values per lane) is loaded once and reused for every block. grid = ceil(R / 16)
+__global__ __launch_bounds__(BCNF_WG) void k_hp(BcnfLayout L, const float* __restrict__ pk,
+                                                const float* __restrict__ h, long long R, float* __restrict__ hp) {
+  constexpr int KSM = 4 * NC16_MAX;                   // max K steps (Cp <= 256)
+  const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lq = l >> 4;
+  const long long r0 = (long long)blockIdx.x * 16;
+  const long long ar = r0 + lr < R ? r0 + lr : R - 1;
+  const float* a = h + ar * L.C;
+  const int C = L.C, Cp = L.Cp, KS = Cp >> 2;
+  float av[KSM];
+#pragma unroll
+  for (int t = 0; t < KSM; ++t) {
+    const int c = 4 * t + lq;
+    av[t] = (t < KS && c < C) ? a[c < C ? c : C - 1] : 0.f;
+  }
+  const float* w1t = pk + L.w1t_off + (long long)lq * 17 + lr;   // W1hT[k][4t + lq][lr] = w1t[(k Cp + 4t) 17]
+  for (int k = wave; k < L.nb; k += 4) {
+    const float* wk = w1t + (long long)k * Cp * 17;
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t0 = 0; t0 < KSM; t0 += 8) {
+      if (t0 < KS) {                                 // uniform; KS is a multiple of 4
+      float bv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) bv[u] = (t0 + u < KS) ? wk[(long long)(4 * (t0 + u)) * 17] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        if (t0 + u < KS) acc0 = mfma4(av[t0 + u], bv[u], acc0);
+        if (t0 + u + 1 < KS) acc1 = mfma4(av[t0 + u + 1], bv[u + 1], acc1);
+      }
+      }
+    }
+    const float b1 = pk[L.pf_off + ((long long)k * 16 + lr) * L.RF + L.rf_b1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long long r = r0 + 4 * lq + i;
+      if (r < R) hp[((long long)k * R + r) * 16 + lr] = (acc0[i] + acc1[i]) + b1;
+    }
   }
 }
 
-// Per-wave K-quarter of HP_k = H (16 x Cp) @ W1h_k^T (Cp x 16) on fp32 MFMA from LDS; the partial
-// tile goes to hpbuf[wave] and the consumer sums the four quarters.
-__device__ __forceinline__ void hp_quarter(const BcnfLayout& L, const float* __restrict__ wt,
-                                           const float* __restrict__ ht, float* __restrict__ hpbuf) {
-  const int wave = threadIdx.x >> 6, l64 = threadIdx.x & 63, q = l64 >> 4, r = l64 & 15;
-  const int nsteps = L.Cp >> 2;
-  const int t0 = (wave * nsteps) >> 2, t1 = ((wave + 1) * nsteps) >> 2;
-  const int hs = L.Cp + 1;
-  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-  int t = t0;
-  for (; t + 4 <= t1; t += 4) {        // all operand reads of 4 steps before their MFMAs
-    float a[4], bv[4];
+// dh for 16 rows x all columns; wave w sums blocks k = w, w + 4, ... ; grid = ceil(B / 16)
+// K index of MFMA step e, lane quarter q: j = 4q + e (A = D1[k][row][4q + e], B = W1hT[k][col][4q + e]).
+__global__ __launch_bounds__(BCNF_WG) void k_dh(BcnfLayout L, const float* __restrict__ pk,
+                                                const float* __restrict__ d1, long long B, float* __restrict__ dh) {
+  __shared__ floatx4 part[4][NC16_MAX][64];
+  const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lq = l >> 4;
+  const long long b0 = (long long)blockIdx.x * 16;
+  const long long bl = b0 + lr < B ? b0 + lr : B - 1;
+  const int NC16 = L.Cp >> 4;
+  const long long Cp17 = (long long)L.Cp * 17;
+  floatx4 acc[NC16_MAX];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      a[u] = ht[r * hs + 4 * (t + u) + q];
-      bv[u] = wt[(4 * (t + u) + q) * 17 + r];
+  for (int u = 0; u < NC16_MAX; ++u) acc[u] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int k = wave; k < L.nb; k += 4) {
+    const floatx4 av = *reinterpret_cast<const floatx4*>(d1 + ((long long)k * B + bl) * 16 + 4 * lq);
+    const float* wk = pk + L.w1t_off + k * Cp17 + lr * 17 + 4 * lq;
+    float bv[NC16_MAX][4];
+#pragma unroll
+    for (int u = 0; u < NC16_MAX; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[u][e] = (u < NC16) ? wk[(long long)(16 * (u < NC16 ? u : 0)) * 17 + e] : 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int u = 0; u < NC16_MAX; ++u)
+        if (u < NC16) acc[u] = mfma4(av[e], bv[u][e], acc[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < NC16_MAX; ++u)
+    if (u < NC16) part[wave][u][l] = acc[u];
+  __syncthreads();
+  for (int idx = tid; idx < NC16 * 64; idx += BCNF_WG) {
+    const int u = idx >> 6, ll = idx & 63, rr = ll & 15, qq = ll >> 4;
+    const floatx4 v = ((part[0][u][ll] + part[1][u][ll]) + part[2][u][ll]) + part[3][u][ll];
+    const int col = 16 * u + rr;
+    if (col < L.C) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long long r = b0 + 4 * qq + i;
+        if (r < B) dh[r * L.C + col] = v[i];
+      }
+    }
+  }
+}
+
+// dW1h partials for one block k (16 rows j) x all columns over one batch split; wave w takes rows
+// m0 + 4w + 16t (+ lane quarter). grid = (nb, splits); work[s][k][16][Cp]
+__global__ __launch_bounds__(BCNF_WG) void k_dw1h(BcnfLayout L, const float* __restrict__ d1,
+                                                  const float* __restrict__ h, long long B, int rows_per_split,
+                                                  float* __restrict__ work) {
+  __shared__ floatx4 part[4][NC16_MAX][64];
+  const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lq = l >> 4;
+  const int k = blockIdx.x, s = blockIdx.y;
+  const long long m0 = (long long)s * rows_per_split;
+  long long m1 = m0 + rows_per_split;
+  if (m1 > B) m1 = B;
+  const int NC16 = L.Cp >> 4, C = L.C;
+  const float* a = d1 + (long long)k * B * 16 + lr;     // A[j = lr][b] = D1[k][b][lr]
+  floatx4 acc[NC16_MAX];
+#pragma unroll
+  for (int u = 0; u < NC16_MAX; ++u) acc[u] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (long long m = m0 + 4 * wave; m < m1; m += 32) {  // two row groups (m, m + 16) per trip
+    float av[2], bv[2][NC16_MAX];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const long long b = m + 16 * g + lq;
+      const bool ok = b < m1;
+      const long long bb = ok ? b : m1 - 1;
+      av[g] = ok ? a[bb * 16] : 0.f;
+      const float* hr = h + bb * C + lr;
+#pragma unroll
+      for (int u = 0; u < NC16_MAX; ++u) bv[g][u] = (ok && u < NC16 && 16 * u + lr < C) ? hr[16 * u] : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc = mfma4(a[u], bv[u], acc);
-  }
-  for (; t < t1; ++t) acc = mfma4(ht[r * hs + 4 * t + q], wt[(4 * t + q) * 17 + r], acc);
-  float* o = hpbuf + wave * 256;
+    for (int g = 0; g < 2; ++g)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) o[(4 * q + i) * 16 + r] = acc[i];
+      for (int u = 0; u < NC16_MAX; ++u)
+        if (u < NC16) acc[u] = mfma4(av[g], bv[g][u], acc[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < NC16_MAX; ++u)
+    if (u < NC16) part[wave][u][l] = acc[u];
+  __syncthreads();
+  float* o = work + (((long long)s * L.nb + k) * 16) * L.Cp;
+  for (int idx = tid; idx < NC16 * 64; idx += BCNF_WG) {
+    const int u = idx >> 6, ll = idx & 63, rr = ll & 15, qq = ll >> 4;
+    const floatx4 v = ((part[0][u][ll] + part[1][u][ll]) + part[2][u][ll]) + part[3][u][ll];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[(long long)(4 * qq + i) * L.Cp + 16 * u + rr] = v[i];
+  }
 }
 
-__device__ __forceinline__ float hp_sum(const float* __restrict__ hpbuf, int s, int j) {
-  const float* p = hpbuf + s * 16 + j;
-  return (p[0] + p[256]) + (p[512] + p[768]);
+__global__ __launch_bounds__(BCNF_WG) void k_dw1h_reduce(BcnfLayout L, const float* __restrict__ work, int splits,
+                                                         float* __restrict__ dparams) {
+  const long long per = 16LL * L.Cp, total = (long long)L.nb * per;
+  const long long i = (long long)blockIdx.x * BCNF_WG + threadIdx.x;
+  if (i >= total) return;
+  const int k = (int)(i / per);
+  const int rem = (int)(i - (long long)k * per);
+  const int j = rem / L.Cp, c = rem - j * L.Cp;
+  if (j >= L.H[1] || c >= L.C) return;
+  float acc = 0.f;
+  int s = 0;
+  for (; s + 8 <= splits; s += 8) {
+    float v[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = work[(long long)(s + t) * total + i];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc += v[t];
+  }
+  for (; s < splits; ++s) acc += work[(long long)s * total + i];
+  dparams[coupling_base(L, k) + L.lin_w[1] + j * L.lin_in[1] + L.Da + c] = acc;
 }
 
 // Compile-time mirror of the forward / backward record layouts of make_layout (checked on the host).
@@ -393,7 +515,8 @@ __device__ __forceinline__ void ld_rec_exp(float* __restrict__ rr, const float* 
 }
 
 // Nested MLP forward on the row layout (cnf.py:98-107) from a register-resident forward record.
-// Input x (layer-1 y-part operand); returns t and s' (pre-tanh). KEEP: also the (masked) activations
+// Input x (layer-1 y-part operand) and hp (its condition part + bias, from k_hp); returns t and s'
+// (pre-tanh). KEEP: also the (masked) activations
 // and masked GELU derivatives for the backward.
 template <int NH, bool KEEP>
 __device__ __forceinline__ void mlp_forward(const BcnfLayout& L, const float* __restrict__ rr, float x, float hp,
@@ -404,7 +527,7 @@ __device__ __forceinline__ void mlp_forward(const BcnfLayout& L, const float* __
 #pragma unroll
   for (int l = 1; l <= NH; ++l) {
     const float* w = (l == 1) ? rr + F::W1 : rr + F::HID + 17 * (l - 2);
-    const float bias = (l == 1) ? rr[F::B1] + hp : w[16];
+    const float bias = (l == 1) ? hp : w[16];            // hp = h W1h^T + b1 (k_hp)
     const float pre = rot16(a, w, bias);
     const float m = drop ? (((bits >> (l - 1)) & 1u) ? L.keep_scale : 0.f) : 1.f;
     if (KEEP) {
@@ -436,46 +559,36 @@ __device__ __forceinline__ void mix(const float* __restrict__ rq, float a, float
 // ------------------------------------------------------------------------------------------------
 template <int NH, bool DROP, bool SAVE>
 __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* __restrict__ pk,
-                                                     const float* __restrict__ y, const float* __restrict__ h,
+                                                     const float* __restrict__ y, const float* __restrict__ hp,
                                                      long long B, float* __restrict__ z, float* __restrict__ ldj_out,
                                                      float* __restrict__ logp, const uint64_t* rng,
                                                      float* __restrict__ ysave, uint32_t* __restrict__ msave,
                                                      float* __restrict__ nll_part, unsigned* __restrict__ sync,
                                                      float* __restrict__ loss_out, uint64_t* rng_w) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int RFL = 16 * L.RF, WTL = L.Cp * 17;
+  const int RFL = 16 * L.RF;
   float* rec = smem;                    // [2][16*RF]
-  float* wt = rec + 2 * RFL;            // [2][Cp*17]   W1h^T ring, staged two blocks ahead
-  float* hpb = wt + 2 * WTL;            // [2][4][256]
-  float* ht = hpb + 2 * 1024;           // [16][Cp+1]
   const int tid = threadIdx.x, j = tid & 15, s = tid >> 4;
   const long long b = (long long)blockIdx.x * 16 + s;
   const long long bc = b < B ? b : B - 1;           // rows past the batch replay the last sample
   const int D = L.D, Da = L.Da, Db = L.Db, nb = L.nb;
   const float* pf = pk + L.pf_off;
-  const float* pw = pk + L.w1t_off;
+  const float* hpl = hp + bc * 16 + j;              // HP[k][bc][j] = hpl[k * B * 16]
+  const long long hps = B * 16;
 
   // every global input the loop reads is loaded before the prologue barrier, so the loop's only
-  // outstanding VMEM ops are its own (unconditional) prefetches and the waitcnt pass never has to
-  // drain them early
+  // outstanding VMEM ops are its own (unconditional) prefetches
   float ya = (j < Da) ? y[bc * D + j] : 0.f;
   float yb = (j < Db) ? y[bc * D + Da + j] : 0.f;
+  float hp_n = hpl[0];
   uint64_t seed = 0, off = 0;
   if (DROP) { seed = rng[0]; off = rng[1]; }
   const float ldc = pk[L.ldc_off];
-  stage_features(L, h, nullptr, B, ht);
   {
     Stage<STAGE_REC> sr;
     sr.load(pf, RFL);
     sr.store(rec, RFL);
-    Stage<STAGE_W1T> sw;
-    sw.load(pw, WTL);
-    sw.store(wt, WTL);
-    sw.load(pw + (long long)(nb > 1 ? 1 : 0) * WTL, WTL);
-    sw.store(wt + WTL, WTL);
   }
-  __syncthreads();
-  hp_quarter(L, wt, ht, hpb);
   __syncthreads();
 
   float ldj = 0.f;
@@ -483,12 +596,11 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
 
   for (int k = 0; k < nb; ++k) {
     const int cur = k & 1;
-    const int k1 = k + 1 < nb ? k + 1 : nb - 1, k2 = k + 2 < nb ? k + 2 : nb - 1;   // clamped: no branches
+    const int k1 = k + 1 < nb ? k + 1 : nb - 1;      // clamped: no branches
     Stage<STAGE_REC> sr;
-    Stage<STAGE_W1T> sw;
     sr.load(pf + (long long)k1 * RFL, RFL);
-    sw.load(pw + (long long)k2 * WTL, WTL);
-    hp_quarter(L, wt + (cur ^ 1) * WTL, ht, hpb + (cur ^ 1) * 1024);
+    const float hpk = hp_n;
+    hp_n = hpl[k1 * hps];
 
     float rr[RecF<NH>::USED];
     ld_rec_exp<0, RecF<NH>::USED>(rr, rec + cur * RFL + j * L.RF);
@@ -502,7 +614,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
     uint32_t bits = 0xffu;
     if (DROP && !(BCNF_EXP & 8)) bits = dropout_bits(L, seed, off, bc, k, j, 0u);
     float T, Sp;
-    mlp_forward<NH, false>(L, rr, xa, hp_sum(hpb + cur * 1024, s, j), bits, DROP, T, Sp, nullptr, nullptr);
+    mlp_forward<NH, false>(L, rr, xa, hpk, bits, DROP, T, Sp, nullptr, nullptr);
     const float S = tanh_bf(Sp);                      // cnf.py:107
     const float zb = fmaf(expf(S), xb, T);            // cnf.py:179
     ldj += S;                                          // cnf.py:190
@@ -515,7 +627,6 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
       }
     }
     sr.store(rec + (cur ^ 1) * RFL, RFL);      // past the end these refill a buffer nobody reads
-    sw.store(wt + cur * WTL, WTL);
     __syncthreads();
   }
   const float ltot = row_sum16(ldj) + ldc;
@@ -528,7 +639,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
   }
   if (nll_part) {   // inn_nll_loss(z, ldj) = mean_b(0.5 |z_b|^2 - ldj_b)   (utils.py:40-46)
     const float q2 = row_sum16(ya * ya + yb * yb);
-    float* red = hpb;                                  // free after the loop's last barrier
+    float* red = rec;                                  // free after the loop's last barrier
     if (j == 0) red[s] = (b < B) ? 0.5f * q2 - ltot : 0.f;
     __syncthreads();
     if (tid == 0) {
@@ -545,7 +656,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
       float acc = 0.f;
       for (int i = tid; i < (int)gridDim.x; i += BCNF_WG)
         acc += __hip_atomic_load(nll_part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      float* r2 = hpb + 32;
+      float* r2 = rec + 32;
       r2[tid] = acc;
       __syncthreads();
       for (int w = BCNF_WG / 2; w > 0; w >>= 1) {
@@ -569,51 +680,41 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
 // ------------------------------------------------------------------------------------------------
 template <int NH, bool DROP>
 __global__ __launch_bounds__(BCNF_WG) void k_inverse(BcnfLayout L, const float* __restrict__ pk,
-                                                     const float* __restrict__ zin, const float* __restrict__ h,
-                                                     const int64_t* __restrict__ cond_index, long long N,
+                                                     const float* __restrict__ zin, const float* __restrict__ hp,
+                                                     long long R, const int64_t* __restrict__ cond_index, long long N,
                                                      float* __restrict__ yout, const uint64_t* __restrict__ rng) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int RFL = 16 * L.RF, WTL = L.Cp * 17;
+  const int RFL = 16 * L.RF;
   float* rec = smem;
-  float* wt = rec + 2 * RFL;
-  float* hpb = wt + 2 * WTL;
-  float* ht = hpb + 2 * 1024;
   const int tid = threadIdx.x, j = tid & 15, s = tid >> 4;
   const long long b = (long long)blockIdx.x * 16 + s;
   const long long bc = b < N ? b : N - 1;
   const int D = L.D, Da = L.Da, Db = L.Db, nb = L.nb;
   const float* pi = pk + L.pi_off;
-  const float* pw = pk + L.w1t_off;
+  const long long hr = cond_index ? (long long)cond_index[bc] : bc;   // projection row of this sample
+  const float* hpl = hp + hr * 16 + j;                                // HP[k][hr][j] = hpl[k * R * 16]
+  const long long hps = R * 16;
 
   float ya = (j < Da) ? zin[bc * D + j] : 0.f;
   float yb = (j < Db) ? zin[bc * D + Da + j] : 0.f;
   uint64_t seed = 0, off = 0;
   if (DROP) { seed = rng[0]; off = rng[1]; }
-  stage_features(L, h, cond_index, N, ht);
   const int kl = nb - 1;
+  float hp_n = hpl[kl * hps];
   {
     Stage<STAGE_REC> sr;
     sr.load(pi + (long long)kl * RFL, RFL);
     sr.store(rec + (kl & 1) * RFL, RFL);
-    Stage<STAGE_W1T> sw;
-    sw.load(pw + (long long)kl * WTL, WTL);
-    sw.store(wt + (kl & 1) * WTL, WTL);
-    const int km = kl >= 1 ? kl - 1 : 0;
-    sw.load(pw + (long long)km * WTL, WTL);
-    sw.store(wt + (km & 1) * WTL, WTL);
   }
-  __syncthreads();
-  hp_quarter(L, wt + (kl & 1) * WTL, ht, hpb + (kl & 1) * 1024);
   __syncthreads();
 
   for (int k = kl; k >= 0; --k) {
     const int cur = k & 1;
-    const int k1 = k >= 1 ? k - 1 : 0, k2 = k >= 2 ? k - 2 : 0;   // clamped: no branches
+    const int k1 = k >= 1 ? k - 1 : 0;                // clamped: no branches
     Stage<STAGE_REC> sr;
-    Stage<STAGE_W1T> sw;
     sr.load(pi + (long long)k1 * RFL, RFL);
-    sw.load(pw + (long long)k2 * WTL, WTL);
-    hp_quarter(L, wt + (cur ^ 1) * WTL, ht, hpb + (cur ^ 1) * 1024);
+    const float hpk = hp_n;
+    hp_n = hpl[k1 * hps];
     float rr[RecF<NH>::USED];
     ld_rec<0, RecF<NH>::USED>(rr, rec + cur * RFL + j * L.RF);
     float za, zb;
@@ -621,13 +722,12 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse(BcnfLayout L, const float* 
     uint32_t bits = 0xffu;
     if (DROP) bits = dropout_bits(L, seed, off, bc, k, j, 0x40000000u);
     float T, Sp;
-    mlp_forward<NH, false>(L, rr, za, hp_sum(hpb + cur * 1024, s, j), bits, DROP, T, Sp, nullptr, nullptr);
+    mlp_forward<NH, false>(L, rr, za, hpk, bits, DROP, T, Sp, nullptr, nullptr);
     const float S = tanh_bf(Sp);
     const float ybn = (zb - T) * expf(-S);             // cnf.py:205
     ya = (j < Da) ? (za - rr[1]) / rr[0] : 0.f;        // ActNorm inverse (cnf.py:353-354); identity where none
     yb = (j < Db) ? (ybn - rr[3]) / rr[2] : 0.f;
     sr.store(rec + (cur ^ 1) * RFL, RFL);
-    sw.store(wt + cur * WTL, WTL);
     __syncthreads();
   }
   if (b < N) {
@@ -654,28 +754,31 @@ struct BwdTiles {   // tile indices inside one tile buffer
 
 // Gradient jobs of one block, built once per workgroup into LDS:
 //   W jobs   (NH + 2): dW of every Linear (the last one as its t and s row halves): 4 fp32 MFMAs over the
-//            workgroup's 16 samples, out[j][i] = sum_s delta[s][j] * act[s][i] ([16][17] LDS tiles)
+//            workgroup's 16 samples, out[j][i] = sum_s delta[s][j] * act[s][i] ([16][17] LDS tiles);
+//            for Linear 1 only the y-part columns (the condition part is the k_dw1h GEMM)
 //   sum jobs (NH + 2 + 4): bias and ActNorm gradients = column sums of a tile over the 16 samples (VALU +
 //            two cross-row permlane swaps; no MFMA against a ones tile)
-//   cond job (1): geometry of the W1 condition part (MFMA against the feature tile, column tiles of 16)
+// Output offsets are in the slab's compact block layout: canonical order without Linear 1's condition
+// columns, i.e. [ActNorm][W1y: H1 x Da][b1][Linear 2 ...] (k_reduce maps it back).
 struct GradDesc {
   int a_tile;   // float offset of the delta tile in the tile buffer
-  int b_tile;   // W jobs: offset of the activation tile; cond job: smem offset of the feature tile
-  int out;      // block-relative output offset of element (0, 0), coupling offset excluded
+  int b_tile;   // W jobs: offset of the activation tile
+  int out;      // compact block-relative output offset of element (0, 0), coupling offset excluded
   int rs;       // output row stride
-  int nrows;    // valid rows (W, cond) / valid elements (sum jobs)
+  int nrows;    // valid rows (W) / valid elements (sum jobs)
   int ncols;    // valid columns
   int flags;    // 1: coupling-relative (add the ActNorm size for blocks that have one), 2: ActNorm job
   int pad;
 };
 constexpr int GD_COUPLING = 1, GD_ACTNORM = 2;
-constexpr int MAX_JOBS = 2 * (BCNF_MAX_HIDDEN + 2) + 4 + 1;
+constexpr int MAX_JOBS = 2 * (BCNF_MAX_HIDDEN + 2) + 4;
 
 template <int NH>
-__device__ void build_jobs(const BcnfLayout& L, GradDesc* gd, int ht_abs) {
+__device__ void build_jobs(const BcnfLayout& L, GradDesc* gd) {
   const BwdTiles TI{NH};
   constexpr int NW = NH + 2, NS = NH + 6;
-  for (int c = threadIdx.x; c < NW + NS + 1; c += BCNF_WG) {
+  const int shift = L.H[1] * L.C;                       // canonical -> compact, past Linear 1's weight
+  for (int c = threadIdx.x; c < NW + NS; c += BCNF_WG) {
     GradDesc d;
     d.pad = 0;
     d.flags = GD_COUPLING;
@@ -687,28 +790,22 @@ __device__ void build_jobs(const BcnfLayout& L, GradDesc* gd, int ht_abs) {
       d.a_tile = TILE * ((c < NH) ? TI.D(l) : (c == NH ? TI.DT() : TI.DS()));
       d.b_tile = TILE * ((c < NH) ? TI.A(l - 1) : TI.A(NH));
       const int row0 = (c == NH + 1) ? L.Db : 0;
-      d.out = L.lin_w[l] + row0 * L.lin_in[l];
-      d.rs = L.lin_in[l];
+      d.rs = (l == 1) ? L.Da : L.lin_in[l];
+      d.out = ((l == 1) ? 0 : L.lin_w[l] - shift) + row0 * d.rs;
       d.nrows = (c < NH) ? L.H[l] : L.Db;
       d.ncols = (l == 1) ? L.Da : L.H[l - 1];
     } else if (c < NW + NH + 2) {                         // bias of Linear l (t half, s half)
       const int cc = c - NW;
       const int l = (cc < NH) ? cc + 1 : NH + 1;
       d.a_tile = TILE * ((cc < NH) ? TI.D(l) : (cc == NH ? TI.DT() : TI.DS()));
-      d.out = L.lin_b[l] + ((cc == NH + 1) ? L.Db : 0);
+      d.out = L.lin_b[l] - shift + ((cc == NH + 1) ? L.Db : 0);
       d.nrows = (cc < NH) ? L.H[l] : L.Db;
-    } else if (c < NW + NS) {                             // ActNorm scale_a, bias_a, scale_b, bias_b
+    } else {                                              // ActNorm scale_a, bias_a, scale_b, bias_b
       const int a = c - (NW + NH + 2);
       d.a_tile = TILE * ((a == 0) ? TI.PA() : (a == 1 ? TI.GA() : (a == 2 ? TI.PB() : TI.GB())));
       d.flags = GD_ACTNORM;
       d.out = ((a & 1) ? L.D : 0) + ((a < 2) ? 0 : L.Da);
       d.nrows = (a < 2) ? L.Da : L.Db;
-    } else {                                              // W1 condition part
-      d.a_tile = TILE * TI.D(1);
-      d.b_tile = ht_abs;
-      d.out = L.lin_w[1] + L.Da;
-      d.rs = L.lin_in[1];
-      d.nrows = L.H[1];
     }
     gd[c] = d;
   }
@@ -723,18 +820,15 @@ __device__ __forceinline__ float sum_rows4(float v) {
   return __uint_as_float(p2[0]) + __uint_as_float(p2[1]);
 }
 
-// MFMA phase of one block: every parameter gradient of block m into the LDS gradient block `gbuf`, and
-// the block's dh contribution into dhacc. Masked-off lanes store into a private dummy slot
-// (gbuf[blk_pad + lane]) so no store needs an exec-mask branch.
+// MFMA phase of one block: every parameter gradient of block m (except W1's condition part) into the
+// LDS gradient block `gbuf`. Masked-off lanes store into a private dummy slot (gbuf[blk_pad + lane]) so
+// no store needs an exec-mask branch.
 template <int NH>
-__device__ __forceinline__ void bwd_mfma_phase(const BcnfLayout& L, const float* __restrict__ smem,
+__device__ __forceinline__ void bwd_mfma_phase(const BcnfLayout& L,
                                                const float* __restrict__ T, const GradDesc* __restrict__ gd,
-                                               const float* __restrict__ wtm, float* __restrict__ gbuf, int m,
-                                               floatx4* dhacc) {
-  const BwdTiles TI{NH};
+                                               float* __restrict__ gbuf, int m) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int l64 = threadIdx.x & 63, q = l64 >> 4, r = l64 & 15;
-  const int NC16 = L.Cp >> 4;
   constexpr int NW = NH + 2, NS = NH + 6;
   constexpr int UW = (NW + 3) / 4, US = (NS + 3) / 4;
   const bool has_an = L.act_norm && m < L.nb - 1;
@@ -795,52 +889,6 @@ __device__ __forceinline__ void bwd_mfma_phase(const BcnfLayout& L, const float*
       *(ok ? gbuf + e[u].out + ((e[u].flags & GD_COUPLING) ? cpl : 0) + r : dummy) = tot;
     }
   }
-  // ---- W1 condition part (column tiles n = wave, wave + 4, ...) and dh[s][c] += sum_j D1[s][j] W1h_m[j][c]
-  const GradDesc dc = gd[NW + NS];
-  const float* D1 = T + TI.D(1) * TILE;
-  float d1a[4], d1t[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    d1a[t] = D1[(4 * t + q) * BCNF_TSTRIDE + r];         // A[s][j] for dW (K = samples)
-    d1t[t] = D1[r * BCNF_TSTRIDE + 4 * t + q];           // A[s][j] transposed for dh (K = neurons)
-  }
-  const int hs = L.Cp + 1;
-  const float* hb = smem + dc.b_tile;
-  const int base_c = dc.out + cpl + __mul24(4 * q, dc.rs) + r;
-#pragma unroll
-  for (int u = 0; u < 4; u += 2) {
-    const int n0 = wave + 4 * u, n1 = n0 + 4;
-    if (n0 >= NC16) break;                               // wave-uniform
-    const bool two = n1 < NC16;
-    const int n1c = two ? n1 : n0;
-    float b0[4], b1[4], w0[4], w1[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      b0[t] = hb[(4 * t + q) * hs + 16 * n0 + r];
-      b1[t] = hb[(4 * t + q) * hs + 16 * n1c + r];
-      w0[t] = wtm[(16 * n0 + r) * 17 + 4 * t + q];
-      w1[t] = wtm[(16 * n1c + r) * 17 + 4 * t + q];
-    }
-    floatx4 g0 = {0.f, 0.f, 0.f, 0.f}, g1 = {0.f, 0.f, 0.f, 0.f};
-    floatx4 h0 = dhacc[u], h1 = dhacc[u + 1];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      g0 = mfma4(d1a[t], b0[t], g0);
-      h0 = mfma4(d1t[t], w0[t], h0);
-      g1 = mfma4(d1a[t], b1[t], g1);
-      h1 = mfma4(d1t[t], w1[t], h1);     // without a second tile this accumulates into an unused slot
-    }
-    dhacc[u] = h0;
-    dhacc[u + 1] = h1;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const bool rowok = (4 * q + i < dc.nrows) && !(BCNF_EXP & 2);
-      const bool ok0 = rowok && 16 * n0 + r < L.C;
-      const bool ok1 = rowok && two && 16 * n1 + r < L.C;
-      *(ok0 ? gbuf + base_c + 16 * n0 + i * dc.rs : dummy) = g0[i];
-      *(ok1 ? gbuf + base_c + 16 * n1 + i * dc.rs : dummy) = g1[i];
-    }
-  }
 }
 
 // LDS gradient block (bwd_mfma_phase output) -> slab block m: CP4 unconditional float4 stores per thread
@@ -878,30 +926,26 @@ __device__ __forceinline__ void copy_out(const BcnfLayout& L, const float* __res
 
 template <int NH, int CP4>
 __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float* __restrict__ pk,
-                                                      const float* __restrict__ h, const float* __restrict__ dz,
+                                                      const float* __restrict__ hp, const float* __restrict__ dz,
                                                       const float* __restrict__ dldj, const float* __restrict__ dloss,
                                                       int nll, long long B,
                                                       const float* __restrict__ ysave, const uint32_t* __restrict__ msave,
-                                                      float* __restrict__ dy, float* __restrict__ dh,
+                                                      float* __restrict__ dy, float* __restrict__ d1,
                                                       float* __restrict__ slab_all, long long slab_stride) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const BwdTiles TI{NH};
-  const int RFL = 16 * L.RF, RBL = 16 * L.RB, WTL = L.Cp * 17;
+  const int RFL = 16 * L.RF, RBL = 16 * L.RB;
   const int NT = TI.count();
   float* recF = smem;                   // [2][16*RF]
   float* recB = recF + 2 * RFL;         // [2][16*RB]
-  float* wt = recB + 2 * RBL;           // [4][Cp*17]  W1h^T ring: block k-1 (HP), k+1 (dh) live at step k
-  float* hpb = wt + 4 * WTL;            // [2][4][256]
-  float* tiles = hpb + 2 * 1024;        // [2][NT][272]
+  float* tiles = recB + 2 * RBL;        // [2][NT][272]
   GradDesc* cd = reinterpret_cast<GradDesc*>(tiles + 2 * NT * TILE);   // [MAX_JOBS]
-  float* ht = tiles + 2 * NT * TILE + MAX_JOBS * 8;                      // [16][Cp+1]
-  float* gbuf = ht + 16 * (L.Cp + 1);                            // [blk_pad + 64] block gradient + dummies
+  float* gbuf = tiles + 2 * NT * TILE + MAX_JOBS * 8;                  // [blk_pad + 64] block gradient + dummies
   float exp_sink = 0.f;
   unsigned long long ph_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long ph_t = (BCNF_EXP & 128) ? __builtin_amdgcn_s_memtime() : 0ULL;
   const int tid = threadIdx.x, j = tid & 15, s = tid >> 4;
-  const int wave = tid >> 6, l64 = tid & 63, q = l64 >> 4, r = l64 & 15;
-  build_jobs<NH>(L, cd, (int)(ht - smem));
+  build_jobs<NH>(L, cd);
   const long long b = (long long)blockIdx.x * 16 + s;
   const bool valid = b < B;
   const long long bc = valid ? b : B - 1;
@@ -910,7 +954,9 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
   const bool drop = msave != nullptr;
   const float* pf = pk + L.pf_off;
   const float* pbk = pk + L.pb_off;
-  const float* pw = pk + L.w1t_off;
+  const float* hpl = hp + bc * 16 + j;              // HP[k][bc][j] = hpl[k * B * 16]
+  float* d1l = d1 + bc * 16 + j;                    // D1[k][b][j]  = d1l[k * B * 16]
+  const long long hps = B * 16;
 
   float gya = 0.f, gyb = 0.f, dl = 0.f;
   if (valid) {                                      // padded rows carry zero gradient
@@ -927,16 +973,16 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
       if (dldj) dl = dldj[b];
     }
   }
-  // saved input / dropout masks of the block about to be processed (prefetched one block ahead)
-  float ya_n, yb_n;
+  // saved input / dropout masks / projection of the block about to be processed (one block ahead)
+  float ya_n, yb_n, hp_n;
   uint32_t mw_n = 0xffffffffu;
   {
     const float* ys = ysave + ((long long)(nb - 1) * B + bc) * 32;
     ya_n = ys[j];
     yb_n = ys[16 + j];
+    hp_n = hpl[(nb - 1) * hps];
     if (drop) mw_n = msave[((long long)((nb - 1) >> 2) * B + bc) * 16 + j];
   }
-  stage_features(L, h, nullptr, B, ht);
   {
     const int kl = nb - 1;
     Stage<STAGE_REC> sr;
@@ -944,25 +990,13 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
     sr.store(recF + (kl & 1) * RFL, RFL);
     sr.load(pbk + (long long)kl * RBL, RBL);
     sr.store(recB + (kl & 1) * RBL, RBL);
-    Stage<STAGE_W1T> sw;
-    sw.load(pw + (long long)kl * WTL, WTL);
-    sw.store(wt + (kl & 3) * WTL, WTL);
-    const int km = kl >= 1 ? kl - 1 : 0;
-    sw.load(pw + (long long)km * WTL, WTL);
-    sw.store(wt + (km & 3) * WTL, WTL);
   }
   __syncthreads();
-  hp_quarter(L, wt + ((nb - 1) & 3) * WTL, ht, hpb + ((nb - 1) & 1) * 1024);
-  __syncthreads();
-
-  floatx4 dhacc[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) dhacc[u] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   for (int k = nb - 1; k >= 0; --k) {
     const int cur = k & 1;
-    const int k1 = k >= 1 ? k - 1 : 0, k2 = k >= 2 ? k - 2 : 0;   // clamped: no branches
-    const float ya = ya_n, yb = yb_n;
+    const int k1 = k >= 1 ? k - 1 : 0;               // clamped: no branches
+    const float ya = ya_n, yb = yb_n, hpk = hp_n;
     const uint32_t mword = mw_n;
     // (0) gradient block k+2 (MFMA phase of the previous iteration) LDS -> slab, before any load of
     // this iteration is issued; then the MFMA phase below may overwrite the LDS block
@@ -971,25 +1005,22 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
       __syncthreads();
     }
     PH(0)
-    // (a) prefetch: next records, W1h^T two blocks ahead, next block's saved input / masks
+    // (a) prefetch: next records and the next block's saved input / masks / projection
     Stage<STAGE_REC> sF, sB;
-    Stage<STAGE_W1T> sw;
     sF.load(pf + (long long)k1 * RFL, RFL);
     sB.load(pbk + (long long)k1 * RBL, RBL);
-    sw.load(pw + (long long)k2 * WTL, WTL);
     {
       const float* ys = ysave + ((long long)k1 * B + bc) * 32;
       ya_n = ys[j];
       yb_n = ys[16 + j];
+      hp_n = hpl[k1 * hps];
       if (drop) mw_n = msave[((long long)(k1 >> 2) * B + bc) * 16 + j];
     }
     PH(1)
-    // (b) MFMA phase: parameter gradients + dh of block k+1, HP of block k-1
+    // (b) MFMA phase: parameter gradients of block k+1
     if (k + 1 < nb && !(BCNF_EXP & 4))
-      bwd_mfma_phase<NH>(L, smem, tiles + ((k + 1) & 1) * NT * TILE, cd, wt + ((k + 1) & 3) * WTL, gbuf, k + 1,
-                         dhacc);
+      bwd_mfma_phase<NH>(L, tiles + ((k + 1) & 1) * NT * TILE, cd, gbuf, k + 1);
     PH(2)
-    hp_quarter(L, wt + (k1 & 3) * WTL, ht, hpb + (cur ^ 1) * 1024);
     PH(3)
     // (c) VALU phase: recompute block k, then back-propagate through it
     float* Tt = tiles + cur * NT * TILE;
@@ -1004,7 +1035,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
     float act[NH], gd[NH];
     float T, Sp;
     PH(4)
-    mlp_forward<NH, true>(L, rf, xa, hp_sum(hpb + cur * 1024, s, j), bits, drop, T, Sp, act, gd);
+    mlp_forward<NH, true>(L, rf, xa, hpk, bits, drop, T, Sp, act, gd);
     PH(5)
     const float S = tanh_bf(Sp);
     const float e = expf(S);
@@ -1030,6 +1061,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
     const float dpre1 = da * gd[0];
     Tt[TI.D(1) * TILE + tix] = dpre1;
     Tt[TI.A(0) * TILE + tix] = xa;
+    if (valid) d1l[k * hps] = dpre1;                   // dL/d pre-activation of Linear 1 (k_dh, k_dw1h)
     const float dxa = rot16(dpre1, rb + RBk::W1T, gza);
     {   // ActNorm tiles (consumed only for blocks that have an ActNorm)
       const float inv_a = (j < Da) ? __builtin_amdgcn_rcpf(rf[0]) : 0.f;
@@ -1045,7 +1077,6 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
     // (d) commit prefetched records (past the end they refill buffers nobody reads)
     sF.store(recF + (cur ^ 1) * RFL, RFL);
     sB.store(recB + (cur ^ 1) * RBL, RBL);
-    if (k >= 2) sw.store(wt + (k2 & 3) * WTL, WTL);
     PH(7)
     __syncthreads();
     PH(8)
@@ -1056,7 +1087,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
     copy_out<CP4>(L, gbuf, slab, 1, exp_sink);
     __syncthreads();
   }
-  bwd_mfma_phase<NH>(L, smem, tiles, cd, wt, gbuf, 0, dhacc);
+  bwd_mfma_phase<NH>(L, tiles, cd, gbuf, 0);
   __syncthreads();
   copy_out<CP4>(L, gbuf, slab, 0, exp_sink);
   if ((BCNF_EXP & 64) && exp_sink == 1234.5f) g_exp_sink = exp_sink;
@@ -1064,53 +1095,56 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
     if (j < Da) dy[b * D + j] = gya;
     if (j < Db) dy[b * D + Da + j] = gyb;
   }
-  if (dh) {
-    const int NC16 = L.Cp >> 4;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int n = wave + 4 * u;
-      const int col = 16 * n + r;
-      if (n < NC16 && col < L.C) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const long long bb = (long long)blockIdx.x * 16 + 4 * q + i;
-          if (bb < B) dh[bb * L.C + col] = dhacc[u][i];
-        }
-      }
-    }
-  }
 }
 
-// Deterministic sum of the per-workgroup gradient slabs (fixed order over workgroups). The slab holds
-// block m's canonical parameters [m * blk_stride, m * blk_stride + size_m) at [m * blk_pad, ...).
+// Deterministic sum of the per-workgroup gradient slabs (fixed order over workgroups). Slab block m holds
+// block m's parameters in the compact layout [ActNorm][W1y: H1 x Da][b1][Linear 2 ...] at [m * blk_pad, ...);
+// this maps them back to canonical positions (W1's condition columns come from k_dw1h_reduce).
+__device__ __forceinline__ long long compact_to_canonical(const BcnfLayout& L, int m, int o) {
+  const int an = (m < L.nb - 1) ? L.an_size : 0;
+  long long rel;
+  if (o < an) {
+    rel = o;
+  } else {
+    const int c = o - an, w1y = L.H[1] * L.Da;
+    if (c < w1y) {
+      const int j = c / L.Da, i = c - j * L.Da;
+      rel = an + j * L.lin_in[1] + i;
+    } else {
+      rel = an + c + L.H[1] * L.C;
+    }
+  }
+  return (long long)m * L.blk_stride + rel;
+}
+
+// 64 output float4 per workgroup x 4 slab groups (group g sums workgroups g, g+4, ...; 8 loads in flight),
+// combined in a fixed order through LDS.
 __global__ __launch_bounds__(BCNF_WG) void k_reduce(BcnfLayout L, const float* __restrict__ slab, long long stride,
                                                     int nwg, float* __restrict__ out) {
-  const long long i = ((long long)blockIdx.x * BCNF_WG + threadIdx.x) * 4;
-  if (i >= stride) return;
+  __shared__ floatx4 part[4][64];
+  const int g = threadIdx.x >> 6, o4 = threadIdx.x & 63;
+  const long long i = ((long long)blockIdx.x * 64 + o4) * 4;
+  const bool live = i < stride;
+  const long long ic = live ? i : 0;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  int w = g;
+  for (; w + 28 < nwg; w += 32) {
+    floatx4 v[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = *reinterpret_cast<const floatx4*>(slab + (long long)(w + 4 * t) * stride + ic);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc += v[t];
+  }
+  for (; w < nwg; w += 4) acc += *reinterpret_cast<const floatx4*>(slab + (long long)w * stride + ic);
+  part[g][o4] = acc;
+  __syncthreads();
+  if (g != 0 || !live) return;
+  const floatx4 tot = ((part[0][o4] + part[1][o4]) + part[2][o4]) + part[3][o4];
   const int m = (int)(i / L.blk_pad), o = (int)(i - (long long)m * L.blk_pad);
-  const int size_m = (m < L.nb - 1) ? L.blk_stride : L.blk_stride - L.an_size;
-  if (o >= size_m) return;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  int w = 0;
-  for (; w + 4 <= nwg; w += 4) {
-    const float4 v0 = *reinterpret_cast<const float4*>(slab + (long long)(w + 0) * stride + i);
-    const float4 v1 = *reinterpret_cast<const float4*>(slab + (long long)(w + 1) * stride + i);
-    const float4 v2 = *reinterpret_cast<const float4*>(slab + (long long)(w + 2) * stride + i);
-    const float4 v3 = *reinterpret_cast<const float4*>(slab + (long long)(w + 3) * stride + i);
-    acc.x += v0.x; acc.y += v0.y; acc.z += v0.z; acc.w += v0.w;
-    acc.x += v1.x; acc.y += v1.y; acc.z += v1.z; acc.w += v1.w;
-    acc.x += v2.x; acc.y += v2.y; acc.z += v2.z; acc.w += v2.w;
-    acc.x += v3.x; acc.y += v3.y; acc.z += v3.z; acc.w += v3.w;
-  }
-  for (; w < nwg; ++w) {
-    const float4 v = *reinterpret_cast<const float4*>(slab + (long long)w * stride + i);
-    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-  }
-  float* dst = out + (long long)m * L.blk_stride + o;
-  dst[0] = acc.x;
-  if (o + 1 < size_m) dst[1] = acc.y;
-  if (o + 2 < size_m) dst[2] = acc.z;
-  if (o + 3 < size_m) dst[3] = acc.w;
+  const int size_m = L.cblk - ((m < L.nb - 1) ? 0 : L.an_size);
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (o + e < size_m) out[compact_to_canonical(L, m, o + e)] = tot[e];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1176,8 +1210,13 @@ struct NllOut {
   uint64_t* rng_w = nullptr;
 };
 
+int launch_hp(const BcnfLayout& L, const float* pk, const float* h, long long R, float* hp, hipStream_t st) {
+  hipLaunchKernelGGL(k_hp, dim3((unsigned)((R + 15) / 16)), dim3(BCNF_WG), 0, st, L, pk, h, R, hp);
+  return check_launch();
+}
+
 template <int NH>
-int fwd_dispatch(const BcnfLayout& L, const float* pk, const float* y, const float* h, long long B, float* z,
+int fwd_dispatch(const BcnfLayout& L, const float* pk, const float* y, const float* hp, long long B, float* z,
                  float* ldj, float* logp, bool drop, const uint64_t* rng, float* ysave, uint32_t* msave,
                  const NllOut& no, hipStream_t st) {
   if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
@@ -1186,9 +1225,9 @@ int fwd_dispatch(const BcnfLayout& L, const float* pk, const float* y, const flo
   const bool save = ysave != nullptr;
   int rc;
 #define BCNF_FWD(DR, SV)                                                                                    \
-  rc = launch_lds(k_forward<NH, DR, SV>, lds);                                                    \
+  rc = launch_lds(k_forward<NH, DR, SV>, lds);                                                              \
   if (rc) return rc;                                                                                        \
-  hipLaunchKernelGGL((k_forward<NH, DR, SV>), grid, dim3(BCNF_WG), lds, st, L, pk, y, h, B, z, ldj, logp,   \
+  hipLaunchKernelGGL((k_forward<NH, DR, SV>), grid, dim3(BCNF_WG), lds, st, L, pk, y, hp, B, z, ldj, logp,  \
                      rng, ysave, msave, no.part, no.sync, no.loss, no.rng_w);
   if (drop) {
     if (save) { BCNF_FWD(true, true) } else { BCNF_FWD(true, false) }
@@ -1200,8 +1239,8 @@ int fwd_dispatch(const BcnfLayout& L, const float* pk, const float* y, const flo
 }
 
 template <int NH>
-int inv_dispatch(const BcnfLayout& L, const float* pk, const float* zin, const float* h, const int64_t* ci,
-                 long long N, float* y, bool drop, const uint64_t* rng, hipStream_t st) {
+int inv_dispatch(const BcnfLayout& L, const float* pk, const float* zin, const float* hp, long long R,
+                 const int64_t* ci, long long N, float* y, bool drop, const uint64_t* rng, hipStream_t st) {
   if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
   const dim3 grid((unsigned)((N + 15) / 16));
   size_t lds = fwd_lds_bytes(L);
@@ -1209,19 +1248,19 @@ int inv_dispatch(const BcnfLayout& L, const float* pk, const float* zin, const f
   if (drop) {
     rc = launch_lds(k_inverse<NH, true>, lds);
     if (rc) return rc;
-    hipLaunchKernelGGL((k_inverse<NH, true>), grid, dim3(BCNF_WG), lds, st, L, pk, zin, h, ci, N, y, rng);
+    hipLaunchKernelGGL((k_inverse<NH, true>), grid, dim3(BCNF_WG), lds, st, L, pk, zin, hp, R, ci, N, y, rng);
   } else {
     rc = launch_lds(k_inverse<NH, false>, lds);
     if (rc) return rc;
-    hipLaunchKernelGGL((k_inverse<NH, false>), grid, dim3(BCNF_WG), lds, st, L, pk, zin, h, ci, N, y, rng);
+    hipLaunchKernelGGL((k_inverse<NH, false>), grid, dim3(BCNF_WG), lds, st, L, pk, zin, hp, R, ci, N, y, rng);
   }
   return check_launch();
 }
 
 template <int NH>
-int bwd_dispatch(const BcnfLayout& L, const float* pk, const float* h, const float* dz, const float* dldj,
+int bwd_dispatch(const BcnfLayout& L, const float* pk, const float* hp, const float* dz, const float* dldj,
                  const float* dloss, int nll, long long B, const float* ysave, const uint32_t* msave, float* dy,
-                 float* dh, float* slab, long long stride, hipStream_t st) {
+                 float* d1, float* slab, long long stride, hipStream_t st) {
   if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
   const dim3 grid((unsigned)((B + 15) / 16));
   size_t lds = bwd_lds_bytes(L);
@@ -1229,8 +1268,8 @@ int bwd_dispatch(const BcnfLayout& L, const float* pk, const float* h, const flo
 #define BCNF_BWD(CP)                                                                                      \
   rc = launch_lds(k_backward<NH, CP>, lds);                                                               \
   if (rc) return rc;                                                                                      \
-  hipLaunchKernelGGL((k_backward<NH, CP>), grid, dim3(BCNF_WG), lds, st, L, pk, h, dz, dldj, dloss, nll, B, \
-                     ysave, msave, dy, dh, slab, stride);
+  hipLaunchKernelGGL((k_backward<NH, CP>), grid, dim3(BCNF_WG), lds, st, L, pk, hp, dz, dldj, dloss, nll, B, \
+                     ysave, msave, dy, d1, slab, stride);
   if (copy4_of(L) == 4) { BCNF_BWD(4) } else { BCNF_BWD(8) }
 #undef BCNF_BWD
   return check_launch();
@@ -1238,45 +1277,56 @@ int bwd_dispatch(const BcnfLayout& L, const float* pk, const float* h, const flo
 
 long long slab_stride_of(const BcnfLayout& L) { return (long long)L.nb * L.blk_pad; }
 
-// Workspace: [saved block inputs nb*B*32][dropout masks ceil(nb/4)*B*16 u32, if dropout][loss partials]
+// split-K geometry of the W1 condition-part gradient
+int w1h_rows_per_split(long long B) {   // <= 8 splits of >= 256 rows
+  long long r = (B + 7) / 8;
+  if (r < 256) r = 256;
+  return (int)((r + 15) & ~15LL);
+}
+long long w1h_splits(long long B) { return (B + w1h_rows_per_split(B) - 1) / w1h_rows_per_split(B); }
+long long w1h_work_floats(const BcnfLayout& L, long long B) { return w1h_splits(B) * L.nb * 16LL * L.Cp; }
+
+// Workspace (floats): [saved block inputs nb*B*32][dropout masks ceil(nb/4)*B*16 u32, if dropout]
+//                     [loss partials][HP nb*B*16][D1 nb*B*16]
 long long ws_mask_off(const BcnfLayout& L, long long B) { return (long long)L.nb * B * 32; }
 long long ws_part_off(const BcnfLayout& L, long long B, bool drop) {
   return ws_mask_off(L, B) + (drop ? (long long)((L.nb + 3) / 4) * B * 16 : 0);
 }
-long long ws_floats(const BcnfLayout& L, long long B, bool drop) {
+long long ws_hp_off(const BcnfLayout& L, long long B, bool drop) {
   return ws_part_off(L, B, drop) + (((B + 15) / 16 + 3) & ~3LL);
 }
+long long ws_d1_off(const BcnfLayout& L, long long B, bool drop) { return ws_hp_off(L, B, drop) + (long long)L.nb * B * 16; }
+long long ws_floats(const BcnfLayout& L, long long B, bool drop) { return ws_d1_off(L, B, drop) + (long long)L.nb * B * 16; }
 
 int forward_impl(const BcnfStackDesc* desc, const void* packed, const float* y, const float* h, int64_t batch,
                  float* z, float* ldj, float* log_prob, int32_t training, const uint64_t* rng_state, void* workspace,
-                 bool nll, unsigned* sync, float* loss_out, void* stream) {
+                 bool save, bool nll, unsigned* sync, float* loss_out, void* stream) {
   BcnfLayout L;
-  const int rc = make_layout(desc, &L);
+  int rc = make_layout(desc, &L);
   if (rc) return rc;
   if (!layout_supported(L, desc)) return BCNF_ERR_UNSUPPORTED;
   if (batch < 0) return BCNF_ERR_ARG;
   if (batch == 0) return nll ? BCNF_ERR_ARG : BCNF_OK;      // the mean over an empty batch is undefined
-  if (!packed || !y || !h || !z) return BCNF_ERR_ARG;
-  if (nll && (!workspace || !sync || !loss_out)) return BCNF_ERR_ARG;
+  if (!packed || !y || !h || !z || !workspace) return BCNF_ERR_ARG;
+  if (nll && (!sync || !loss_out)) return BCNF_ERR_ARG;
   const bool drop = training && L.p > 0.f;
   if (drop && !rng_state) return BCNF_ERR_ARG;
-  float* ysave = nullptr;
-  uint32_t* msave = nullptr;
+  float* ws = (float*)workspace;
+  float* ysave = (save || nll) ? ws : nullptr;
+  uint32_t* msave = (ysave && drop) ? (uint32_t*)(ws + ws_mask_off(L, batch)) : nullptr;
+  float* hp = ws + ws_hp_off(L, batch, drop);
   NllOut no;
-  if (workspace) {
-    ysave = (float*)workspace;
-    if (drop) msave = (uint32_t*)(ysave + ws_mask_off(L, batch));
-    if (nll) {
-      no.part = ysave + ws_part_off(L, batch, drop);
-      no.sync = sync;
-      no.loss = loss_out;
-      no.rng_w = drop ? const_cast<uint64_t*>(rng_state) : nullptr;
-    }
+  if (nll) {
+    no.part = ws + ws_part_off(L, batch, drop);
+    no.sync = sync;
+    no.loss = loss_out;
+    no.rng_w = drop ? const_cast<uint64_t*>(rng_state) : nullptr;
   }
   const float* pk = (const float*)packed;
   hipStream_t st = (hipStream_t)stream;
+  if ((rc = launch_hp(L, pk, h, batch, hp, st))) return rc;
   switch (L.NH) {
-#define BCNF_CASE(N) case N: return fwd_dispatch<N>(L, pk, y, h, batch, z, ldj, log_prob, drop, rng_state, ysave, msave, no, st);
+#define BCNF_CASE(N) case N: return fwd_dispatch<N>(L, pk, y, hp, batch, z, ldj, log_prob, drop, rng_state, ysave, msave, no, st);
     BCNF_CASE(1) BCNF_CASE(2) BCNF_CASE(3) BCNF_CASE(4) BCNF_CASE(5) BCNF_CASE(6) BCNF_CASE(7) BCNF_CASE(8)
 #undef BCNF_CASE
     default: return BCNF_ERR_UNSUPPORTED;
@@ -1284,7 +1334,7 @@ int forward_impl(const BcnfStackDesc* desc, const void* packed, const float* y, 
 }
 
 int backward_impl(const BcnfStackDesc* desc, const void* packed, const float* h, const float* dz, const float* dldj,
-                  const float* dloss, int nll, int64_t batch, int32_t training, const void* workspace, float* dy,
+                  const float* dloss, int nll, int64_t batch, int32_t training, void* workspace, float* dy,
                   float* dh, float* dparams, void* slab, void* stream);
 
 }  // namespace
@@ -1332,7 +1382,16 @@ int bcnf_slab_bytes(const BcnfStackDesc* desc, int64_t batch, int64_t* bytes) {
   const int rc = make_layout(desc, &L);
   if (rc) return rc;
   if (!bytes || batch < 0) return BCNF_ERR_ARG;
-  *bytes = (int64_t)((batch + 15) / 16) * slab_stride_of(L) * 4;
+  *bytes = ((int64_t)((batch + 15) / 16) * slab_stride_of(L) + w1h_work_floats(L, batch)) * 4;
+  return BCNF_OK;
+}
+
+int bcnf_inverse_scratch_bytes(const BcnfStackDesc* desc, int64_t h_rows, int64_t* bytes) {
+  BcnfLayout L;
+  const int rc = make_layout(desc, &L);
+  if (rc) return rc;
+  if (!bytes || h_rows < 0) return BCNF_ERR_ARG;
+  *bytes = (int64_t)L.nb * h_rows * 16 * 4;
   return BCNF_OK;
 }
 
@@ -1349,60 +1408,78 @@ int bcnf_pack_params(const BcnfStackDesc* desc, const float* params, const float
 
 int bcnf_stack_forward(const BcnfStackDesc* desc, const void* packed, const float* y, const float* h, int64_t batch,
                        float* z, float* ldj, float* log_prob, int32_t training, const uint64_t* rng_state,
-                       void* workspace, void* stream) {
-  return forward_impl(desc, packed, y, h, batch, z, ldj, log_prob, training, rng_state, workspace, false, nullptr,
-                      nullptr, stream);
+                       void* workspace, int32_t save, void* stream) {
+  return forward_impl(desc, packed, y, h, batch, z, ldj, log_prob, training, rng_state, workspace, save != 0, false,
+                      nullptr, nullptr, stream);
 }
 
 int bcnf_nll_forward(const BcnfStackDesc* desc, const void* packed, const float* y, const float* h, int64_t batch,
                      float* z, float* ldj, int32_t training, uint64_t* rng_state, void* workspace, uint32_t* sync,
                      float* loss_out, void* stream) {
-  return forward_impl(desc, packed, y, h, batch, z, ldj, nullptr, training, rng_state, workspace, true,
+  return forward_impl(desc, packed, y, h, batch, z, ldj, nullptr, training, rng_state, workspace, true, true,
                       (unsigned*)sync, loss_out, stream);
 }
 
 int bcnf_stack_backward(const BcnfStackDesc* desc, const void* packed, const float* h, const float* dz,
-                        const float* dldj, int64_t batch, int32_t training, const void* workspace, float* dy,
+                        const float* dldj, int64_t batch, int32_t training, void* workspace, float* dy,
                         float* dh, float* dparams, void* slab, void* stream) {
   return backward_impl(desc, packed, h, dz, dldj, nullptr, 0, batch, training, workspace, dy, dh, dparams, slab,
                        stream);
 }
 
 int bcnf_nll_backward(const BcnfStackDesc* desc, const void* packed, const float* h, const float* z,
-                      const float* dloss, int64_t batch, int32_t training, const void* workspace, float* dy,
+                      const float* dloss, int64_t batch, int32_t training, void* workspace, float* dy,
                       float* dh, float* dparams, void* slab, void* stream) {
   if (!z && batch > 0) return BCNF_ERR_ARG;
   return backward_impl(desc, packed, h, z, nullptr, dloss, 1, batch, training, workspace, dy, dh, dparams, slab,
                        stream);
 }
 
-int bcnf_grad_reduce(const BcnfStackDesc* desc, const void* slab, int64_t batch, float* dparams, void* stream) {
+int bcnf_grad_reduce(const BcnfStackDesc* desc, const void* slab, const float* h, const void* workspace,
+                     int64_t batch, int32_t training, float* dparams, void* stream) {
   BcnfLayout L;
-  const int rc = make_layout(desc, &L);
+  int rc = make_layout(desc, &L);
   if (rc) return rc;
-  if (!slab || !dparams || batch < 1) return BCNF_ERR_ARG;
+  if (!slab || !h || !workspace || !dparams || batch < 1) return BCNF_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
   const long long S = slab_stride_of(L);
-  const unsigned nblk = (unsigned)((S / 4 + BCNF_WG - 1) / BCNF_WG);
-  hipLaunchKernelGGL(k_reduce, dim3(nblk), dim3(BCNF_WG), 0, (hipStream_t)stream, L, (const float*)slab, S,
-                     (int)((batch + 15) / 16), dparams);
+  const int nwg = (int)((batch + 15) / 16);
+  hipLaunchKernelGGL(k_reduce, dim3((unsigned)((S / 4 + 63) / 64)), dim3(BCNF_WG), 0, st, L, (const float*)slab, S,
+                     nwg, dparams);
+  if ((rc = check_launch())) return rc;
+  // W1 condition columns: split-K GEMM over the batch, then a fixed-order reduce
+  const bool drop = training && L.p > 0.f;
+  const float* d1 = (const float*)workspace + ws_d1_off(L, batch, drop);
+  float* work = (float*)slab + (long long)nwg * S;
+  const int rps = w1h_rows_per_split(batch);
+  const long long splits = w1h_splits(batch);
+  hipLaunchKernelGGL(k_dw1h, dim3((unsigned)L.nb, (unsigned)splits), dim3(BCNF_WG), 0, st, L, d1, h, (long long)batch,
+                     rps, work);
+  if ((rc = check_launch())) return rc;
+  const long long outs = (long long)L.nb * 16 * L.Cp;
+  hipLaunchKernelGGL(k_dw1h_reduce, dim3((unsigned)((outs + BCNF_WG - 1) / BCNF_WG)), dim3(BCNF_WG), 0, st, L,
+                     (const float*)work, (int)splits, dparams);
   return check_launch();
 }
 
-int bcnf_stack_inverse(const BcnfStackDesc* desc, const void* packed, const float* z, const float* h,
+int bcnf_stack_inverse(const BcnfStackDesc* desc, const void* packed, const float* z, const float* h, int64_t h_rows,
                        const int64_t* cond_index, int64_t n_rows, float* y, int32_t training,
-                       const uint64_t* rng_state, void* stream) {
+                       const uint64_t* rng_state, void* scratch, void* stream) {
   BcnfLayout L;
-  const int rc = make_layout(desc, &L);
+  int rc = make_layout(desc, &L);
   if (rc) return rc;
   if (!layout_supported(L, desc)) return BCNF_ERR_UNSUPPORTED;
   if (n_rows == 0) return BCNF_OK;
-  if (n_rows < 0 || !packed || !z || !h || !y) return BCNF_ERR_ARG;
+  if (n_rows < 0 || h_rows < 1 || !packed || !z || !h || !y || !scratch) return BCNF_ERR_ARG;
+  if (!cond_index && h_rows != n_rows) return BCNF_ERR_ARG;
   const bool drop = training && L.p > 0.f;
   if (drop && !rng_state) return BCNF_ERR_ARG;
   const float* pk = (const float*)packed;
   hipStream_t st = (hipStream_t)stream;
+  float* hp = (float*)scratch;
+  if ((rc = launch_hp(L, pk, h, h_rows, hp, st))) return rc;
   switch (L.NH) {
-#define BCNF_CASE(N) case N: return inv_dispatch<N>(L, pk, z, h, cond_index, n_rows, y, drop, rng_state, st);
+#define BCNF_CASE(N) case N: return inv_dispatch<N>(L, pk, z, hp, h_rows, cond_index, n_rows, y, drop, rng_state, st);
     BCNF_CASE(1) BCNF_CASE(2) BCNF_CASE(3) BCNF_CASE(4) BCNF_CASE(5) BCNF_CASE(6) BCNF_CASE(7) BCNF_CASE(8)
 #undef BCNF_CASE
     default: return BCNF_ERR_UNSUPPORTED;
@@ -1432,7 +1509,7 @@ int bcnf_debug_phases(unsigned long long* out) {
 namespace {
 
 int backward_impl(const BcnfStackDesc* desc, const void* packed, const float* h, const float* dz, const float* dldj,
-                  const float* dloss, int nll, int64_t batch, int32_t training, const void* workspace, float* dy,
+                  const float* dloss, int nll, int64_t batch, int32_t training, void* workspace, float* dy,
                   float* dh, float* dparams, void* slab, void* stream) {
   BcnfLayout L;
   int rc = make_layout(desc, &L);
@@ -1447,21 +1524,28 @@ int backward_impl(const BcnfStackDesc* desc, const void* packed, const float* h,
   }
   // `training` must match the forward call that filled the workspace: it says whether dropout masks
   // were saved behind the block inputs.
-  const float* ysave = (const float*)workspace;
-  const uint32_t* msave = nullptr;
-  if (training && L.p > 0.f) msave = (const uint32_t*)(ysave + ws_mask_off(L, batch));
+  const bool drop = training && L.p > 0.f;
+  float* ws = (float*)workspace;
+  const float* ysave = ws;
+  const uint32_t* msave = drop ? (const uint32_t*)(ws + ws_mask_off(L, batch)) : nullptr;
+  const float* hp = ws + ws_hp_off(L, batch, drop);
+  float* d1 = ws + ws_d1_off(L, batch, drop);
   const float* pk = (const float*)packed;
   const long long stride = slab_stride_of(L);
   switch (L.NH) {
-#define BCNF_CASE(N) case N: rc = bwd_dispatch<N>(L, pk, h, dz, dldj, dloss, nll, batch, ysave, msave, dy, dh, (float*)slab, stride, st); break;
+#define BCNF_CASE(N) case N: rc = bwd_dispatch<N>(L, pk, hp, dz, dldj, dloss, nll, batch, ysave, msave, dy, d1, (float*)slab, stride, st); break;
     BCNF_CASE(1) BCNF_CASE(2) BCNF_CASE(3) BCNF_CASE(4) BCNF_CASE(5) BCNF_CASE(6) BCNF_CASE(7) BCNF_CASE(8)
 #undef BCNF_CASE
     default: return BCNF_ERR_UNSUPPORTED;
   }
   if (rc) return rc;
+  if (dh) {   // dL/dh = sum_k D1_k W1h_k
+    hipLaunchKernelGGL(k_dh, dim3((unsigned)((batch + 15) / 16)), dim3(BCNF_WG), 0, st, L, pk, (const float*)d1,
+                       (long long)batch, dh);
+    if ((rc = check_launch())) return rc;
+  }
   if (!dparams) return BCNF_OK;   // caller reduces with bcnf_grad_reduce
-  return bcnf_grad_reduce(desc, slab, batch, dparams, stream);
+  return bcnf_grad_reduce(desc, slab, h, workspace, batch, training, dparams, stream);
 }
 
 }  // namespace
-

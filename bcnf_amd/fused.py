@@ -210,10 +210,8 @@ class FusedStack:
         logp = torch.empty(B, dtype=torch.float32, device=dev) if want_logp else None
         drop = training and self.cfg.dropout > 0.0
         rng = self.rng_state() if drop else None
-        ws = None
-        if save:
-            wb, _ = self.workspace_bytes(B, training)
-            ws = torch.empty(max(wb // 4, 1), dtype=torch.float32, device=dev)
+        wb, _ = self.workspace_bytes(B, training)      # also holds the condition projection
+        ws = torch.empty(max(wb // 4, 1), dtype=torch.float32, device=dev)
         pk = self.packed(fresh=save)
         tm = self.timers
         if tm is not None:
@@ -222,7 +220,7 @@ class FusedStack:
             e0.record()
         rc = N.lib().bcnf_stack_forward(self._pdesc, N.ptr(pk), N.ptr(y), N.ptr(h), ctypes.c_int64(B), N.ptr(z),
                                         N.ptr(ldj), N.ptr(logp), ctypes.c_int32(int(training)), N.ptr(rng), N.ptr(ws),
-                                        N.stream_handle(dev))
+                                        ctypes.c_int32(int(save)), N.stream_handle(dev))
         N.check(rc, "bcnf_stack_forward")
         if tm is not None:
             e1.record()
@@ -253,8 +251,8 @@ class FusedStack:
         N.check(rc, "bcnf_stack_backward")
         if tm is not None:
             e1.record()
-        N.check(N.lib().bcnf_grad_reduce(self._pdesc, N.ptr(slab), ctypes.c_int64(B), N.ptr(dparams), stream),
-                "bcnf_grad_reduce")
+        N.check(N.lib().bcnf_grad_reduce(self._pdesc, N.ptr(slab), N.ptr(h), N.ptr(ws), ctypes.c_int64(B),
+                                         ctypes.c_int32(int(training)), N.ptr(dparams), stream), "bcnf_grad_reduce")
         if tm is not None:
             e2.record()
             tm.setdefault("k_backward", []).append((e0, e1))
@@ -321,8 +319,8 @@ class FusedStack:
         N.check(rc, "bcnf_nll_backward")
         if tm is not None:
             e1.record()
-        N.check(N.lib().bcnf_grad_reduce(self._pdesc, N.ptr(slab), ctypes.c_int64(B), N.ptr(dparams), stream),
-                "bcnf_grad_reduce")
+        N.check(N.lib().bcnf_grad_reduce(self._pdesc, N.ptr(slab), N.ptr(h), N.ptr(ws), ctypes.c_int64(B),
+                                         ctypes.c_int32(int(training)), N.ptr(dparams), stream), "bcnf_grad_reduce")
         if tm is not None:
             e2.record()
             tm.setdefault("k_backward", []).append((e0, e1))
@@ -339,9 +337,12 @@ class FusedStack:
         rng = self.rng_state() if drop else None
         if cond_index is not None:
             cond_index = cond_index.to(device=z.device, dtype=torch.int64).contiguous()
-        rc = N.lib().bcnf_stack_inverse(self._pdesc, N.ptr(self.packed()), N.ptr(z), N.ptr(h), N.ptr(cond_index),
-                                        ctypes.c_int64(n), N.ptr(y), ctypes.c_int32(int(training)), N.ptr(rng),
-                                        N.stream_handle(z.device))
+        hr = h.shape[0]
+        sb = N.query_i64(N.lib().bcnf_inverse_scratch_bytes, self._pdesc, ctypes.c_int64(hr))
+        scratch = torch.empty(max(sb // 4, 1), dtype=torch.float32, device=z.device)
+        rc = N.lib().bcnf_stack_inverse(self._pdesc, N.ptr(self.packed()), N.ptr(z), N.ptr(h), ctypes.c_int64(hr),
+                                        N.ptr(cond_index), ctypes.c_int64(n), N.ptr(y), ctypes.c_int32(int(training)),
+                                        N.ptr(rng), N.ptr(scratch), N.stream_handle(z.device))
         N.check(rc, "bcnf_stack_inverse")
         if drop:
             rng[1:2].add_(1)

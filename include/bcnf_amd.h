@@ -72,12 +72,17 @@ int bcnf_param_count(const BcnfStackDesc* desc, int64_t* n_trainable, int64_t* n
 /* Bytes of the packed-parameter buffer written by bcnf_pack_params. */
 int bcnf_packed_bytes(const BcnfStackDesc* desc, int64_t* bytes);
 
-/* Bytes of the forward->backward workspace (saved block inputs + dropout masks + per-workgroup
- * loss partials) for a batch. */
+/* Bytes of the forward->backward workspace for a batch: saved block inputs, dropout masks, loss
+ * partials, the hoisted condition projection HP[k][b][16] = h W1h_k^T + b1_k and the Linear-1 deltas
+ * D1[k][b][16] written by the backward. Required by every forward and backward call. */
 int bcnf_workspace_bytes(const BcnfStackDesc* desc, int64_t batch, int32_t training, int64_t* bytes);
 
-/* Bytes of the per-workgroup gradient slab used by bcnf_stack_backward for a batch. */
+/* Bytes of the gradient scratch ("slab") of a backward over `batch` samples: per-workgroup partial
+ * gradients plus the split-K partials of the W1 condition columns. */
 int bcnf_slab_bytes(const BcnfStackDesc* desc, int64_t batch, int64_t* bytes);
+
+/* Bytes of the inverse's scratch (the condition projection of h_rows feature rows). */
+int bcnf_inverse_scratch_bytes(const BcnfStackDesc* desc, int64_t h_rows, int64_t* bytes);
 
 /* Re-lay params (canonical flat, n_trainable floats) and qmats ((n_blocks-1)*D*D floats) into
  * `packed` (bcnf_packed_bytes). Also writes the ActNorm log|det| constant used by the forward. */
@@ -86,30 +91,32 @@ int bcnf_pack_params(const BcnfStackDesc* desc, const float* params, const float
 
 /* Forward of the whole stack given features h (B x C): z (B x D), ldj (B), optional log_prob (B).
  * training != 0 applies dropout with the counter-based RNG keyed by rng_state[0] (seed) and
- * rng_state[1] (offset), both read from DEVICE memory (graph-replay safe).
- * workspace != NULL saves what bcnf_stack_backward needs (bcnf_workspace_bytes). */
+ * rng_state[1] (offset), both read from DEVICE memory (graph-replay safe). `workspace`
+ * (bcnf_workspace_bytes) is required; save != 0 also keeps what bcnf_stack_backward needs. */
 int bcnf_stack_forward(const BcnfStackDesc* desc, const void* packed, const float* y, const float* h,
                        int64_t batch, float* z, float* ldj, float* log_prob, int32_t training,
-                       const uint64_t* rng_state, void* workspace, void* stream);
+                       const uint64_t* rng_state, void* workspace, int32_t save, void* stream);
 
 /* Backward: given dz (B x D) and dldj (B) (either may be NULL = zeros), writes dh (B x C,
- * overwritten, nullable), dy (B x D, nullable) and the per-workgroup gradient slabs into `slab`
- * (bcnf_slab_bytes). With dparams != NULL it then reduces the slabs into dparams (canonical flat,
- * n_trainable floats, overwritten); with dparams == NULL the caller runs bcnf_grad_reduce.
- * `training` and `workspace` must be those of the forward call. */
+ * overwritten, nullable), dy (B x D, nullable) and the gradient scratch `slab` (bcnf_slab_bytes).
+ * With dparams != NULL it then reduces into dparams (canonical flat, n_trainable floats, overwritten);
+ * with dparams == NULL the caller runs bcnf_grad_reduce. `training` and `workspace` must be those of
+ * the (save != 0) forward call. */
 int bcnf_stack_backward(const BcnfStackDesc* desc, const void* packed, const float* h, const float* dz,
-                        const float* dldj, int64_t batch, int32_t training, const void* workspace, float* dy,
+                        const float* dldj, int64_t batch, int32_t training, void* workspace, float* dy,
                         float* dh, float* dparams, void* slab, void* stream);
 
-/* Deterministic (fixed-order) sum of the slabs of a backward over `batch` samples into dparams.
- * Replaces autograd's implicit batch reduction of the parameter gradients. */
-int bcnf_grad_reduce(const BcnfStackDesc* desc, const void* slab, int64_t batch, float* dparams, void* stream);
+/* Deterministic (fixed-order) reduction of a backward's gradient scratch into dparams, including the
+ * W1 condition columns (split-K GEMM of D1 with h). Replaces autograd's implicit batch reduction. */
+int bcnf_grad_reduce(const BcnfStackDesc* desc, const void* slab, const float* h, const void* workspace,
+                     int64_t batch, int32_t training, float* dparams, void* stream);
 
-/* Inverse of the whole stack: y (N x D) from z (N x D). Row r uses feature row
- * cond_index[r] of h when cond_index != NULL (h then has any number of rows), else row r. */
+/* Inverse of the whole stack: y (N x D) from z (N x D). h has h_rows rows; row r uses feature row
+ * cond_index[r] when cond_index != NULL (h_rows may then be anything), else row r (h_rows == N).
+ * `scratch`: bcnf_inverse_scratch_bytes(h_rows) -- the projection is computed once per feature row. */
 int bcnf_stack_inverse(const BcnfStackDesc* desc, const void* packed, const float* z, const float* h,
-                       const int64_t* cond_index, int64_t n_rows, float* y, int32_t training,
-                       const uint64_t* rng_state, void* stream);
+                       int64_t h_rows, const int64_t* cond_index, int64_t n_rows, float* y, int32_t training,
+                       const uint64_t* rng_state, void* scratch, void* stream);
 
 /* ---- NLL training pass (forward + inn_nll_loss + backward without any host round trip) ---------
  * bcnf_nll_forward = bcnf_stack_forward (workspace required) plus, in the same launch,
@@ -127,7 +134,7 @@ int bcnf_nll_forward(const BcnfStackDesc* desc, const void* packed, const float*
  * i.e. loss.backward(); mse carries no gradient). z is the forward's output. Otherwise as
  * bcnf_stack_backward. */
 int bcnf_nll_backward(const BcnfStackDesc* desc, const void* packed, const float* h, const float* z,
-                      const float* dloss, int64_t batch, int32_t training, const void* workspace, float* dy,
+                      const float* dloss, int64_t batch, int32_t training, void* workspace, float* dy,
                       float* dh, float* dparams, void* slab, void* stream);
 
 /* ---- Optimizer ------------------------------------------------------------------------------------
