@@ -46,7 +46,10 @@ struct BcnfLayout {
   int rf_b1, rf_w1, rf_hid, rf_t, rf_s, rf_q;
   int rb_w1t, rb_hid, rb_tt, rb_st, rb_qt;
   // packed buffer offsets (floats)
-  long long pf_off, pb_off, pi_off, w1t_off, w1h_off, ldc_off, total;
+  // W1 condition part, two contiguous copies for the projection GEMMs (NKp = nb*16 rounded up to 64):
+  //   W1hC [Cp][NKp]  (c, k*16+j)   W1hR [NKp][Cp]  (k*16+j, c)   b1c [NKp]
+  int NKp;
+  long long pf_off, pb_off, pi_off, w1c_off, w1r_off, b1c_off, ldc_off, total;
 };
 
 __device__ __forceinline__ int coupling_base(const BcnfLayout& L, int k) {

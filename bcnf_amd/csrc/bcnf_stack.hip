@@ -103,9 +103,11 @@ int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
   L->pf_off = 0;
   L->pb_off = L->pf_off + nbl * 16 * L->RF;
   L->pi_off = L->pb_off + nbl * 16 * L->RB;
-  L->w1t_off = L->pi_off + nbl * 16 * L->RF;
-  L->w1h_off = L->w1t_off;                     // (single padded W1h^T copy serves HP, dh and dW1h)
-  L->ldc_off = L->w1t_off + nbl * (long long)L->Cp * 17;
+  L->NKp = ((L->nb * 16 + 63) / 64) * 64;
+  L->w1c_off = L->pi_off + nbl * 16 * L->RF;
+  L->w1r_off = L->w1c_off + (long long)L->Cp * L->NKp;
+  L->b1c_off = L->w1r_off + (long long)L->NKp * L->Cp;
+  L->ldc_off = L->b1c_off + L->NKp;
   L->total = L->ldc_off + 4;
   return BCNF_OK;
 }
@@ -130,6 +132,7 @@ bool layout_supported(const BcnfLayout& L, const BcnfStackDesc* d) {
   for (int l = 1; l <= L.NH; ++l)
     if (L.H[l] > 16) return false;
   if (L.C < 1 || L.Cp > 16 * NC16_MAX) return false;
+  if (sizeof(float) * (size_t)(64 * 132 + 128 * (L.Cp + 32)) > LDS_MAX) return false;   // k_dw1h staging
   if (16 * L.RF > 4 * 4 * BCNF_WG || 16 * L.RB > 4 * 4 * BCNF_WG) return false;
   if (fwd_lds_bytes(L) > LDS_MAX || bwd_lds_bytes(L) > LDS_MAX) return false;
   if (L.blk_pad / 4 > COPY4_MAX * BCNF_WG) return false;
@@ -249,8 +252,8 @@ __global__ __launch_bounds__(BCNF_WG) void k_pack(BcnfLayout L, const float* __r
   // every packed section is < 2^31 floats (layout_supported bounds the shapes), so 32-bit index math
   const int n_pf = L.nb * 16 * L.RF;
   const int n_pb = L.nb * 16 * L.RB;
-  const int n_w = L.nb * L.Cp * 17;
-  const int total = 2 * n_pf + n_pb + n_w;
+  const int n_w = L.Cp * L.NKp;                       // each of W1hC, W1hR
+  const int total = 2 * n_pf + n_pb + 2 * n_w + L.NKp;
   for (int i = blockIdx.x * BCNF_WG + threadIdx.x; i < total; i += PACK_WG * BCNF_WG) {
     float v;
     long long o;
@@ -268,12 +271,20 @@ __global__ __launch_bounds__(BCNF_WG) void k_pack(BcnfLayout L, const float* __r
       const int kj = ii / L.RF, e = ii - kj * L.RF;
       v = rec_f(L, P, Q, kj >> 4, kj & 15, e, true);
       o = L.pi_off + ii;
-    } else {                                          // W1h^T [k][c][17] (column 16 = pad)
+    } else if (i < 2 * n_pf + n_pb + n_w) {           // W1hC [c][kj]
       const int ii = i - 2 * n_pf - n_pb;
-      const int kc = ii / 17, j = ii - kc * 17;
-      const int k = kc / L.Cp, c = kc - k * L.Cp;
-      v = (j < 16 && j < L.H[1] && c < L.C) ? cW(L, P, k, 1, j, L.Da + c) : 0.f;
-      o = L.w1t_off + ii;
+      const int c = ii / L.NKp, kj = ii - c * L.NKp, k = kj >> 4, j = kj & 15;
+      v = (k < L.nb && j < L.H[1] && c < L.C) ? cW(L, P, k, 1, j, L.Da + c) : 0.f;
+      o = L.w1c_off + ii;
+    } else if (i < 2 * n_pf + n_pb + 2 * n_w) {       // W1hR [kj][c]
+      const int ii = i - 2 * n_pf - n_pb - n_w;
+      const int kj = ii / L.Cp, c = ii - kj * L.Cp, k = kj >> 4, j = kj & 15;
+      v = (k < L.nb && j < L.H[1] && c < L.C) ? cW(L, P, k, 1, j, L.Da + c) : 0.f;
+      o = L.w1r_off + ii;
+    } else {                                          // b1c [kj]
+      const int kj = i - 2 * n_pf - n_pb - 2 * n_w, k = kj >> 4, j = kj & 15;
+      v = (k < L.nb && j < L.H[1]) ? cB(L, P, k, 1, j) : 0.f;
+      o = L.b1c_off + kj;
     }
     out[o] = v;
   }
@@ -316,143 +327,251 @@ constexpr int STAGE_REC = 4;   // 16 * RF floats  <= 4 float4 per thread (RF <= 
 // W1h^T comes from the packed buffer ([k][Cp][17], zero-padded); D1 = dL/d pre-activation of Linear 1.
 // MFMA lane roles: A[l&15][l>>4], B[l>>4][l&15], D[4(l>>4)+i][l&15].
 // ------------------------------------------------------------------------------------------------
-// Shape of the three GEMMs: one workgroup per 16-row slice; a wave keeps its A fragment in registers and
-// reuses it for every output column tile; the 4 waves split the reduction dimension and their partial
-// tiles are summed through LDS in a fixed order (deterministic).
+// The three projection GEMMs (FC_small: 4096 x 512 x 80, 4096 x 80 x 512, 512 x 80 x 4096). They are
+// bound by load issue / round trips rather than MFMA, so: operands come from contiguous packed copies
+// (W1hC, W1hR) with float4 loads, a workgroup stages a K-chunk of up to 128 of both operands in LDS per
+// round trip (next chunk in flight), and the K loops issue all LDS reads of 4-8 steps before their MFMAs.
+// VEC: C % 4 == 0 (h rows are float4-aligned).
+constexpr int KC = 128;                // K-chunk
+// LDS strides for the MFMA operand reads: [row = lane&15][k = 4t + lane>>4] wants stride = 4 (mod 32),
+// [k = 4t + lane>>4][col = lane&15] wants stride = 16 (mod 32): 64 lanes then hit every bank exactly twice.
+constexpr int KCP = KC + 4;            // A tiles [64][KC]
+constexpr int BNS = 80;                // k_hp B tile [KC][64]
+__host__ __device__ constexpr int bstride16(int n) { return n + ((16 - (n & 31)) & 31); }   // >= n, = 16 mod 32
 
-// HP[k][r][j] for 16 rows r; wave w computes blocks k = w, w + 4, ... The A fragment (the 16 h rows,
-// Cp/4 values per lane) is loaded once and reused for every block. grid = ceil(R / 16)
+// Stage rows [r0, r0 + 64) x cols [c0, c0 + KC) of a row-major (nrows x ncols, ld) matrix into regs
+// (8 float4 per thread: row = i4 / 32, col = 4 (i4 % 32)), zero outside.
+template <bool VEC>
+__device__ __forceinline__ void load_rows64(const float* __restrict__ M, long long nrows, int ncols, long long ld,
+                                            long long r0, int c0, floatx4* reg) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int i4 = threadIdx.x + 256 * e, row = i4 >> 5, col = c0 + (i4 & 31) * 4;
+    const long long r = r0 + row < nrows ? r0 + row : nrows - 1;
+    if (VEC) {
+      const floatx4 v = *reinterpret_cast<const floatx4*>(M + r * ld + (col < ncols ? col : 0));
+      reg[e] = v * ((r0 + row < nrows && col < ncols) ? 1.f : 0.f);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int cq = col + q;
+        const float v = M[r * ld + (cq < ncols ? cq : ncols - 1)];
+        reg[e][q] = (r0 + row < nrows && cq < ncols) ? v : 0.f;
+      }
+    }
+  }
+}
+
+// HP tile: 64 rows x 64 columns kj. grid = (ceil(R/64), NKp/64)
+template <bool VEC>
 __global__ __launch_bounds__(BCNF_WG) void k_hp(BcnfLayout L, const float* __restrict__ pk,
                                                 const float* __restrict__ h, long long R, float* __restrict__ hp) {
-  constexpr int KSM = 4 * NC16_MAX;                   // max K steps (Cp <= 256)
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* As = smem;                    // [64][KCP]  (row, c)
+  float* Bs = smem + 64 * KCP;         // [KC][BNS]  (c, kj)
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lq = l >> 4;
-  const long long r0 = (long long)blockIdx.x * 16;
-  const long long ar = r0 + lr < R ? r0 + lr : R - 1;
-  const float* a = h + ar * L.C;
-  const int C = L.C, Cp = L.Cp, KS = Cp >> 2;
-  float av[KSM];
+  const long long b0 = (long long)blockIdx.x * 64;
+  const int n0 = blockIdx.y * 64;
+  const int Cp = L.Cp, NKp = L.NKp;
+  const float* w1c = pk + L.w1c_off;
+  floatx4 ra[8], rb[8];
+  auto load = [&](int c0) {
+    load_rows64<VEC>(h, R, L.C, L.C, b0, c0, ra);
 #pragma unroll
-  for (int t = 0; t < KSM; ++t) {
-    const int c = 4 * t + lq;
-    av[t] = (t < KS && c < C) ? a[c < C ? c : C - 1] : 0.f;
-  }
-  const float* w1t = pk + L.w1t_off + (long long)lq * 17 + lr;   // W1hT[k][4t + lq][lr] = w1t[(k Cp + 4t) 17]
-  for (int k = wave; k < L.nb; k += 4) {
-    const float* wk = w1t + (long long)k * Cp * 17;
-    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t0 = 0; t0 < KSM; t0 += 8) {
-      if (t0 < KS) {                                 // uniform; KS is a multiple of 4
-      float bv[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) bv[u] = (t0 + u < KS) ? wk[(long long)(4 * (t0 + u)) * 17] : 0.f;
-#pragma unroll
-      for (int u = 0; u < 8; u += 2) {
-        if (t0 + u < KS) acc0 = mfma4(av[t0 + u], bv[u], acc0);
-        if (t0 + u + 1 < KS) acc1 = mfma4(av[t0 + u + 1], bv[u + 1], acc1);
-      }
-      }
+    for (int e = 0; e < 8; ++e) {                    // B: [KC rows c][64 cols]: row = i4 / 16, col4
+      const int i4 = tid + 256 * e, row = c0 + (i4 >> 4), col = n0 + (i4 & 15) * 4;
+      const floatx4 v = *reinterpret_cast<const floatx4*>(w1c + (long long)(row < Cp ? row : Cp - 1) * NKp + col);
+      rb[e] = v * (row < Cp ? 1.f : 0.f);
     }
-    const float b1 = pk[L.pf_off + ((long long)k * 16 + lr) * L.RF + L.rf_b1];
+  };
+  auto store = [&]() {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const long long r = r0 + 4 * lq + i;
-      if (r < R) hp[((long long)k * R + r) * 16 + lr] = (acc0[i] + acc1[i]) + b1;
+    for (int e = 0; e < 8; ++e) {
+      const int i4 = tid + 256 * e;
+      *reinterpret_cast<floatx4*>(As + (i4 >> 5) * KCP + (i4 & 31) * 4) = ra[e];
+      *reinterpret_cast<floatx4*>(Bs + (i4 >> 4) * BNS + (i4 & 15) * 4) = rb[e];
     }
-  }
-}
-
-// dh for 16 rows x all columns; wave w sums blocks k = w, w + 4, ... ; grid = ceil(B / 16)
-// K index of MFMA step e, lane quarter q: j = 4q + e (A = D1[k][row][4q + e], B = W1hT[k][col][4q + e]).
-__global__ __launch_bounds__(BCNF_WG) void k_dh(BcnfLayout L, const float* __restrict__ pk,
-                                                const float* __restrict__ d1, long long B, float* __restrict__ dh) {
-  __shared__ floatx4 part[4][NC16_MAX][64];
-  const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lq = l >> 4;
-  const long long b0 = (long long)blockIdx.x * 16;
-  const long long bl = b0 + lr < B ? b0 + lr : B - 1;
-  const int NC16 = L.Cp >> 4;
-  const long long Cp17 = (long long)L.Cp * 17;
-  floatx4 acc[NC16_MAX];
+  };
+  floatx4 acc[4];
 #pragma unroll
-  for (int u = 0; u < NC16_MAX; ++u) acc[u] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int k = wave; k < L.nb; k += 4) {
-    const floatx4 av = *reinterpret_cast<const floatx4*>(d1 + ((long long)k * B + bl) * 16 + 4 * lq);
-    const float* wk = pk + L.w1t_off + k * Cp17 + lr * 17 + 4 * lq;
-    float bv[NC16_MAX][4];
+  for (int u = 0; u < 4; ++u) acc[u] = floatx4{0.f, 0.f, 0.f, 0.f};
+  load(0);
+  for (int c0 = 0; c0 < Cp; c0 += KC) {
+    store();
+    __syncthreads();
+    if (c0 + KC < Cp) load(c0 + KC);
+    const int ks = (Cp - c0 < KC ? Cp - c0 : KC) >> 2;   // multiple of 4
+    for (int t0 = 0; t0 < ks; t0 += 4) {
+      float a[4], bv[4][4];
 #pragma unroll
-    for (int u = 0; u < NC16_MAX; ++u)
+      for (int t = 0; t < 4; ++t) {
+        a[t] = As[(16 * wave + lr) * KCP + 4 * (t0 + t) + lq];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) bv[u][e] = (u < NC16) ? wk[(long long)(16 * (u < NC16 ? u : 0)) * 17 + e] : 0.f;
+        for (int u = 0; u < 4; ++u) bv[t][u] = Bs[(4 * (t0 + t) + lq) * BNS + 16 * u + lr];
+      }
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int u = 0; u < NC16_MAX; ++u)
-        if (u < NC16) acc[u] = mfma4(av[e], bv[u][e], acc[u]);
+        for (int u = 0; u < 4; ++u) acc[u] = mfma4(a[t], bv[t][u], acc[u]);
+    }
+    __syncthreads();
   }
 #pragma unroll
-  for (int u = 0; u < NC16_MAX; ++u)
-    if (u < NC16) part[wave][u][l] = acc[u];
-  __syncthreads();
-  for (int idx = tid; idx < NC16 * 64; idx += BCNF_WG) {
-    const int u = idx >> 6, ll = idx & 63, rr = ll & 15, qq = ll >> 4;
-    const floatx4 v = ((part[0][u][ll] + part[1][u][ll]) + part[2][u][ll]) + part[3][u][ll];
-    const int col = 16 * u + rr;
-    if (col < L.C) {
+  for (int u = 0; u < 4; ++u) {
+    const int kj = n0 + 16 * u + lr, k = kj >> 4;
+    if (k < L.nb) {
+      const float b1 = pk[L.b1c_off + kj];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const long long r = b0 + 4 * qq + i;
-        if (r < B) dh[r * L.C + col] = v[i];
+        const long long r = b0 + 16 * wave + 4 * lq + i;
+        if (r < R) hp[((long long)k * R + r) * 16 + lr] = acc[u][i] + b1;
       }
     }
   }
 }
 
-// dW1h partials for one block k (16 rows j) x all columns over one batch split; wave w takes rows
-// m0 + 4w + 16t (+ lane quarter). grid = (nb, splits); work[s][k][16][Cp]
+// dh tile: 64 rows x 16 columns; K = nb * 16 (kj) in chunks of 128 (8 blocks). grid = (ceil(B/64), Cp/16)
+__global__ __launch_bounds__(BCNF_WG) void k_dh(BcnfLayout L, const float* __restrict__ pk,
+                                                const float* __restrict__ d1, long long B, float* __restrict__ dh) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* As = smem;                    // [64][KCP] (row b, kj)
+  float* Bs = smem + 64 * KCP;         // [KC][16]  (kj, c)
+  const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lq = l >> 4;
+  const long long b0 = (long long)blockIdx.x * 64;
+  const int n = blockIdx.y;
+  const int K = L.nb * 16, Cp = L.Cp;
+  const float* w1r = pk + L.w1r_off + 16 * n;
+  floatx4 ra[8], rb[2];
+  const int arow = tid >> 2, aj4 = (tid & 3) * 4;
+  const long long ab = b0 + arow < B ? b0 + arow : B - 1;
+  auto load = [&](int kj0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {                    // A: block (kj0 / 16 + e), rows [b0, b0 + 64) x 16
+      const int k = (kj0 >> 4) + e;
+      const floatx4 v = *reinterpret_cast<const floatx4*>(d1 + ((long long)(k < L.nb ? k : L.nb - 1) * B + ab) * 16 + aj4);
+      ra[e] = v * (k < L.nb ? 1.f : 0.f);
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {                    // B: [128 kj][16 c]: row = i4 / 4, col4
+      const int i4 = tid + 256 * e, kj = kj0 + (i4 >> 2);
+      const floatx4 v = *reinterpret_cast<const floatx4*>(w1r + (long long)(kj < K ? kj : K - 1) * Cp + (i4 & 3) * 4);
+      rb[e] = v * (kj < K ? 1.f : 0.f);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) *reinterpret_cast<floatx4*>(As + arow * KCP + 16 * e + aj4) = ra[e];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) *reinterpret_cast<floatx4*>(Bs + (tid + 256 * e) * 4) = rb[e];
+  };
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  load(0);
+  for (int kj0 = 0; kj0 < K; kj0 += KC) {
+    store();
+    __syncthreads();
+    if (kj0 + KC < K) load(kj0 + KC);
+    const int ks = (K - kj0 < KC ? K - kj0 : KC) >> 2;   // multiple of 4
+    for (int t0 = 0; t0 < ks; t0 += 4) {
+      float a[4], bv[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        a[t] = As[(16 * wave + lr) * KCP + 4 * (t0 + t) + lq];
+        bv[t] = Bs[(4 * (t0 + t) + lq) * 16 + lr];
+      }
+      acc = mfma4(a[0], bv[0], acc);
+      acc1 = mfma4(a[1], bv[1], acc1);
+      acc = mfma4(a[2], bv[2], acc);
+      acc1 = mfma4(a[3], bv[3], acc1);
+    }
+    __syncthreads();
+  }
+  acc += acc1;
+  const int col = 16 * n + lr;
+  if (col < L.C) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long long r = b0 + 16 * wave + 4 * lq + i;
+      if (r < B) dh[r * L.C + col] = acc[i];
+    }
+  }
+}
+
+// dW1h split-K partials: 64 kj (4 blocks, one per wave) x all columns over one split of KC rows.
+// grid = (ceil(nb/4), splits); work[s][k][16][Cp]
+template <bool VEC>
 __global__ __launch_bounds__(BCNF_WG) void k_dw1h(BcnfLayout L, const float* __restrict__ d1,
                                                   const float* __restrict__ h, long long B, int rows_per_split,
                                                   float* __restrict__ work) {
-  __shared__ floatx4 part[4][NC16_MAX][64];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int hs = bstride16(L.Cp);
+  float* As = smem;                    // [64][KCP] (kj, b)
+  float* Bs = smem + 64 * KCP;         // [KC][hs]  (b, c)
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lq = l >> 4;
-  const int k = blockIdx.x, s = blockIdx.y;
+  const int k0 = blockIdx.x * 4, s = blockIdx.y;
   const long long m0 = (long long)s * rows_per_split;
   long long m1 = m0 + rows_per_split;
   if (m1 > B) m1 = B;
-  const int NC16 = L.Cp >> 4, C = L.C;
-  const float* a = d1 + (long long)k * B * 16 + lr;     // A[j = lr][b] = D1[k][b][lr]
-  floatx4 acc[NC16_MAX];
+  const int NC16 = L.Cp >> 4;
+  {
+    const int row = tid >> 1, j8 = (tid & 1) * 8;     // A: 4 blocks x [KC rows][16], transposed into [kj][b]
+    const long long b = m0 + row;
+    const bool ok = b < m1;
+    const long long bb = ok ? b : m1 - 1;
 #pragma unroll
-  for (int u = 0; u < NC16_MAX; ++u) acc[u] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (long long m = m0 + 4 * wave; m < m1; m += 32) {  // two row groups (m, m + 16) per trip
-    float av[2], bv[2][NC16_MAX];
+    for (int kk = 0; kk < 4; ++kk) {
+      const int k = k0 + kk < L.nb ? k0 + kk : L.nb - 1;
+      const floatx4* src = reinterpret_cast<const floatx4*>(d1 + ((long long)k * B + bb) * 16 + j8);
+      const float m = (ok && k0 + kk < L.nb) ? 1.f : 0.f;
+      const floatx4 v0 = src[0] * m, v1 = src[1] * m;
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      const long long b = m + 16 * g + lq;
-      const bool ok = b < m1;
-      const long long bb = ok ? b : m1 - 1;
-      av[g] = ok ? a[bb * 16] : 0.f;
-      const float* hr = h + bb * C + lr;
-#pragma unroll
-      for (int u = 0; u < NC16_MAX; ++u) bv[g][u] = (ok && u < NC16 && 16 * u + lr < C) ? hr[16 * u] : 0.f;
+      for (int q = 0; q < 4; ++q) {
+        As[(kk * 16 + j8 + q) * KCP + row] = v0[q];
+        As[(kk * 16 + j8 + 4 + q) * KCP + row] = v1[q];
+      }
     }
+    // B: the split's h rows [KC][Cp] (zero-padded), in 64-row halves
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
+    for (int half = 0; half < 2; ++half) {
+      for (int c0 = 0; c0 < L.Cp; c0 += KC) {
+        floatx4 rv[8];
+        load_rows64<VEC>(h, m1, L.C, L.C, m0 + 64 * half, c0, rv);
 #pragma unroll
-      for (int u = 0; u < NC16_MAX; ++u)
-        if (u < NC16) acc[u] = mfma4(av[g], bv[g][u], acc[u]);
+        for (int e = 0; e < 8; ++e) {
+          const int i4 = tid + 256 * e, row = 64 * half + (i4 >> 5), col = c0 + (i4 & 31) * 4;
+          if (col < L.Cp) *reinterpret_cast<floatx4*>(Bs + row * hs + col) = rv[e];
+        }
+      }
+    }
   }
-#pragma unroll
-  for (int u = 0; u < NC16_MAX; ++u)
-    if (u < NC16) part[wave][u][l] = acc[u];
   __syncthreads();
-  float* o = work + (((long long)s * L.nb + k) * 16) * L.Cp;
-  for (int idx = tid; idx < NC16 * 64; idx += BCNF_WG) {
-    const int u = idx >> 6, ll = idx & 63, rr = ll & 15, qq = ll >> 4;
-    const floatx4 v = ((part[0][u][ll] + part[1][u][ll]) + part[2][u][ll]) + part[3][u][ll];
+  const int k = k0 + wave;
+  float* o = work + (((long long)s * L.nb + (k < L.nb ? k : 0)) * 16) * L.Cp;
+  for (int n = 0; n < NC16; ++n) {
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    for (int t0 = 0; t0 < KC / 4; t0 += 8) {            // LDS reads of 8 steps, then 8 MFMAs (2 chains)
+      float a[8], bv[8];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) o[(long long)(4 * qq + i) * L.Cp + 16 * u + rr] = v[i];
+      for (int t = 0; t < 8; ++t) {
+        a[t] = As[(16 * wave + lr) * KCP + 4 * (t0 + t) + lq];
+        bv[t] = Bs[(4 * (t0 + t) + lq) * hs + 16 * n + lr];
+      }
+#pragma unroll
+      for (int t = 0; t < 8; t += 2) {
+        acc = mfma4(a[t], bv[t], acc);
+        acc1 = mfma4(a[t + 1], bv[t + 1], acc1);
+      }
+    }
+    acc += acc1;
+    if (k < L.nb) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[(long long)(4 * lq + i) * L.Cp + 16 * n + lr] = acc[i];
+    }
   }
 }
+
+size_t hp_lds_bytes() { return sizeof(float) * (size_t)(64 * KCP + KC * BNS); }
+size_t dh_lds_bytes() { return sizeof(float) * (size_t)(64 * KCP + KC * 16); }
+size_t dw1h_lds_bytes(const BcnfLayout& L) { return sizeof(float) * (size_t)(64 * KCP + KC * bstride16(L.Cp)); }
 
 __global__ __launch_bounds__(BCNF_WG) void k_dw1h_reduce(BcnfLayout L, const float* __restrict__ work, int splits,
                                                          float* __restrict__ dparams) {
@@ -1211,7 +1330,16 @@ struct NllOut {
 };
 
 int launch_hp(const BcnfLayout& L, const float* pk, const float* h, long long R, float* hp, hipStream_t st) {
-  hipLaunchKernelGGL(k_hp, dim3((unsigned)((R + 15) / 16)), dim3(BCNF_WG), 0, st, L, pk, h, R, hp);
+  size_t lds = hp_lds_bytes();
+  const dim3 grid((unsigned)((R + 63) / 64), (unsigned)(L.NKp / 64));
+  int rc;
+  if (L.C % 4 == 0) {
+    if ((rc = launch_lds(k_hp<true>, lds))) return rc;
+    hipLaunchKernelGGL(k_hp<true>, grid, dim3(BCNF_WG), lds, st, L, pk, h, R, hp);
+  } else {
+    if ((rc = launch_lds(k_hp<false>, lds))) return rc;
+    hipLaunchKernelGGL(k_hp<false>, grid, dim3(BCNF_WG), lds, st, L, pk, h, R, hp);
+  }
   return check_launch();
 }
 
@@ -1278,11 +1406,7 @@ int bwd_dispatch(const BcnfLayout& L, const float* pk, const float* hp, const fl
 long long slab_stride_of(const BcnfLayout& L) { return (long long)L.nb * L.blk_pad; }
 
 // split-K geometry of the W1 condition-part gradient
-int w1h_rows_per_split(long long B) {   // <= 8 splits of >= 256 rows
-  long long r = (B + 7) / 8;
-  if (r < 256) r = 256;
-  return (int)((r + 15) & ~15LL);
-}
+int w1h_rows_per_split(long long) { return KC; }   // one LDS chunk of rows per split
 long long w1h_splits(long long B) { return (B + w1h_rows_per_split(B) - 1) / w1h_rows_per_split(B); }
 long long w1h_work_floats(const BcnfLayout& L, long long B) { return w1h_splits(B) * L.nb * 16LL * L.Cp; }
 
@@ -1453,8 +1577,15 @@ int bcnf_grad_reduce(const BcnfStackDesc* desc, const void* slab, const float* h
   float* work = (float*)slab + (long long)nwg * S;
   const int rps = w1h_rows_per_split(batch);
   const long long splits = w1h_splits(batch);
-  hipLaunchKernelGGL(k_dw1h, dim3((unsigned)L.nb, (unsigned)splits), dim3(BCNF_WG), 0, st, L, d1, h, (long long)batch,
-                     rps, work);
+  size_t lds = dw1h_lds_bytes(L);
+  const dim3 grid((unsigned)((L.nb + 3) / 4), (unsigned)splits);
+  if (L.C % 4 == 0) {
+    if ((rc = launch_lds(k_dw1h<true>, lds))) return rc;
+    hipLaunchKernelGGL(k_dw1h<true>, grid, dim3(BCNF_WG), lds, st, L, d1, h, (long long)batch, rps, work);
+  } else {
+    if ((rc = launch_lds(k_dw1h<false>, lds))) return rc;
+    hipLaunchKernelGGL(k_dw1h<false>, grid, dim3(BCNF_WG), lds, st, L, d1, h, (long long)batch, rps, work);
+  }
   if ((rc = check_launch())) return rc;
   const long long outs = (long long)L.nb * 16 * L.Cp;
   hipLaunchKernelGGL(k_dw1h_reduce, dim3((unsigned)((outs + BCNF_WG - 1) / BCNF_WG)), dim3(BCNF_WG), 0, st, L,
@@ -1540,8 +1671,10 @@ int backward_impl(const BcnfStackDesc* desc, const void* packed, const float* h,
   }
   if (rc) return rc;
   if (dh) {   // dL/dh = sum_k D1_k W1h_k
-    hipLaunchKernelGGL(k_dh, dim3((unsigned)((batch + 15) / 16)), dim3(BCNF_WG), 0, st, L, pk, (const float*)d1,
-                       (long long)batch, dh);
+    size_t lds = dh_lds_bytes();
+    if ((rc = launch_lds(k_dh, lds))) return rc;
+    hipLaunchKernelGGL(k_dh, dim3((unsigned)((batch + 63) / 64), (unsigned)(L.Cp >> 4)), dim3(BCNF_WG), lds, st, L, pk,
+                       (const float*)d1, (long long)batch, dh);
     if ((rc = check_launch())) return rc;
   }
   if (!dparams) return BCNF_OK;   // caller reduces with bcnf_grad_reduce

@@ -12,7 +12,8 @@ acc = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(os.path.join(root, "gpurun_out", f"pmc_{tag}", "p*", "*counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        short = next((k for k in ("k_forward", "k_backward", "k_reduce", "k_inverse", "k_pack") if k in name), None)
+        short = next((k for k in ("k_forward", "k_backward", "k_reduce", "k_inverse", "k_pack", "k_hp", "k_dh",
+                                  "k_dw1h_reduce", "k_dw1h") if k in name), None)
         if short is None:
             continue
         acc[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
