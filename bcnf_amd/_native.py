@@ -28,7 +28,7 @@ EXPORTS = (
     "bcnf_stack_inverse", "bcnf_grad_reduce", "bcnf_status_string", "bcnf_last_hip_error",
     "bcnf_nll_forward", "bcnf_nll_backward", "bcnf_grad_partials", "bcnf_adam_step", "bcnf_grad_sumsq",
     "bcnf_clip_grad_norm", "bcnf_linear_forward", "bcnf_linear_work_bytes", "bcnf_linear_backward",
-    "bcnf_inverse_scratch_bytes",
+    "bcnf_inverse_scratch_bytes", "bcnf_stack_dh", "bcnf_backward_tail", "bcnf_gather_rows2",
 )
 MAX_TENSORS = 16
 
@@ -81,6 +81,9 @@ def _bind(lib):
         "bcnf_slab_bytes": (_i32, [_pdesc, _i64, _pi64]),
         "bcnf_pack_params": (_i32, [_pdesc, _vp, _vp, _vp, _vp]),
         "bcnf_inverse_scratch_bytes": (_i32, [_pdesc, _i64, _pi64]),
+        "bcnf_stack_dh": (_i32, [_pdesc, _vp, _vp, _i64, _i32, _vp, _vp]),
+        "bcnf_backward_tail": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp]),
+        "bcnf_gather_rows2": (_i32, [_vp, _i64, _vp, _i32, _vp, _vp, _i32, _vp, _vp]),
         "bcnf_stack_forward": (_i32, [_pdesc, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _vp]),
         "bcnf_stack_backward": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
         "bcnf_stack_inverse": (_i32, [_pdesc, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i32, _vp, _vp, _vp]),

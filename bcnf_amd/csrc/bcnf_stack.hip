@@ -431,14 +431,13 @@ __global__ __launch_bounds__(BCNF_WG) void k_hp(BcnfLayout L, const float* __res
 }
 
 // dh tile: 64 rows x 16 columns; K = nb * 16 (kj) in chunks of 128 (8 blocks). grid = (ceil(B/64), Cp/16)
-__global__ __launch_bounds__(BCNF_WG) void k_dh(BcnfLayout L, const float* __restrict__ pk,
-                                                const float* __restrict__ d1, long long B, float* __restrict__ dh) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+__device__ __forceinline__ void dh_body(const BcnfLayout& L, const float* __restrict__ pk, const float* __restrict__ d1,
+                                        long long B, float* __restrict__ dh, int bx, int by, float* __restrict__ smem) {
   float* As = smem;                    // [64][KCP] (row b, kj)
   float* Bs = smem + 64 * KCP;         // [KC][16]  (kj, c)
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lq = l >> 4;
-  const long long b0 = (long long)blockIdx.x * 64;
-  const int n = blockIdx.y;
+  const long long b0 = (long long)bx * 64;
+  const int n = by;
   const int K = L.nb * 16, Cp = L.Cp;
   const float* w1r = pk + L.w1r_off + 16 * n;
   floatx4 ra[8], rb[2];
@@ -496,18 +495,23 @@ __global__ __launch_bounds__(BCNF_WG) void k_dh(BcnfLayout L, const float* __res
   }
 }
 
+__global__ __launch_bounds__(BCNF_WG) void k_dh(BcnfLayout L, const float* __restrict__ pk,
+                                                const float* __restrict__ d1, long long B, float* __restrict__ dh) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  dh_body(L, pk, d1, B, dh, blockIdx.x, blockIdx.y, smem);
+}
+
 // dW1h split-K partials: 64 kj (4 blocks, one per wave) x all columns over one split of KC rows.
 // grid = (ceil(nb/4), splits); work[s][k][16][Cp]
 template <bool VEC>
-__global__ __launch_bounds__(BCNF_WG) void k_dw1h(BcnfLayout L, const float* __restrict__ d1,
-                                                  const float* __restrict__ h, long long B, int rows_per_split,
-                                                  float* __restrict__ work) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+__device__ __forceinline__ void dw1h_body(const BcnfLayout& L, const float* __restrict__ d1, const float* __restrict__ h,
+                                          long long B, int rows_per_split, float* __restrict__ work, int bx, int by,
+                                          float* __restrict__ smem) {
   const int hs = bstride16(L.Cp);
   float* As = smem;                    // [64][KCP] (kj, b)
   float* Bs = smem + 64 * KCP;         // [KC][hs]  (b, c)
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lq = l >> 4;
-  const int k0 = blockIdx.x * 4, s = blockIdx.y;
+  const int k0 = bx * 4, s = by;
   const long long m0 = (long long)s * rows_per_split;
   long long m1 = m0 + rows_per_split;
   if (m1 > B) m1 = B;
@@ -567,6 +571,14 @@ __global__ __launch_bounds__(BCNF_WG) void k_dw1h(BcnfLayout L, const float* __r
       for (int i = 0; i < 4; ++i) o[(long long)(4 * lq + i) * L.Cp + 16 * n + lr] = acc[i];
     }
   }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(BCNF_WG) void k_dw1h(BcnfLayout L, const float* __restrict__ d1,
+                                                  const float* __restrict__ h, long long B, int rows_per_split,
+                                                  float* __restrict__ work) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  dw1h_body<VEC>(L, d1, h, B, rows_per_split, work, blockIdx.x, blockIdx.y, smem);
 }
 
 size_t hp_lds_bytes() { return sizeof(float) * (size_t)(64 * KCP + KC * BNS); }
@@ -1238,11 +1250,11 @@ __device__ __forceinline__ long long compact_to_canonical(const BcnfLayout& L, i
 
 // 64 output float4 per workgroup x 4 slab groups (group g sums workgroups g, g+4, ...; 8 loads in flight),
 // combined in a fixed order through LDS.
-__global__ __launch_bounds__(BCNF_WG) void k_reduce(BcnfLayout L, const float* __restrict__ slab, long long stride,
-                                                    int nwg, float* __restrict__ out) {
-  __shared__ floatx4 part[4][64];
+__device__ __forceinline__ void reduce_body(const BcnfLayout& L, const float* __restrict__ slab, long long stride,
+                                            int nwg, float* __restrict__ out, int bx, float* __restrict__ smem) {
+  floatx4 (*part)[64] = reinterpret_cast<floatx4 (*)[64]>(smem);   // [4][64]
   const int g = threadIdx.x >> 6, o4 = threadIdx.x & 63;
-  const long long i = ((long long)blockIdx.x * 64 + o4) * 4;
+  const long long i = ((long long)bx * 64 + o4) * 4;
   const bool live = i < stride;
   const long long ic = live ? i : 0;
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -1264,6 +1276,43 @@ __global__ __launch_bounds__(BCNF_WG) void k_reduce(BcnfLayout L, const float* _
 #pragma unroll
   for (int e = 0; e < 4; ++e)
     if (o + e < size_m) out[compact_to_canonical(L, m, o + e)] = tot[e];
+}
+
+__global__ __launch_bounds__(BCNF_WG) void k_reduce(BcnfLayout L, const float* __restrict__ slab, long long stride,
+                                                    int nwg, float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float smem[4 * 64 * 4];
+  reduce_body(L, slab, stride, nwg, out, blockIdx.x, smem);
+}
+
+// The backward's tail in ONE launch: dL/dh tiles, the slab reduction and the W1 condition-part split-K
+// partials are independent, so their workgroups share a grid (role by block index) and run
+// concurrently instead of paying three launch floors back to back.
+struct TailGrid {
+  int n_dh, gx_dh;      // dh tiles: (gx_dh x Cp/16), 0 if dh is not requested
+  int n_red;            // slab-reduce workgroups
+  int gx_dw;            // dW1h: (gx_dw x splits)
+};
+
+template <bool VEC>
+__global__ __launch_bounds__(BCNF_WG) void k_bwd_tail(BcnfLayout L, TailGrid G, const float* __restrict__ pk,
+                                                      const float* __restrict__ d1, const float* __restrict__ h,
+                                                      long long B, float* __restrict__ dh,
+                                                      const float* __restrict__ slab, long long stride, int nwg,
+                                                      float* __restrict__ dparams, int rows_per_split,
+                                                      float* __restrict__ work) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  int i = blockIdx.x;
+  if (i < G.n_dh) {
+    dh_body(L, pk, d1, B, dh, i % G.gx_dh, i / G.gx_dh, smem);
+    return;
+  }
+  i -= G.n_dh;
+  if (i < G.n_red) {
+    reduce_body(L, slab, stride, nwg, dparams, i, smem);
+    return;
+  }
+  i -= G.n_red;
+  dw1h_body<VEC>(L, d1, h, B, rows_per_split, work, i % G.gx_dw, i / G.gx_dw, smem);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1559,37 +1608,66 @@ int bcnf_nll_backward(const BcnfStackDesc* desc, const void* packed, const float
                        stream);
 }
 
-int bcnf_grad_reduce(const BcnfStackDesc* desc, const void* slab, const float* h, const void* workspace,
-                     int64_t batch, int32_t training, float* dparams, void* stream) {
+int bcnf_backward_tail(const BcnfStackDesc* desc, const void* packed, const void* slab, const float* h,
+                       const void* workspace, int64_t batch, int32_t training, float* dh, float* dparams,
+                       void* stream) {
   BcnfLayout L;
   int rc = make_layout(desc, &L);
   if (rc) return rc;
-  if (!slab || !h || !workspace || !dparams || batch < 1) return BCNF_ERR_ARG;
+  if (!layout_supported(L, desc)) return BCNF_ERR_UNSUPPORTED;
+  if (!packed || !slab || !h || !workspace || !dparams || batch < 1) return BCNF_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   const long long S = slab_stride_of(L);
   const int nwg = (int)((batch + 15) / 16);
-  hipLaunchKernelGGL(k_reduce, dim3((unsigned)((S / 4 + 63) / 64)), dim3(BCNF_WG), 0, st, L, (const float*)slab, S,
-                     nwg, dparams);
-  if ((rc = check_launch())) return rc;
-  // W1 condition columns: split-K GEMM over the batch, then a fixed-order reduce
   const bool drop = training && L.p > 0.f;
   const float* d1 = (const float*)workspace + ws_d1_off(L, batch, drop);
   float* work = (float*)slab + (long long)nwg * S;
   const int rps = w1h_rows_per_split(batch);
   const long long splits = w1h_splits(batch);
+  TailGrid G;
+  G.gx_dh = (int)((batch + 63) / 64);
+  G.n_dh = dh ? G.gx_dh * (L.Cp >> 4) : 0;
+  G.n_red = (int)((S / 4 + 63) / 64);
+  G.gx_dw = (L.nb + 3) / 4;
+  const long long n_dw = (long long)G.gx_dw * splits;
   size_t lds = dw1h_lds_bytes(L);
-  const dim3 grid((unsigned)((L.nb + 3) / 4), (unsigned)splits);
+  if (dh_lds_bytes() > lds) lds = dh_lds_bytes();
+  const dim3 grid((unsigned)(G.n_dh + G.n_red + n_dw));
   if (L.C % 4 == 0) {
-    if ((rc = launch_lds(k_dw1h<true>, lds))) return rc;
-    hipLaunchKernelGGL(k_dw1h<true>, grid, dim3(BCNF_WG), lds, st, L, d1, h, (long long)batch, rps, work);
+    if ((rc = launch_lds(k_bwd_tail<true>, lds))) return rc;
+    hipLaunchKernelGGL(k_bwd_tail<true>, grid, dim3(BCNF_WG), lds, st, L, G, (const float*)packed, d1, h,
+                       (long long)batch, dh, (const float*)slab, S, nwg, dparams, rps, work);
   } else {
-    if ((rc = launch_lds(k_dw1h<false>, lds))) return rc;
-    hipLaunchKernelGGL(k_dw1h<false>, grid, dim3(BCNF_WG), lds, st, L, d1, h, (long long)batch, rps, work);
+    if ((rc = launch_lds(k_bwd_tail<false>, lds))) return rc;
+    hipLaunchKernelGGL(k_bwd_tail<false>, grid, dim3(BCNF_WG), lds, st, L, G, (const float*)packed, d1, h,
+                       (long long)batch, dh, (const float*)slab, S, nwg, dparams, rps, work);
   }
   if ((rc = check_launch())) return rc;
   const long long outs = (long long)L.nb * 16 * L.Cp;
   hipLaunchKernelGGL(k_dw1h_reduce, dim3((unsigned)((outs + BCNF_WG - 1) / BCNF_WG)), dim3(BCNF_WG), 0, st, L,
                      (const float*)work, (int)splits, dparams);
+  return check_launch();
+}
+
+int bcnf_grad_reduce(const BcnfStackDesc* desc, const void* slab, const float* h, const void* workspace,
+                     int64_t batch, int32_t training, float* dparams, void* stream) {
+  // (packed is only read by the dh role, which is off here)
+  return bcnf_backward_tail(desc, slab, slab, h, workspace, batch, training, nullptr, dparams, stream);
+}
+
+int bcnf_stack_dh(const BcnfStackDesc* desc, const void* packed, const void* workspace, int64_t batch, int32_t training,
+                  float* dh, void* stream) {
+  BcnfLayout L;
+  int rc = make_layout(desc, &L);
+  if (rc) return rc;
+  if (!layout_supported(L, desc)) return BCNF_ERR_UNSUPPORTED;
+  if (batch < 0 || !packed || !workspace || !dh) return BCNF_ERR_ARG;
+  if (batch == 0) return BCNF_OK;
+  const float* d1 = (const float*)workspace + ws_d1_off(L, batch, training && L.p > 0.f);
+  size_t lds = dh_lds_bytes();
+  if ((rc = launch_lds(k_dh, lds))) return rc;
+  hipLaunchKernelGGL(k_dh, dim3((unsigned)((batch + 63) / 64), (unsigned)(L.Cp >> 4)), dim3(BCNF_WG), lds,
+                     (hipStream_t)stream, L, (const float*)packed, d1, (long long)batch, dh);
   return check_launch();
 }
 
@@ -1670,15 +1748,9 @@ int backward_impl(const BcnfStackDesc* desc, const void* packed, const float* h,
     default: return BCNF_ERR_UNSUPPORTED;
   }
   if (rc) return rc;
-  if (dh) {   // dL/dh = sum_k D1_k W1h_k
-    size_t lds = dh_lds_bytes();
-    if ((rc = launch_lds(k_dh, lds))) return rc;
-    hipLaunchKernelGGL(k_dh, dim3((unsigned)((batch + 63) / 64), (unsigned)(L.Cp >> 4)), dim3(BCNF_WG), lds, st, L, pk,
-                       (const float*)d1, (long long)batch, dh);
-    if ((rc = check_launch())) return rc;
-  }
-  if (!dparams) return BCNF_OK;   // caller reduces with bcnf_grad_reduce
-  return bcnf_grad_reduce(desc, slab, h, workspace, batch, training, dparams, stream);
+  if (dparams) return bcnf_backward_tail(desc, packed, slab, h, workspace, batch, training, dh, dparams, stream);
+  if (dh) return bcnf_stack_dh(desc, packed, workspace, batch, training, dh, stream);
+  return BCNF_OK;   // caller finishes with bcnf_backward_tail / bcnf_grad_reduce
 }
 
 }  // namespace

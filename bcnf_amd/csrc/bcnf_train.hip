@@ -283,6 +283,22 @@ __global__ __launch_bounds__(BCNF_WG) void k_wt_reduce(const float* __restrict__
 
 using bcnf_rt::launched;
 
+// dst0[r] = src0[idx[r]] (cols0 floats), dst1[r] = src1[idx[r]] (cols1 floats), one launch for both.
+__global__ __launch_bounds__(BCNF_WG) void k_gather2(const int64_t* __restrict__ idx, long long n,
+                                                     const float* __restrict__ s0, int c0, float* __restrict__ d0,
+                                                     const float* __restrict__ s1, int c1, float* __restrict__ d1) {
+  const long long t0 = n * c0, total = t0 + n * c1;
+  for (long long i = (long long)blockIdx.x * BCNF_WG + threadIdx.x; i < total; i += (long long)gridDim.x * BCNF_WG) {
+    if (i < t0) {
+      const long long r = i / c0;
+      d0[i] = s0[idx[r] * c0 + (i - r * c0)];
+    } else {
+      const long long j = i - t0, r = j / c1;
+      d1[j] = s1[idx[r] * c1 + (j - r * c1)];
+    }
+  }
+}
+
 int make_tlist(int n, float* const* p, float* const* g, float* const* m, float* const* v, const int64_t* numel,
                TList* T) {
   if (n < 1 || n > BCNF_MAX_TENSORS || !g || !numel) return BCNF_ERR_ARG;
@@ -347,6 +363,19 @@ int bcnf_clip_grad_norm(int32_t n_tensors, float* const* grads, const int64_t* n
   const long long np = bcnf_grad_partials(T.start[T.n]);
   hipLaunchKernelGGL(k_clip, dim3((unsigned)np), dim3(BCNF_WG), 0, (hipStream_t)stream, T, grad_partials, (int)np,
                      max_norm, total_norm);
+  return launched();
+}
+
+int bcnf_gather_rows2(const int64_t* idx, int64_t n, const float* src0, int32_t cols0, float* dst0,
+                      const float* src1, int32_t cols1, float* dst1, void* stream) {
+  if (n < 0 || cols0 < 1 || cols1 < 1) return BCNF_ERR_ARG;
+  if (n == 0) return BCNF_OK;
+  if (!idx || !src0 || !dst0 || !src1 || !dst1) return BCNF_ERR_ARG;
+  const long long total = n * (long long)(cols0 + cols1);
+  long long nblk = (total + BCNF_WG - 1) / BCNF_WG;
+  if (nblk > 2048) nblk = 2048;
+  hipLaunchKernelGGL(k_gather2, dim3((unsigned)nblk), dim3(BCNF_WG), 0, (hipStream_t)stream, idx, (long long)n, src0,
+                     cols0, dst0, src1, cols1, dst1);
   return launched();
 }
 

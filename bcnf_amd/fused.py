@@ -240,24 +240,32 @@ class FusedStack:
         dy = torch.empty((B, self.cfg.size), dtype=torch.float32, device=dev) if want_dy else None
         stream = N.stream_handle(dev)
         tm = self.timers
+        e0 = None
         if tm is not None:
             e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e2 = torch.cuda.Event(enable_timing=True)
             e0.record()
         rc = N.lib().bcnf_stack_backward(self._pdesc, N.ptr(pk), N.ptr(h), N.ptr(dz), N.ptr(dldj),
                                          ctypes.c_int64(B), ctypes.c_int32(int(training)), N.ptr(ws), N.ptr(dy),
-                                         N.ptr(dh), None, N.ptr(slab), stream)
+                                         None, None, N.ptr(slab), stream)
         N.check(rc, "bcnf_stack_backward")
-        if tm is not None:
-            e1.record()
-        N.check(N.lib().bcnf_grad_reduce(self._pdesc, N.ptr(slab), N.ptr(h), N.ptr(ws), ctypes.c_int64(B),
-                                         ctypes.c_int32(int(training)), N.ptr(dparams), stream), "bcnf_grad_reduce")
-        if tm is not None:
-            e2.record()
-            tm.setdefault("k_backward", []).append((e0, e1))
-            tm.setdefault("k_reduce", []).append((e1, e2))
+        self._backward_tail(h, ws, pk, slab, dh, dparams, B, training, stream, tm, e0)
         return dy, dh, dparams
+
+    def _backward_tail(self, h, ws, pk, slab, dh, dparams, B, training, stream, tm, e0):
+        """dL/dh and the deterministic parameter-gradient reduction after a backward launch (one fused tail
+        launch + the split-K finish); with timers, the backward and the tail get HIP-event pairs."""
+        if tm is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            tm.setdefault("k_backward", []).append((e0, e1))
+            e0 = e1
+        N.check(N.lib().bcnf_backward_tail(self._pdesc, N.ptr(pk), N.ptr(slab), N.ptr(h), N.ptr(ws), ctypes.c_int64(B),
+                                           ctypes.c_int32(int(training)), N.ptr(dh), N.ptr(dparams), stream),
+                "bcnf_backward_tail")
+        if tm is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            tm.setdefault("k_bwd_tail", []).append((e0, e1))
 
     def sync_word(self):
         """One zero-initialised uint32 of device memory for the kernels' last-workgroup handshake."""
@@ -308,24 +316,57 @@ class FusedStack:
         dy = torch.empty((B, self.cfg.size), dtype=torch.float32, device=dev) if want_dy else None
         stream = N.stream_handle(dev)
         tm = self.timers
+        e0 = None
         if tm is not None:
             e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e2 = torch.cuda.Event(enable_timing=True)
             e0.record()
         rc = N.lib().bcnf_nll_backward(self._pdesc, N.ptr(pk), N.ptr(h), N.ptr(z), N.ptr(dvals), ctypes.c_int64(B),
-                                       ctypes.c_int32(int(training)), N.ptr(ws), N.ptr(dy), N.ptr(dh), None,
+                                       ctypes.c_int32(int(training)), N.ptr(ws), N.ptr(dy), None, None,
                                        N.ptr(slab), stream)
         N.check(rc, "bcnf_nll_backward")
-        if tm is not None:
-            e1.record()
-        N.check(N.lib().bcnf_grad_reduce(self._pdesc, N.ptr(slab), N.ptr(h), N.ptr(ws), ctypes.c_int64(B),
-                                         ctypes.c_int32(int(training)), N.ptr(dparams), stream), "bcnf_grad_reduce")
-        if tm is not None:
-            e2.record()
-            tm.setdefault("k_backward", []).append((e0, e1))
-            tm.setdefault("k_reduce", []).append((e1, e2))
+        self._backward_tail(h, ws, pk, slab, dh, dparams, B, training, stream, tm, e0)
         return dy, dh, dparams
+
+    @torch.no_grad()
+    def time_kernels(self, y, h, training: bool = True, iters: int = 20):
+        """Average device time (us) of each launch of one NLL training pass, measured with HIP events on the
+        launch stream around `iters` back-to-back launches of the same (idempotent) call, so host launch
+        latency is amortised: 'forward' (k_hp + k_forward), 'k_backward' (the backward kernel alone) and
+        'tail' (dh + slab reduce + W1 condition part)."""
+        L = N.lib()
+        dev = y.device
+        stream = N.stream_handle(dev)
+        B = y.shape[0]
+        z, _, vals, (ws, pk) = self.launch_nll_forward(y, h, training)
+        _, sb = self.workspace_bytes(B, training)
+        slab = torch.empty(max(sb // 4, 1), dtype=torch.float32, device=dev)
+        dh = torch.empty_like(h)
+        dparams = torch.empty_like(self.flat)
+        ldj = torch.empty(B, dtype=torch.float32, device=dev)
+        rng = self.rng_state() if (training and self.cfg.dropout > 0.0) else None
+        calls = {
+            "forward": lambda: L.bcnf_nll_forward(self._pdesc, N.ptr(pk), N.ptr(y), N.ptr(h), ctypes.c_int64(B), N.ptr(z),
+                                                  N.ptr(ldj), ctypes.c_int32(int(training)), N.ptr(rng), N.ptr(ws),
+                                                  N.ptr(self.sync_word()), N.ptr(vals), stream),
+            "k_backward": lambda: L.bcnf_nll_backward(self._pdesc, N.ptr(pk), N.ptr(h), N.ptr(z), None, ctypes.c_int64(B),
+                                                      ctypes.c_int32(int(training)), N.ptr(ws), None, None, None,
+                                                      N.ptr(slab), stream),
+            "tail": lambda: L.bcnf_backward_tail(self._pdesc, N.ptr(pk), N.ptr(slab), N.ptr(h), N.ptr(ws),
+                                                 ctypes.c_int64(B), ctypes.c_int32(int(training)), N.ptr(dh),
+                                                 N.ptr(dparams), stream),
+        }
+        out = {}
+        for name, fn in calls.items():
+            N.check(fn(), name)                       # warm (code object, LDS attributes)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(iters):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            out[name] = e0.elapsed_time(e1) * 1e3 / iters
+        return out
 
     def launch_inverse(self, z, h, cond_index=None, training: bool = False):
         self._check_inputs(z, h, "inverse")

@@ -96,9 +96,18 @@ class TrainStep:
         return vals
 
     def _gather(self):
+        """pool rows of the static index buffer, both tensors in one native launch"""
+        from bcnf_amd import _native as N
         sidx = self._static[2]
         py, pt = self._pool
-        return py.index_select(0, sidx), pt.index_select(0, sidx)
+        n = sidx.shape[0]
+        y = torch.empty((n,) + tuple(py.shape[1:]), dtype=py.dtype, device=py.device)
+        t = torch.empty((n,) + tuple(pt.shape[1:]), dtype=pt.dtype, device=pt.device)
+        cy = py[0].numel() if py.shape[0] else 1
+        ct = pt[0].numel() if pt.shape[0] else 1
+        N.check(N.lib().bcnf_gather_rows2(N.ptr(sidx), n, N.ptr(py), cy, N.ptr(y), N.ptr(pt), ct, N.ptr(t),
+                                          N.stream_handle(py.device)), "bcnf_gather_rows2")
+        return y, t
 
     def _snapshot(self):
         with torch.no_grad():
@@ -182,15 +191,19 @@ class TrainStep:
         """Serve batches by index from device-resident tensors (the gather becomes part of the graph)."""
         if self._graphs is not None:
             raise RuntimeError("set_pool() must precede the first step")
+        for t in (y_pool, traj_pool):
+            if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
+                raise ValueError("set_pool: contiguous fp32 device tensors required")
         self._pool = (y_pool, traj_pool)
 
     def step_indexed(self, idx):
         """step(pool_y[idx], pool_traj[idx]) with the gather captured in the graph."""
         if self._pool is None:
             raise RuntimeError("step_indexed() needs set_pool()")
+        idx = idx.to(dtype=torch.int64).contiguous()
         if not self.capture:
-            py, pt = self._pool
-            return tuple(self.eager_step(py.index_select(0, idx), pt.index_select(0, idx)).tolist())
+            self._static = (None, None, idx)
+            return tuple(self.eager_step(*self._gather()).tolist())
         if self._graphs is None:
             py, pt = self._pool
             self._build_graphs(py.index_select(0, idx), pt.index_select(0, idx), idx=idx)

@@ -106,6 +106,17 @@ int bcnf_stack_backward(const BcnfStackDesc* desc, const void* packed, const flo
                         const float* dldj, int64_t batch, int32_t training, void* workspace, float* dy,
                         float* dh, float* dparams, void* slab, void* stream);
 
+/* dL/dh (B x C, overwritten) = sum_k D1_k W1h_k from the deltas a backward left in `workspace` (what
+ * bcnf_stack_backward does itself when its dh != NULL). */
+int bcnf_stack_dh(const BcnfStackDesc* desc, const void* packed, const void* workspace, int64_t batch,
+                  int32_t training, float* dh, void* stream);
+
+/* Everything after bcnf_stack_backward(dh = dparams = NULL) in one go: dh (nullable) and dparams, as
+ * bcnf_stack_dh + bcnf_grad_reduce but with the independent pieces sharing one launch. */
+int bcnf_backward_tail(const BcnfStackDesc* desc, const void* packed, const void* slab, const float* h,
+                       const void* workspace, int64_t batch, int32_t training, float* dh, float* dparams,
+                       void* stream);
+
 /* Deterministic (fixed-order) reduction of a backward's gradient scratch into dparams, including the
  * W1 condition columns (split-K GEMM of D1 with h). Replaces autograd's implicit batch reduction. */
 int bcnf_grad_reduce(const BcnfStackDesc* desc, const void* slab, const float* h, const void* workspace,
@@ -161,6 +172,12 @@ int bcnf_grad_sumsq(int32_t n_tensors, float* const* grads, const int64_t* numel
  * total_norm (device float, nullable) receives the pre-clip norm. */
 int bcnf_clip_grad_norm(int32_t n_tensors, float* const* grads, const int64_t* numel, const float* grad_partials,
                         float max_norm, float* total_norm, void* stream);
+
+/* ---- Batch feed: dst0[r] = src0[idx[r]], dst1[r] = src1[idx[r]] (row-major rows of cols0 / cols1
+ * floats) in one launch -- the shuffled-batch gather of the Trainer's DataLoader (trainer.py:164-166)
+ * from device-resident data. */
+int bcnf_gather_rows2(const int64_t* idx, int64_t n, const float* src0, int32_t cols0, float* dst0,
+                      const float* src1, int32_t cols1, float* dst1, void* stream);
 
 /* ---- nn.Linear (row-major, weight out_features x in_features) ------------------------------------ */
 int bcnf_linear_forward(const float* x, const float* weight, const float* bias, int64_t rows, int32_t in_features,
