@@ -29,6 +29,7 @@ EXPORTS = (
     "bcnf_nll_forward", "bcnf_nll_backward", "bcnf_grad_partials", "bcnf_adam_step", "bcnf_grad_sumsq",
     "bcnf_clip_grad_norm", "bcnf_linear_forward", "bcnf_linear_work_bytes", "bcnf_linear_backward",
     "bcnf_inverse_scratch_bytes", "bcnf_stack_dh", "bcnf_backward_tail", "bcnf_gather_rows2",
+    "bcnf_gather_batch", "bcnf_advance_counters",
 )
 MAX_TENSORS = 16
 
@@ -84,17 +85,20 @@ def _bind(lib):
         "bcnf_stack_dh": (_i32, [_pdesc, _vp, _vp, _i64, _i32, _vp, _vp]),
         "bcnf_backward_tail": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp]),
         "bcnf_gather_rows2": (_i32, [_vp, _i64, _vp, _i32, _vp, _vp, _i32, _vp, _vp]),
+        "bcnf_gather_batch": (_i32, [_vp, _vp, _i64, _vp, _i32, _vp, _vp, _i32, _vp, _vp]),
+        "bcnf_advance_counters": (_i32, [_vp, _vp, _i64, _vp]),
         "bcnf_stack_forward": (_i32, [_pdesc, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _vp]),
         "bcnf_stack_backward": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
         "bcnf_stack_inverse": (_i32, [_pdesc, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i32, _vp, _vp, _vp]),
         "bcnf_grad_reduce": (_i32, [_pdesc, _vp, _vp, _vp, _i64, _i32, _vp, _vp]),
-        "bcnf_nll_forward": (_i32, [_pdesc, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp]),
-        "bcnf_nll_backward": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+        "bcnf_nll_forward": (_i32, [_pdesc, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _i32, _vp, _vp]),
+        "bcnf_nll_backward": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                     _vp]),
         "bcnf_grad_partials": (_i64, [_i64]),
         "bcnf_adam_step": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double,
-                                  ctypes.c_double, ctypes.c_double, ctypes.c_double, _vp, _vp, _vp]),
+                                  ctypes.c_double, ctypes.c_double, ctypes.c_double, _vp, _i32, _vp]),
         "bcnf_grad_sumsq": (_i32, [_i32, _vp, _vp, _vp, _vp]),
-        "bcnf_clip_grad_norm": (_i32, [_i32, _vp, _vp, _vp, ctypes.c_float, _vp, _vp]),
+        "bcnf_clip_grad_norm": (_i32, [_i32, _vp, _vp, _vp, ctypes.c_float, _vp, _vp, _vp, _i64, _vp]),
         "bcnf_linear_forward": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp]),
         "bcnf_linear_work_bytes": (_i64, [_i64, _i32, _i32]),
         "bcnf_linear_backward": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),

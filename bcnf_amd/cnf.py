@@ -382,17 +382,18 @@ class CondRealNVP_v2(ConditionalInvertibleLayer):
             return z, condition
         return z
 
-    def nll_loss(self, y: torch.Tensor, *conditions: torch.Tensor) -> torch.Tensor:
+    def nll_loss(self, y: torch.Tensor, *conditions: torch.Tensor, defer_reduction: bool = False) -> torch.Tensor:
         """The Trainer's training loss in one fused pass (trainer.py:260-266 with hybrid_weight = 0):
         returns vals = [loss, nll, mse] where loss = nll = inn_nll_loss(z, log_det_J) and mse = 0.
         `vals` is differentiable (backprop loss via vals[0] or with cotangent [1, 0, 0]); the feature
         network runs through autograd as usual, the coupling stack and the loss through the fused
-        kernels with no dz / dldj tensors in between."""
+        kernels with no dz / dldj tensors in between. defer_reduction=True (a backward certainly follows)
+        moves the loss reduction into the backward launch; vals is then valid only after backward."""
         self._check_supported()
         condition = self._features(conditions)
         if y.dim() == 1:
             y = y.unsqueeze(0)
-        return stack_nll(self._fused, y, condition, self.training)
+        return stack_nll(self._fused, y, condition, self.training, defer=defer_reduction)
 
     def log_prob(self, y: torch.Tensor, *conditions: torch.Tensor) -> torch.Tensor:
         """log p(y | conditions) = -0.5 |z|^2 + log|det J| - D/2 log(2 pi). The reference has no such

@@ -29,6 +29,7 @@ inline int launched() {
 }
 }  // namespace bcnf_rt
 
+
 // Host-computed layout of one stack (passed by value to every kernel).
 struct BcnfLayout {
   int D, Da, Db, C, Cp, NH, nb, act_norm;

@@ -694,8 +694,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
                                                      long long B, float* __restrict__ z, float* __restrict__ ldj_out,
                                                      float* __restrict__ logp, const uint64_t* rng,
                                                      float* __restrict__ ysave, uint32_t* __restrict__ msave,
-                                                     float* __restrict__ nll_part, unsigned* __restrict__ sync,
-                                                     float* __restrict__ loss_out, uint64_t* rng_w) {
+                                                     float* __restrict__ nll_part) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int RFL = 16 * L.RF;
   float* rec = smem;                    // [2][16*RF]
@@ -768,7 +767,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
     const float q2 = row_sum16(ya * ya + yb * yb);
     if (j == 0) logp[bc] = -(0.5f * q2 - ltot) - 0.5f * (float)D * 1.8378770664093454836f;
   }
-  if (nll_part) {   // inn_nll_loss(z, ldj) = mean_b(0.5 |z_b|^2 - ldj_b)   (utils.py:40-46)
+  if (nll_part) {   // per-workgroup partial of inn_nll_loss (utils.py:40-46); reduced by nll_finalize
     const float q2 = row_sum16(ya * ya + yb * yb);
     float* red = rec;                                  // free after the loop's last barrier
     if (j == 0) red[s] = (b < B) ? 0.5f * q2 - ltot : 0.f;
@@ -777,33 +776,36 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
       float acc = 0.f;
       for (int i = 0; i < 16; ++i) acc += red[i];
       nll_part[blockIdx.x] = acc;
-      __threadfence();                                 // release the partial before counting in
-      const unsigned prev = atomicAdd(sync, 1u);
-      red[16] = (prev == gridDim.x - 1) ? 1.f : 0.f;
-    }
-    __syncthreads();
-    if (red[16] != 0.f) {                              // last workgroup: all partials are visible
-      __threadfence();
-      float acc = 0.f;
-      for (int i = tid; i < (int)gridDim.x; i += BCNF_WG)
-        acc += __hip_atomic_load(nll_part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      float* r2 = rec + 32;
-      r2[tid] = acc;
-      __syncthreads();
-      for (int w = BCNF_WG / 2; w > 0; w >>= 1) {
-        if (tid < w) r2[tid] += r2[tid + w];
-        __syncthreads();
-      }
-      if (tid == 0) {
-        const float nll = r2[0] / (float)B;
-        loss_out[0] = nll;                             // (nll + mse * 0) / (1 + 0)   (trainer.py:264)
-        loss_out[1] = nll;
-        loss_out[2] = 0.f;
-        if (rng_w) rng_w[1] += 1;                      // every workgroup has read the offset
-        *sync = 0u;
-      }
     }
   }
+}
+
+// Mean of the forward's per-workgroup NLL partials -> loss_out = [loss, nll, mse = 0] (trainer.py:260-266)
+// and the dropout RNG offset advance, by ONE workgroup that runs strictly after the forward (a separate
+// launch, or workgroup 0 of the backward): no cross-workgroup synchronisation inside any kernel.
+__device__ void nll_finalize(const float* __restrict__ part, int nparts, long long B, float* __restrict__ loss_out,
+                             uint64_t* rng_w, float* __restrict__ red) {
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += BCNF_WG) acc += part[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = BCNF_WG / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float nll = red[0] / (float)B;
+    loss_out[0] = nll;                                 // (nll + mse * 0) / (1 + 0)   (trainer.py:264)
+    loss_out[1] = nll;
+    loss_out[2] = 0.f;
+    if (rng_w) rng_w[1] += 1;                          // the forward has read the offset
+  }
+}
+
+__global__ __launch_bounds__(BCNF_WG) void k_nll_finalize(const float* __restrict__ part, int nparts, long long B,
+                                                          float* __restrict__ loss_out, uint64_t* rng_w) {
+  __shared__ float red[BCNF_WG];
+  nll_finalize(part, nparts, B, loss_out, rng_w, red);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1062,7 +1064,9 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
                                                       int nll, long long B,
                                                       const float* __restrict__ ysave, const uint32_t* __restrict__ msave,
                                                       float* __restrict__ dy, float* __restrict__ d1,
-                                                      float* __restrict__ slab_all, long long slab_stride) {
+                                                      float* __restrict__ slab_all, long long slab_stride,
+                                                      const float* __restrict__ nll_part, float* __restrict__ loss_out,
+                                                      uint64_t* rng_w) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const BwdTiles TI{NH};
   const int RFL = 16 * L.RF, RBL = 16 * L.RB;
@@ -1226,6 +1230,10 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
     if (j < Da) dy[b * D + j] = gya;
     if (j < Db) dy[b * D + Da + j] = gyb;
   }
+  if (loss_out && blockIdx.x == 0) {                 // deferred NLL reduction of the forward
+    __syncthreads();
+    nll_finalize(nll_part, (int)gridDim.x, B, loss_out, rng_w, gbuf);
+  }
 }
 
 // Deterministic sum of the per-workgroup gradient slabs (fixed order over workgroups). Slab block m holds
@@ -1373,9 +1381,6 @@ bool layout_matches(const BcnfLayout& L) {
 
 struct NllOut {
   float* part = nullptr;
-  unsigned* sync = nullptr;
-  float* loss = nullptr;
-  uint64_t* rng_w = nullptr;
 };
 
 int launch_hp(const BcnfLayout& L, const float* pk, const float* h, long long R, float* hp, hipStream_t st) {
@@ -1405,7 +1410,7 @@ int fwd_dispatch(const BcnfLayout& L, const float* pk, const float* y, const flo
   rc = launch_lds(k_forward<NH, DR, SV>, lds);                                                              \
   if (rc) return rc;                                                                                        \
   hipLaunchKernelGGL((k_forward<NH, DR, SV>), grid, dim3(BCNF_WG), lds, st, L, pk, y, hp, B, z, ldj, logp,  \
-                     rng, ysave, msave, no.part, no.sync, no.loss, no.rng_w);
+                     rng, ysave, msave, no.part);
   if (drop) {
     if (save) { BCNF_FWD(true, true) } else { BCNF_FWD(true, false) }
   } else {
@@ -1437,7 +1442,8 @@ int inv_dispatch(const BcnfLayout& L, const float* pk, const float* zin, const f
 template <int NH>
 int bwd_dispatch(const BcnfLayout& L, const float* pk, const float* hp, const float* dz, const float* dldj,
                  const float* dloss, int nll, long long B, const float* ysave, const uint32_t* msave, float* dy,
-                 float* d1, float* slab, long long stride, hipStream_t st) {
+                 float* d1, float* slab, long long stride, const float* part, float* loss_out, uint64_t* rng_w,
+                 hipStream_t st) {
   if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
   const dim3 grid((unsigned)((B + 15) / 16));
   size_t lds = bwd_lds_bytes(L);
@@ -1446,7 +1452,7 @@ int bwd_dispatch(const BcnfLayout& L, const float* pk, const float* hp, const fl
   rc = launch_lds(k_backward<NH, CP>, lds);                                                               \
   if (rc) return rc;                                                                                      \
   hipLaunchKernelGGL((k_backward<NH, CP>), grid, dim3(BCNF_WG), lds, st, L, pk, hp, dz, dldj, dloss, nll, B, \
-                     ysave, msave, dy, d1, slab, stride);
+                     ysave, msave, dy, d1, slab, stride, part, loss_out, rng_w);
   if (copy4_of(L) == 4) { BCNF_BWD(4) } else { BCNF_BWD(8) }
 #undef BCNF_BWD
   return check_launch();
@@ -1473,7 +1479,7 @@ long long ws_floats(const BcnfLayout& L, long long B, bool drop) { return ws_d1_
 
 int forward_impl(const BcnfStackDesc* desc, const void* packed, const float* y, const float* h, int64_t batch,
                  float* z, float* ldj, float* log_prob, int32_t training, const uint64_t* rng_state, void* workspace,
-                 bool save, bool nll, unsigned* sync, float* loss_out, void* stream) {
+                 bool save, bool nll, bool finalize, float* loss_out, void* stream) {
   BcnfLayout L;
   int rc = make_layout(desc, &L);
   if (rc) return rc;
@@ -1481,7 +1487,7 @@ int forward_impl(const BcnfStackDesc* desc, const void* packed, const float* y, 
   if (batch < 0) return BCNF_ERR_ARG;
   if (batch == 0) return nll ? BCNF_ERR_ARG : BCNF_OK;      // the mean over an empty batch is undefined
   if (!packed || !y || !h || !z || !workspace) return BCNF_ERR_ARG;
-  if (nll && (!sync || !loss_out)) return BCNF_ERR_ARG;
+  if (nll && finalize && !loss_out) return BCNF_ERR_ARG;
   const bool drop = training && L.p > 0.f;
   if (drop && !rng_state) return BCNF_ERR_ARG;
   float* ws = (float*)workspace;
@@ -1489,26 +1495,25 @@ int forward_impl(const BcnfStackDesc* desc, const void* packed, const float* y, 
   uint32_t* msave = (ysave && drop) ? (uint32_t*)(ws + ws_mask_off(L, batch)) : nullptr;
   float* hp = ws + ws_hp_off(L, batch, drop);
   NllOut no;
-  if (nll) {
-    no.part = ws + ws_part_off(L, batch, drop);
-    no.sync = sync;
-    no.loss = loss_out;
-    no.rng_w = drop ? const_cast<uint64_t*>(rng_state) : nullptr;
-  }
+  if (nll) no.part = ws + ws_part_off(L, batch, drop);
   const float* pk = (const float*)packed;
   hipStream_t st = (hipStream_t)stream;
   if ((rc = launch_hp(L, pk, h, batch, hp, st))) return rc;
   switch (L.NH) {
-#define BCNF_CASE(N) case N: return fwd_dispatch<N>(L, pk, y, hp, batch, z, ldj, log_prob, drop, rng_state, ysave, msave, no, st);
+#define BCNF_CASE(N) case N: rc = fwd_dispatch<N>(L, pk, y, hp, batch, z, ldj, log_prob, drop, rng_state, ysave, msave, no, st); break;
     BCNF_CASE(1) BCNF_CASE(2) BCNF_CASE(3) BCNF_CASE(4) BCNF_CASE(5) BCNF_CASE(6) BCNF_CASE(7) BCNF_CASE(8)
 #undef BCNF_CASE
     default: return BCNF_ERR_UNSUPPORTED;
   }
+  if (rc || !nll || !finalize) return rc;
+  hipLaunchKernelGGL(k_nll_finalize, dim3(1), dim3(BCNF_WG), 0, st, (const float*)no.part, (int)((batch + 15) / 16),
+                     (long long)batch, loss_out, drop ? const_cast<uint64_t*>(rng_state) : nullptr);
+  return check_launch();
 }
 
 int backward_impl(const BcnfStackDesc* desc, const void* packed, const float* h, const float* dz, const float* dldj,
                   const float* dloss, int nll, int64_t batch, int32_t training, void* workspace, float* dy,
-                  float* dh, float* dparams, void* slab, void* stream);
+                  float* dh, float* dparams, void* slab, float* loss_out, uint64_t* rng_state, void* stream);
 
 }  // namespace
 
@@ -1583,29 +1588,29 @@ int bcnf_stack_forward(const BcnfStackDesc* desc, const void* packed, const floa
                        float* z, float* ldj, float* log_prob, int32_t training, const uint64_t* rng_state,
                        void* workspace, int32_t save, void* stream) {
   return forward_impl(desc, packed, y, h, batch, z, ldj, log_prob, training, rng_state, workspace, save != 0, false,
-                      nullptr, nullptr, stream);
+                      false, nullptr, stream);
 }
 
 int bcnf_nll_forward(const BcnfStackDesc* desc, const void* packed, const float* y, const float* h, int64_t batch,
-                     float* z, float* ldj, int32_t training, uint64_t* rng_state, void* workspace, uint32_t* sync,
+                     float* z, float* ldj, int32_t training, uint64_t* rng_state, void* workspace, int32_t finalize,
                      float* loss_out, void* stream) {
   return forward_impl(desc, packed, y, h, batch, z, ldj, nullptr, training, rng_state, workspace, true, true,
-                      (unsigned*)sync, loss_out, stream);
+                      finalize != 0, loss_out, stream);
 }
 
 int bcnf_stack_backward(const BcnfStackDesc* desc, const void* packed, const float* h, const float* dz,
                         const float* dldj, int64_t batch, int32_t training, void* workspace, float* dy,
                         float* dh, float* dparams, void* slab, void* stream) {
   return backward_impl(desc, packed, h, dz, dldj, nullptr, 0, batch, training, workspace, dy, dh, dparams, slab,
-                       stream);
+                       nullptr, nullptr, stream);
 }
 
 int bcnf_nll_backward(const BcnfStackDesc* desc, const void* packed, const float* h, const float* z,
                       const float* dloss, int64_t batch, int32_t training, void* workspace, float* dy,
-                      float* dh, float* dparams, void* slab, void* stream) {
+                      float* dh, float* dparams, void* slab, float* loss_out, uint64_t* rng_state, void* stream) {
   if (!z && batch > 0) return BCNF_ERR_ARG;
   return backward_impl(desc, packed, h, z, nullptr, dloss, 1, batch, training, workspace, dy, dh, dparams, slab,
-                       stream);
+                       loss_out, rng_state, stream);
 }
 
 int bcnf_backward_tail(const BcnfStackDesc* desc, const void* packed, const void* slab, const float* h,
@@ -1719,7 +1724,7 @@ namespace {
 
 int backward_impl(const BcnfStackDesc* desc, const void* packed, const float* h, const float* dz, const float* dldj,
                   const float* dloss, int nll, int64_t batch, int32_t training, void* workspace, float* dy,
-                  float* dh, float* dparams, void* slab, void* stream) {
+                  float* dh, float* dparams, void* slab, float* loss_out, uint64_t* rng_state, void* stream) {
   BcnfLayout L;
   int rc = make_layout(desc, &L);
   if (rc) return rc;
@@ -1741,8 +1746,10 @@ int backward_impl(const BcnfStackDesc* desc, const void* packed, const float* h,
   float* d1 = ws + ws_d1_off(L, batch, drop);
   const float* pk = (const float*)packed;
   const long long stride = slab_stride_of(L);
+  const float* part = ws + ws_part_off(L, batch, drop);
+  uint64_t* rng_w = (loss_out && drop) ? rng_state : nullptr;
   switch (L.NH) {
-#define BCNF_CASE(N) case N: rc = bwd_dispatch<N>(L, pk, hp, dz, dldj, dloss, nll, batch, ysave, msave, dy, d1, (float*)slab, stride, st); break;
+#define BCNF_CASE(N) case N: rc = bwd_dispatch<N>(L, pk, hp, dz, dldj, dloss, nll, batch, ysave, msave, dy, d1, (float*)slab, stride, part, loss_out, rng_w, st); break;
     BCNF_CASE(1) BCNF_CASE(2) BCNF_CASE(3) BCNF_CASE(4) BCNF_CASE(5) BCNF_CASE(6) BCNF_CASE(7) BCNF_CASE(8)
 #undef BCNF_CASE
     default: return BCNF_ERR_UNSUPPORTED;

@@ -53,11 +53,9 @@ __device__ __forceinline__ float wg_sum(float v, float* red) {
 //   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
 // Hyper-parameters arrive as doubles (Python floats) and every scalar is derived in double, then
 // rounded once, as torch does (1 - beta2 in fp32 from 0.999f would be off by 1e-5 relative).
-__global__ __launch_bounds__(BCNF_WG) void k_adam(TList T, float* __restrict__ step, double lr, double b1d,
-                                                  double b2d, double epsd, double wdd, float* __restrict__ part,
-                                                  unsigned* __restrict__ sync) {
+__global__ __launch_bounds__(BCNF_WG) void k_adam(TList T, const float* __restrict__ step, double lr, double b1d,
+                                                  double b2d, double epsd, double wdd, float* __restrict__ part) {
   __shared__ float red[BCNF_WG];
-  __shared__ int last;
   __shared__ float sc[2];
   const float st = step[0] + 1.0f;
   if (threadIdx.x == 0) {                          // double pow once per workgroup, not per thread
@@ -91,17 +89,21 @@ __global__ __launch_bounds__(BCNF_WG) void k_adam(TList T, float* __restrict__ s
     }
   }
   const float s = wg_sum(ss, red);
-  if (threadIdx.x == 0) {
-    if (part) part[blockIdx.x] = s;
-    __threadfence();
-    const unsigned prev = atomicAdd(sync, 1u);
-    last = (prev == gridDim.x - 1);
+  if (threadIdx.x == 0 && part) part[blockIdx.x] = s;
+}
+
+// End-of-step bookkeeping by one thread of a LATER launch (every reader of these counters is done):
+// the Adam step count (torch keeps it as a float tensor) and an epoch cursor.
+__device__ __forceinline__ void advance_counters(float* step, long long* cursor, long long n_batches) {
+  if (step) step[0] += 1.0f;
+  if (cursor) {
+    const long long c = cursor[0] + 1;
+    cursor[0] = c < n_batches ? c : 0;
   }
-  __syncthreads();
-  if (last && threadIdx.x == 0) {   // every workgroup has read step[0]: publish the increment
-    step[0] = st;
-    *sync = 0u;
-  }
+}
+
+__global__ void k_advance(float* step, long long* cursor, long long n_batches) {
+  if (threadIdx.x == 0) advance_counters(step, cursor, n_batches);
 }
 
 __global__ __launch_bounds__(BCNF_WG) void k_sumsq(TList T, float* __restrict__ part) {
@@ -123,7 +125,8 @@ __global__ __launch_bounds__(BCNF_WG) void k_sumsq(TList T, float* __restrict__ 
 
 // torch.nn.utils.clip_grad_norm_: coef = min(max_norm / (||g||_2 + 1e-6), 1); g *= coef.
 __global__ __launch_bounds__(BCNF_WG) void k_clip(TList T, const float* __restrict__ part, int nparts, float max_norm,
-                                                  float* __restrict__ norm_out) {
+                                                  float* __restrict__ norm_out, float* step, long long* cursor,
+                                                  long long n_batches) {
   __shared__ float red[BCNF_WG];
   float acc = 0.f;
   for (int i = threadIdx.x; i < nparts; i += BCNF_WG) acc += part[i];
@@ -138,7 +141,10 @@ __global__ __launch_bounds__(BCNF_WG) void k_clip(TList T, const float* __restri
       T.g[t][i - T.start[t]] *= coef;
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && norm_out) norm_out[0] = tot;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (norm_out) norm_out[0] = tot;
+    advance_counters(step, cursor, n_batches);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -283,18 +289,41 @@ __global__ __launch_bounds__(BCNF_WG) void k_wt_reduce(const float* __restrict__
 
 using bcnf_rt::launched;
 
-// dst0[r] = src0[idx[r]] (cols0 floats), dst1[r] = src1[idx[r]] (cols1 floats), one launch for both.
-__global__ __launch_bounds__(BCNF_WG) void k_gather2(const int64_t* __restrict__ idx, long long n,
+// dst0[r] = src0[idx[r]] (cols0 floats), dst1[r] = src1[idx[r]] (cols1 floats), one launch for both;
+// workgroup w copies rows [w * rpw, (w + 1) * rpw) (32-bit index math: n * (cols0 + cols1) < 2^31), each
+// thread GU elements per round with every index and data load issued before the stores. With
+// `cursor` != NULL the rows are idx[cursor[0] * n + r] (the cursor is advanced by a later launch).
+constexpr int GU = 8;
+__global__ __launch_bounds__(BCNF_WG) void k_gather2(const int64_t* __restrict__ idx, int n, int rpw,
                                                      const float* __restrict__ s0, int c0, float* __restrict__ d0,
-                                                     const float* __restrict__ s1, int c1, float* __restrict__ d1) {
-  const long long t0 = n * c0, total = t0 + n * c1;
-  for (long long i = (long long)blockIdx.x * BCNF_WG + threadIdx.x; i < total; i += (long long)gridDim.x * BCNF_WG) {
-    if (i < t0) {
-      const long long r = i / c0;
-      d0[i] = s0[idx[r] * c0 + (i - r * c0)];
-    } else {
-      const long long j = i - t0, r = j / c1;
-      d1[j] = s1[idx[r] * c1 + (j - r * c1)];
+                                                     const float* __restrict__ s1, int c1, float* __restrict__ d1,
+                                                     const long long* __restrict__ cursor) {
+  if (cursor) idx += cursor[0] * n;
+  const int r0 = blockIdx.x * rpw, r1 = r0 + rpw < n ? r0 + rpw : n;
+  const int cw = c0 + c1, total = (r1 - r0) * cw;
+  for (int e0 = 0; e0 < total; e0 += GU * BCNF_WG) {
+    int r[GU], col[GU];
+    long long src[GU];
+    float v[GU];
+#pragma unroll
+    for (int u = 0; u < GU; ++u) {
+      int e = e0 + u * BCNF_WG + threadIdx.x;
+      e = e < total ? e : total - 1;
+      const int rr = e / cw;
+      r[u] = r0 + rr;
+      col[u] = e - rr * cw;
+      src[u] = idx[r[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < GU; ++u)
+      v[u] = col[u] < c0 ? s0[src[u] * c0 + col[u]] : s1[src[u] * c1 + (col[u] - c0)];
+#pragma unroll
+    for (int u = 0; u < GU; ++u) {
+      if (e0 + u * BCNF_WG + (int)threadIdx.x >= total) continue;
+      if (col[u] < c0)
+        d0[r[u] * c0 + col[u]] = v[u];
+      else
+        d1[r[u] * c1 + (col[u] - c0)] = v[u];
     }
   }
 }
@@ -329,19 +358,20 @@ int64_t bcnf_grad_partials(int64_t total_numel) { return total_numel <= 0 ? 1 : 
 
 int bcnf_adam_step(int32_t n_tensors, float* const* params, float* const* grads, float* const* exp_avg,
                    float* const* exp_avg_sq, const int64_t* numel, float* step, double lr, double beta1,
-                   double beta2, double eps, double weight_decay, float* grad_partials, uint32_t* sync,
+                   double beta2, double eps, double weight_decay, float* grad_partials, int32_t advance_step,
                    void* stream) {
   TList T;
   int rc = make_tlist(n_tensors, params, grads, exp_avg, exp_avg_sq, numel, &T);
   if (rc) return rc;
-  if (!params || !exp_avg || !exp_avg_sq || !step || !sync) return BCNF_ERR_ARG;
+  if (!params || !exp_avg || !exp_avg_sq || !step) return BCNF_ERR_ARG;
   for (int i = 0; i < n_tensors; ++i)
     if (!T.p[i] || !T.m[i] || !T.v[i]) return BCNF_ERR_ARG;
   const long long total = T.start[T.n];
   const unsigned nwg = (unsigned)bcnf_grad_partials(total);
   hipLaunchKernelGGL(k_adam, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, step, lr, beta1, beta2, eps,
-                     weight_decay, grad_partials, (unsigned*)sync);
-  return launched();
+                     weight_decay, grad_partials);
+  if ((rc = launched()) || !advance_step) return rc;
+  return bcnf_advance_counters(step, nullptr, 0, stream);
 }
 
 int bcnf_grad_sumsq(int32_t n_tensors, float* const* grads, const int64_t* numel, float* grad_partials, void* stream) {
@@ -355,27 +385,50 @@ int bcnf_grad_sumsq(int32_t n_tensors, float* const* grads, const int64_t* numel
 }
 
 int bcnf_clip_grad_norm(int32_t n_tensors, float* const* grads, const int64_t* numel, const float* grad_partials,
-                        float max_norm, float* total_norm, void* stream) {
+                        float max_norm, float* total_norm, float* advance_step, int64_t* advance_cursor,
+                        int64_t cursor_modulo, void* stream) {
   TList T;
   int rc = make_tlist(n_tensors, nullptr, grads, nullptr, nullptr, numel, &T);
   if (rc) return rc;
   if (!grad_partials) return BCNF_ERR_ARG;
   const long long np = bcnf_grad_partials(T.start[T.n]);
+  if (advance_cursor && cursor_modulo < 1) return BCNF_ERR_ARG;
   hipLaunchKernelGGL(k_clip, dim3((unsigned)np), dim3(BCNF_WG), 0, (hipStream_t)stream, T, grad_partials, (int)np,
-                     max_norm, total_norm);
+                     max_norm, total_norm, advance_step, (long long*)advance_cursor, (long long)cursor_modulo);
   return launched();
 }
+
+namespace {
+int gather_launch(const int64_t* idx, int64_t n, const float* src0, int32_t cols0, float* dst0, const float* src1,
+                  int32_t cols1, float* dst1, const int64_t* cursor, void* stream) {
+  if (n * (int64_t)(cols0 + cols1) >= (1LL << 31)) return BCNF_ERR_UNSUPPORTED;
+  const int nwg = n < 512 ? (int)n : 512;
+  const int rpw = (int)((n + nwg - 1) / nwg);
+  hipLaunchKernelGGL(k_gather2, dim3((unsigned)((n + rpw - 1) / rpw)), dim3(BCNF_WG), 0, (hipStream_t)stream, idx,
+                     (int)n, rpw, src0, cols0, dst0, src1, cols1, dst1, (const long long*)cursor);
+  return launched();
+}
+}  // namespace
 
 int bcnf_gather_rows2(const int64_t* idx, int64_t n, const float* src0, int32_t cols0, float* dst0,
                       const float* src1, int32_t cols1, float* dst1, void* stream) {
   if (n < 0 || cols0 < 1 || cols1 < 1) return BCNF_ERR_ARG;
   if (n == 0) return BCNF_OK;
   if (!idx || !src0 || !dst0 || !src1 || !dst1) return BCNF_ERR_ARG;
-  const long long total = n * (long long)(cols0 + cols1);
-  long long nblk = (total + BCNF_WG - 1) / BCNF_WG;
-  if (nblk > 2048) nblk = 2048;
-  hipLaunchKernelGGL(k_gather2, dim3((unsigned)nblk), dim3(BCNF_WG), 0, (hipStream_t)stream, idx, (long long)n, src0,
-                     cols0, dst0, src1, cols1, dst1);
+  return gather_launch(idx, n, src0, cols0, dst0, src1, cols1, dst1, nullptr, stream);
+}
+
+int bcnf_gather_batch(const int64_t* order, const int64_t* cursor, int64_t batch, const float* src0, int32_t cols0,
+                      float* dst0, const float* src1, int32_t cols1, float* dst1, void* stream) {
+  if (batch < 1 || cols0 < 1 || cols1 < 1) return BCNF_ERR_ARG;
+  if (!order || !cursor || !src0 || !dst0 || !src1 || !dst1) return BCNF_ERR_ARG;
+  return gather_launch(order, batch, src0, cols0, dst0, src1, cols1, dst1, cursor, stream);
+}
+
+int bcnf_advance_counters(float* step, int64_t* cursor, int64_t n_batches, void* stream) {
+  if (cursor && n_batches < 1) return BCNF_ERR_ARG;
+  hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, (hipStream_t)stream, step, (long long*)cursor,
+                     (long long)n_batches);
   return launched();
 }
 

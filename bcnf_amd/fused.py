@@ -267,15 +267,10 @@ class FusedStack:
             e1.record()
             tm.setdefault("k_bwd_tail", []).append((e0, e1))
 
-    def sync_word(self):
-        """One zero-initialised uint32 of device memory for the kernels' last-workgroup handshake."""
-        if getattr(self, "_sync", None) is None or self._sync.device != self.flat.device:
-            self._sync = torch.zeros(1, dtype=torch.int32, device=self.flat.device)
-        return self._sync
-
-    def launch_nll_forward(self, y, h, training: bool):
+    def launch_nll_forward(self, y, h, training: bool, finalize: bool = True):
         """Stack forward fused with inn_nll_loss (trainer.py:260-266): returns z, ldj, vals=[loss, nll, mse]
-        and the saved state for launch_nll_backward. The kernel itself advances the dropout RNG offset."""
+        and the saved state for launch_nll_backward. With finalize=False the loss reduction and the
+        dropout-RNG advance are deferred to the backward (vals is valid only after it)."""
         self._check_inputs(y, h, "forward")
         if h.shape[0] != y.shape[0]:
             raise ValueError(f"bcnf_amd forward: {y.shape[0]} samples but {h.shape[0]} feature rows")
@@ -298,14 +293,15 @@ class FusedStack:
             e0.record()
         rc = N.lib().bcnf_nll_forward(self._pdesc, N.ptr(pk), N.ptr(y), N.ptr(h), ctypes.c_int64(B), N.ptr(z),
                                       N.ptr(ldj), ctypes.c_int32(int(training)), N.ptr(rng), N.ptr(ws),
-                                      N.ptr(self.sync_word()), N.ptr(vals), N.stream_handle(dev))
+                                      ctypes.c_int32(int(finalize)), N.ptr(vals), N.stream_handle(dev))
         N.check(rc, "bcnf_nll_forward")
         if tm is not None:
             e1.record()
             tm.setdefault("k_forward", []).append((e0, e1))
         return z, ldj, vals, (ws, pk)
 
-    def launch_nll_backward(self, h, z, dvals, training: bool, saved, want_dy: bool, want_dh: bool):
+    def launch_nll_backward(self, h, z, dvals, training: bool, saved, want_dy: bool, want_dh: bool,
+                            finalize_into=None):
         ws, pk = saved
         B = h.shape[0]
         dev = h.device
@@ -320,9 +316,10 @@ class FusedStack:
         if tm is not None:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
+        rng = self.rng_state() if (finalize_into is not None and training and self.cfg.dropout > 0.0) else None
         rc = N.lib().bcnf_nll_backward(self._pdesc, N.ptr(pk), N.ptr(h), N.ptr(z), N.ptr(dvals), ctypes.c_int64(B),
                                        ctypes.c_int32(int(training)), N.ptr(ws), N.ptr(dy), None, None,
-                                       N.ptr(slab), stream)
+                                       N.ptr(slab), N.ptr(finalize_into), N.ptr(rng), stream)
         N.check(rc, "bcnf_nll_backward")
         self._backward_tail(h, ws, pk, slab, dh, dparams, B, training, stream, tm, e0)
         return dy, dh, dparams
@@ -337,7 +334,7 @@ class FusedStack:
         dev = y.device
         stream = N.stream_handle(dev)
         B = y.shape[0]
-        z, _, vals, (ws, pk) = self.launch_nll_forward(y, h, training)
+        z, _, vals, (ws, pk) = self.launch_nll_forward(y, h, training, finalize=False)
         _, sb = self.workspace_bytes(B, training)
         slab = torch.empty(max(sb // 4, 1), dtype=torch.float32, device=dev)
         dh = torch.empty_like(h)
@@ -347,10 +344,10 @@ class FusedStack:
         calls = {
             "forward": lambda: L.bcnf_nll_forward(self._pdesc, N.ptr(pk), N.ptr(y), N.ptr(h), ctypes.c_int64(B), N.ptr(z),
                                                   N.ptr(ldj), ctypes.c_int32(int(training)), N.ptr(rng), N.ptr(ws),
-                                                  N.ptr(self.sync_word()), N.ptr(vals), stream),
+                                                  ctypes.c_int32(0), N.ptr(vals), stream),
             "k_backward": lambda: L.bcnf_nll_backward(self._pdesc, N.ptr(pk), N.ptr(h), N.ptr(z), None, ctypes.c_int64(B),
                                                       ctypes.c_int32(int(training)), N.ptr(ws), None, None, None,
-                                                      N.ptr(slab), stream),
+                                                      N.ptr(slab), None, None, stream),
             "tail": lambda: L.bcnf_backward_tail(self._pdesc, N.ptr(pk), N.ptr(slab), N.ptr(h), N.ptr(ws),
                                                  ctypes.c_int64(B), ctypes.c_int32(int(training)), N.ptr(dh),
                                                  N.ptr(dparams), stream),
@@ -423,32 +420,36 @@ class _StackNLL(torch.autograd.Function):
     backward (no dz / dldj tensors, no elementwise loss kernels)."""
 
     @staticmethod
-    def forward(ctx, y, h, flat_param, stack: FusedStack, training: bool):
-        z, _, vals, saved = stack.launch_nll_forward(y, h, training)
+    def forward(ctx, y, h, flat_param, stack: FusedStack, training: bool, defer: bool):
+        z, _, vals, saved = stack.launch_nll_forward(y, h, training, finalize=not defer)
         ctx.stack = stack
         ctx.training = training
         ctx.saved = saved
-        ctx.save_for_backward(h, z)
+        ctx.defer = defer
+        ctx.save_for_backward(h, z, vals)
         return vals
 
     @staticmethod
     def backward(ctx, dvals):
-        h, z = ctx.saved_tensors
+        h, z, vals = ctx.saved_tensors
         need_y, need_h, need_p = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
         dy, dh, dparams = ctx.stack.launch_nll_backward(h, z, dvals.contiguous(), ctx.training, ctx.saved,
-                                                        want_dy=need_y, want_dh=need_h)
-        return dy, dh, (dparams if need_p else None), None, None
+                                                        want_dy=need_y, want_dh=need_h,
+                                                        finalize_into=vals if ctx.defer else None)
+        return dy, dh, (dparams if need_p else None), None, None, None
 
 
-def stack_nll(stack: FusedStack, y, h, training: bool):
-    """[loss, nll, mse] (mse = 0, hybrid_weight = 0) of the Trainer's loss on the fused stack."""
+def stack_nll(stack: FusedStack, y, h, training: bool, defer: bool = False):
+    """[loss, nll, mse] (mse = 0, hybrid_weight = 0) of the Trainer's loss on the fused stack. defer=True
+    (for a backward that certainly follows, e.g. TrainStep) lets the backward do the loss reduction and
+    the dropout-RNG advance: one launch less, but vals is only valid after the backward."""
     y = y.contiguous()
     h = h.contiguous()
     stack.sync_grad_state()
     params_grad = stack.trainable[0].requires_grad
     fp = stack.flat_param
     if torch.is_grad_enabled() and (params_grad or y.requires_grad or h.requires_grad):
-        return _StackNLL.apply(y, h, fp if params_grad else fp.detach(), stack, training)
+        return _StackNLL.apply(y, h, fp if params_grad else fp.detach(), stack, training, defer)
     return stack.launch_nll_forward(y, h, training)[2]
 
 

@@ -32,7 +32,7 @@ class FusedAdam(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay))
         self._partials = None      # per-workgroup sum(g^2) of the last step, consumed by the clip
         self._partials_for = None
-        self._sync = None
+        self._pending_steps = []   # step counts whose advance the following clip performs
 
     def _state(self, p):
         st = self.state[p]
@@ -43,7 +43,9 @@ class FusedAdam(torch.optim.Optimizer):
         return st
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, defer_step_count: bool = False):
+        """One Adam update. defer_step_count=True leaves the device step count to be advanced by the
+        following clip_grad_norm_after_step (one launch less per training step)."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -59,8 +61,6 @@ class FusedAdam(torch.optim.Optimizer):
                     raise RuntimeError("bcnf_amd FusedAdam: parameters and grads must be contiguous fp32 GPU tensors")
             b1, b2 = group["betas"]
             dev = params[0].device
-            if self._sync is None or self._sync.device != dev:
-                self._sync = torch.zeros(1, dtype=torch.int32, device=dev)
             for chunk in _groups(params):
                 states = [self._state(p) for p in chunk]
                 step = states[0]["step"]
@@ -76,26 +76,41 @@ class FusedAdam(torch.optim.Optimizer):
                                       N.ptr_array([s["exp_avg_sq"] for s in states]), numel, N.ptr(step),
                                       ctypes.c_double(group["lr"]), ctypes.c_double(b1), ctypes.c_double(b2),
                                       ctypes.c_double(group["eps"]), ctypes.c_double(group["weight_decay"]),
-                                      N.ptr(part), N.ptr(self._sync), N.stream_handle(dev))
+                                      N.ptr(part), ctypes.c_int32(0 if defer_step_count else 1),
+                                      N.stream_handle(dev))
                 N.check(rc, "bcnf_adam_step")
                 all_grads.append((chunk, grads, numel, part))
+                if defer_step_count:
+                    self._pending_steps.append(step)
         self._partials = all_grads
         self._partials_for = [p for chunk, _, _, _ in all_grads for p in chunk]
         return loss
 
     @torch.no_grad()
-    def clip_grad_norm_after_step(self, max_norm: float = 1.0):
+    def clip_grad_norm_after_step(self, max_norm: float = 1.0, cursor=None):
         """clip_grad_norm_(params, max_norm) for exactly the gradients the last step() consumed (unchanged
-        since), reusing that step's squared-gradient partials. Returns the pre-clip total norm (device)."""
+        since), reusing that step's squared-gradient partials. Also performs the end-of-step bookkeeping:
+        a deferred step count, and `cursor` = (device int64 counter, modulo) of an epoch walk.
+        Returns the pre-clip total norm (device)."""
         if not self._partials:
             raise RuntimeError("bcnf_amd FusedAdam: clip_grad_norm_after_step() needs a preceding step()")
-        if len(self._partials) != 1:   # several launches: recompute the norm over all of them
-            return clip_grad_norm_(self._partials_for, max_norm)
+        L = N.lib()
+        pending, self._pending_steps = self._pending_steps, []
+        cur, mod = cursor if cursor is not None else (None, 0)
+        if len(self._partials) != 1 or len(pending) > 1:   # several launches: generic path
+            norm = clip_grad_norm_(self._partials_for, max_norm)
+            dev = norm.device
+            for st in pending:
+                N.check(L.bcnf_advance_counters(N.ptr(st), None, 0, N.stream_handle(dev)), "bcnf_advance_counters")
+            if cur is not None:
+                N.check(L.bcnf_advance_counters(None, N.ptr(cur), mod, N.stream_handle(dev)), "bcnf_advance_counters")
+            return norm
         _, grads, numel, part = self._partials[0]
         dev = grads[0].device
         norm = torch.empty((), dtype=torch.float32, device=dev)
-        rc = N.lib().bcnf_clip_grad_norm(len(grads), N.ptr_array(grads), numel, N.ptr(part),
-                                         ctypes.c_float(max_norm), N.ptr(norm), N.stream_handle(dev))
+        rc = L.bcnf_clip_grad_norm(len(grads), N.ptr_array(grads), numel, N.ptr(part), ctypes.c_float(max_norm),
+                                   N.ptr(norm), N.ptr(pending[0] if pending else None), N.ptr(cur),
+                                   ctypes.c_int64(mod), N.stream_handle(dev))
         N.check(rc, "bcnf_clip_grad_norm")
         return norm
 
@@ -121,5 +136,5 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0):
     N.check(L.bcnf_grad_sumsq(len(grads), N.ptr_array(grads), numel, N.ptr(part), stream), "bcnf_grad_sumsq")
     norm = torch.empty((), dtype=torch.float32, device=dev)
     N.check(L.bcnf_clip_grad_norm(len(grads), N.ptr_array(grads), numel, N.ptr(part), ctypes.c_float(max_norm),
-                                  N.ptr(norm), stream), "bcnf_clip_grad_norm")
+                                  N.ptr(norm), None, None, ctypes.c_int64(0), stream), "bcnf_clip_grad_norm")
     return norm

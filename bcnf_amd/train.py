@@ -51,12 +51,13 @@ class TrainStep:
         self._graphs = None
         self._static = None
         self._pool = None
+        self._epoch = None      # (order, cursor, n_batches, batch) for the device-cursor batch walk
 
     # ------------------------------------------------------------------ step pieces
     def _forward_backward(self, y, traj):
         self.opt.zero_grad(set_to_none=True)
         if self.fused_loss:
-            vals = self.model.nll_loss(y, traj)
+            vals = self.model.nll_loss(y, traj, defer_reduction=True)   # reduced in the backward launch
             if self._cot is None or self._cot.device != vals.device:
                 self._cot = torch.tensor([1.0, 0.0, 0.0], device=vals.device)
             torch.autograd.backward(vals, self._cot)      # loss.backward()
@@ -77,8 +78,11 @@ class TrainStep:
                 p.grad.mul_(1.0 / self.world)
 
     def _update(self):
-        self.opt.step()
-        self.opt.clip_grad_norm_after_step(self.max_norm)
+        """Adam, then clip_grad_norm_ after the step (trainer.py:270-272); the clip launch also advances the
+        Adam step count and, in epoch mode, the batch cursor (end-of-step bookkeeping, no extra launch)."""
+        self.opt.step(defer_step_count=True)
+        cursor = (self._epoch[1], self._epoch[2]) if self._epoch is not None else None
+        self.opt.clip_grad_norm_after_step(self.max_norm, cursor=cursor)
 
     def broadcast_parameters(self, src: int = 0):
         """Identical initial replicas (the RNG-seeded init differs per process otherwise)."""
@@ -96,17 +100,23 @@ class TrainStep:
         return vals
 
     def _gather(self):
-        """pool rows of the static index buffer, both tensors in one native launch"""
+        """Pool rows of the current batch, both tensors in one native launch: the static index buffer, or
+        (epoch mode) batch `cursor` of the device-resident epoch order, the cursor advancing on the device."""
         from bcnf_amd import _native as N
-        sidx = self._static[2]
         py, pt = self._pool
-        n = sidx.shape[0]
+        n = self._epoch[3] if self._epoch is not None else self._static[2].shape[0]
         y = torch.empty((n,) + tuple(py.shape[1:]), dtype=py.dtype, device=py.device)
         t = torch.empty((n,) + tuple(pt.shape[1:]), dtype=pt.dtype, device=pt.device)
-        cy = py[0].numel() if py.shape[0] else 1
-        ct = pt[0].numel() if pt.shape[0] else 1
-        N.check(N.lib().bcnf_gather_rows2(N.ptr(sidx), n, N.ptr(py), cy, N.ptr(y), N.ptr(pt), ct, N.ptr(t),
-                                          N.stream_handle(py.device)), "bcnf_gather_rows2")
+        cy = py[0].numel()
+        ct = pt[0].numel()
+        st = N.stream_handle(py.device)
+        if self._epoch is not None:
+            order, cursor = self._epoch[0], self._epoch[1]
+            N.check(N.lib().bcnf_gather_batch(N.ptr(order), N.ptr(cursor), n, N.ptr(py), cy, N.ptr(y), N.ptr(pt), ct,
+                                              N.ptr(t), st), "bcnf_gather_batch")
+        else:
+            N.check(N.lib().bcnf_gather_rows2(N.ptr(self._static[2]), n, N.ptr(py), cy, N.ptr(y), N.ptr(pt), ct,
+                                              N.ptr(t), st), "bcnf_gather_rows2")
         return y, t
 
     def _snapshot(self):
@@ -115,11 +125,14 @@ class TrainStep:
             opt = {id(p): {k: v.clone() for k, v in st.items() if torch.is_tensor(v)}
                    for p, st in self.opt.state.items()}
             rng = self.model.fused.rng_state().clone()
-        return params, opt, rng
+            cur = self._epoch[1].clone() if self._epoch is not None else None
+        return params, opt, rng, cur
 
     def _restore(self, snap):
-        params, opt, rng = snap
+        params, opt, rng, cur = snap
         with torch.no_grad():
+            if cur is not None:
+                self._epoch[1].copy_(cur)
             for p, v in zip(self.model.parameters(), params):
                 p.copy_(v)
             for p, st in self.opt.state.items():
@@ -173,6 +186,8 @@ class TrainStep:
         return self._host_values()
 
     def _host_values(self):
+        """The step's three logged values (the Trainer's .item() calls): one stream sync after the graph's
+        device-to-host copy, then a read of the pinned buffer."""
         torch.cuda.current_stream().synchronize()
         return tuple(self._host_vals.tolist())
 
@@ -208,6 +223,41 @@ class TrainStep:
             py, pt = self._pool
             self._build_graphs(py.index_select(0, idx), pt.index_select(0, idx), idx=idx)
         self._static[2].copy_(idx, non_blocking=True)
+        self._replay()
+        return self._host_values()
+
+    # ------------------------------------------------------------------ device-resident epoch order
+    def set_epoch(self, order, batch: int):
+        """Walk `order` (device int64, n_batches * batch pool indices, e.g. concatenated shuffled epochs)
+        batch by batch with step_epoch(); the graph reads batch `cursor` and advances the cursor itself, so
+        a step needs no host-to-device traffic. A later call replaces the order (same size) and rewinds."""
+        if self._pool is None:
+            raise RuntimeError("set_epoch() needs set_pool()")
+        order = order.to(dtype=torch.int64).contiguous()
+        nb = order.numel() // batch
+        if nb < 1 or order.numel() != nb * batch:
+            raise ValueError("set_epoch: order must hold a whole number of batches")
+        if self._epoch is None:
+            if self._graphs is not None:
+                raise RuntimeError("set_epoch() must precede the first step of a non-epoch TrainStep")
+            dev = order.device
+            self._epoch = (order.clone(), torch.zeros(1, dtype=torch.int64, device=dev), nb, batch)
+        else:
+            o, cursor, nb0, b0 = self._epoch
+            if nb != nb0 or batch != b0:
+                raise ValueError("set_epoch: a captured TrainStep keeps its order size")
+            o.copy_(order)
+            cursor.zero_()
+
+    def step_epoch(self):
+        """The next batch of the epoch order (see set_epoch)."""
+        if self._epoch is None:
+            raise RuntimeError("step_epoch() needs set_epoch()")
+        if not self.capture:
+            return tuple(self.eager_step(*self._gather()).tolist())
+        if self._graphs is None:
+            y, t = self._gather()
+            self._build_graphs(y, t, idx=torch.zeros(1, dtype=torch.int64, device=y.device))
         self._replay()
         return self._host_values()
 

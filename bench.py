@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=12)
     ap.add_argument("--kernel-iters", type=int, default=20)
+    ap.add_argument("--indexed", action="store_true", help="per-step index copy instead of the device epoch cursor")
     return ap.parse_args()
 
 
@@ -147,17 +148,21 @@ def main():
     step = TrainStep(model, lr=2e-4, capture=not args.no_graph)
     step.broadcast_parameters()
     step.set_pool(data.y, data.traj)
+    # the shuffled batch order of the whole run lives on the device; the graph walks it with a device cursor
+    batches = [data.next_indices() for _ in range(args.warmup + args.steps)]
+    if not args.indexed:
+        step.set_epoch(torch.cat(batches), args.batch)
+    run = (lambda i: step.step_indexed(batches[i])) if args.indexed else (lambda i: step.step_epoch())
 
-    for _ in range(args.warmup):
-        step.step_indexed(data.next_indices())
-    batches = [data.next_indices() for _ in range(args.steps)]
+    for i in range(args.warmup):
+        run(i)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     losses = None
-    for idx in batches:
-        losses = step.step_indexed(idx)
+    for i in range(args.warmup, args.warmup + args.steps):
+        losses = run(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

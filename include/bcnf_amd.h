@@ -130,23 +130,25 @@ int bcnf_stack_inverse(const BcnfStackDesc* desc, const void* packed, const floa
                        const uint64_t* rng_state, void* scratch, void* stream);
 
 /* ---- NLL training pass (forward + inn_nll_loss + backward without any host round trip) ---------
- * bcnf_nll_forward = bcnf_stack_forward (workspace required) plus, in the same launch,
- *   loss_out[0] = loss = (nll + 0 * mse) / (1 + 0), loss_out[1] = nll = mean_b(0.5 |z_b|^2 - ldj_b),
- *   loss_out[2] = mse = 0            (the Trainer's three logged values with hybrid_weight == 0)
- * The last workgroup to finish reduces the per-workgroup partials in a fixed order and, when dropout
- * is active, advances rng_state[1] by one (so graph replays draw fresh masks). `sync` is one uint32 of
- * device memory that must be zero before the first call; every call leaves it zero. */
+ * bcnf_nll_forward = bcnf_stack_forward (workspace required, save on) plus per-workgroup partials of
+ *   nll = mean_b(0.5 |z_b|^2 - ldj_b)  (utils.py:40-46). With finalize != 0 a one-workgroup launch then
+ *   writes loss_out[0] = loss = (nll + 0 * mse) / (1 + 0), loss_out[1] = nll, loss_out[2] = mse = 0 (the
+ *   Trainer's three logged values with hybrid_weight == 0) and, when dropout is active, advances
+ *   rng_state[1] by one (so graph replays draw fresh masks). With finalize == 0 that reduction is
+ *   deferred to bcnf_nll_backward(loss_out, rng_state) (saves a launch in a training step). No kernel
+ *   synchronises across workgroups. */
 int bcnf_nll_forward(const BcnfStackDesc* desc, const void* packed, const float* y, const float* h, int64_t batch,
-                     float* z, float* ldj, int32_t training, uint64_t* rng_state, void* workspace, uint32_t* sync,
+                     float* z, float* ldj, int32_t training, uint64_t* rng_state, void* workspace, int32_t finalize,
                      float* loss_out, void* stream);
 
 /* Backward through loss_out w.r.t. y, h and the stack parameters: dz = z * g / B, dldj = -g / B with
  * g = dloss[0] + dloss[1], dloss being the device cotangent of loss_out[0..2] (NULL means d loss = 1,
- * i.e. loss.backward(); mse carries no gradient). z is the forward's output. Otherwise as
+ * i.e. loss.backward(); mse carries no gradient). z is the forward's output. With loss_out != NULL it
+ * also performs the forward's deferred loss reduction (finalize == 0 there). Otherwise as
  * bcnf_stack_backward. */
 int bcnf_nll_backward(const BcnfStackDesc* desc, const void* packed, const float* h, const float* z,
                       const float* dloss, int64_t batch, int32_t training, void* workspace, float* dy,
-                      float* dh, float* dparams, void* slab, void* stream);
+                      float* dh, float* dparams, void* slab, float* loss_out, uint64_t* rng_state, void* stream);
 
 /* ---- Optimizer ------------------------------------------------------------------------------------
  * Tensors are passed as arrays of n_tensors (<= BCNF_MAX_TENSORS) device pointers + element counts and
@@ -156,28 +158,39 @@ int64_t bcnf_grad_partials(int64_t total_numel);
 
 /* One torch.optim.Adam step (amsgrad = maximize = False) over every tensor; hyper-parameters are
  * doubles (derived scalars such as 1 - beta2 are formed in double and rounded once, as torch does);
- * `step` is the device-side
- * float step count (incremented by the call, as Adam(capturable=True) keeps it). With grad_partials !=
- * NULL it also writes the per-workgroup sums of squared gradients for bcnf_clip_grad_norm. `sync`: one
- * zero-initialised uint32 of device memory (left zero). */
+ * `step` is the device-side float step count (as Adam(capturable=True) keeps it): the update uses
+ * step + 1, and advance_step != 0 then stores it (a one-thread launch). With advance_step == 0 the
+ * caller advances it later (bcnf_clip_grad_norm(advance_step = step)), saving that launch. With
+ * grad_partials != NULL the per-workgroup sums of squared gradients for bcnf_clip_grad_norm are written. */
 int bcnf_adam_step(int32_t n_tensors, float* const* params, float* const* grads, float* const* exp_avg,
                    float* const* exp_avg_sq, const int64_t* numel, float* step, double lr, double beta1,
-                   double beta2, double eps, double weight_decay, float* grad_partials, uint32_t* sync,
+                   double beta2, double eps, double weight_decay, float* grad_partials, int32_t advance_step,
                    void* stream);
 
 /* Per-workgroup sums of squared gradients (when no bcnf_adam_step produced them). */
 int bcnf_grad_sumsq(int32_t n_tensors, float* const* grads, const int64_t* numel, float* grad_partials, void* stream);
 
 /* clip_grad_norm_(max_norm, norm_type=2): total = sqrt(sum partials); g *= min(max_norm/(total+1e-6), 1).
- * total_norm (device float, nullable) receives the pre-clip norm. */
+ * total_norm (device float, nullable) receives the pre-clip norm. End-of-step bookkeeping (nullable):
+ * advance_step[0] += 1 (a deferred Adam step count) and advance_cursor[0] = (cursor + 1) % cursor_modulo
+ * (an epoch cursor of bcnf_gather_batch). */
 int bcnf_clip_grad_norm(int32_t n_tensors, float* const* grads, const int64_t* numel, const float* grad_partials,
-                        float max_norm, float* total_norm, void* stream);
+                        float max_norm, float* total_norm, float* advance_step, int64_t* advance_cursor,
+                        int64_t cursor_modulo, void* stream);
+
+/* The same bookkeeping as a one-thread launch. */
+int bcnf_advance_counters(float* step, int64_t* cursor, int64_t n_batches, void* stream);
 
 /* ---- Batch feed: dst0[r] = src0[idx[r]], dst1[r] = src1[idx[r]] (row-major rows of cols0 / cols1
  * floats) in one launch -- the shuffled-batch gather of the Trainer's DataLoader (trainer.py:164-166)
  * from device-resident data. */
 int bcnf_gather_rows2(const int64_t* idx, int64_t n, const float* src0, int32_t cols0, float* dst0,
                       const float* src1, int32_t cols1, float* dst1, void* stream);
+/* The same for batch number cursor[0] of an epoch order (device int64 indices, batch per batch): rows
+ * order[cursor[0] * batch + r]. The cursor is advanced by a later launch (bcnf_clip_grad_norm /
+ * bcnf_advance_counters), so the gather needs no cross-workgroup synchronisation (graph-replay safe). */
+int bcnf_gather_batch(const int64_t* order, const int64_t* cursor, int64_t batch, const float* src0, int32_t cols0,
+                      float* dst0, const float* src1, int32_t cols1, float* dst1, void* stream);
 
 /* ---- nn.Linear (row-major, weight out_features x in_features) ------------------------------------ */
 int bcnf_linear_forward(const float* x, const float* weight, const float* bias, int64_t rows, int32_t in_features,

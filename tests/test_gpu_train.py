@@ -194,15 +194,20 @@ def test_trainstep_graph_replay_equals_eager(g1):
     pool_t = torch.randn(512, 30, 3, generator=gen).to(DEV)
     idxs = [torch.randperm(512, generator=gen)[:256].to(DEV) for _ in range(3)]
     res = []
-    for capture in (False, True):
+    for capture, epoch in ((False, False), (True, False), (True, True)):
         m = fresh_model(g1, train=True)
         m.fused.set_seed(77)
         st = TrainStep(m, lr=2e-4, capture=capture)
         st.set_pool(pool_y, pool_t)
-        losses = [st.step_indexed(i) for i in idxs]
+        if epoch:    # device-resident order + device cursor: no per-step index traffic
+            st.set_epoch(torch.cat(idxs), 256)
+            losses = [st.step_epoch() for _ in idxs]
+        else:
+            losses = [st.step_indexed(i) for i in idxs]
         res.append((losses, [p.detach().clone() for p in m.parameters()], int(m.fused.rng_state()[1].item())))
-    (l0, p0, r0), (l1, p1, r1) = res
-    assert l0 == l1
-    assert r0 == r1 == 3
-    for a, b in zip(p0, p1):
-        assert torch.equal(a, b)
+    (l0, p0, r0) = res[0]
+    for (l1, p1, r1) in res[1:]:
+        assert l0 == l1
+        assert r0 == r1 == 3
+        for a, b in zip(p0, p1):
+            assert torch.equal(a, b)

@@ -41,6 +41,17 @@ def main():
         if it >= 3:
             for k, (a, b) in {"fwd+pack": (0, 1), "bwd+reduce": (1, 2), "inverse+pack": (2, 3)}.items():
                 res.setdefault(k, []).append(e[a].elapsed_time(e[b]) * 1e3)
+    # NLL-fused forward (last-workgroup epilogue) vs plain forward
+    for name, fn in (("fwd plain", lambda: st.launch_forward(y, h, train, save=True)),
+                     ("fwd nll", lambda: st.launch_nll_forward(y, h, train))):
+        for it in range(args.iters + 3):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            torch.cuda.synchronize()
+            if it >= 3:
+                res.setdefault(name, []).append(a.elapsed_time(b) * 1e3)
     for k, v in res.items():
         v.sort()
         print(f"{k:14s} median {v[len(v)//2]:8.1f} us   min {v[0]:8.1f} us")
