@@ -45,7 +45,7 @@ struct BcnfLayout {
   int RF, RB;           // per-lane record floats (forward/inverse, backward)
   // record offsets (floats, per lane)
   int rf_b1, rf_w1, rf_hid, rf_t, rf_s, rf_q;
-  int rb_w1t, rb_hid, rb_tt, rb_st, rb_qt;
+  int rb_w1t, rb_hid, rb_tt, rb_st, rb_qt, rb_an;
   // packed buffer offsets (floats)
   // W1 condition part, two contiguous copies for the projection GEMMs (NKp = nb*16 rounded up to 64):
   //   W1hC [Cp][NKp]  (c, k*16+j)   W1hR [NKp][Cp]  (k*16+j, c)   b1c [NKp]

@@ -98,7 +98,8 @@ int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
   L->rb_tt = 16 + 16 * (L->NH > 0 ? L->NH - 1 : 0);
   L->rb_st = L->rb_tt + 16;
   L->rb_qt = L->rb_st + 16;
-  L->RB = round_rec(L->rb_qt + 64);
+  L->rb_an = L->rb_qt + 64;                    // ActNorm [sa ba sb bb] (the backward needs no forward record)
+  L->RB = round_rec(L->rb_an + 4);
   long long nbl = L->nb;
   L->pf_off = 0;
   L->pb_off = L->pf_off + nbl * 16 * L->RF;
@@ -115,9 +116,9 @@ int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
 size_t fwd_lds_bytes(const BcnfLayout& L) {   // forward / inverse record ring (2 blocks)
   return sizeof(float) * (size_t)(2 * 16 * L.RF);
 }
-size_t bwd_lds_bytes(const BcnfLayout& L) {   // F/B record rings, gradient tiles (2), job table, gradient block
+size_t bwd_lds_bytes(const BcnfLayout& L) {   // backward record ring, gradient tiles (2), job table, gradient block
   const int NT = 2 * L.NH + NT_EXTRA;
-  return sizeof(float) * (size_t)(2 * 16 * L.RF + 2 * 16 * L.RB + 2 * NT * TILE + 8 * (2 * (BCNF_MAX_HIDDEN + 2) + 4) +
+  return sizeof(float) * (size_t)(2 * 16 * L.RB + 2 * NT * TILE + 8 * (2 * (BCNF_MAX_HIDDEN + 2) + 4) +
                                   L.blk_pad + 64);
 }
 // float4 stores per thread that copy one block's gradient partials from LDS to the slab (fixed count)
@@ -221,6 +222,7 @@ __device__ float rec_b(const BcnfLayout& L, const float* P, const float* Q, int 
     return (j < L.H[NH] && src < Db) ? cW(L, P, k, NH + 1, half * Db + src, j) : 0.f;
   }
   if (e >= L.rb_qt && e < L.rb_qt + 64) return rec_f(L, P, Q, k, j, L.rf_q + (e - L.rb_qt), true);
+  if (e >= L.rb_an && e < L.rb_an + 4) return rec_f(L, P, Q, k, j, e - L.rb_an, false);
   return 0.f;
 }
 
@@ -615,8 +617,17 @@ struct RecF {
 };
 template <int NH>
 struct RecB {
-  static constexpr int W1T = 0, HID = 16, TT = 16 + 16 * (NH - 1), ST = TT + 16, QT = ST + 16, USED = QT + 64;
+  static constexpr int W1T = 0, HID = 16, TT = 16 + 16 * (NH - 1), ST = TT + 16, QT = ST + 16, AN = QT + 64;
+  static constexpr int USED = AN + 4;
 };
+// Activation record a training forward saves per (block, sample, lane) for the backward, so the backward
+// never recomputes the MLP: masked activations, masked GELU derivatives, tanh(s), and the block input.
+template <int NH>
+struct ActRec {
+  static constexpr int ACT = 0, GD = NH, S = 2 * NH, YA = 2 * NH + 1, YB = 2 * NH + 2;
+  static constexpr int AR = (2 * NH + 3 + 3) & ~3;   // floats per lane (float4 aligned)
+};
+__host__ __device__ constexpr int act_rec_floats(int NH) { return (2 * NH + 3 + 3) & ~3; }
 
 // Burst-load floats [lo, hi) of this lane's LDS record into registers (compile-time indices, so the
 // array lives in VGPRs): one LDS wait per block instead of one per layer.
@@ -693,8 +704,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
                                                      const float* __restrict__ y, const float* __restrict__ hp,
                                                      long long B, float* __restrict__ z, float* __restrict__ ldj_out,
                                                      float* __restrict__ logp, const uint64_t* rng,
-                                                     float* __restrict__ ysave, uint32_t* __restrict__ msave,
-                                                     float* __restrict__ nll_part) {
+                                                     float* __restrict__ arec, float* __restrict__ nll_part) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int RFL = 16 * L.RF;
   float* rec = smem;                    // [2][16*RF]
@@ -722,7 +732,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
   __syncthreads();
 
   float ldj = 0.f;
-  uint32_t mword = 0;
+  using AR = ActRec<NH>;
 
   for (int k = 0; k < nb; ++k) {
     const int cur = k & 1;
@@ -734,28 +744,32 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
 
     float rr[RecF<NH>::USED];
     ld_rec_exp<0, RecF<NH>::USED>(rr, rec + cur * RFL + j * L.RF);
-    if (SAVE) {
-      float* ys = ysave + ((long long)k * B + bc) * 32;
-      ys[j] = ya;
-      ys[16 + j] = yb;
-    }
     const float xa = fmaf(rr[0], ya, rr[1]);          // ActNorm (cnf.py:349)
     const float xb = fmaf(rr[2], yb, rr[3]);
     uint32_t bits = 0xffu;
     if (DROP && !(BCNF_EXP & 8)) bits = dropout_bits(L, seed, off, bc, k, j, 0u);
     float T, Sp;
-    mlp_forward<NH, false>(L, rr, xa, hpk, bits, DROP, T, Sp, nullptr, nullptr);
+    float ar[AR::AR];                                   // activation record of this block (SAVE)
+    if (SAVE)
+      mlp_forward<NH, true>(L, rr, xa, hpk, bits, DROP, T, Sp, ar + AR::ACT, ar + AR::GD);
+    else
+      mlp_forward<NH, false>(L, rr, xa, hpk, bits, DROP, T, Sp, nullptr, nullptr);
     const float S = tanh_bf(Sp);                      // cnf.py:107
     const float zb = fmaf(expf(S), xb, T);            // cnf.py:179
     ldj += S;                                          // cnf.py:190
-    mix(rr + RecF<NH>::Q, xa, zb, ya, yb);             // y @ Q (cnf.py:335); identity after the last block
-    if (SAVE && DROP) {
-      mword |= bits << (8 * (k & 3));
-      if ((k & 3) == 3 || k == nb - 1) {
-        msave[((long long)(k >> 2) * B + bc) * 16 + j] = mword;
-        mword = 0;
-      }
+    if (SAVE) {                                        // 16-B stores, a lane's record contiguous
+      ar[AR::S] = S;
+      ar[AR::YA] = ya;
+      ar[AR::YB] = yb;
+#pragma unroll
+      for (int i = AR::YB + 1; i < AR::AR; ++i) ar[i] = 0.f;
+      // record [k][workgroup][AR/4][256 threads] float4: every store coalesced across the wave
+      floatx4* dst = reinterpret_cast<floatx4*>(arec) + ((long long)k * gridDim.x + blockIdx.x) * (AR::AR / 4) * BCNF_WG + tid;
+#pragma unroll
+      for (int i = 0; i < AR::AR / 4; ++i)
+        dst[i * BCNF_WG] = floatx4{ar[4 * i], ar[4 * i + 1], ar[4 * i + 2], ar[4 * i + 3]};
     }
+    mix(rr + RecF<NH>::Q, xa, zb, ya, yb);             // y @ Q (cnf.py:335); identity after the last block
     sr.store(rec + (cur ^ 1) * RFL, RFL);      // past the end these refill a buffer nobody reads
     __syncthreads();
   }
@@ -1059,20 +1073,20 @@ __device__ __forceinline__ void copy_out(const BcnfLayout& L, const float* __res
 
 template <int NH, int CP4>
 __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float* __restrict__ pk,
-                                                      const float* __restrict__ hp, const float* __restrict__ dz,
-                                                      const float* __restrict__ dldj, const float* __restrict__ dloss,
-                                                      int nll, long long B,
-                                                      const float* __restrict__ ysave, const uint32_t* __restrict__ msave,
+                                                      const float* __restrict__ dz, const float* __restrict__ dldj,
+                                                      const float* __restrict__ dloss, int nll, long long B,
+                                                      const float* __restrict__ arec,
                                                       float* __restrict__ dy, float* __restrict__ d1,
                                                       float* __restrict__ slab_all, long long slab_stride,
                                                       const float* __restrict__ nll_part, float* __restrict__ loss_out,
                                                       uint64_t* rng_w) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const BwdTiles TI{NH};
-  const int RFL = 16 * L.RF, RBL = 16 * L.RB;
+  using AR = ActRec<NH>;
+  using RBk = RecB<NH>;
+  const int RBL = 16 * L.RB;
   const int NT = TI.count();
-  float* recF = smem;                   // [2][16*RF]
-  float* recB = recF + 2 * RFL;         // [2][16*RB]
+  float* recB = smem;                   // [2][16*RB]
   float* tiles = recB + 2 * RBL;        // [2][NT][272]
   GradDesc* cd = reinterpret_cast<GradDesc*>(tiles + 2 * NT * TILE);   // [MAX_JOBS]
   float* gbuf = tiles + 2 * NT * TILE + MAX_JOBS * 8;                  // [blk_pad + 64] block gradient + dummies
@@ -1086,10 +1100,10 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
   const long long bc = valid ? b : B - 1;
   const int D = L.D, Da = L.Da, Db = L.Db, nb = L.nb;
   float* slab = slab_all + ((BCNF_EXP & 32) ? 0LL : (long long)blockIdx.x * slab_stride);
-  const bool drop = msave != nullptr;
-  const float* pf = pk + L.pf_off;
   const float* pbk = pk + L.pb_off;
-  const float* hpl = hp + bc * 16 + j;              // HP[k][bc][j] = hpl[k * B * 16]
+  // activation records [k][workgroup][AR/4][256 threads] float4 (k_forward)
+  const floatx4* arl = reinterpret_cast<const floatx4*>(arec) + (long long)blockIdx.x * (AR::AR / 4) * BCNF_WG + tid;
+  const long long ars = (long long)gridDim.x * (AR::AR / 4) * BCNF_WG;
   float* d1l = d1 + bc * 16 + j;                    // D1[k][b][j]  = d1l[k * B * 16]
   const long long hps = B * 16;
 
@@ -1108,21 +1122,13 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
       if (dldj) dl = dldj[b];
     }
   }
-  // saved input / dropout masks / projection of the block about to be processed (one block ahead)
-  float ya_n, yb_n, hp_n;
-  uint32_t mw_n = 0xffffffffu;
-  {
-    const float* ys = ysave + ((long long)(nb - 1) * B + bc) * 32;
-    ya_n = ys[j];
-    yb_n = ys[16 + j];
-    hp_n = hpl[(nb - 1) * hps];
-    if (drop) mw_n = msave[((long long)((nb - 1) >> 2) * B + bc) * 16 + j];
-  }
+  // activation record of the block about to be processed (saved by the forward; one block ahead)
+  floatx4 ar_n[AR::AR / 4];
+#pragma unroll
+  for (int i = 0; i < AR::AR / 4; ++i) ar_n[i] = arl[(long long)(nb - 1) * ars + i * BCNF_WG];
   {
     const int kl = nb - 1;
     Stage<STAGE_REC> sr;
-    sr.load(pf + (long long)kl * RFL, RFL);
-    sr.store(recF + (kl & 1) * RFL, RFL);
     sr.load(pbk + (long long)kl * RBL, RBL);
     sr.store(recB + (kl & 1) * RBL, RBL);
   }
@@ -1131,8 +1137,14 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
   for (int k = nb - 1; k >= 0; --k) {
     const int cur = k & 1;
     const int k1 = k >= 1 ? k - 1 : 0;               // clamped: no branches
-    const float ya = ya_n, yb = yb_n, hpk = hp_n;
-    const uint32_t mword = mw_n;
+    float ar[AR::AR];
+#pragma unroll
+    for (int i = 0; i < AR::AR / 4; ++i) {
+      ar[4 * i] = ar_n[i][0];
+      ar[4 * i + 1] = ar_n[i][1];
+      ar[4 * i + 2] = ar_n[i][2];
+      ar[4 * i + 3] = ar_n[i][3];
+    }
     // (0) gradient block k+2 (MFMA phase of the previous iteration) LDS -> slab, before any load of
     // this iteration is issued; then the MFMA phase below may overwrite the LDS block
     if (k + 2 < nb) {
@@ -1140,39 +1152,30 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
       __syncthreads();
     }
     PH(0)
-    // (a) prefetch: next records and the next block's saved input / masks / projection
-    Stage<STAGE_REC> sF, sB;
-    sF.load(pf + (long long)k1 * RFL, RFL);
+    // (a) prefetch: next backward record and the next block's activation record
+    Stage<STAGE_REC> sB;
     sB.load(pbk + (long long)k1 * RBL, RBL);
-    {
-      const float* ys = ysave + ((long long)k1 * B + bc) * 32;
-      ya_n = ys[j];
-      yb_n = ys[16 + j];
-      hp_n = hpl[k1 * hps];
-      if (drop) mw_n = msave[((long long)(k1 >> 2) * B + bc) * 16 + j];
-    }
+#pragma unroll
+    for (int i = 0; i < AR::AR / 4; ++i) ar_n[i] = arl[(long long)k1 * ars + i * BCNF_WG];
     PH(1)
     // (b) MFMA phase: parameter gradients of block k+1
     if (k + 1 < nb && !(BCNF_EXP & 4))
       bwd_mfma_phase<NH>(L, tiles + ((k + 1) & 1) * NT * TILE, cd, gbuf, k + 1);
     PH(2)
     PH(3)
-    // (c) VALU phase: recompute block k, then back-propagate through it
+    // (c) VALU phase: back-propagate through block k from its saved activations (no recompute)
     float* Tt = tiles + cur * NT * TILE;
     const int tix = s * BCNF_TSTRIDE + j;
-    using RBk = RecB<NH>;
-    float rf[RecF<NH>::MLP_END], rb[RBk::USED];
-    ld_rec_exp<0, RecF<NH>::MLP_END>(rf, recF + cur * RFL + j * L.RF);   // recompute part (no forward mix)
+    float rb[RBk::USED];
     ld_rec_exp<0, RBk::USED>(rb, recB + cur * RBL + j * L.RB);
-    const float xa = fmaf(rf[0], ya, rf[1]);
-    const float xb = fmaf(rf[2], yb, rf[3]);
-    const uint32_t bits = (mword >> (8 * (k & 3))) & 0xffu;
-    float act[NH], gd[NH];
-    float T, Sp;
+    const float ya = ar[AR::YA], yb = ar[AR::YB], S = ar[AR::S];
+    const float* act = ar + AR::ACT;
+    const float* gd = ar + AR::GD;
+    const float an_sa = rb[RBk::AN], an_ba = rb[RBk::AN + 1], an_sb = rb[RBk::AN + 2], an_bb = rb[RBk::AN + 3];
+    const float xa = fmaf(an_sa, ya, an_ba);
+    const float xb = fmaf(an_sb, yb, an_bb);
     PH(4)
-    mlp_forward<NH, true>(L, rf, xa, hpk, bits, drop, T, Sp, act, gd);
     PH(5)
-    const float S = tanh_bf(Sp);
     const float e = expf(S);
     float gza, gzb;
     mix(rb + RBk::QT, gya, gyb, gza, gzb);            // g @ Q^T (identity for the last block)
@@ -1199,18 +1202,17 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
     if (valid) d1l[k * hps] = dpre1;                   // dL/d pre-activation of Linear 1 (k_dh, k_dw1h)
     const float dxa = rot16(dpre1, rb + RBk::W1T, gza);
     {   // ActNorm tiles (consumed only for blocks that have an ActNorm)
-      const float inv_a = (j < Da) ? __builtin_amdgcn_rcpf(rf[0]) : 0.f;
-      const float inv_b = (j < Db) ? __builtin_amdgcn_rcpf(rf[2]) : 0.f;
+      const float inv_a = (j < Da) ? __builtin_amdgcn_rcpf(an_sa) : 0.f;
+      const float inv_b = (j < Db) ? __builtin_amdgcn_rcpf(an_sb) : 0.f;
       Tt[TI.PA() * TILE + tix] = fmaf(dxa, ya, dl * inv_a);
       Tt[TI.GA() * TILE + tix] = dxa;
       Tt[TI.PB() * TILE + tix] = fmaf(dxb, yb, dl * inv_b);
       Tt[TI.GB() * TILE + tix] = dxb;
     }
-    gya = rf[0] * dxa;
-    gyb = rf[2] * dxb;
+    gya = an_sa * dxa;
+    gyb = an_sb * dxb;
     PH(6)
-    // (d) commit prefetched records (past the end they refill buffers nobody reads)
-    sF.store(recF + (cur ^ 1) * RFL, RFL);
+    // (d) commit the prefetched record (past the end it refills a buffer nobody reads)
     sB.store(recB + (cur ^ 1) * RBL, RBL);
     PH(7)
     __syncthreads();
@@ -1376,7 +1378,7 @@ bool layout_matches(const BcnfLayout& L) {
   return L.rf_b1 == RecF<NH>::B1 && L.rf_w1 == RecF<NH>::W1 && L.rf_hid == RecF<NH>::HID && L.rf_t == RecF<NH>::T &&
          L.rf_s == RecF<NH>::S && L.rf_q == RecF<NH>::Q && L.RF >= RecF<NH>::USED && L.rb_w1t == RecB<NH>::W1T &&
          L.rb_hid == RecB<NH>::HID && L.rb_tt == RecB<NH>::TT && L.rb_st == RecB<NH>::ST && L.rb_qt == RecB<NH>::QT &&
-         L.RB >= RecB<NH>::USED;
+         L.rb_an == RecB<NH>::AN && L.RB >= RecB<NH>::USED;
 }
 
 struct NllOut {
@@ -1399,18 +1401,18 @@ int launch_hp(const BcnfLayout& L, const float* pk, const float* h, long long R,
 
 template <int NH>
 int fwd_dispatch(const BcnfLayout& L, const float* pk, const float* y, const float* hp, long long B, float* z,
-                 float* ldj, float* logp, bool drop, const uint64_t* rng, float* ysave, uint32_t* msave,
-                 const NllOut& no, hipStream_t st) {
+                 float* ldj, float* logp, bool drop, const uint64_t* rng, float* arec, const NllOut& no,
+                 hipStream_t st) {
   if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
   const dim3 grid((unsigned)((B + 15) / 16));
   size_t lds = fwd_lds_bytes(L);
-  const bool save = ysave != nullptr;
+  const bool save = arec != nullptr;
   int rc;
 #define BCNF_FWD(DR, SV)                                                                                    \
   rc = launch_lds(k_forward<NH, DR, SV>, lds);                                                              \
   if (rc) return rc;                                                                                        \
   hipLaunchKernelGGL((k_forward<NH, DR, SV>), grid, dim3(BCNF_WG), lds, st, L, pk, y, hp, B, z, ldj, logp,  \
-                     rng, ysave, msave, no.part);
+                     rng, arec, no.part);
   if (drop) {
     if (save) { BCNF_FWD(true, true) } else { BCNF_FWD(true, false) }
   } else {
@@ -1440,10 +1442,9 @@ int inv_dispatch(const BcnfLayout& L, const float* pk, const float* zin, const f
 }
 
 template <int NH>
-int bwd_dispatch(const BcnfLayout& L, const float* pk, const float* hp, const float* dz, const float* dldj,
-                 const float* dloss, int nll, long long B, const float* ysave, const uint32_t* msave, float* dy,
-                 float* d1, float* slab, long long stride, const float* part, float* loss_out, uint64_t* rng_w,
-                 hipStream_t st) {
+int bwd_dispatch(const BcnfLayout& L, const float* pk, const float* dz, const float* dldj, const float* dloss,
+                 int nll, long long B, const float* arec, float* dy, float* d1, float* slab, long long stride,
+                 const float* part, float* loss_out, uint64_t* rng_w, hipStream_t st) {
   if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
   const dim3 grid((unsigned)((B + 15) / 16));
   size_t lds = bwd_lds_bytes(L);
@@ -1451,8 +1452,8 @@ int bwd_dispatch(const BcnfLayout& L, const float* pk, const float* hp, const fl
 #define BCNF_BWD(CP)                                                                                      \
   rc = launch_lds(k_backward<NH, CP>, lds);                                                               \
   if (rc) return rc;                                                                                      \
-  hipLaunchKernelGGL((k_backward<NH, CP>), grid, dim3(BCNF_WG), lds, st, L, pk, hp, dz, dldj, dloss, nll, B, \
-                     ysave, msave, dy, d1, slab, stride, part, loss_out, rng_w);
+  hipLaunchKernelGGL((k_backward<NH, CP>), grid, dim3(BCNF_WG), lds, st, L, pk, dz, dldj, dloss, nll, B, arec, \
+                     dy, d1, slab, stride, part, loss_out, rng_w);
   if (copy4_of(L) == 4) { BCNF_BWD(4) } else { BCNF_BWD(8) }
 #undef BCNF_BWD
   return check_launch();
@@ -1465,11 +1466,10 @@ int w1h_rows_per_split(long long) { return KC; }   // one LDS chunk of rows per 
 long long w1h_splits(long long B) { return (B + w1h_rows_per_split(B) - 1) / w1h_rows_per_split(B); }
 long long w1h_work_floats(const BcnfLayout& L, long long B) { return w1h_splits(B) * L.nb * 16LL * L.Cp; }
 
-// Workspace (floats): [saved block inputs nb*B*32][dropout masks ceil(nb/4)*B*16 u32, if dropout]
-//                     [loss partials][HP nb*B*16][D1 nb*B*16]
-long long ws_mask_off(const BcnfLayout& L, long long B) { return (long long)L.nb * B * 32; }
-long long ws_part_off(const BcnfLayout& L, long long B, bool drop) {
-  return ws_mask_off(L, B) + (drop ? (long long)((L.nb + 3) / 4) * B * 16 : 0);
+// Workspace (floats): [activation records nb*B*16*AR][loss partials][HP nb*B*16][D1 nb*B*16]
+// (`drop` no longer changes the layout: the records hold the masked activations)
+long long ws_part_off(const BcnfLayout& L, long long B, bool) {
+  return (long long)L.nb * ((B + 15) / 16) * BCNF_WG * act_rec_floats(L.NH);   // padded rows own slots
 }
 long long ws_hp_off(const BcnfLayout& L, long long B, bool drop) {
   return ws_part_off(L, B, drop) + (((B + 15) / 16 + 3) & ~3LL);
@@ -1491,8 +1491,7 @@ int forward_impl(const BcnfStackDesc* desc, const void* packed, const float* y, 
   const bool drop = training && L.p > 0.f;
   if (drop && !rng_state) return BCNF_ERR_ARG;
   float* ws = (float*)workspace;
-  float* ysave = (save || nll) ? ws : nullptr;
-  uint32_t* msave = (ysave && drop) ? (uint32_t*)(ws + ws_mask_off(L, batch)) : nullptr;
+  float* arec = (save || nll) ? ws : nullptr;
   float* hp = ws + ws_hp_off(L, batch, drop);
   NllOut no;
   if (nll) no.part = ws + ws_part_off(L, batch, drop);
@@ -1500,7 +1499,7 @@ int forward_impl(const BcnfStackDesc* desc, const void* packed, const float* y, 
   hipStream_t st = (hipStream_t)stream;
   if ((rc = launch_hp(L, pk, h, batch, hp, st))) return rc;
   switch (L.NH) {
-#define BCNF_CASE(N) case N: rc = fwd_dispatch<N>(L, pk, y, hp, batch, z, ldj, log_prob, drop, rng_state, ysave, msave, no, st); break;
+#define BCNF_CASE(N) case N: rc = fwd_dispatch<N>(L, pk, y, hp, batch, z, ldj, log_prob, drop, rng_state, arec, no, st); break;
     BCNF_CASE(1) BCNF_CASE(2) BCNF_CASE(3) BCNF_CASE(4) BCNF_CASE(5) BCNF_CASE(6) BCNF_CASE(7) BCNF_CASE(8)
 #undef BCNF_CASE
     default: return BCNF_ERR_UNSUPPORTED;
@@ -1740,16 +1739,14 @@ int backward_impl(const BcnfStackDesc* desc, const void* packed, const float* h,
   // were saved behind the block inputs.
   const bool drop = training && L.p > 0.f;
   float* ws = (float*)workspace;
-  const float* ysave = ws;
-  const uint32_t* msave = drop ? (const uint32_t*)(ws + ws_mask_off(L, batch)) : nullptr;
-  const float* hp = ws + ws_hp_off(L, batch, drop);
+  const float* arec = ws;
   float* d1 = ws + ws_d1_off(L, batch, drop);
   const float* pk = (const float*)packed;
   const long long stride = slab_stride_of(L);
   const float* part = ws + ws_part_off(L, batch, drop);
   uint64_t* rng_w = (loss_out && drop) ? rng_state : nullptr;
   switch (L.NH) {
-#define BCNF_CASE(N) case N: rc = bwd_dispatch<N>(L, pk, hp, dz, dldj, dloss, nll, batch, ysave, msave, dy, d1, (float*)slab, stride, part, loss_out, rng_w, st); break;
+#define BCNF_CASE(N) case N: rc = bwd_dispatch<N>(L, pk, dz, dldj, dloss, nll, batch, arec, dy, d1, (float*)slab, stride, part, loss_out, rng_w, st); break;
     BCNF_CASE(1) BCNF_CASE(2) BCNF_CASE(3) BCNF_CASE(4) BCNF_CASE(5) BCNF_CASE(6) BCNF_CASE(7) BCNF_CASE(8)
 #undef BCNF_CASE
     default: return BCNF_ERR_UNSUPPORTED;
