@@ -91,14 +91,15 @@ def _bind(lib):
         "bcnf_stack_backward": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
         "bcnf_stack_inverse": (_i32, [_pdesc, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i32, _vp, _vp, _vp]),
         "bcnf_grad_reduce": (_i32, [_pdesc, _vp, _vp, _vp, _i64, _i32, _vp, _vp]),
-        "bcnf_nll_forward": (_i32, [_pdesc, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _i32, _vp, _vp]),
+        "bcnf_nll_forward": (_i32, [_pdesc, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _i32, _vp, _vp, _vp]),
         "bcnf_nll_backward": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                     _vp]),
+                                     _vp, _vp]),
         "bcnf_grad_partials": (_i64, [_i64]),
         "bcnf_adam_step": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double,
-                                  ctypes.c_double, ctypes.c_double, ctypes.c_double, _vp, _i32, _vp]),
+                                  ctypes.c_double, ctypes.c_double, ctypes.c_double, _vp, _i32, _vp, _vp]),
         "bcnf_grad_sumsq": (_i32, [_i32, _vp, _vp, _vp, _vp]),
-        "bcnf_clip_grad_norm": (_i32, [_i32, _vp, _vp, _vp, ctypes.c_float, _vp, _vp, _vp, _i64, _vp]),
+        "bcnf_clip_grad_norm": (_i32, [_i32, _vp, _vp, _vp, ctypes.c_float, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                       _vp]),
         "bcnf_linear_forward": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp]),
         "bcnf_linear_work_bytes": (_i64, [_i64, _i32, _i32]),
         "bcnf_linear_backward": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),

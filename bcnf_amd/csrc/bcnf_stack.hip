@@ -797,8 +797,12 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
 // Mean of the forward's per-workgroup NLL partials -> loss_out = [loss, nll, mse = 0] (trainer.py:260-266)
 // and the dropout RNG offset advance, by ONE workgroup that runs strictly after the forward (a separate
 // launch, or workgroup 0 of the backward): no cross-workgroup synchronisation inside any kernel.
+// Divergence guard (int32[4], BCNF_GUARD_*): a step whose loss exceeds 1e5 or is NaN while checking is
+// enabled raises `diverged` (trainer.py:168 raises after that step's update); the NEXT step's finalize
+// then raises `halted`, which turns that step's RNG advance, Adam update, clip and counter advances into
+// no-ops -- so an epoch replayed without host syncs stops with the state the reference raises in.
 __device__ void nll_finalize(const float* __restrict__ part, int nparts, long long B, float* __restrict__ loss_out,
-                             uint64_t* rng_w, float* __restrict__ red) {
+                             uint64_t* rng_w, int32_t* guard, float* __restrict__ red) {
   float acc = 0.f;
   for (int i = threadIdx.x; i < nparts; i += BCNF_WG) acc += part[i];
   red[threadIdx.x] = acc;
@@ -812,14 +816,24 @@ __device__ void nll_finalize(const float* __restrict__ part, int nparts, long lo
     loss_out[0] = nll;                                 // (nll + mse * 0) / (1 + 0)   (trainer.py:264)
     loss_out[1] = nll;
     loss_out[2] = 0.f;
-    if (rng_w) rng_w[1] += 1;                          // the forward has read the offset
+    bool halt = false;
+    if (guard) {
+      if (guard[BCNF_GUARD_DIVERGED]) {
+        guard[BCNF_GUARD_HALTED] = 1;
+        halt = true;
+      } else if (guard[BCNF_GUARD_CHECK] && (nll > 1e5f || isnan(nll))) {
+        guard[BCNF_GUARD_DIVERGED] = 1;
+      }
+    }
+    if (rng_w && !halt) rng_w[1] += 1;                 // the forward has read the offset
   }
 }
 
 __global__ __launch_bounds__(BCNF_WG) void k_nll_finalize(const float* __restrict__ part, int nparts, long long B,
-                                                          float* __restrict__ loss_out, uint64_t* rng_w) {
+                                                          float* __restrict__ loss_out, uint64_t* rng_w,
+                                                          int32_t* guard) {
   __shared__ float red[BCNF_WG];
-  nll_finalize(part, nparts, B, loss_out, rng_w, red);
+  nll_finalize(part, nparts, B, loss_out, rng_w, guard, red);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1079,7 +1093,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
                                                       float* __restrict__ dy, float* __restrict__ d1,
                                                       float* __restrict__ slab_all, long long slab_stride,
                                                       const float* __restrict__ nll_part, float* __restrict__ loss_out,
-                                                      uint64_t* rng_w) {
+                                                      uint64_t* rng_w, int32_t* guard) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const BwdTiles TI{NH};
   using AR = ActRec<NH>;
@@ -1234,7 +1248,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
   }
   if (loss_out && blockIdx.x == 0) {                 // deferred NLL reduction of the forward
     __syncthreads();
-    nll_finalize(nll_part, (int)gridDim.x, B, loss_out, rng_w, gbuf);
+    nll_finalize(nll_part, (int)gridDim.x, B, loss_out, rng_w, guard, gbuf);
   }
 }
 
@@ -1444,7 +1458,7 @@ int inv_dispatch(const BcnfLayout& L, const float* pk, const float* zin, const f
 template <int NH>
 int bwd_dispatch(const BcnfLayout& L, const float* pk, const float* dz, const float* dldj, const float* dloss,
                  int nll, long long B, const float* arec, float* dy, float* d1, float* slab, long long stride,
-                 const float* part, float* loss_out, uint64_t* rng_w, hipStream_t st) {
+                 const float* part, float* loss_out, uint64_t* rng_w, int32_t* guard, hipStream_t st) {
   if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
   const dim3 grid((unsigned)((B + 15) / 16));
   size_t lds = bwd_lds_bytes(L);
@@ -1453,7 +1467,7 @@ int bwd_dispatch(const BcnfLayout& L, const float* pk, const float* dz, const fl
   rc = launch_lds(k_backward<NH, CP>, lds);                                                               \
   if (rc) return rc;                                                                                      \
   hipLaunchKernelGGL((k_backward<NH, CP>), grid, dim3(BCNF_WG), lds, st, L, pk, dz, dldj, dloss, nll, B, arec, \
-                     dy, d1, slab, stride, part, loss_out, rng_w);
+                     dy, d1, slab, stride, part, loss_out, rng_w, guard);
   if (copy4_of(L) == 4) { BCNF_BWD(4) } else { BCNF_BWD(8) }
 #undef BCNF_BWD
   return check_launch();
@@ -1479,7 +1493,7 @@ long long ws_floats(const BcnfLayout& L, long long B, bool drop) { return ws_d1_
 
 int forward_impl(const BcnfStackDesc* desc, const void* packed, const float* y, const float* h, int64_t batch,
                  float* z, float* ldj, float* log_prob, int32_t training, const uint64_t* rng_state, void* workspace,
-                 bool save, bool nll, bool finalize, float* loss_out, void* stream) {
+                 bool save, bool nll, bool finalize, float* loss_out, int32_t* guard, void* stream) {
   BcnfLayout L;
   int rc = make_layout(desc, &L);
   if (rc) return rc;
@@ -1506,13 +1520,14 @@ int forward_impl(const BcnfStackDesc* desc, const void* packed, const float* y, 
   }
   if (rc || !nll || !finalize) return rc;
   hipLaunchKernelGGL(k_nll_finalize, dim3(1), dim3(BCNF_WG), 0, st, (const float*)no.part, (int)((batch + 15) / 16),
-                     (long long)batch, loss_out, drop ? const_cast<uint64_t*>(rng_state) : nullptr);
+                     (long long)batch, loss_out, drop ? const_cast<uint64_t*>(rng_state) : nullptr, guard);
   return check_launch();
 }
 
 int backward_impl(const BcnfStackDesc* desc, const void* packed, const float* h, const float* dz, const float* dldj,
                   const float* dloss, int nll, int64_t batch, int32_t training, void* workspace, float* dy,
-                  float* dh, float* dparams, void* slab, float* loss_out, uint64_t* rng_state, void* stream);
+                  float* dh, float* dparams, void* slab, float* loss_out, uint64_t* rng_state, int32_t* guard,
+                  void* stream);
 
 }  // namespace
 
@@ -1587,29 +1602,30 @@ int bcnf_stack_forward(const BcnfStackDesc* desc, const void* packed, const floa
                        float* z, float* ldj, float* log_prob, int32_t training, const uint64_t* rng_state,
                        void* workspace, int32_t save, void* stream) {
   return forward_impl(desc, packed, y, h, batch, z, ldj, log_prob, training, rng_state, workspace, save != 0, false,
-                      false, nullptr, stream);
+                      false, nullptr, nullptr, stream);
 }
 
 int bcnf_nll_forward(const BcnfStackDesc* desc, const void* packed, const float* y, const float* h, int64_t batch,
                      float* z, float* ldj, int32_t training, uint64_t* rng_state, void* workspace, int32_t finalize,
-                     float* loss_out, void* stream) {
+                     float* loss_out, int32_t* guard, void* stream) {
   return forward_impl(desc, packed, y, h, batch, z, ldj, nullptr, training, rng_state, workspace, true, true,
-                      finalize != 0, loss_out, stream);
+                      finalize != 0, loss_out, guard, stream);
 }
 
 int bcnf_stack_backward(const BcnfStackDesc* desc, const void* packed, const float* h, const float* dz,
                         const float* dldj, int64_t batch, int32_t training, void* workspace, float* dy,
                         float* dh, float* dparams, void* slab, void* stream) {
   return backward_impl(desc, packed, h, dz, dldj, nullptr, 0, batch, training, workspace, dy, dh, dparams, slab,
-                       nullptr, nullptr, stream);
+                       nullptr, nullptr, nullptr, stream);
 }
 
 int bcnf_nll_backward(const BcnfStackDesc* desc, const void* packed, const float* h, const float* z,
                       const float* dloss, int64_t batch, int32_t training, void* workspace, float* dy,
-                      float* dh, float* dparams, void* slab, float* loss_out, uint64_t* rng_state, void* stream) {
+                      float* dh, float* dparams, void* slab, float* loss_out, uint64_t* rng_state, int32_t* guard,
+                      void* stream) {
   if (!z && batch > 0) return BCNF_ERR_ARG;
   return backward_impl(desc, packed, h, z, nullptr, dloss, 1, batch, training, workspace, dy, dh, dparams, slab,
-                       loss_out, rng_state, stream);
+                       loss_out, rng_state, guard, stream);
 }
 
 int bcnf_backward_tail(const BcnfStackDesc* desc, const void* packed, const void* slab, const float* h,
@@ -1723,7 +1739,8 @@ namespace {
 
 int backward_impl(const BcnfStackDesc* desc, const void* packed, const float* h, const float* dz, const float* dldj,
                   const float* dloss, int nll, int64_t batch, int32_t training, void* workspace, float* dy,
-                  float* dh, float* dparams, void* slab, float* loss_out, uint64_t* rng_state, void* stream) {
+                  float* dh, float* dparams, void* slab, float* loss_out, uint64_t* rng_state, int32_t* guard,
+                  void* stream) {
   BcnfLayout L;
   int rc = make_layout(desc, &L);
   if (rc) return rc;
@@ -1746,7 +1763,7 @@ int backward_impl(const BcnfStackDesc* desc, const void* packed, const float* h,
   const float* part = ws + ws_part_off(L, batch, drop);
   uint64_t* rng_w = (loss_out && drop) ? rng_state : nullptr;
   switch (L.NH) {
-#define BCNF_CASE(N) case N: rc = bwd_dispatch<N>(L, pk, dz, dldj, dloss, nll, batch, arec, dy, d1, (float*)slab, stride, part, loss_out, rng_w, st); break;
+#define BCNF_CASE(N) case N: rc = bwd_dispatch<N>(L, pk, dz, dldj, dloss, nll, batch, arec, dy, d1, (float*)slab, stride, part, loss_out, rng_w, guard, st); break;
     BCNF_CASE(1) BCNF_CASE(2) BCNF_CASE(3) BCNF_CASE(4) BCNF_CASE(5) BCNF_CASE(6) BCNF_CASE(7) BCNF_CASE(8)
 #undef BCNF_CASE
     default: return BCNF_ERR_UNSUPPORTED;

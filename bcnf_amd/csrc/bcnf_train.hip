@@ -54,9 +54,11 @@ __device__ __forceinline__ float wg_sum(float v, float* red) {
 // Hyper-parameters arrive as doubles (Python floats) and every scalar is derived in double, then
 // rounded once, as torch does (1 - beta2 in fp32 from 0.999f would be off by 1e-5 relative).
 __global__ __launch_bounds__(BCNF_WG) void k_adam(TList T, const float* __restrict__ step, double lr, double b1d,
-                                                  double b2d, double epsd, double wdd, float* __restrict__ part) {
+                                                  double b2d, double epsd, double wdd, float* __restrict__ part,
+                                                  const int32_t* __restrict__ guard) {
   __shared__ float red[BCNF_WG];
   __shared__ float sc[2];
+  if (guard && guard[BCNF_GUARD_HALTED]) return;   // a halted step (see nll_finalize) leaves all state
   const float st = step[0] + 1.0f;
   if (threadIdx.x == 0) {                          // double pow once per workgroup, not per thread
     sc[0] = (float)(lr / (1.0 - pow(b1d, (double)st)));
@@ -102,7 +104,8 @@ __device__ __forceinline__ void advance_counters(float* step, long long* cursor,
   }
 }
 
-__global__ void k_advance(float* step, long long* cursor, long long n_batches) {
+__global__ void k_advance(float* step, long long* cursor, long long n_batches, const int32_t* guard) {
+  if (guard && guard[BCNF_GUARD_HALTED]) return;
   if (threadIdx.x == 0) advance_counters(step, cursor, n_batches);
 }
 
@@ -126,8 +129,10 @@ __global__ __launch_bounds__(BCNF_WG) void k_sumsq(TList T, float* __restrict__ 
 // torch.nn.utils.clip_grad_norm_: coef = min(max_norm / (||g||_2 + 1e-6), 1); g *= coef.
 __global__ __launch_bounds__(BCNF_WG) void k_clip(TList T, const float* __restrict__ part, int nparts, float max_norm,
                                                   float* __restrict__ norm_out, float* step, long long* cursor,
-                                                  long long n_batches) {
+                                                  long long n_batches, const float* __restrict__ log_values,
+                                                  float* log_history, const int32_t* __restrict__ guard) {
   __shared__ float red[BCNF_WG];
+  if (guard && guard[BCNF_GUARD_HALTED]) return;
   float acc = 0.f;
   for (int i = threadIdx.x; i < nparts; i += BCNF_WG) acc += part[i];
   const float tot = sqrtf(wg_sum(acc, red));
@@ -143,6 +148,13 @@ __global__ __launch_bounds__(BCNF_WG) void k_clip(TList T, const float* __restri
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (norm_out) norm_out[0] = tot;
+    if (log_values && log_history) {   // the step's logged values -> history slot of this batch (host memory:
+      float* dst = log_history + 3 * (cursor ? cursor[0] : 0LL);   // system-scope stores, read after a sync)
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        __hip_atomic_store(dst + i, log_values[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __threadfence_system();
+    }
     advance_counters(step, cursor, n_batches);
   }
 }
@@ -359,7 +371,7 @@ int64_t bcnf_grad_partials(int64_t total_numel) { return total_numel <= 0 ? 1 : 
 int bcnf_adam_step(int32_t n_tensors, float* const* params, float* const* grads, float* const* exp_avg,
                    float* const* exp_avg_sq, const int64_t* numel, float* step, double lr, double beta1,
                    double beta2, double eps, double weight_decay, float* grad_partials, int32_t advance_step,
-                   void* stream) {
+                   const int32_t* guard, void* stream) {
   TList T;
   int rc = make_tlist(n_tensors, params, grads, exp_avg, exp_avg_sq, numel, &T);
   if (rc) return rc;
@@ -369,9 +381,10 @@ int bcnf_adam_step(int32_t n_tensors, float* const* params, float* const* grads,
   const long long total = T.start[T.n];
   const unsigned nwg = (unsigned)bcnf_grad_partials(total);
   hipLaunchKernelGGL(k_adam, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, step, lr, beta1, beta2, eps,
-                     weight_decay, grad_partials);
+                     weight_decay, grad_partials, guard);
   if ((rc = launched()) || !advance_step) return rc;
-  return bcnf_advance_counters(step, nullptr, 0, stream);
+  hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, (hipStream_t)stream, step, (long long*)nullptr, 0LL, guard);
+  return launched();
 }
 
 int bcnf_grad_sumsq(int32_t n_tensors, float* const* grads, const int64_t* numel, float* grad_partials, void* stream) {
@@ -386,7 +399,8 @@ int bcnf_grad_sumsq(int32_t n_tensors, float* const* grads, const int64_t* numel
 
 int bcnf_clip_grad_norm(int32_t n_tensors, float* const* grads, const int64_t* numel, const float* grad_partials,
                         float max_norm, float* total_norm, float* advance_step, int64_t* advance_cursor,
-                        int64_t cursor_modulo, void* stream) {
+                        int64_t cursor_modulo, const float* log_values, float* log_history, const int32_t* guard,
+                        void* stream) {
   TList T;
   int rc = make_tlist(n_tensors, nullptr, grads, nullptr, nullptr, numel, &T);
   if (rc) return rc;
@@ -394,7 +408,8 @@ int bcnf_clip_grad_norm(int32_t n_tensors, float* const* grads, const int64_t* n
   const long long np = bcnf_grad_partials(T.start[T.n]);
   if (advance_cursor && cursor_modulo < 1) return BCNF_ERR_ARG;
   hipLaunchKernelGGL(k_clip, dim3((unsigned)np), dim3(BCNF_WG), 0, (hipStream_t)stream, T, grad_partials, (int)np,
-                     max_norm, total_norm, advance_step, (long long*)advance_cursor, (long long)cursor_modulo);
+                     max_norm, total_norm, advance_step, (long long*)advance_cursor, (long long)cursor_modulo,
+                     log_values, log_history, guard);
   return launched();
 }
 
@@ -428,7 +443,7 @@ int bcnf_gather_batch(const int64_t* order, const int64_t* cursor, int64_t batch
 int bcnf_advance_counters(float* step, int64_t* cursor, int64_t n_batches, void* stream) {
   if (cursor && n_batches < 1) return BCNF_ERR_ARG;
   hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, (hipStream_t)stream, step, (long long*)cursor,
-                     (long long)n_batches);
+                     (long long)n_batches, (const int32_t*)nullptr);
   return launched();
 }
 

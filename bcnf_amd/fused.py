@@ -54,6 +54,7 @@ class FusedStack:
         self._rng_state = None
         self.seed = None
         self.timers = None       # dict -> per-kernel HIP-event pairs (bench.py kernel timing phase)
+        self.guard = None        # device int32[BCNF_GUARD_WORDS] divergence guard of a TrainStep, or None
         if bind:
             self.flatten()
         else:   # standalone layer: flat params are provided per call (see stack_forward(flat=...))
@@ -293,7 +294,8 @@ class FusedStack:
             e0.record()
         rc = N.lib().bcnf_nll_forward(self._pdesc, N.ptr(pk), N.ptr(y), N.ptr(h), ctypes.c_int64(B), N.ptr(z),
                                       N.ptr(ldj), ctypes.c_int32(int(training)), N.ptr(rng), N.ptr(ws),
-                                      ctypes.c_int32(int(finalize)), N.ptr(vals), N.stream_handle(dev))
+                                      ctypes.c_int32(int(finalize)), N.ptr(vals), N.ptr(self.guard if finalize else None),
+                                      N.stream_handle(dev))
         N.check(rc, "bcnf_nll_forward")
         if tm is not None:
             e1.record()
@@ -319,7 +321,8 @@ class FusedStack:
         rng = self.rng_state() if (finalize_into is not None and training and self.cfg.dropout > 0.0) else None
         rc = N.lib().bcnf_nll_backward(self._pdesc, N.ptr(pk), N.ptr(h), N.ptr(z), N.ptr(dvals), ctypes.c_int64(B),
                                        ctypes.c_int32(int(training)), N.ptr(ws), N.ptr(dy), None, None,
-                                       N.ptr(slab), N.ptr(finalize_into), N.ptr(rng), stream)
+                                       N.ptr(slab), N.ptr(finalize_into), N.ptr(rng),
+                                       N.ptr(self.guard if finalize_into is not None else None), stream)
         N.check(rc, "bcnf_nll_backward")
         self._backward_tail(h, ws, pk, slab, dh, dparams, B, training, stream, tm, e0)
         return dy, dh, dparams
@@ -344,10 +347,10 @@ class FusedStack:
         calls = {
             "forward": lambda: L.bcnf_nll_forward(self._pdesc, N.ptr(pk), N.ptr(y), N.ptr(h), ctypes.c_int64(B), N.ptr(z),
                                                   N.ptr(ldj), ctypes.c_int32(int(training)), N.ptr(rng), N.ptr(ws),
-                                                  ctypes.c_int32(0), N.ptr(vals), stream),
+                                                  ctypes.c_int32(0), N.ptr(vals), None, stream),
             "k_backward": lambda: L.bcnf_nll_backward(self._pdesc, N.ptr(pk), N.ptr(h), N.ptr(z), None, ctypes.c_int64(B),
                                                       ctypes.c_int32(int(training)), N.ptr(ws), None, None, None,
-                                                      N.ptr(slab), None, None, stream),
+                                                      N.ptr(slab), None, None, None, stream),
             "tail": lambda: L.bcnf_backward_tail(self._pdesc, N.ptr(pk), N.ptr(slab), N.ptr(h), N.ptr(ws),
                                                  ctypes.c_int64(B), ctypes.c_int32(int(training)), N.ptr(dh),
                                                  N.ptr(dparams), stream),

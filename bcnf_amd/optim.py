@@ -43,9 +43,10 @@ class FusedAdam(torch.optim.Optimizer):
         return st
 
     @torch.no_grad()
-    def step(self, closure=None, defer_step_count: bool = False):
+    def step(self, closure=None, defer_step_count: bool = False, guard=None):
         """One Adam update. defer_step_count=True leaves the device step count to be advanced by the
-        following clip_grad_norm_after_step (one launch less per training step)."""
+        following clip_grad_norm_after_step (one launch less per training step). `guard` (device int32[4],
+        include/bcnf_amd.h) turns the update into a no-op on a halted step."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -76,7 +77,7 @@ class FusedAdam(torch.optim.Optimizer):
                                       N.ptr_array([s["exp_avg_sq"] for s in states]), numel, N.ptr(step),
                                       ctypes.c_double(group["lr"]), ctypes.c_double(b1), ctypes.c_double(b2),
                                       ctypes.c_double(group["eps"]), ctypes.c_double(group["weight_decay"]),
-                                      N.ptr(part), ctypes.c_int32(0 if defer_step_count else 1),
+                                      N.ptr(part), ctypes.c_int32(0 if defer_step_count else 1), N.ptr(guard),
                                       N.stream_handle(dev))
                 N.check(rc, "bcnf_adam_step")
                 all_grads.append((chunk, grads, numel, part))
@@ -87,17 +88,20 @@ class FusedAdam(torch.optim.Optimizer):
         return loss
 
     @torch.no_grad()
-    def clip_grad_norm_after_step(self, max_norm: float = 1.0, cursor=None):
+    def clip_grad_norm_after_step(self, max_norm: float = 1.0, cursor=None, log=None, guard=None):
         """clip_grad_norm_(params, max_norm) for exactly the gradients the last step() consumed (unchanged
         since), reusing that step's squared-gradient partials. Also performs the end-of-step bookkeeping:
-        a deferred step count, and `cursor` = (device int64 counter, modulo) of an epoch walk.
-        Returns the pre-clip total norm (device)."""
+        a deferred step count, `cursor` = (device int64 counter, modulo) of an epoch walk, and
+        `log` = (device values[3], history[n, 3] possibly pinned host memory): values -> history[cursor].
+        `guard`: a halted step clips nothing and advances nothing. Returns the pre-clip total norm (device)."""
         if not self._partials:
             raise RuntimeError("bcnf_amd FusedAdam: clip_grad_norm_after_step() needs a preceding step()")
         L = N.lib()
         pending, self._pending_steps = self._pending_steps, []
         cur, mod = cursor if cursor is not None else (None, 0)
         if len(self._partials) != 1 or len(pending) > 1:   # several launches: generic path
+            if log is not None or guard is not None:
+                raise NotImplementedError("bcnf_amd FusedAdam: log/guard need a single-launch parameter set")
             norm = clip_grad_norm_(self._partials_for, max_norm)
             dev = norm.device
             for st in pending:
@@ -110,7 +114,8 @@ class FusedAdam(torch.optim.Optimizer):
         norm = torch.empty((), dtype=torch.float32, device=dev)
         rc = L.bcnf_clip_grad_norm(len(grads), N.ptr_array(grads), numel, N.ptr(part), ctypes.c_float(max_norm),
                                    N.ptr(norm), N.ptr(pending[0] if pending else None), N.ptr(cur),
-                                   ctypes.c_int64(mod), N.stream_handle(dev))
+                                   ctypes.c_int64(mod), N.ptr(log[0] if log else None), N.ptr(log[1] if log else None),
+                                   N.ptr(guard), N.stream_handle(dev))
         N.check(rc, "bcnf_clip_grad_norm")
         return norm
 
@@ -136,5 +141,6 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0):
     N.check(L.bcnf_grad_sumsq(len(grads), N.ptr_array(grads), numel, N.ptr(part), stream), "bcnf_grad_sumsq")
     norm = torch.empty((), dtype=torch.float32, device=dev)
     N.check(L.bcnf_clip_grad_norm(len(grads), N.ptr_array(grads), numel, N.ptr(part), ctypes.c_float(max_norm),
-                                  N.ptr(norm), None, None, ctypes.c_int64(0), stream), "bcnf_clip_grad_norm")
+                                  N.ptr(norm), None, None, ctypes.c_int64(0), None, None, None, stream),
+            "bcnf_clip_grad_norm")
     return norm

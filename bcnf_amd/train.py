@@ -24,14 +24,23 @@ MI355X specifics:
 * the whole step is captured once into a HIP graph and replayed (world > 1: the RCCL all-reduce runs
   between two captured segments). `step_indexed` also captures the batch gather from a
   device-resident pool, so a replay needs only the index copy.
+* the three logged values are stored by the clip launch straight into pinned host memory (a history
+  row per batch of the epoch), so no copy node and, with `run_epoch`, no host sync per step: the epoch's
+  steps are replayed back to back and the Trainer's per-batch divergence check (trainer.py:168) runs
+  on the device (guard, include/bcnf_amd.h), halting the epoch in the state the reference raises in.
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
 
+import math
+
+from bcnf_amd.errors import TrainingDivergedError
 from bcnf_amd.optim import FusedAdam, clip_grad_norm_
 from bcnf_amd.utils import inn_nll_loss
+
+GUARD_CHECK, GUARD_DIVERGED, GUARD_HALTED, GUARD_WORDS = 0, 1, 2, 4    # include/bcnf_amd.h
 
 
 class TrainStep:
@@ -52,6 +61,14 @@ class TrainStep:
         self._static = None
         self._pool = None
         self._epoch = None      # (order, cursor, n_batches, batch) for the device-cursor batch walk
+        self._host_cursor = 0   # host mirror of the epoch cursor (the history row of the next step)
+        dev = self.params[0].device
+        self._guard = None
+        self._hist = None
+        if dev.type == "cuda":
+            self._guard = torch.zeros(GUARD_WORDS, dtype=torch.int32, device=dev)
+            model.fused.guard = self._guard
+            self._hist = torch.zeros((1, 3), dtype=torch.float32, pin_memory=True)
 
     # ------------------------------------------------------------------ step pieces
     def _forward_backward(self, y, traj):
@@ -77,12 +94,14 @@ class TrainStep:
                 dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, group=self.pg)
                 p.grad.mul_(1.0 / self.world)
 
-    def _update(self):
+    def _update(self, vals=None):
         """Adam, then clip_grad_norm_ after the step (trainer.py:270-272); the clip launch also advances the
-        Adam step count and, in epoch mode, the batch cursor (end-of-step bookkeeping, no extra launch)."""
-        self.opt.step(defer_step_count=True)
+        Adam step count and, in epoch mode, the batch cursor, and stores the logged values into the pinned
+        history (end-of-step bookkeeping, no extra launch)."""
+        self.opt.step(defer_step_count=True, guard=self._guard)
         cursor = (self._epoch[1], self._epoch[2]) if self._epoch is not None else None
-        self.opt.clip_grad_norm_after_step(self.max_norm, cursor=cursor)
+        log = (vals, self._hist) if (vals is not None and self._hist is not None) else None
+        self.opt.clip_grad_norm_after_step(self.max_norm, cursor=cursor, log=log, guard=self._guard)
 
     def broadcast_parameters(self, src: int = 0):
         """Identical initial replicas (the RNG-seeded init differs per process otherwise)."""
@@ -96,7 +115,7 @@ class TrainStep:
     def eager_step(self, y, traj):
         vals = self._forward_backward(y, traj)
         self._allreduce()
-        self._update()
+        self._update(vals)
         return vals
 
     def _gather(self):
@@ -159,23 +178,20 @@ class TrainStep:
             self._restore(snap)
         torch.cuda.current_stream().wait_stream(s)
         self.opt.zero_grad(set_to_none=True)
-        # the three logged values land in pinned host memory as the graph's last node: the host reads
-        # them after one stream sync instead of issuing a separate device-to-host copy per step
-        self._host_vals = torch.empty(3, dtype=torch.float32, pin_memory=True)
+        # the three logged values are stored into the pinned history by the clip launch: the host reads
+        # them after a stream sync, without a device-to-host copy node
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1):
             if indexed:
                 sy, st = self._gather()
             vals = self._forward_backward(sy, st)
             if self.world == 1:
-                self._update()
-                self._host_vals.copy_(vals, non_blocking=True)
+                self._update(vals)
         g2 = None
         if self.world > 1:
             g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g2):
-                self._update()
-                self._host_vals.copy_(vals, non_blocking=True)
+                self._update(vals)
         self._graphs = (g1, g2, vals)
 
     def step(self, y, traj):
@@ -185,11 +201,11 @@ class TrainStep:
             return tuple(vals.tolist())
         return self._host_values()
 
-    def _host_values(self):
-        """The step's three logged values (the Trainer's .item() calls): one stream sync after the graph's
-        device-to-host copy, then a read of the pinned buffer."""
+    def _host_values(self, row: int = 0):
+        """The step's three logged values (the Trainer's .item() calls): one stream sync, then a read of the
+        pinned history row the clip launch stored them in."""
         torch.cuda.current_stream().synchronize()
-        return tuple(self._host_vals.tolist())
+        return tuple(self._hist[row].tolist())
 
     def step_async(self, y, traj):
         if not self.capture:
@@ -242,24 +258,70 @@ class TrainStep:
                 raise RuntimeError("set_epoch() must precede the first step of a non-epoch TrainStep")
             dev = order.device
             self._epoch = (order.clone(), torch.zeros(1, dtype=torch.int64, device=dev), nb, batch)
+            self._hist = torch.zeros((nb, 3), dtype=torch.float32, pin_memory=True)
         else:
             o, cursor, nb0, b0 = self._epoch
             if nb != nb0 or batch != b0:
                 raise ValueError("set_epoch: a captured TrainStep keeps its order size")
             o.copy_(order)
             cursor.zero_()
+        self._host_cursor = 0
 
     def step_epoch(self):
         """The next batch of the epoch order (see set_epoch)."""
         if self._epoch is None:
             raise RuntimeError("step_epoch() needs set_epoch()")
+        row = self._host_cursor
+        self._host_cursor = (row + 1) % self._epoch[2]
         if not self.capture:
             return tuple(self.eager_step(*self._gather()).tolist())
+        self._ensure_epoch_graphs()
+        self._replay()
+        return self._host_values(row)
+
+    def _ensure_epoch_graphs(self):
         if self._graphs is None:
             y, t = self._gather()
             self._build_graphs(y, t, idx=torch.zeros(1, dtype=torch.int64, device=y.device))
-        self._replay()
-        return self._host_values()
+
+    def run_epoch(self, n_steps=None, check_divergence: bool = False):
+        """The remaining batches of the epoch order (or the next n_steps of them) replayed back to back with
+        ONE host sync at the end; returns their (loss, nll, mse) triples in order -- the values the
+        Trainer's per-batch .item() calls read (trainer.py:166-173). With check_divergence (the Trainer
+        checks after epoch 10) a loss > 1e5 or NaN halts the epoch on the device right after that step's
+        update and TrainingDivergedError is raised here, with the model, optimizer, RNG offset and cursor
+        as the reference leaves them when it raises (only .grad holds the discarded next batch's gradient)."""
+        if self._epoch is None:
+            raise RuntimeError("run_epoch() needs set_epoch()")
+        nb = self._epoch[2]
+        start = self._host_cursor
+        n = nb - start if n_steps is None else int(n_steps)
+        if n < 0 or start + n > nb:
+            raise ValueError(f"run_epoch: {n} steps from batch {start} exceed the epoch's {nb} batches")
+        if n == 0:
+            return []
+        if not self.capture or not self.fused_loss:    # per-step host check (the device guard sits in
+            out = [self.step_epoch() for _ in range(n)]   # the fused loss finalize)
+            for i, v in enumerate(out):
+                if check_divergence and (v[0] > 1e5 or math.isnan(v[0])):
+                    raise TrainingDivergedError(f"Loss exploded to {v[0]} at batch {start + i}")
+            return out
+        self._ensure_epoch_graphs()
+        self._guard.zero_()
+        if check_divergence:
+            self._guard[GUARD_CHECK] = 1
+        for _ in range(n):
+            self._replay()
+        torch.cuda.current_stream().synchronize()
+        vals = [tuple(r) for r in self._hist[start:start + n].tolist()]
+        self._host_cursor = (start + n) % nb
+        if check_divergence and int(self._guard[GUARD_DIVERGED].item()):
+            for i, v in enumerate(vals):
+                if v[0] > 1e5 or math.isnan(v[0]):
+                    self._host_cursor = (start + i + 1) % nb
+                    self._guard.zero_()
+                    raise TrainingDivergedError(f"Loss exploded to {v[0]} at batch {start + i}")
+        return vals
 
     def _replay(self):
         g1, g2, vals = self._graphs
@@ -270,4 +332,4 @@ class TrainStep:
         return vals
 
 
-__all__ = ["TrainStep", "FusedAdam", "clip_grad_norm_"]
+__all__ = ["TrainStep", "FusedAdam", "clip_grad_norm_", "TrainingDivergedError"]

@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=12)
     ap.add_argument("--kernel-iters", type=int, default=20)
     ap.add_argument("--indexed", action="store_true", help="per-step index copy instead of the device epoch cursor")
+    ap.add_argument("--per-step-sync", action="store_true",
+                    help="one host sync + logged-value read per step (the Trainer loop shape) instead of run_epoch")
     return ap.parse_args()
 
 
@@ -152,17 +154,27 @@ def main():
     batches = [data.next_indices() for _ in range(args.warmup + args.steps)]
     if not args.indexed:
         step.set_epoch(torch.cat(batches), args.batch)
-    run = (lambda i: step.step_indexed(batches[i])) if args.indexed else (lambda i: step.step_epoch())
+    # default: the epoch's steps replayed back to back, logged values read once at the end (run_epoch);
+    # --per-step-sync: the Trainer's loop shape, one host sync + read per step (step_epoch)
+    if args.indexed or args.per_step_sync:
+        run = (lambda i: step.step_indexed(batches[i])) if args.indexed else (lambda i: step.step_epoch())
 
-    for i in range(args.warmup):
-        run(i)
+        def run_range(a, b):
+            out = None
+            for i in range(a, b):
+                out = run(i)
+            return out
+    else:
+        def run_range(a, b):
+            vals = step.run_epoch(b - a)
+            return vals[-1] if vals else None
+
+    run_range(0, args.warmup)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    losses = None
-    for i in range(args.warmup, args.warmup + args.steps):
-        losses = run(i)
+    losses = run_range(args.warmup, args.warmup + args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -139,7 +139,7 @@ int bcnf_stack_inverse(const BcnfStackDesc* desc, const void* packed, const floa
  *   synchronises across workgroups. */
 int bcnf_nll_forward(const BcnfStackDesc* desc, const void* packed, const float* y, const float* h, int64_t batch,
                      float* z, float* ldj, int32_t training, uint64_t* rng_state, void* workspace, int32_t finalize,
-                     float* loss_out, void* stream);
+                     float* loss_out, int32_t* guard, void* stream);
 
 /* Backward through loss_out w.r.t. y, h and the stack parameters: dz = z * g / B, dldj = -g / B with
  * g = dloss[0] + dloss[1], dloss being the device cotangent of loss_out[0..2] (NULL means d loss = 1,
@@ -148,7 +148,8 @@ int bcnf_nll_forward(const BcnfStackDesc* desc, const void* packed, const float*
  * bcnf_stack_backward. */
 int bcnf_nll_backward(const BcnfStackDesc* desc, const void* packed, const float* h, const float* z,
                       const float* dloss, int64_t batch, int32_t training, void* workspace, float* dy,
-                      float* dh, float* dparams, void* slab, float* loss_out, uint64_t* rng_state, void* stream);
+                      float* dh, float* dparams, void* slab, float* loss_out, uint64_t* rng_state, int32_t* guard,
+                      void* stream);
 
 /* ---- Optimizer ------------------------------------------------------------------------------------
  * Tensors are passed as arrays of n_tensors (<= BCNF_MAX_TENSORS) device pointers + element counts and
@@ -165,7 +166,7 @@ int64_t bcnf_grad_partials(int64_t total_numel);
 int bcnf_adam_step(int32_t n_tensors, float* const* params, float* const* grads, float* const* exp_avg,
                    float* const* exp_avg_sq, const int64_t* numel, float* step, double lr, double beta1,
                    double beta2, double eps, double weight_decay, float* grad_partials, int32_t advance_step,
-                   void* stream);
+                   const int32_t* guard, void* stream);
 
 /* Per-workgroup sums of squared gradients (when no bcnf_adam_step produced them). */
 int bcnf_grad_sumsq(int32_t n_tensors, float* const* grads, const int64_t* numel, float* grad_partials, void* stream);
@@ -176,7 +177,22 @@ int bcnf_grad_sumsq(int32_t n_tensors, float* const* grads, const int64_t* numel
  * (an epoch cursor of bcnf_gather_batch). */
 int bcnf_clip_grad_norm(int32_t n_tensors, float* const* grads, const int64_t* numel, const float* grad_partials,
                         float max_norm, float* total_norm, float* advance_step, int64_t* advance_cursor,
-                        int64_t cursor_modulo, void* stream);
+                        int64_t cursor_modulo, const float* log_values, float* log_history, const int32_t* guard,
+                        void* stream);
+
+/* Training-loop guard, int32[4] in device memory (nullable everywhere): [BCNF_GUARD_CHECK] is set by the
+ * host (the Trainer checks for divergence after epoch 10, trainer.py:168); the loss finalize of
+ * bcnf_nll_forward / bcnf_nll_backward raises [BCNF_GUARD_DIVERGED] when loss > 1e5 or NaN and, one step
+ * later, [BCNF_GUARD_HALTED], which makes that step's RNG advance, bcnf_adam_step and bcnf_clip_grad_norm
+ * no-ops. Steps can so be replayed back to back without a host sync per step: the host reads the logged
+ * values afterwards and raises where the reference would, with the state it would have had.
+ * bcnf_clip_grad_norm also stores log_values[0..2] (the step's loss, nll, mse) into
+ * log_history[3 * cursor ...] (cursor = advance_cursor[0] before the advance, else 0); log_history may be
+ * pinned host memory (system-scope stores). */
+#define BCNF_GUARD_CHECK 0
+#define BCNF_GUARD_DIVERGED 1
+#define BCNF_GUARD_HALTED 2
+#define BCNF_GUARD_WORDS 4
 
 /* The same bookkeeping as a one-thread launch. */
 int bcnf_advance_counters(float* step, int64_t* cursor, int64_t n_batches, void* stream);

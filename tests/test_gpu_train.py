@@ -211,3 +211,72 @@ def test_trainstep_graph_replay_equals_eager(g1):
         assert r0 == r1 == 3
         for a, b in zip(p0, p1):
             assert torch.equal(a, b)
+
+
+def _epoch_pool(gen, n=768, blow_up=None):
+    y = torch.randn(n, 19, generator=gen)
+    traj = torch.randn(n, 30, 3, generator=gen)
+    if blow_up is not None:            # rows whose NLL is ~1e8: the Trainer's divergence condition
+        y[blow_up] *= 1e4
+    return y.to(DEV), traj.to(DEV)
+
+
+def test_run_epoch_equals_per_step_loop(g1):
+    """run_epoch (back-to-back replays, one sync) == step_epoch per step: same logged values, parameters,
+    Adam state, RNG offset and cursor, bit for bit."""
+    from bcnf_amd.train import TrainStep
+    gen = torch.Generator().manual_seed(21)
+    py, pt = _epoch_pool(gen)
+    order = torch.randperm(768, generator=gen)[:4 * 192].to(DEV)
+    res = []
+    for batched in (False, True):
+        m = fresh_model(g1, train=True)
+        m.fused.set_seed(5)
+        st = TrainStep(m, lr=2e-4)
+        st.set_pool(py, pt)
+        st.set_epoch(order, 192)
+        if batched:
+            vals = st.run_epoch(1) + st.run_epoch()          # a partial run, then the rest of the epoch
+        else:
+            vals = [st.step_epoch() for _ in range(4)]
+        state = [v.clone() for s in st.opt.state.values() for v in s.values()]
+        res.append((vals, [p.detach().clone() for p in m.parameters()], state,
+                    m.fused.rng_state().clone(), st._epoch[1].item()))
+    (v0, p0, s0, r0, c0), (v1, p1, s1, r1, c1) = res
+    assert v0 == v1 and len(v1) == 4
+    assert c0 == c1 == 0 and torch.equal(r0, r1)
+    for a, b in zip(p0 + s0, p1 + s1):
+        assert torch.equal(a, b)
+
+
+def test_run_epoch_divergence_halts_like_the_trainer(g1):
+    """A batch with loss > 1e5 under check_divergence: run_epoch raises TrainingDivergedError and leaves
+    parameters, Adam state, step count, RNG offset and cursor exactly as after that step (the reference
+    raises right after the update of the diverged batch, trainer.py:166-169); later steps are no-ops."""
+    from bcnf_amd.train import TrainStep, TrainingDivergedError
+    gen = torch.Generator().manual_seed(22)
+    order = torch.randperm(768, generator=gen)[:5 * 128]
+    bad = order[2 * 128:3 * 128]                              # batch 2 diverges
+    py, pt = _epoch_pool(gen, blow_up=bad)
+    order = order.to(DEV)
+    res = []
+    for mode in ("per_step", "epoch"):
+        m = fresh_model(g1, train=True)
+        m.fused.set_seed(9)
+        st = TrainStep(m, lr=2e-4)
+        st.set_pool(py, pt)
+        st.set_epoch(order, 128)
+        if mode == "per_step":
+            vals = [st.step_epoch() for _ in range(3)]
+            assert vals[2][0] > 1e5 and all(v[0] < 1e5 for v in vals[:2])
+        else:
+            with pytest.raises(TrainingDivergedError, match="at batch 2"):
+                st.run_epoch(check_divergence=True)
+        state = [v.clone() for s in st.opt.state.values() for v in s.values()]
+        res.append(([p.detach().clone() for p in m.parameters()], state, m.fused.rng_state().clone(),
+                    st._epoch[1].item()))
+    (p0, s0, r0, c0), (p1, s1, r1, c1) = res
+    assert c0 == c1 == 3 and torch.equal(r0, r1)
+    for a, b in zip(p0 + s0, p1 + s1):
+        assert torch.equal(a, b)
+    assert float(s1[0]) == 3.0                               # Adam step count: three updates applied
