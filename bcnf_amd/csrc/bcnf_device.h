@@ -131,33 +131,13 @@ __device__ __forceinline__ void ld16(float* __restrict__ w, const float* __restr
 }
 
 // ---------------------------------------------------------------------------------------------
-// Branch-free fp32 erf / tanh (coefficients fitted and verified in emulated fp32 by
-// tools/fit_erf.py: erf <= 2.3 ulp / 1.1e-7 abs, tanh <= 1.3 ulp). Both regions are evaluated and
-// selected, so a GELU never splits the block body into divergent basic blocks (ocml's erff does).
+// Branch-free fp32 transcendentals for the block bodies (no divergent basic blocks, unlike ocml's
+// erff / expf range checks). tanh: both regions evaluated and selected (coefficients fitted and
+// verified in emulated fp32 by tools/fit_erf.py, <= 1.3 ulp).
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ float erf_bf(float a) {
-  const float t = fabsf(a), s = a * a;
-  float p = 8.397787315e-05f;                       // |a| < 0.921875 : a * P(a^2)
-  p = fmaf(p, s, -8.149803616e-04f);
-  p = fmaf(p, s, 5.201715976e-03f);
-  p = fmaf(p, s, -2.685970254e-02f);
-  p = fmaf(p, s, 1.128370166e-01f);
-  p = fmaf(p, s, -3.761263490e-01f);
-  p = fmaf(p, s, 1.128379226e+00f);
-  const float ra = a * p;
-  float q = -8.156862918e-07f;                      // otherwise   : 1 - exp(-t Q(t))
-  q = fmaf(q, t, 3.048476174e-05f);
-  q = fmaf(q, t, -4.713801318e-04f);
-  q = fmaf(q, t, 4.200363066e-03f);
-  q = fmaf(q, t, -2.491468750e-02f);
-  q = fmaf(q, t, 1.075745374e-01f);
-  q = fmaf(q, t, 6.343348026e-01f);
-  q = fmaf(q, t, 1.128852129e+00f);
-  float rb = 1.0f - expf(-(q * t));
-  rb = (t >= 3.9375f) ? 1.0f : rb;
-  rb = copysignf(rb, a);
-  return (t < 0.921875f) ? ra : rb;
-}
+// exp(x) as one v_exp_f32 (2^x, 1 ulp) of x log2(e): relative error < 1 ulp + |x| 2^-24, no range
+// checks (overflow -> inf, underflow -> 0, which every caller tolerates).
+__device__ __forceinline__ float exp_fast(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896340736f); }
 
 __device__ __forceinline__ float tanh_bf(float a) {
   const float t = fabsf(a), s = a * a;
@@ -168,21 +148,45 @@ __device__ __forceinline__ float tanh_bf(float a) {
   p = fmaf(p, s, 1.333331466e-01f);
   p = fmaf(p, s, -3.333333433e-01f);
   const float rs = fmaf(a * s, p, a);
-  const float e = expf(2.0f * t);                   // otherwise   : 1 - 2 / (exp(2t) + 1)
+  const float e = exp_fast(2.0f * t);               // otherwise   : 1 - 2 / (exp(2t) + 1)
   float rl = 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
   rl = copysignf(rl, a);
   return (t < 0.625f) ? rs : rl;
 }
 
-// Exact-erf GELU as nn.GELU(approximate='none') (cnf.py:81 via LayerFactory).
-__device__ __forceinline__ float gelu_f(float x) {
-  return 0.5f * x * (1.0f + erf_bf(x * 0.70710678118654752440f));
+// Exact-erf GELU as nn.GELU(approximate='none') (cnf.py:81 via LayerFactory): x Phi(x), with the normal
+// CDF from the complementary error function, Phi(x) = erfc(-x/sqrt2) / 2, and
+//   erfc(z) = t exp(-z^2 + P(t)),  t = 1 / (1 + z/2),  z >= 0
+// (Chebyshev fit, |relative error| < 1.2e-7 for all z >= 0; Press et al., Numerical Recipes, erfcc).
+// Branch-free; no cancellation for x < 0. In fp32: |Phi error| < 2.2e-7, |GELU error| < 3.9e-7 against
+// the double-precision function (the fp32 0.5 x (1 + erf(x/sqrt2)) of the reference: < 4.5e-7).
+__device__ __forceinline__ float erfc_poly(float t) {
+  float p = 1.7087277e-01f;
+  p = fmaf(p, t, -8.2215223e-01f);
+  p = fmaf(p, t, 1.48851587f);
+  p = fmaf(p, t, -1.13520398f);
+  p = fmaf(p, t, 2.7886807e-01f);
+  p = fmaf(p, t, -1.8628806e-01f);
+  p = fmaf(p, t, 9.678418e-02f);
+  p = fmaf(p, t, 3.7409196e-01f);
+  p = fmaf(p, t, 1.00002368f);
+  return fmaf(p, t, -1.26551223f);
 }
-// GELU and its derivative Phi(x) + x phi(x), sharing one erf.
+__device__ __forceinline__ float gelu_f(float x) {
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
+  const float h = 0.5f * t * exp_fast(erfc_poly(t) - z * z);      // erfc(z) / 2
+  return x * (x < 0.f ? h : 1.0f - h);
+}
+// GELU and its derivative Phi(x) + x phi(x) (phi from the same exp(-z^2)).
 __device__ __forceinline__ void gelu_fg(float x, float& g, float& dg) {
-  const float cdf = 0.5f * (1.0f + erf_bf(x * 0.70710678118654752440f));
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
+  const float ez = exp_fast(-(z * z));                              // exp(-x^2 / 2)
+  const float h = 0.5f * t * ez * exp_fast(erfc_poly(t));
+  const float cdf = x < 0.f ? h : 1.0f - h;
   g = x * cdf;
-  dg = fmaf(x, expf(-0.5f * x * x) * 0.39894228040143267794f, cdf);
+  dg = fmaf(x, ez * 0.39894228040143267794f, cdf);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -190,9 +194,10 @@ __device__ __forceinline__ void gelu_fg(float x, float& g, float& dg) {
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
 #pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+  for (int i = 0; i < 10; ++i) {     // one 32x32->64 multiply (v_mad_u64_u32) per product
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
     c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
     k.x += 0x9E3779B9u;
     k.y += 0xBB67AE85u;

@@ -755,7 +755,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
     else
       mlp_forward<NH, false>(L, rr, xa, hpk, bits, DROP, T, Sp, nullptr, nullptr);
     const float S = tanh_bf(Sp);                      // cnf.py:107
-    const float zb = fmaf(expf(S), xb, T);            // cnf.py:179
+    const float zb = fmaf(exp_fast(S), xb, T);        // cnf.py:179
     ldj += S;                                          // cnf.py:190
     if (SAVE) {                                        // 16-B stores, a lane's record contiguous
       ar[AR::S] = S;
@@ -885,7 +885,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse(BcnfLayout L, const float* 
     float T, Sp;
     mlp_forward<NH, false>(L, rr, za, hpk, bits, DROP, T, Sp, nullptr, nullptr);
     const float S = tanh_bf(Sp);
-    const float ybn = (zb - T) * expf(-S);             // cnf.py:205
+    const float ybn = (zb - T) * exp_fast(-S);         // cnf.py:205
     ya = (j < Da) ? (za - rr[1]) / rr[0] : 0.f;        // ActNorm inverse (cnf.py:353-354); identity where none
     yb = (j < Db) ? (ybn - rr[3]) / rr[2] : 0.f;
     sr.store(rec + (cur ^ 1) * RFL, RFL);
@@ -1190,7 +1190,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
     const float xb = fmaf(an_sb, yb, an_bb);
     PH(4)
     PH(5)
-    const float e = expf(S);
+    const float e = exp_fast(S);
     float gza, gzb;
     mix(rb + RBk::QT, gya, gyb, gza, gzb);            // g @ Q^T (identity for the last block)
     const float dT = gzb;                              // z_b = exp(s) y_b + t
