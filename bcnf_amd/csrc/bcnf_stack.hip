@@ -36,6 +36,8 @@ namespace {
 constexpr int NT_EXTRA = 7;
 constexpr int NC16_MAX = 16;           // C <= 256: register-resident column tiles of k_hp / k_dh / k_dw1h            // tiles: D_1..D_NH, D_T, D_S, A_0..A_NH, PA, GA, PB, GB
 constexpr int TILE = BCNF_ROWS * BCNF_TSTRIDE;   // 272 floats
+constexpr int STAGE_REC = 4;   // 16 * RF (RB) floats  <= 4 float4 per thread (RF, RB <= 256)
+constexpr int RING = STAGE_REC * BCNF_WG * 4;    // floats per record-ring slot: a Stage stores all of it
 
 // ------------------------------------------------------------------------------------------------
 // Host-side layout
@@ -114,11 +116,11 @@ int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
 }
 
 size_t fwd_lds_bytes(const BcnfLayout& L) {   // forward / inverse record ring (2 blocks)
-  return sizeof(float) * (size_t)(2 * 16 * L.RF);
+  return sizeof(float) * (size_t)(2 * RING);
 }
 size_t bwd_lds_bytes(const BcnfLayout& L) {   // backward record ring, gradient tiles (2), job table, gradient block
   const int NT = 2 * L.NH + NT_EXTRA;
-  return sizeof(float) * (size_t)(2 * 16 * L.RB + 2 * NT * TILE + 8 * (2 * (BCNF_MAX_HIDDEN + 2) + 4) +
+  return sizeof(float) * (size_t)(2 * RING + 2 * NT * TILE + 8 * (2 * (BCNF_MAX_HIDDEN + 2) + 4) +
                                   L.blk_pad + 64);
 }
 // float4 stores per thread that copy one block's gradient partials from LDS to the slab (fixed count)
@@ -309,17 +311,14 @@ struct Stage {
       r[i] = g4[idx < n4 ? idx : 0];   // unconditional (clamped) so r[] stays in VGPRs
     }
   }
-  __device__ __forceinline__ void store(float* __restrict__ s, int n) const {
+  // all N float4 per thread, no bounds branch: the destination is a RING-sized slot
+  __device__ __forceinline__ void store(float* __restrict__ s) const {
     floatx4* s4 = reinterpret_cast<floatx4*>(s);
-    const int n4 = n >> 2, t = (int)threadIdx.x;
+    const int t = (int)threadIdx.x;
 #pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const int idx = t + i * BCNF_WG;
-      if (idx < n4) s4[idx] = r[i];
-    }
+    for (int i = 0; i < N; ++i) s4[t + i * BCNF_WG] = r[i];
   }
 };
-constexpr int STAGE_REC = 4;   // 16 * RF floats  <= 4 float4 per thread (RF <= 256)
 
 // ------------------------------------------------------------------------------------------------
 // Condition projection, hoisted out of the stack kernels (one fp32 MFMA GEMM per direction):
@@ -727,7 +726,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
   {
     Stage<STAGE_REC> sr;
     sr.load(pf, RFL);
-    sr.store(rec, RFL);
+    sr.store(rec);
   }
   __syncthreads();
 
@@ -741,9 +740,10 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
     sr.load(pf + (long long)k1 * RFL, RFL);
     const float hpk = hp_n;
     hp_n = hpl[k1 * hps];
+    __builtin_amdgcn_sched_barrier(0);                // the prefetch is issued HERE, not sunk to its use
 
     float rr[RecF<NH>::USED];
-    ld_rec_exp<0, RecF<NH>::USED>(rr, rec + cur * RFL + j * L.RF);
+    ld_rec_exp<0, RecF<NH>::USED>(rr, rec + cur * RING + j * L.RF);
     const float xa = fmaf(rr[0], ya, rr[1]);          // ActNorm (cnf.py:349)
     const float xb = fmaf(rr[2], yb, rr[3]);
     uint32_t bits = 0xffu;
@@ -770,7 +770,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
         dst[i * BCNF_WG] = floatx4{ar[4 * i], ar[4 * i + 1], ar[4 * i + 2], ar[4 * i + 3]};
     }
     mix(rr + RecF<NH>::Q, xa, zb, ya, yb);             // y @ Q (cnf.py:335); identity after the last block
-    sr.store(rec + (cur ^ 1) * RFL, RFL);      // past the end these refill a buffer nobody reads
+    sr.store(rec + (cur ^ 1) * RING);          // past the end these refill a buffer nobody reads
     __syncthreads();
   }
   const float ltot = row_sum16(ldj) + ldc;
@@ -865,7 +865,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse(BcnfLayout L, const float* 
   {
     Stage<STAGE_REC> sr;
     sr.load(pi + (long long)kl * RFL, RFL);
-    sr.store(rec + (kl & 1) * RFL, RFL);
+    sr.store(rec + (kl & 1) * RING);
   }
   __syncthreads();
 
@@ -876,8 +876,9 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse(BcnfLayout L, const float* 
     sr.load(pi + (long long)k1 * RFL, RFL);
     const float hpk = hp_n;
     hp_n = hpl[k1 * hps];
+    __builtin_amdgcn_sched_barrier(0);
     float rr[RecF<NH>::USED];
-    ld_rec<0, RecF<NH>::USED>(rr, rec + cur * RFL + j * L.RF);
+    ld_rec<0, RecF<NH>::USED>(rr, rec + cur * RING + j * L.RF);
     float za, zb;
     mix(rr + RecF<NH>::Q, ya, yb, za, zb);             // z @ Q^T (cnf.py:339); identity for the last block
     uint32_t bits = 0xffu;
@@ -888,7 +889,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse(BcnfLayout L, const float* 
     const float ybn = (zb - T) * exp_fast(-S);         // cnf.py:205
     ya = (j < Da) ? (za - rr[1]) / rr[0] : 0.f;        // ActNorm inverse (cnf.py:353-354); identity where none
     yb = (j < Db) ? (ybn - rr[3]) / rr[2] : 0.f;
-    sr.store(rec + (cur ^ 1) * RFL, RFL);
+    sr.store(rec + (cur ^ 1) * RING);
     __syncthreads();
   }
   if (b < N) {
@@ -984,6 +985,15 @@ __device__ __forceinline__ float sum_rows4(float v) {
 // MFMA phase of one block: every parameter gradient of block m (except W1's condition part) into the
 // LDS gradient block `gbuf`. Masked-off lanes store into a private dummy slot (gbuf[blk_pad + lane]) so
 // no store needs an exec-mask branch.
+// c ? a : b through an all-ones / zero mask the optimizer cannot see through: per-lane
+// select-then-store sequences stay straight-line VALU code (a plain select whose operands are only
+// needed on one side is otherwise turned into exec-mask branches around the stores).
+__device__ __forceinline__ int lane_select(bool c, int a, int b) {
+  int m = c ? -1 : 0;
+  asm("" : "+v"(m));
+  return b + ((a - b) & m);
+}
+
 template <int NH>
 __device__ __forceinline__ void bwd_mfma_phase(const BcnfLayout& L,
                                                const float* __restrict__ T, const GradDesc* __restrict__ gd,
@@ -994,7 +1004,7 @@ __device__ __forceinline__ void bwd_mfma_phase(const BcnfLayout& L,
   constexpr int UW = (NW + 3) / 4, US = (NS + 3) / 4;
   const bool has_an = L.act_norm && m < L.nb - 1;
   const int cpl = has_an ? L.an_size : 0;
-  float* dummy = gbuf + L.blk_pad + l64;
+  const int dummy = L.blk_pad + l64;     // per-lane dummy slot of the masked stores
   // ---- weight gradients (MFMA), all operand reads first, independent chains interleaved
   {
     GradDesc d[UW];
@@ -1019,14 +1029,13 @@ __device__ __forceinline__ void bwd_mfma_phase(const BcnfLayout& L,
 #pragma unroll
       for (int u = 0; u < UW; ++u) acc[u] = mfma4(a[u][t], bv[u][t], acc[u]);
 #pragma unroll
-    for (int u = 0; u < UW; ++u) {
-      if (wave + 4 * u >= NW) continue;                   // wave-uniform
+    for (int u = 0; u < UW; ++u) {                        // no branches: surplus jobs store to dummies
       const int base = d[u].out + cpl + __mul24(4 * q, d[u].rs) + r;
-      const bool colok = r < d[u].ncols;
+      const bool colok = (r < d[u].ncols) & (wave + 4 * u < NW);   // & : no short-circuit branches
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const bool ok = colok && (4 * q + i < d[u].nrows) && !(BCNF_EXP & 2);
-        *(ok ? gbuf + base + i * d[u].rs : dummy) = acc[u][i];
+        const bool ok = colok & (4 * q + i < d[u].nrows) & !(BCNF_EXP & 2);
+        gbuf[lane_select(ok, base + i * d[u].rs, dummy)] = acc[u][i];
       }
     }
   }
@@ -1043,11 +1052,10 @@ __device__ __forceinline__ void bwd_mfma_phase(const BcnfLayout& L,
     }
 #pragma unroll
     for (int u = 0; u < US; ++u) {
-      if (wave + 4 * u >= NS) continue;                   // wave-uniform
       const float tot = sum_rows4((v[u][0] + v[u][1]) + (v[u][2] + v[u][3]));
-      const bool live = !(e[u].flags & GD_ACTNORM) || has_an;
-      const bool ok = live && q == 0 && r < e[u].nrows && !(BCNF_EXP & 2);
-      *(ok ? gbuf + e[u].out + ((e[u].flags & GD_COUPLING) ? cpl : 0) + r : dummy) = tot;
+      const bool live = (!(e[u].flags & GD_ACTNORM) | has_an) & (wave + 4 * u < NS);
+      const bool ok = live & (q == 0) & (r < e[u].nrows) & !(BCNF_EXP & 2);
+      gbuf[lane_select(ok, e[u].out + ((e[u].flags & GD_COUPLING) ? cpl : 0) + r, dummy)] = tot;
     }
   }
 }
@@ -1101,7 +1109,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
   const int RBL = 16 * L.RB;
   const int NT = TI.count();
   float* recB = smem;                   // [2][16*RB]
-  float* tiles = recB + 2 * RBL;        // [2][NT][272]
+  float* tiles = recB + 2 * RING;       // [2][NT][272]
   GradDesc* cd = reinterpret_cast<GradDesc*>(tiles + 2 * NT * TILE);   // [MAX_JOBS]
   float* gbuf = tiles + 2 * NT * TILE + MAX_JOBS * 8;                  // [blk_pad + 64] block gradient + dummies
   float exp_sink = 0.f;
@@ -1119,6 +1127,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
   const floatx4* arl = reinterpret_cast<const floatx4*>(arec) + (long long)blockIdx.x * (AR::AR / 4) * BCNF_WG + tid;
   const long long ars = (long long)gridDim.x * (AR::AR / 4) * BCNF_WG;
   float* d1l = d1 + bc * 16 + j;                    // D1[k][b][j]  = d1l[k * B * 16]
+  float* d1_dummy = d1 + (long long)nb * B * 16 + j; // rows past the batch (workspace slack)
   const long long hps = B * 16;
 
   float gya = 0.f, gyb = 0.f, dl = 0.f;
@@ -1144,7 +1153,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
     const int kl = nb - 1;
     Stage<STAGE_REC> sr;
     sr.load(pbk + (long long)kl * RBL, RBL);
-    sr.store(recB + (kl & 1) * RBL, RBL);
+    sr.store(recB + (kl & 1) * RING);
   }
   __syncthreads();
 
@@ -1170,10 +1179,14 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
     Stage<STAGE_REC> sB;
     sB.load(pbk + (long long)k1 * RBL, RBL);
 #pragma unroll
-    for (int i = 0; i < AR::AR / 4; ++i) ar_n[i] = arl[(long long)k1 * ars + i * BCNF_WG];
+    for (int i = 0; i < AR::AR / 4; ++i)
+      ar_n[i] = (BCNF_EXP & 512) ? ar_n[i] : arl[(long long)k1 * ars + i * BCNF_WG];
+    __builtin_amdgcn_sched_barrier(0);                // the prefetch is issued HERE, not sunk to its use
     PH(1)
-    // (b) MFMA phase: parameter gradients of block k+1
-    if (k + 1 < nb && !(BCNF_EXP & 4))
+    // (b) MFMA phase: parameter gradients of block k+1 (in the first iteration, of no block: its LDS
+    // output is never copied out). Unconditional, so (b) and (c) form one basic block and the MFMA
+    // chains can overlap the VALU back-propagation.
+    if (!(BCNF_EXP & 4))
       bwd_mfma_phase<NH>(L, tiles + ((k + 1) & 1) * NT * TILE, cd, gbuf, k + 1);
     PH(2)
     PH(3)
@@ -1181,7 +1194,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
     float* Tt = tiles + cur * NT * TILE;
     const int tix = s * BCNF_TSTRIDE + j;
     float rb[RBk::USED];
-    ld_rec_exp<0, RBk::USED>(rb, recB + cur * RBL + j * L.RB);
+    ld_rec_exp<0, RBk::USED>(rb, recB + cur * RING + j * L.RB);
     const float ya = ar[AR::YA], yb = ar[AR::YB], S = ar[AR::S];
     const float* act = ar + AR::ACT;
     const float* gd = ar + AR::GD;
@@ -1213,7 +1226,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
     const float dpre1 = da * gd[0];
     Tt[TI.D(1) * TILE + tix] = dpre1;
     Tt[TI.A(0) * TILE + tix] = xa;
-    if (valid) d1l[k * hps] = dpre1;                   // dL/d pre-activation of Linear 1 (k_dh, k_dw1h)
+    if (!(BCNF_EXP & 1024)) *(valid ? d1l + k * hps : d1_dummy) = dpre1;   // dL/d pre-activation of Linear 1 (k_dh, k_dw1h)
     const float dxa = rot16(dpre1, rb + RBk::W1T, gza);
     {   // ActNorm tiles (consumed only for blocks that have an ActNorm)
       const float inv_a = (j < Da) ? __builtin_amdgcn_rcpf(an_sa) : 0.f;
@@ -1227,7 +1240,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float*
     gyb = an_sb * dxb;
     PH(6)
     // (d) commit the prefetched record (past the end it refills a buffer nobody reads)
-    sB.store(recB + (cur ^ 1) * RBL, RBL);
+    sB.store(recB + (cur ^ 1) * RING);
     PH(7)
     __syncthreads();
     PH(8)
@@ -1489,7 +1502,9 @@ long long ws_hp_off(const BcnfLayout& L, long long B, bool drop) {
   return ws_part_off(L, B, drop) + (((B + 15) / 16 + 3) & ~3LL);
 }
 long long ws_d1_off(const BcnfLayout& L, long long B, bool drop) { return ws_hp_off(L, B, drop) + (long long)L.nb * B * 16; }
-long long ws_floats(const BcnfLayout& L, long long B, bool drop) { return ws_d1_off(L, B, drop) + (long long)L.nb * B * 16; }
+long long ws_floats(const BcnfLayout& L, long long B, bool drop) {
+  return ws_d1_off(L, B, drop) + (long long)L.nb * B * 16 + 16;   // + D1 dummy row
+}
 
 int forward_impl(const BcnfStackDesc* desc, const void* packed, const float* y, const float* h, int64_t batch,
                  float* z, float* ldj, float* log_prob, int32_t training, const uint64_t* rng_state, void* workspace,
