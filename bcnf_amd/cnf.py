@@ -26,6 +26,7 @@ import torch.nn as nn
 from bcnf_amd.factories import FeatureNetworkFactory, LayerFactory
 from bcnf_amd.feature_network import FeatureNetwork, FeatureNetworkStack
 from bcnf_amd.fused import FusedStack, StackConfig, stack_forward, stack_inverse, stack_nll
+from bcnf_amd.wide import make_stack
 from bcnf_amd.utils import ParameterIndexMapping, log_prob_from_latent
 
 
@@ -156,7 +157,7 @@ class ConditionalAffineCouplingLayer(ConditionalInvertibleLayer):
         key = (cfg, )
         st = getattr(self, "_solo", None)
         if st is None or st[0] != key:
-            st = (key, FusedStack(cfg, [], [], bind=False))
+            st = (key, make_stack(cfg, [], [], bind=False))
             object.__setattr__(self, "_solo", st)
         flat = torch.cat([p.reshape(-1) for p in self.canonical_params()])
         return st[1], flat
@@ -285,7 +286,7 @@ class CondRealNVP_v2(ConditionalInvertibleLayer):
         cfg = StackConfig(self.size, tuple(self.nested_sizes), self.n_blocks, self.n_conditions, self.dropout,
                           self.act_norm, self.two_way)
         trainable, frozen = self._canonical()
-        object.__setattr__(self, "_fused", FusedStack(cfg, trainable, frozen))
+        object.__setattr__(self, "_fused", make_stack(cfg, trainable, frozen))
 
     def _apply(self, fn, recurse=True):
         out = super()._apply(fn, recurse)
@@ -319,9 +320,9 @@ class CondRealNVP_v2(ConditionalInvertibleLayer):
             raise NotImplementedError("bcnf_amd: two_way coupling is not implemented by the HIP kernels yet")
         if not self._fused.supported:
             raise NotImplementedError(
-                "bcnf_amd: this stack shape is outside the fused small-width kernel family (hidden sizes <= 16, "
-                "size <= 32, n_conditions <= 256, <= 8 nested layers); the wide-MLP (FC_large-class) MFMA path is "
-                "not built yet")
+                "bcnf_amd: this stack shape fits neither HIP kernel family: the register-resident small family "
+                "(hidden sizes <= 16, size <= 32, n_conditions <= 256) nor the wide-MLP MFMA family (equal nested "
+                "sizes, size <= 32, n_conditions % 4 == 0)")
 
     # ------------------------------------------------------------------ reference API
     def verify(self) -> None:

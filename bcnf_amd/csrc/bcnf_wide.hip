@@ -1,0 +1,1428 @@
+// Wide-MLP family of the CondRealNVP_v2 coupling stack on gfx950 (CDNA4): trajectory_FC_large /
+// trajectory_LSTM_large shapes (D = 19, C = 1360, nested_sizes = [526] * 5, 26 blocks), i.e. every stack whose
+// nested MLP is too wide for the register-resident small family of bcnf_stack.hip.
+//
+// Reference (psaegert/bcnf, src/bcnf/models/cnf.py): ConditionalNestedNeuralNetwork (:49-107),
+// ConditionalAffineCouplingLayer.forward / .inverse (:165-213), OrthonormalTransformation (:312-339), ActNorm
+// (:342-354), CondRealNVP_v2.forward / .inverse layer loops (:467-508); autograd backward of all of it.
+//
+// Shape of the work: per block, the nested MLP is Linear(Da + C -> H), (GELU, Dropout, Linear(H -> H)) x (NH-1),
+// GELU, Dropout, Linear(H -> 2 Db). At H = 526 the H x H layers are MFMA-bound GEMMs (fp32 MFMA,
+// v_mfma_f32_32x32x2_f32, exact f32, the only fp32 matrix path on gfx950). The kernels:
+//
+//   k_wgemm<...>   LDS-tiled fp32-MFMA GEMM, three operand layouts (NT forward, NN dX, TN dW), group index in
+//                  blockIdx.z, fused epilogues: bias + exact-erf GELU + Philox dropout (writing the activation
+//                  and its derivative factor G = mask * GELU'(pre) / (1 - p)), dZ = acc * G, and Linear-gradient
+//                  stores straight into the canonical flat gradient (weight rows + bias via a ones column).
+//   k_wlink_*      one wavefront per two samples: the end of block k (last Linear, tanh, exp-affine coupling,
+//                  log|det J|, orthonormal mix) fused with the start of block k+1 (ActNorm, Linear-1 y-part from
+//                  the hoisted condition projection, GELU, dropout); and the mirror image for the backward and
+//                  for the inverse.
+//   hoisted condition projection: P = h W0h_all^T for ALL blocks in one GEMM (h does not change between
+//   blocks); its transposes give dh = dZ0_all W0h_all and dW0h = dZ0_all^T h, again one GEMM each.
+//
+// Activation rows are padded to HP = round_up(H + 1, 4) floats: column H holds 1.0 (so the dW GEMM emits the
+// bias gradient as one more output column) and the padded weight copies are zero beyond H, so every GEMM runs
+// with K = HP and no K masks.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "bcnf_amd.h"
+#include "bcnf_device.h"
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr int WWG = 256;      // threads per workgroup of every wide kernel
+constexpr int LINK_ROWS = 2;  // samples per wavefront in the link kernels
+constexpr int DM = 32;        // max D of the wide family (register arrays of the link kernels)
+
+inline int pad4(int x) { return (x + 3) & ~3; }
+inline long long pad4l(long long x) { return (x + 3) & ~3LL; }
+
+struct WideLayout {
+  int D, Da, Db, C, H, NH, nb, an;
+  int HP, UP, OP, XP, SP, AP;   // row strides: activations, [u_a | 1], dO, block inputs, tanh(s), ActNorm partials
+  int in0;                      // Da + C
+  long long blk_stride;
+  long long lin_w[BCNF_MAX_HIDDEN + 1], lin_b[BCNF_MAX_HIDDEN + 1];
+  long long n_trainable;
+  float p, keep_scale;
+  uint32_t thresh;              // drop if philox u32 < thresh
+  // packed buffer (floats)
+  long long pk_w0h;             // [nb * HP][C]     row k*HP + n = W0_k[n][Da + c], rows n >= H zero
+  long long pk_hid;             // [nb][NH-1][HP][HP]  W_l (l = 1..NH-1), zero beyond H
+  long long pk_w0y;             // [nb][Da][HP]     W0_k[n][j] transposed
+  long long pk_wl;              // [nb][2 Db][HP]   last Linear, zero beyond H
+  long long pk_q;               // [nb-1][D][D]
+  long long pk_ldc;             // [nb]             sum_i log|scale_k,i| (0 without ActNorm)
+  long long total;
+};
+
+__host__ __device__ inline long long wcb(const WideLayout& L, int k) {
+  return (long long)k * L.blk_stride + ((k < L.nb - 1) ? L.an : 0);
+}
+
+int wide_layout(const BcnfStackDesc* d, WideLayout* L) {
+  if (!d || !L) return BCNF_ERR_ARG;
+  memset(L, 0, sizeof(*L));
+  if (d->size < 2 || d->n_blocks < 1 || d->n_hidden < 1 || d->n_hidden > BCNF_MAX_HIDDEN || d->n_conditions < 0)
+    return BCNF_ERR_ARG;
+  if (!(d->dropout >= 0.f && d->dropout < 1.f)) return BCNF_ERR_ARG;
+  for (int i = 0; i < d->n_hidden; ++i)
+    if (d->hidden[i] < 1) return BCNF_ERR_ARG;
+  if (d->two_way) return BCNF_ERR_UNSUPPORTED;
+  for (int i = 1; i < d->n_hidden; ++i)
+    if (d->hidden[i] != d->hidden[0]) return BCNF_ERR_UNSUPPORTED;     // equal widths (every shipped config)
+  if (d->size > DM || d->n_conditions < 1 || (d->n_conditions & 3) || d->hidden[0] > 8192) return BCNF_ERR_UNSUPPORTED;
+  L->D = d->size;
+  L->Da = (d->size + 1) / 2;
+  L->Db = d->size / 2;
+  L->C = d->n_conditions;
+  L->H = d->hidden[0];
+  L->NH = d->n_hidden;
+  L->nb = d->n_blocks;
+  L->an = d->act_norm ? 2 * d->size : 0;
+  L->HP = pad4(L->H + 1);
+  L->UP = pad4(L->Da + 1);
+  L->OP = pad4(2 * L->Db);
+  L->XP = pad4(L->D);
+  L->SP = pad4(L->Db);
+  L->AP = pad4(2 * L->D);
+  L->in0 = L->Da + L->C;
+  long long off = 0;
+  for (int l = 0; l <= L->NH; ++l) {
+    const long long in = (l == 0) ? L->in0 : L->H;
+    const long long out = (l == L->NH) ? 2 * L->Db : L->H;
+    L->lin_w[l] = off;
+    off += in * out;
+    L->lin_b[l] = off;
+    off += out;
+  }
+  L->blk_stride = L->an + off;
+  L->n_trainable = (long long)(L->nb - 1) * L->blk_stride + off;
+  L->p = d->dropout;
+  L->keep_scale = 1.0f / (1.0f - d->dropout);
+  const double t = (double)d->dropout * 4294967296.0;
+  L->thresh = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+  long long o = 0;
+  L->pk_w0h = o; o += pad4l((long long)L->nb * L->HP * L->C);
+  L->pk_hid = o; o += pad4l((long long)L->nb * (L->NH - 1) * L->HP * L->HP);
+  L->pk_w0y = o; o += pad4l((long long)L->nb * L->Da * L->HP);
+  L->pk_wl = o;  o += pad4l((long long)L->nb * 2 * L->Db * L->HP);
+  L->pk_q = o;   o += pad4l((long long)(L->nb - 1) * L->D * L->D);
+  L->pk_ldc = o; o += pad4l(L->nb);
+  L->total = o;
+  return BCNF_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Packing: padded, GEMM-friendly copies of the weights (one launch per parameter update).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(WWG) void k_wpack(const WideLayout L, const float* __restrict__ prm,
+                                               const float* __restrict__ q, float* __restrict__ pk) {
+  const long long stride = (long long)gridDim.x * WWG;
+  for (long long e = (long long)blockIdx.x * WWG + threadIdx.x; e < L.pk_ldc; e += stride) {
+    float v = 0.f;
+    if (e < L.pk_hid) {
+      const long long r = e / L.C;
+      const int c = (int)(e - r * L.C);
+      const int k = (int)(r / L.HP), n = (int)(r - (long long)k * L.HP);
+      if (k < L.nb && n < L.H) v = prm[wcb(L, k) + L.lin_w[0] + (long long)n * L.in0 + L.Da + c];
+    } else if (e < L.pk_w0y) {
+      const long long i = e - L.pk_hid;
+      const long long per = (long long)L.HP * L.HP;
+      const long long kl = i / per;
+      const long long rem = i - kl * per;
+      const int n = (int)(rem / L.HP), kk = (int)(rem - (long long)n * L.HP);
+      if (L.NH > 1 && kl < (long long)L.nb * (L.NH - 1) && n < L.H && kk < L.H) {
+        const int k = (int)(kl / (L.NH - 1)), l = (int)(kl % (L.NH - 1)) + 1;
+        v = prm[wcb(L, k) + L.lin_w[l] + (long long)n * L.H + kk];
+      }
+    } else if (e < L.pk_wl) {
+      const long long i = e - L.pk_w0y;
+      const long long per = (long long)L.Da * L.HP;
+      const int k = (int)(i / per);
+      const long long rem = i - (long long)k * per;
+      const int j = (int)(rem / L.HP), n = (int)(rem - (long long)j * L.HP);
+      if (k < L.nb && n < L.H) v = prm[wcb(L, k) + L.lin_w[0] + (long long)n * L.in0 + j];
+    } else if (e < L.pk_q) {
+      const long long i = e - L.pk_wl;
+      const long long per = (long long)2 * L.Db * L.HP;
+      const int k = (int)(i / per);
+      const long long rem = i - (long long)k * per;
+      const int j = (int)(rem / L.HP), n = (int)(rem - (long long)j * L.HP);
+      if (k < L.nb && n < L.H) v = prm[wcb(L, k) + L.lin_w[L.NH] + (long long)j * L.H + n];
+    } else {
+      const long long i = e - L.pk_q;
+      if (i < (long long)(L.nb - 1) * L.D * L.D) v = q[i];
+    }
+    pk[e] = v;
+  }
+}
+
+// ActNorm log|det J| constant per block (ActNorm.forward, cnf.py:348-351: torch.sum(log|scale|)).
+__global__ void k_wpack_ldc(const WideLayout L, const float* __restrict__ prm, float* __restrict__ pk) {
+  const int k = threadIdx.x;
+  if (k >= L.nb) return;
+  float s = 0.f;
+  if (L.an && k < L.nb - 1)
+    for (int i = 0; i < L.D; ++i) s += logf(fabsf(prm[(long long)k * L.blk_stride + i]));
+  pk[L.pk_ldc + k] = s;
+}
+
+// ------------------------------------------------------------------------------------------------
+// fp32-MFMA GEMM  C[m][n] = sum_k A(m, k) B(k, n), v_mfma_f32_32x32x2_f32.
+//   A(m, k): AKC ? A[m * lda + k] : A[k * lda + m]      B(k, n): BKC ? B[n * ldb + k] : B[k * ldb + n]
+// 256 threads = 2 x 2 waves; each wave owns (BM/2) x (BN/2) as 32x32 accumulators. Tiles are staged global ->
+// registers -> LDS (two buffers, one barrier per K tile). K-contiguous operands keep [mn][BK+4] in LDS and are
+// read as float4; the others [BK][mn+4] (conflict-free scalar reads). Inside a K tile, lane half h consumes
+// k = h*BK/2 + s at MFMA step s (any k order is a valid fp32 sum order; A and B use the same one).
+// Requirements (checked by the host): lda, ldb, ldc % 4 == 0, 16-byte aligned bases, K % 4 == 0 when an
+// operand is K-contiguous.
+// ------------------------------------------------------------------------------------------------
+enum { EPI_STORE = 0, EPI_ACT = 1, EPI_GRAD = 2, EPI_LINGRAD = 3, EPI_ROWMAP = 4 };
+
+struct GemmArgs {
+  int M, N, K, G0;              // groups: blockIdx.z = g1 * G0 + g0
+  const float* A; long long lda, sA1, sA0;
+  const float* B; long long ldb, sB1, sB0;
+  float* C; long long ldc, sC1, sC0;
+  // EPI_ACT: out = dropout(GELU(acc + bias[n])) for n < n_real, 1 at n == n_real, 0 beyond; aux = G factor
+  const float* bias;
+  float* aux; long long ldaux, saux1, saux0;   // EPI_ACT: G out (nullable); EPI_GRAD: G in
+  int n_real;
+  const uint64_t* rng; uint32_t thresh; float keep_scale; uint32_t tag, tag_s1;   // tag of group = tag + g1*tag_s1
+  // EPI_LINGRAD: row r, col c: c < wcols -> C[r * ldc + c], c == wcols -> C[boff + r]
+  int wcols; long long boff;
+  // flat-gradient group base (EPI_LINGRAD / EPI_ROWMAP): C + g1 * cb_stride + (g1 < cb_nb - 1 ? cb_an : 0) + g0 * sC0
+  long long cb_stride; int cb_an, cb_nb, use_cb;
+  // EPI_ROWMAP: row r -> block r / rm_hp, n = r % rm_hp (skipped when >= rm_h): C + cb(block) + rm_off + n*ldc + col
+  int rm_hp, rm_h; long long rm_off;
+};
+
+__device__ __forceinline__ floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
+__device__ __forceinline__ void st4(float* p, floatx4 v) { *reinterpret_cast<floatx4*>(p) = v; }
+
+template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI>
+__global__ __launch_bounds__(WWG, 2) void k_wgemm(const GemmArgs g) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TI = WM / 32, TJ = WN / 32;
+  constexpr int ASZ = AKC ? BM * (BK + 4) : BK * (BM + 4);
+  constexpr int BSZ = BKC ? BN * (BK + 4) : BK * (BN + 4);
+  constexpr int AV = BM * BK / 4 / WWG, BV = BN * BK / 4 / WWG;
+  static_assert(AV >= 1 && BV >= 1, "tile too small for 256 threads");
+  __shared__ __attribute__((aligned(16))) float lds[2 * (ASZ + BSZ)];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, c32 = lane & 31, hh = lane >> 5;
+  const int z = blockIdx.z, g1 = z / g.G0, g0 = z - g1 * g.G0;
+  const float* __restrict__ A = g.A + g1 * g.sA1 + g0 * g.sA0;
+  const float* __restrict__ B = g.B + g1 * g.sB1 + g0 * g.sB0;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int M = g.M, N = g.N, K = g.K;
+
+  floatx4 ra[AV], rb[BV];
+  auto load_a = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < AV; ++i) {
+      const int e = tid + WWG * i;
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if (AKC) {
+        const int row = e / (BK / 4), kq = e % (BK / 4);
+        const int gm = m0 + row, gk = k0 + 4 * kq;
+        if (gm < M && gk < K) v = ld4(A + (long long)gm * g.lda + gk);
+      } else {
+        const int kr = e / (BM / 4), mq = e % (BM / 4);
+        const int gk = k0 + kr, gm = m0 + 4 * mq;
+        if (gk < K) {
+          const float* p = A + (long long)gk * g.lda + gm;
+          if (gm + 3 < M) v = ld4(p);
+          else {
+            if (gm < M) v.x = p[0];
+            if (gm + 1 < M) v.y = p[1];
+            if (gm + 2 < M) v.z = p[2];
+          }
+        }
+      }
+      ra[i] = v;
+    }
+  };
+  auto load_b = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < BV; ++i) {
+      const int e = tid + WWG * i;
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if (BKC) {
+        const int row = e / (BK / 4), kq = e % (BK / 4);
+        const int gn = n0 + row, gk = k0 + 4 * kq;
+        if (gn < N && gk < K) v = ld4(B + (long long)gn * g.ldb + gk);
+      } else {
+        const int kr = e / (BN / 4), nq = e % (BN / 4);
+        const int gk = k0 + kr, gn = n0 + 4 * nq;
+        if (gk < K) {
+          const float* p = B + (long long)gk * g.ldb + gn;
+          if (gn + 3 < N) v = ld4(p);
+          else {
+            if (gn < N) v.x = p[0];
+            if (gn + 1 < N) v.y = p[1];
+            if (gn + 2 < N) v.z = p[2];
+          }
+        }
+      }
+      rb[i] = v;
+    }
+  };
+  auto store_tiles = [&](float* As, float* Bs) {
+#pragma unroll
+    for (int i = 0; i < AV; ++i) {
+      const int e = tid + WWG * i;
+      if (AKC) st4(As + (e / (BK / 4)) * (BK + 4) + 4 * (e % (BK / 4)), ra[i]);
+      else st4(As + (e / (BM / 4)) * (BM + 4) + 4 * (e % (BM / 4)), ra[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < BV; ++i) {
+      const int e = tid + WWG * i;
+      if (BKC) st4(Bs + (e / (BK / 4)) * (BK + 4) + 4 * (e % (BK / 4)), rb[i]);
+      else st4(Bs + (e / (BN / 4)) * (BN + 4) + 4 * (e % (BN / 4)), rb[i]);
+    }
+  };
+
+  floatx16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nk = (K + BK - 1) / BK;
+  load_a(0);
+  load_b(0);
+  store_tiles(lds, lds + ASZ);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    float* As = lds + (kt & 1) * (ASZ + BSZ);
+    float* Bs = As + ASZ;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      load_a((kt + 1) * BK);
+      load_b((kt + 1) * BK);
+    }
+#pragma unroll
+    for (int sq = 0; sq < BK / 8; ++sq) {
+      const int kb = hh * (BK / 2) + 4 * sq;
+      floatx4 af[TI], bf[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int row = wm * WM + 32 * i + c32;
+        if (AKC) af[i] = ld4(As + row * (BK + 4) + kb);
+        else af[i] = floatx4{As[(kb + 0) * (BM + 4) + row], As[(kb + 1) * (BM + 4) + row],
+                             As[(kb + 2) * (BM + 4) + row], As[(kb + 3) * (BM + 4) + row]};
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int col = wn * WN + 32 * j + c32;
+        if (BKC) bf[j] = ld4(Bs + col * (BK + 4) + kb);
+        else bf[j] = floatx4{Bs[(kb + 0) * (BN + 4) + col], Bs[(kb + 1) * (BN + 4) + col],
+                             Bs[(kb + 2) * (BN + 4) + col], Bs[(kb + 3) * (BN + 4) + col]};
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      float* An = lds + ((kt + 1) & 1) * (ASZ + BSZ);
+      store_tiles(An, An + ASZ);
+    }
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  // accumulator element r of lane (c32, hh): row = (r & 3) + 8 (r >> 2) + 4 hh, col = c32
+  float* __restrict__ Cg = g.C;
+  if (EPI == EPI_LINGRAD || EPI == EPI_ROWMAP) {
+    if (g.use_cb) Cg += g1 * g.cb_stride + ((g1 < g.cb_nb - 1) ? g.cb_an : 0) + g0 * g.sC0;
+  } else {
+    Cg += g1 * g.sC1 + g0 * g.sC0;
+  }
+  float* __restrict__ Xg = (EPI == EPI_ACT || EPI == EPI_GRAD) && g.aux ? g.aux + g1 * g.saux1 + g0 * g.saux0 : nullptr;
+  uint64_t seed = 0, offs = 0;
+  if (EPI == EPI_ACT && g.rng) {
+    seed = g.rng[0];
+    offs = g.rng[1];
+  }
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int col = n0 + wn * WN + 32 * j + c32;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rbase = m0 + wm * WM + 32 * i + 8 * q + 4 * hh;
+        uint4 rnd = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+        if (EPI == EPI_ACT && g.rng) {
+          const uint32_t tag = g.tag + (uint32_t)g1 * g.tag_s1;
+          rnd = philox4x32_10(make_uint4((uint32_t)rbase, (uint32_t)col, tag, (uint32_t)offs),
+                              make_uint2((uint32_t)seed, (uint32_t)(seed >> 32) ^ (uint32_t)(offs >> 32)));
+        }
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int row = rbase + rr;
+          const float v = acc[i][j][4 * q + rr];
+          if (row >= M || col >= N) continue;
+          if (EPI == EPI_STORE) {
+            Cg[(long long)row * g.ldc + col] = v;
+          } else if (EPI == EPI_ACT) {
+            float a = 0.f, gd = 0.f;
+            if (col < g.n_real) {
+              float ge, dg;
+              gelu_fg(v + g.bias[col], ge, dg);
+              if (g.rng) {
+                const uint32_t u = rr == 0 ? rnd.x : rr == 1 ? rnd.y : rr == 2 ? rnd.z : rnd.w;
+                const float m = u >= g.thresh ? g.keep_scale : 0.f;
+                a = ge * m;
+                gd = dg * m;
+              } else {
+                a = ge;
+                gd = dg;
+              }
+            } else if (col == g.n_real) {
+              a = 1.f;
+            }
+            Cg[(long long)row * g.ldc + col] = a;
+            if (Xg) Xg[(long long)row * g.ldaux + col] = gd;
+          } else if (EPI == EPI_GRAD) {
+            Cg[(long long)row * g.ldc + col] = v * Xg[(long long)row * g.ldaux + col];
+          } else if (EPI == EPI_LINGRAD) {
+            if (col < g.wcols) Cg[(long long)row * g.ldc + col] = v;
+            else if (col == g.wcols) Cg[g.boff + row] = v;
+          } else {   // EPI_ROWMAP
+            const int blk = row / g.rm_hp, n = row - blk * g.rm_hp;
+            if (n < g.rm_h)
+              Cg[(long long)blk * g.cb_stride + ((blk < g.cb_nb - 1) ? g.cb_an : 0) + g.rm_off + (long long)n * g.ldc + col] = v;
+          }
+        }
+      }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Link kernels: one wavefront per LINK_ROWS samples, 4 wavefronts per workgroup.
+// Cross-lane sums: DPP rotations inside each 16-lane row, then the four row sums via readlane.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xf, 0xf, true));  // row_ror:8
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xf, 0xf, true));  // row_ror:4
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x122, 0xf, 0xf, true));  // row_ror:2
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x121, 0xf, 0xf, true));  // row_ror:1
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return (r0 + r1) + (r2 + r3);
+}
+__device__ __forceinline__ float bcast(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+struct LinkArgs {
+  long long B;
+  int kt, kh;                   // tail block (-1: none), head block (-1: none)
+  const float* prm;             // canonical flat parameters
+  const float* pk;              // packed
+  // tail
+  const float* Alast;           // [B][HP] last hidden activation of block kt
+  const float* Xt;              // block kt's saved input rows (forward: pre-ActNorm x; inverse: v = x Q^T)
+  float* S;                     // forward save: tanh(s) of block kt [B][SP] (nullable)
+  float* z;                     // last block: z / inverse output y [B][D] (ld D)
+  float* ldj;                   // [B]
+  float* nllp;                  // last block: 0.5 |z|^2 - ldj per row (nullable)
+  // head
+  const float* xin;             // head-only launch: input rows (ld D): y (forward) or z (inverse)
+  float* Xh;                    // block kh's saved input rows [B][XP]
+  const float* P; long long ldP; const int64_t* cidx;   // hoisted projection rows (row r uses cidx[r])
+  float* A0; float* G0;         // [B][HP] first hidden activation and its derivative factor (G0 nullable)
+  float* U;                     // forward save: [u_a | 1 | 0] of block kh [B][UP] (nullable)
+  const uint64_t* rng;          // dropout (nullable = off)
+};
+
+// Dropout mask for a float4 group (4 consecutive columns n..n+3 of one row).
+__device__ __forceinline__ uint4 drop4(const uint64_t* rng, uint64_t seed, uint64_t offs, long long row, int n,
+                                       uint32_t tag) {
+  return philox4x32_10(make_uint4((uint32_t)row, (uint32_t)n | 0x80000000u, tag, (uint32_t)offs),
+                       make_uint2((uint32_t)seed, (uint32_t)(seed >> 32) ^ (uint32_t)(offs >> 32)));
+}
+
+// Forward (INV = false): tail(kt) = last Linear, t / tanh(s), z_b = exp(s) u_b + t, ldj += sum s, x Q_kt;
+//                        head(kh) = ActNorm, Linear-1 from P + u_a W0y^T + b0, GELU, dropout.
+// Inverse (INV = true):  tail(kt) = last Linear, y_b = (z_b - t) exp(-s), ActNorm^-1;
+//                        head(kh) = v = x Q_kh^T, Linear-1 as above.   (cnf.py:198-213, 337-339, 353-354)
+template <bool INV>
+__global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int HP = L.HP, H = L.H, D = L.D, Da = L.Da, Db = L.Db, O2 = 2 * Db;
+  float* Wl = sm;                       // [2Db][HP] last Linear of block kt
+  float* W0 = sm + (a.kt >= 0 ? O2 * HP : 0);   // [Da][HP] W0y^T of block kh
+  if (a.kt >= 0) {
+    const float* src = a.pk + L.pk_wl + (long long)a.kt * O2 * HP;
+    for (int e = tid; e < O2 * HP / 4; e += WWG) st4(Wl + 4 * e, ld4(src + 4 * e));
+  }
+  if (a.kh >= 0) {
+    const float* src = a.pk + L.pk_w0y + (long long)a.kh * Da * HP;
+    for (int e = tid; e < Da * HP / 4; e += WWG) st4(W0 + 4 * e, ld4(src + 4 * e));
+  }
+  __syncthreads();
+
+  const long long row0 = ((long long)blockIdx.x * 4 + wave) * LINK_ROWS;
+  if (row0 >= a.B) return;
+  const int nq = HP / 4;                // float4 groups per activation row
+  uint64_t seed = 0, offs = 0;
+  if (a.rng) {
+    seed = a.rng[0];
+    offs = a.rng[1];
+  }
+
+  for (int rr = 0; rr < LINK_ROWS; ++rr) {
+    const long long row = row0 + rr;
+    if (row >= a.B) break;
+    float x[DM];                          // the sample's D-vector (wave-uniform)
+    // ------------------------------------------------------------ tail of block kt
+    if (a.kt >= 0) {
+      const int k = a.kt;
+      float o[DM];
+#pragma unroll
+      for (int j = 0; j < DM; ++j) o[j] = 0.f;
+      const float* arow = a.Alast + row * HP;
+      for (int q = lane; q < nq; q += 64) {
+        const floatx4 av = ld4(arow + 4 * q);
+#pragma unroll
+        for (int j = 0; j < DM; ++j) {
+          if (j < O2) {
+            const floatx4 w = ld4(Wl + j * HP + 4 * q);
+            o[j] = fmaf(av.x, w.x, fmaf(av.y, w.y, fmaf(av.z, w.z, fmaf(av.w, w.w, o[j]))));
+          }
+        }
+      }
+      const float* bl = a.prm + wcb(L, k) + L.lin_b[L.NH];
+#pragma unroll
+      for (int j = 0; j < DM; ++j)
+        if (j < O2) o[j] = wave_sum(o[j]) + bl[j];
+      // block kt's input row as the coupling sees it
+      const float* xt = a.Xt + row * L.XP;
+#pragma unroll
+      for (int i = 0; i < DM; ++i)
+        if (i < D) x[i] = xt[i];
+      float ssum = 0.f;
+      if (!INV) {
+        if (L.an && k < L.nb - 1) {
+          const float* sc = a.prm + (long long)k * L.blk_stride;
+#pragma unroll
+          for (int i = 0; i < DM; ++i)
+            if (i < D) x[i] = sc[i] * x[i] + sc[D + i];        // ActNorm (cnf.py:350)
+        }
+#pragma unroll
+        for (int i = 0; i < DM / 2; ++i) {
+          if (i < Db) {
+            const float s = tanh_bf(o[Db + i]);
+            ssum += s;
+            x[Da + i] = fmaf(exp_fast(s), x[Da + i], o[i]);    // z_b = exp(s) y_b + t (cnf.py:179)
+            if (a.S && lane == 0) a.S[row * L.SP + i] = s;
+          }
+        }
+        float lj = a.ldj[row] + ssum;
+        if (k < L.nb - 1) {
+          // x <- x Q_k (cnf.py:333-335): lane j computes column j, then broadcast
+          const float* Q = a.pk + L.pk_q + (long long)k * D * D;
+          float cj = 0.f;
+          const int lj_ = lane < D ? lane : 0;
+#pragma unroll
+          for (int i = 0; i < DM; ++i)
+            if (i < D) cj = fmaf(x[i], Q[i * D + lj_], cj);
+#pragma unroll
+          for (int j = 0; j < DM; ++j)
+            if (j < D) x[j] = bcast(cj, j);
+          if (lane == 0) a.ldj[row] = lj;
+        } else {
+          // z and the per-sample NLL term 0.5 |z|^2 - ldj (utils.py:40-46)
+          float zz = 0.f;
+#pragma unroll
+          for (int i = 0; i < DM; ++i)
+            if (i < D) zz = fmaf(x[i], x[i], zz);
+          if (lane == 0) {
+            a.ldj[row] = lj;
+            if (a.nllp) a.nllp[row] = 0.5f * zz - lj;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < DM / 2; ++i) {
+          if (i < Db) {
+            const float s = tanh_bf(o[Db + i]);
+            x[Da + i] = (x[Da + i] - o[i]) * exp_fast(-s);    // y_b = (z_b - t) exp(-s) (cnf.py:201)
+          }
+        }
+        if (L.an && k < L.nb - 1) {
+          const float* sc = a.prm + (long long)k * L.blk_stride;
+#pragma unroll
+          for (int i = 0; i < DM; ++i)
+            if (i < D) x[i] = (x[i] - sc[D + i]) / sc[i];      // ActNorm inverse (cnf.py:354)
+        }
+        if (k == 0) {
+          float mine = 0.f;
+#pragma unroll
+          for (int i = 0; i < DM; ++i)
+            if (i == lane) mine = x[i];
+          if (lane < D) a.z[row * D + lane] = mine;
+        }
+      }
+    } else {
+      const float* xr = a.xin + row * D;
+#pragma unroll
+      for (int i = 0; i < DM; ++i)
+        if (i < D) x[i] = xr[i];
+      if (!INV && lane == 0) a.ldj[row] = 0.f;
+    }
+    // the last-block store above used x[lane]: redo it with a register select (no dynamic indexing)
+    if (!INV && a.kt == L.nb - 1) {
+      float mine = 0.f;
+#pragma unroll
+      for (int i = 0; i < DM; ++i)
+        if (i == lane) mine = x[i];
+      if (lane < D) a.z[row * D + lane] = mine;
+    }
+    // ------------------------------------------------------------ head of block kh
+    if (a.kh >= 0) {
+      const int k = a.kh;
+      float u[DM / 2];
+      {
+        float mine = 0.f;
+#pragma unroll
+        for (int i = 0; i < DM; ++i)
+          if (i == lane) mine = x[i];
+        if (!INV) {
+          if (lane < D) a.Xh[row * L.XP + lane] = mine;        // saved pre-ActNorm input
+          if (L.an && k < L.nb - 1) {
+            const float* sc = a.prm + (long long)k * L.blk_stride;
+#pragma unroll
+            for (int i = 0; i < DM; ++i)
+              if (i < D) x[i] = sc[i] * x[i] + sc[D + i];
+            if (lane == 0) a.ldj[row] += a.pk[L.pk_ldc + k];  // ActNorm log|det J| (cnf.py:349)
+          }
+        } else {
+          if (k < L.nb - 1) {
+            // v = x Q_k^T (cnf.py:337-339): lane i computes v_i = sum_j x_j Q[i][j]
+            const float* Q = a.pk + L.pk_q + (long long)k * D * D;
+            float ci = 0.f;
+            const int li_ = lane < D ? lane : 0;
+#pragma unroll
+            for (int j = 0; j < DM; ++j)
+              if (j < D) ci = fmaf(x[j], Q[li_ * D + j], ci);
+#pragma unroll
+            for (int j = 0; j < DM; ++j)
+              if (j < D) x[j] = bcast(ci, j);
+            mine = 0.f;
+#pragma unroll
+            for (int i = 0; i < DM; ++i)
+              if (i == lane) mine = x[i];
+          }
+          if (lane < D) a.Xh[row * L.XP + lane] = mine;        // v, read back by this block's tail
+        }
+#pragma unroll
+        for (int i = 0; i < DM / 2; ++i) u[i] = i < Da ? x[i] : 0.f;
+        if (a.U && lane < L.UP) {
+          float uv = 0.f;
+#pragma unroll
+          for (int i = 0; i < DM / 2; ++i)
+            if (i == lane) uv = u[i];
+          a.U[row * L.UP + lane] = lane < Da ? uv : (lane == Da ? 1.f : 0.f);
+        }
+      }
+      const float* b0 = a.prm + wcb(L, k) + L.lin_b[0];
+      const long long prow = a.cidx ? a.cidx[row] : row;
+      const float* Pr = a.P + prow * a.ldP + (long long)k * HP;
+      const uint32_t tag = (uint32_t)k * 16u;
+      for (int q = lane; q < nq; q += 64) {
+        const int n = 4 * q;
+        floatx4 pre = ld4(Pr + n);
+#pragma unroll
+        for (int j = 0; j < DM / 2; ++j) {
+          if (j < Da) {
+            const floatx4 w = ld4(W0 + j * HP + n);
+            pre.x = fmaf(u[j], w.x, pre.x);
+            pre.y = fmaf(u[j], w.y, pre.y);
+            pre.z = fmaf(u[j], w.z, pre.z);
+            pre.w = fmaf(u[j], w.w, pre.w);
+          }
+        }
+        uint4 rnd = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+        if (a.rng) rnd = drop4(a.rng, seed, offs, row, n, tag);
+        float av[4], gv[4];
+        const float pv[4] = {pre.x, pre.y, pre.z, pre.w};
+        const uint32_t rv[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = n + e;
+          if (c < H) {
+            float ge, dg;
+            gelu_fg(pv[e] + b0[c], ge, dg);
+            const float m = a.rng ? (rv[e] >= L.thresh ? L.keep_scale : 0.f) : 1.f;
+            av[e] = ge * m;
+            gv[e] = dg * m;
+          } else {
+            av[e] = c == H ? 1.f : 0.f;
+            gv[e] = 0.f;
+          }
+        }
+        st4(a.A0 + row * HP + n, floatx4{av[0], av[1], av[2], av[3]});
+        if (a.G0) st4(a.G0 + row * HP + n, floatx4{gv[0], gv[1], gv[2], gv[3]});
+      }
+    }
+  }
+}
+
+// Backward links.
+//   head-B(k): dv = dX Q_k^T (k < nb-1) or dX = dz (last); coupling backward -> dO = [dt, ds'] (stored),
+//              du_b, dv_a (stored in DV); dZ_{NH-1} = (dO W_NH) * G_{NH-1} (stored).
+//   tail-B(k): du_a = dv_a + dZ_0 W0y; ActNorm backward (per-row partials of dscale, dbias) -> dX_k.
+// One launch = tail-B(kt) then head-B(kt - 1) (kt = -1: head-B(nb-1) only).
+struct LinkBArgs {
+  long long B;
+  int kt, kh;
+  const float* prm; const float* pk;
+  const float* X;  long long sX;      // saved block inputs, block k at X + k * sX
+  const float* S;  long long sS;      // saved tanh(s)
+  const float* dz; const float* dldj; // head-B(nb-1) input (dz nullable in NLL mode), dldj nullable
+  const float* zn; const float* dvals; int nll;   // NLL mode: dz = z g / B, dldj = -g / B, g = dvals[0] + dvals[1]
+  // tail-B(kt)
+  const float* dZ0; long long ldZ0;   // dZ_0 of block kt (row stride ldZ0)
+  float* DV;                          // [B][XP]: dv_a (Da) | du_b (Db)  (written by head-B, read by tail-B)
+  float* ANP;                         // [B][AP] ActNorm partials of block kt (du*x | du)
+  float* dy;                          // kt == 0: dL/dy (nullable)
+  // head-B(kh)
+  float* Ob;                          // [B][OP] dO of block kh
+  const float* Gl;                    // [B][HP] G_{NH-1} of block kh
+  float* dZl;  long long ldZl;        // dZ_{NH-1} of block kh
+};
+
+__global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const LinkBArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int HP = L.HP, H = L.H, D = L.D, Da = L.Da, Db = L.Db, O2 = 2 * Db;
+  float* W0 = sm;                                   // [Da][HP] W0y^T of block kt
+  float* Wl = sm + (a.kt >= 0 ? Da * HP : 0);       // [2Db][HP] last Linear of block kh
+  if (a.kt >= 0) {
+    const float* src = a.pk + L.pk_w0y + (long long)a.kt * Da * HP;
+    for (int e = tid; e < Da * HP / 4; e += WWG) st4(W0 + 4 * e, ld4(src + 4 * e));
+  }
+  if (a.kh >= 0) {
+    const float* src = a.pk + L.pk_wl + (long long)a.kh * O2 * HP;
+    for (int e = tid; e < O2 * HP / 4; e += WWG) st4(Wl + 4 * e, ld4(src + 4 * e));
+  }
+  __syncthreads();
+  const long long row0 = ((long long)blockIdx.x * 4 + wave) * LINK_ROWS;
+  if (row0 >= a.B) return;
+  const int nq = HP / 4;
+  float gscale = 1.f;
+  if (a.nll) gscale = (a.dvals ? a.dvals[0] + a.dvals[1] : 1.f) / (float)a.B;
+
+  for (int rr = 0; rr < LINK_ROWS; ++rr) {
+    const long long row = row0 + rr;
+    if (row >= a.B) break;
+    float dx[DM];
+    // ------------------------------------------------------------ tail-B of block kt
+    if (a.kt >= 0) {
+      const int k = a.kt;
+      float da[DM / 2];
+#pragma unroll
+      for (int j = 0; j < DM / 2; ++j) da[j] = 0.f;
+      const float* zr = a.dZ0 + row * a.ldZ0;
+      for (int q = lane; q < nq; q += 64) {
+        const floatx4 dzv = ld4(zr + 4 * q);
+#pragma unroll
+        for (int j = 0; j < DM / 2; ++j) {
+          if (j < Da) {
+            const floatx4 w = ld4(W0 + j * HP + 4 * q);
+            da[j] = fmaf(dzv.x, w.x, fmaf(dzv.y, w.y, fmaf(dzv.z, w.z, fmaf(dzv.w, w.w, da[j]))));
+          }
+        }
+      }
+      const float* dvr = a.DV + row * L.XP;
+#pragma unroll
+      for (int i = 0; i < DM; ++i) dx[i] = 0.f;
+#pragma unroll
+      for (int j = 0; j < DM / 2; ++j)
+        if (j < Da) dx[j] = wave_sum(da[j]) + dvr[j];
+#pragma unroll
+      for (int i = 0; i < DM / 2; ++i)
+        if (i < Db) dx[Da + i] = dvr[Da + i];
+      if (L.an && k < L.nb - 1) {
+        const float* sc = a.prm + (long long)k * L.blk_stride;
+        const float* xr = a.X + k * a.sX + row * L.XP;
+        float mine_s = 0.f, mine_b = 0.f;
+#pragma unroll
+        for (int i = 0; i < DM; ++i) {
+          if (i < D) {
+            if (i == lane) {
+              mine_s = dx[i] * xr[i];
+              mine_b = dx[i];
+            }
+            dx[i] *= sc[i];                                     // d x = d u * scale
+          }
+        }
+        if (lane < D) {
+          a.ANP[row * L.AP + lane] = mine_s;
+          a.ANP[row * L.AP + D + lane] = mine_b;
+        }
+      }
+      if (k == 0 && a.dy) {
+        float mine = 0.f;
+#pragma unroll
+        for (int i = 0; i < DM; ++i)
+          if (i == lane) mine = dx[i];
+        if (lane < D) a.dy[row * D + lane] = mine;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < DM; ++i) dx[i] = 0.f;
+      if (a.nll) {
+        const float* zr = a.zn + row * D;
+#pragma unroll
+        for (int i = 0; i < DM; ++i)
+          if (i < D) dx[i] = zr[i] * gscale;
+      } else if (a.dz) {
+        const float* zr = a.dz + row * D;
+#pragma unroll
+        for (int i = 0; i < DM; ++i)
+          if (i < D) dx[i] = zr[i];
+      }
+    }
+    // ------------------------------------------------------------ head-B of block kh
+    if (a.kh >= 0) {
+      const int k = a.kh;
+      if (k < L.nb - 1) {
+        const float* Q = a.pk + L.pk_q + (long long)k * D * D;
+        float ci = 0.f;
+        const int li_ = lane < D ? lane : 0;
+#pragma unroll
+        for (int j = 0; j < DM; ++j)
+          if (j < D) ci = fmaf(dx[j], Q[li_ * D + j], ci);
+#pragma unroll
+        for (int j = 0; j < DM; ++j)
+          if (j < D) dx[j] = bcast(ci, j);
+      }
+      float dl = a.nll ? -gscale : (a.dldj ? a.dldj[row] : 0.f);
+      const float* xr = a.X + k * a.sX + row * L.XP;
+      const float* sr = a.S + k * a.sS + row * L.SP;
+      const bool anb = L.an && k < L.nb - 1;
+      const float* sc = a.prm + (long long)k * L.blk_stride;
+      float dO[DM];
+#pragma unroll
+      for (int j = 0; j < DM; ++j) dO[j] = 0.f;
+      float dub[DM / 2];
+#pragma unroll
+      for (int i = 0; i < DM / 2; ++i) {
+        dub[i] = 0.f;
+        if (i < Db) {
+          float ub = xr[Da + i];
+          if (anb) ub = sc[Da + i] * ub + sc[D + Da + i];
+          const float s = sr[i];
+          const float es = exp_fast(s);
+          const float dvb = dx[Da + i];
+          dub[i] = dvb * es;
+          const float ds = fmaf(dvb * ub, es, dl);
+          dO[i] = dvb;                                   // dt
+          dO[Db + i] = ds * (1.f - s * s);               // d s' through tanh
+        }
+      }
+      {
+        float mo = 0.f, mv = 0.f;
+#pragma unroll
+        for (int j = 0; j < DM; ++j)
+          if (j == lane) mo = dO[j];
+#pragma unroll
+        for (int i = 0; i < DM / 2; ++i) {
+          if (i == lane && i < Da) mv = dx[i];
+          if (i < Db && lane == Da + i) mv = dub[i];
+        }
+        if (lane < L.OP) a.Ob[row * L.OP + lane] = lane < O2 ? mo : 0.f;
+        if (lane < L.XP) a.DV[row * L.XP + lane] = lane < D ? mv : 0.f;
+      }
+      const float* gr = a.Gl + row * HP;
+      float* out = a.dZl + row * a.ldZl;
+      for (int q = lane; q < nq; q += 64) {
+        const int n = 4 * q;
+        floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < DM; ++j) {
+          if (j < O2) {
+            const floatx4 w = ld4(Wl + j * HP + n);
+            s4.x = fmaf(dO[j], w.x, s4.x);
+            s4.y = fmaf(dO[j], w.y, s4.y);
+            s4.z = fmaf(dO[j], w.z, s4.z);
+            s4.w = fmaf(dO[j], w.w, s4.w);
+          }
+        }
+        const floatx4 gv = ld4(gr + n);
+        st4(out + n, floatx4{s4.x * gv.x, s4.y * gv.y, s4.z * gv.z, s4.w * gv.w});
+      }
+    }
+  }
+  (void)H;
+}
+
+// ActNorm gradients of every block: dscale_i = sum_b du_i x_i + (sum_b dldj_b) / scale_i  (the log|scale| term of
+// ActNorm.log_det_J, cnf.py:349), dbias_i = sum_b du_i. Fixed-order reduction, one workgroup per block.
+__global__ __launch_bounds__(WWG) void k_wactnorm_grad(const WideLayout L, const float* __restrict__ ANP, long long B,
+                                                       const float* __restrict__ dldj, const float* __restrict__ zn,
+                                                       const float* __restrict__ dvals, int nll,
+                                                       const float* __restrict__ prm, float* __restrict__ dprm) {
+  __shared__ float red[WWG];
+  __shared__ float dsum_s;
+  const int k = blockIdx.x, tid = threadIdx.x;
+  const int ncol = 2 * L.D;
+  const float* P = ANP + (long long)k * B * L.AP;
+  // sum of dldj over the batch
+  float acc = 0.f;
+  if (nll) {
+    if (tid == 0) acc = -(dvals ? dvals[0] + dvals[1] : 1.f);
+  } else if (dldj) {
+    for (long long r = tid; r < B; r += WWG) acc += dldj[r];
+  }
+  red[tid] = acc;
+  __syncthreads();
+  for (int w = WWG / 2; w > 0; w >>= 1) {
+    if (tid < w) red[tid] += red[tid + w];
+    __syncthreads();
+  }
+  if (tid == 0) dsum_s = red[0];
+  __syncthreads();
+  const float dsum = dsum_s;
+  // columns: 4 row phases x 64 columns
+  const int c = tid & 63, ph = tid >> 6;
+  float s = 0.f;
+  if (c < ncol)
+    for (long long r = ph; r < B; r += 4) s += P[r * L.AP + c];
+  __syncthreads();
+  red[tid] = s;
+  __syncthreads();
+  if (ph == 0 && c < ncol) {
+    float t = (red[c] + red[64 + c]) + (red[128 + c] + red[192 + c]);
+    const long long base = (long long)k * L.blk_stride;
+    if (c < L.D) t += dsum / prm[base + c];
+    dprm[base + c] = t;
+  }
+  (void)zn;
+}
+
+// Mean of the per-sample NLL terms -> [loss, nll, mse = 0] (trainer.py:260-266) plus the dropout RNG advance and
+// the divergence guard, exactly as bcnf_stack.hip's nll_finalize (include/bcnf_amd.h, BCNF_GUARD_*).
+__global__ __launch_bounds__(WWG) void k_wnll_finalize(const float* __restrict__ part, long long B, float* __restrict__ out,
+                                                       uint64_t* rng, int32_t* guard) {
+  __shared__ float red[WWG];
+  float acc = 0.f;
+  for (long long i = threadIdx.x; i < B; i += WWG) acc += part[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = WWG / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float nll = red[0] / (float)B;
+    out[0] = nll;
+    out[1] = nll;
+    out[2] = 0.f;
+    bool halt = false;
+    if (guard) {
+      if (guard[BCNF_GUARD_DIVERGED]) {
+        guard[BCNF_GUARD_HALTED] = 1;
+        halt = true;
+      } else if (guard[BCNF_GUARD_CHECK] && (nll > 1e5f || isnan(nll))) {
+        guard[BCNF_GUARD_DIVERGED] = 1;
+      }
+    }
+    if (rng && !halt) rng[1] += 1;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Host side
+// ------------------------------------------------------------------------------------------------
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+GemmArgs gemm_args(int M, int N, int K, const float* A, long long lda, const float* B, long long ldb, float* C,
+                   long long ldc) {
+  GemmArgs g;
+  memset(&g, 0, sizeof(g));
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.G0 = 1;
+  g.A = A;
+  g.lda = lda;
+  g.B = B;
+  g.ldb = ldb;
+  g.C = C;
+  g.ldc = ldc;
+  g.keep_scale = 1.f;
+  return g;
+}
+
+template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI>
+int launch_cfg(const GemmArgs& g, int groups, hipStream_t st) {
+  dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, groups);
+  hipLaunchKernelGGL((k_wgemm<BM, BN, BK, AKC, BKC, EPI>), grid, dim3(WWG), 0, st, g);
+  return bcnf_rt::launched();
+}
+
+// Tile choice: 128x128 when that still gives >= 2 workgroups per CU (256 CUs), else 64x64.
+template <bool AKC, bool BKC, int EPI>
+int gemm(const GemmArgs& g, int groups, hipStream_t st) {
+  if (g.M <= 0 || g.N <= 0 || groups <= 0) return BCNF_OK;
+  if ((g.lda & 3) || (g.ldb & 3) || (!aligned16(g.A)) || (!aligned16(g.B))) return BCNF_ERR_ARG;
+  if ((AKC || BKC) && (g.K & 3)) return BCNF_ERR_ARG;
+  const long long t128 = (long long)((g.M + 127) / 128) * ((g.N + 127) / 128) * groups;
+  if (t128 >= 512) return launch_cfg<128, 128, 16, AKC, BKC, EPI>(g, groups, st);
+  return launch_cfg<64, 64, 32, AKC, BKC, EPI>(g, groups, st);
+}
+
+struct WideWs {       // workspace carve-up (floats)
+  float *P, *A, *G, *dZ, *dZ0, *X, *S, *U, *O, *DV, *ANP, *nllp;
+  long long total;
+};
+
+WideWs carve(const WideLayout& L, long long B, bool train, float* base) {
+  WideWs w;
+  memset(&w, 0, sizeof(w));
+  long long o = 0;
+  auto take = [&](long long n) {
+    float* p = base ? base + o : nullptr;
+    o += pad4l(n) + 64;     // keep every region 16-B aligned (and apart)
+    return p;
+  };
+  const long long slab = B * L.HP;
+  w.P = take(B * (long long)L.nb * L.HP);
+  w.nllp = take(B);
+  if (train) {
+    w.A = take((long long)L.nb * L.NH * slab);
+    w.G = take((long long)L.nb * L.NH * slab);
+    w.dZ = take((long long)L.nb * (L.NH - 1) * slab);
+    w.dZ0 = take(B * (long long)L.nb * L.HP);
+    w.X = take((long long)(L.nb + 1) * B * L.XP);
+    w.S = take((long long)L.nb * B * L.SP);
+    w.U = take((long long)L.nb * B * L.UP);
+    w.O = take((long long)L.nb * B * L.OP);
+    w.DV = take(B * (long long)L.XP);
+    w.ANP = take((long long)L.nb * B * L.AP);
+  } else {
+    w.A = take(2 * slab);     // ping-pong
+    w.X = take(B * (long long)L.XP);
+  }
+  w.total = o;
+  return w;
+}
+
+size_t link_lds(const WideLayout& L, bool tail, bool head) {
+  return (size_t)((tail ? 2 * L.Db * L.HP : 0) + (head ? L.Da * L.HP : 0)) * sizeof(float);
+}
+
+int link_launch(const WideLayout& L, const LinkArgs& a, bool inv, hipStream_t st) {
+  const int rows_per_wg = 4 * LINK_ROWS;
+  dim3 grid((unsigned)((a.B + rows_per_wg - 1) / rows_per_wg));
+  const size_t lds = link_lds(L, a.kt >= 0, a.kh >= 0);
+  if (inv) hipLaunchKernelGGL(k_wlink<true>, grid, dim3(WWG), lds, st, L, a);
+  else hipLaunchKernelGGL(k_wlink<false>, grid, dim3(WWG), lds, st, L, a);
+  return bcnf_rt::launched();
+}
+
+int linkb_launch(const WideLayout& L, const LinkBArgs& a, hipStream_t st) {
+  const int rows_per_wg = 4 * LINK_ROWS;
+  dim3 grid((unsigned)((a.B + rows_per_wg - 1) / rows_per_wg));
+  const size_t lds = (size_t)((a.kt >= 0 ? L.Da * L.HP : 0) + (a.kh >= 0 ? 2 * L.Db * L.HP : 0)) * sizeof(float);
+  hipLaunchKernelGGL(k_wlink_bwd, grid, dim3(WWG), lds, st, L, a);
+  return bcnf_rt::launched();
+}
+
+bool lds_attr_done = false;
+void ensure_lds_attrs() {
+  if (lds_attr_done) return;
+  (void)hipFuncSetAttribute((const void*)k_wlink<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)k_wlink<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)k_wlink_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  lds_attr_done = true;
+}
+
+#define WCHK(x)            \
+  do {                     \
+    const int _rc = (x);   \
+    if (_rc) return _rc;   \
+  } while (0)
+
+// P = h W0h_all^T  (rows x nb*HP)
+int projection(const WideLayout& L, const float* pk, const float* h, long long rows, float* P, hipStream_t st) {
+  GemmArgs g = gemm_args((int)rows, L.nb * L.HP, L.C, h, L.C, pk + L.pk_w0h, L.C, P, (long long)L.nb * L.HP);
+  return gemm<true, true, EPI_STORE>(g, 1, st);
+}
+
+// hidden Linear l (1..NH-1) of block k: A_l = dropout(GELU(A_{l-1} W_l^T + b_l)), G_l
+int hidden_fwd(const WideLayout& L, const float* prm, const float* pk, int k, int l, long long B, const float* Ain,
+               float* Aout, float* Gout, const uint64_t* rng, hipStream_t st) {
+  GemmArgs g = gemm_args((int)B, L.HP, L.HP, Ain, L.HP, pk + L.pk_hid + ((long long)k * (L.NH - 1) + (l - 1)) * L.HP * L.HP,
+                         L.HP, Aout, L.HP);
+  g.bias = prm + wcb(L, k) + L.lin_b[l];
+  g.aux = Gout;
+  g.ldaux = L.HP;
+  g.n_real = L.H;
+  g.rng = rng;
+  g.thresh = L.thresh;
+  g.keep_scale = L.keep_scale;
+  g.tag = (uint32_t)k * 16u + (uint32_t)l;
+  return gemm<true, true, EPI_ACT>(g, 1, st);
+}
+
+int wide_forward(const WideLayout& L, const float* prm, const float* pk, const float* y, const float* h, long long B,
+                 float* z, float* ldj, bool training, const uint64_t* rng, float* ws, bool save, hipStream_t st) {
+  if (B == 0) return BCNF_OK;
+  ensure_lds_attrs();
+  const bool drop = training && L.p > 0.f && rng;
+  const WideWs w = carve(L, B, save, ws);
+  const long long slab = B * L.HP;
+  WCHK(projection(L, pk, h, B, w.P, st));
+  auto Aptr = [&](int k, int l) -> float* { return save ? w.A + ((long long)k * L.NH + l) * slab : w.A + (l & 1) * slab; };
+  auto Gptr = [&](int k, int l) -> float* { return save ? w.G + ((long long)k * L.NH + l) * slab : nullptr; };
+  for (int k = -1; k < L.nb; ++k) {
+    if (k >= 0)
+      for (int l = 1; l < L.NH; ++l)
+        WCHK(hidden_fwd(L, prm, pk, k, l, B, Aptr(k, l - 1), Aptr(k, l), Gptr(k, l), drop ? rng : nullptr, st));
+    LinkArgs a;
+    memset(&a, 0, sizeof(a));
+    a.B = B;
+    a.kt = k;
+    a.kh = (k + 1 < L.nb) ? k + 1 : -1;
+    a.prm = prm;
+    a.pk = pk;
+    if (k >= 0) {
+      a.Alast = Aptr(k, L.NH - 1);
+      a.Xt = save ? w.X + (long long)k * B * L.XP : w.X;
+      a.S = save ? w.S + (long long)k * B * L.SP : nullptr;
+    }
+    a.z = z;
+    a.ldj = ldj;
+    a.nllp = w.nllp;
+    a.xin = y;
+    if (a.kh >= 0) {
+      a.Xh = save ? w.X + (long long)a.kh * B * L.XP : w.X;
+      a.P = w.P;
+      a.ldP = (long long)L.nb * L.HP;
+      a.A0 = Aptr(a.kh, 0);
+      a.G0 = Gptr(a.kh, 0);
+      a.U = save ? w.U + (long long)a.kh * B * L.UP : nullptr;
+    }
+    a.rng = drop ? rng : nullptr;
+    WCHK(link_launch(L, a, false, st));
+  }
+  return BCNF_OK;
+}
+
+int wide_backward(const WideLayout& L, const float* prm, const float* pk, const float* h, const float* zn,
+                  const float* dz, const float* dldj, const float* dvals, int nll, long long B, float* ws, float* dy,
+                  float* dh, float* dprm, hipStream_t st) {
+  if (B == 0) return BCNF_OK;
+  ensure_lds_attrs();
+  const WideWs w = carve(L, B, true, ws);
+  const long long slab = B * L.HP;
+  const long long ld0 = (long long)L.nb * L.HP;
+  auto Aptr = [&](int k, int l) -> float* { return w.A + ((long long)k * L.NH + l) * slab; };
+  auto Gptr = [&](int k, int l) -> float* { return w.G + ((long long)k * L.NH + l) * slab; };
+  // dZ_l (l = 1..NH-1) of block k; dZ_0 of block k is the column slice k*HP of dZ0_all
+  auto dZptr = [&](int k, int l, long long* ld) -> float* {
+    if (l == 0) {
+      *ld = ld0;
+      return w.dZ0 + (long long)k * L.HP;
+    }
+    *ld = L.HP;
+    return w.dZ + ((long long)k * (L.NH - 1) + (l - 1)) * slab;
+  };
+  for (int k = L.nb; k >= 0; --k) {
+    // link: tail-B(k) (k < nb), head-B(k-1)
+    LinkBArgs a;
+    memset(&a, 0, sizeof(a));
+    a.B = B;
+    a.kt = (k < L.nb) ? k : -1;
+    a.kh = k - 1;
+    a.prm = prm;
+    a.pk = pk;
+    a.X = w.X;
+    a.sX = B * L.XP;
+    a.S = w.S;
+    a.sS = B * L.SP;
+    a.dz = dz;
+    a.dldj = dldj;
+    a.zn = zn;
+    a.dvals = dvals;
+    a.nll = nll;
+    a.DV = w.DV;
+    a.dy = dy;
+    if (a.kt >= 0) {
+      a.dZ0 = dZptr(k, 0, &a.ldZ0);
+      a.ANP = w.ANP + (long long)k * B * L.AP;
+    }
+    if (a.kh >= 0) {
+      a.Ob = w.O + (long long)a.kh * B * L.OP;
+      a.Gl = Gptr(a.kh, L.NH - 1);
+      a.dZl = dZptr(a.kh, L.NH - 1, &a.ldZl);
+    }
+    WCHK(linkb_launch(L, a, st));
+    if (a.kh < 0) break;
+    const int kb = a.kh;
+    // dZ_{l-1} = (dZ_l W_l) * G_{l-1}, l = NH-1 .. 1
+    for (int l = L.NH - 1; l >= 1; --l) {
+      long long ldi, ldo;
+      const float* din = dZptr(kb, l, &ldi);
+      float* dout = dZptr(kb, l - 1, &ldo);
+      GemmArgs g = gemm_args((int)B, L.HP, L.HP, din, ldi,
+                             pk + L.pk_hid + ((long long)kb * (L.NH - 1) + (l - 1)) * L.HP * L.HP, L.HP, dout, ldo);
+      g.aux = Gptr(kb, l - 1);
+      g.ldaux = L.HP;
+      WCHK((gemm<true, false, EPI_GRAD>(g, 1, st)));
+    }
+  }
+  // ---- parameter gradients (canonical flat, every element written exactly once) ----
+  if (dprm) {
+    if (L.NH > 1) {   // hidden Linears: [dW_l | db_l] = dZ_l^T [A_{l-1} | 1]
+      GemmArgs g = gemm_args(L.H, L.H + 1, (int)B, w.dZ, L.HP, w.A, L.HP, dprm, L.H);
+      g.G0 = L.NH - 1;
+      g.sA1 = (long long)(L.NH - 1) * slab;
+      g.sA0 = slab;
+      g.sB1 = (long long)L.NH * slab;
+      g.sB0 = slab;
+      g.use_cb = 1;
+      g.cb_stride = L.blk_stride;
+      g.cb_an = L.an;
+      g.cb_nb = L.nb;
+      g.C = dprm + L.lin_w[1];
+      g.sC0 = (L.NH > 2) ? (L.lin_w[2] - L.lin_w[1]) : 0;
+      g.wcols = L.H;
+      g.boff = (long long)L.H * L.H;
+      WCHK((gemm<false, false, EPI_LINGRAD>(g, L.nb * (L.NH - 1), st)));
+    }
+    {   // last Linear: [dW | db] = dO^T [A_{NH-1} | 1]
+      GemmArgs g = gemm_args(2 * L.Db, L.H + 1, (int)B, w.O, L.OP, w.A + (long long)(L.NH - 1) * slab, L.HP, dprm, L.H);
+      g.sA1 = B * L.OP;
+      g.sB1 = (long long)L.NH * slab;
+      g.use_cb = 1;
+      g.cb_stride = L.blk_stride;
+      g.cb_an = L.an;
+      g.cb_nb = L.nb;
+      g.C = dprm + L.lin_w[L.NH];
+      g.wcols = L.H;
+      g.boff = (long long)2 * L.Db * L.H;
+      WCHK((gemm<false, false, EPI_LINGRAD>(g, L.nb, st)));
+    }
+    {   // Linear-1, y columns + bias: [dW0[:, :Da] | db0] = dZ_0^T [u_a | 1]
+      GemmArgs g = gemm_args(L.H, L.Da + 1, (int)B, w.dZ0, ld0, w.U, L.UP, dprm, L.in0);
+      g.sA1 = L.HP;
+      g.sB1 = B * L.UP;
+      g.use_cb = 1;
+      g.cb_stride = L.blk_stride;
+      g.cb_an = L.an;
+      g.cb_nb = L.nb;
+      g.C = dprm + L.lin_w[0];
+      g.wcols = L.Da;
+      g.boff = (long long)L.H * L.in0;
+      WCHK((gemm<false, false, EPI_LINGRAD>(g, L.nb, st)));
+    }
+    {   // Linear-1, condition columns of every block in one GEMM: dW0h_all = dZ0_all^T h
+      GemmArgs g = gemm_args(L.nb * L.HP, L.C, (int)B, w.dZ0, ld0, h, L.C, dprm, L.in0);
+      g.cb_stride = L.blk_stride;
+      g.cb_an = L.an;
+      g.cb_nb = L.nb;
+      g.rm_hp = L.HP;
+      g.rm_h = L.H;
+      g.rm_off = L.lin_w[0] + L.Da;
+      WCHK((gemm<false, false, EPI_ROWMAP>(g, 1, st)));
+    }
+    if (L.an && L.nb > 1) {
+      hipLaunchKernelGGL(k_wactnorm_grad, dim3(L.nb - 1), dim3(WWG), 0, st, L, w.ANP, B, dldj, zn, dvals, nll, prm, dprm);
+      WCHK(bcnf_rt::launched());
+    }
+  }
+  if (dh) {   // dh = dZ0_all W0h_all
+    GemmArgs g = gemm_args((int)B, L.C, L.nb * L.HP, w.dZ0, ld0, pk + L.pk_w0h, L.C, dh, L.C);
+    WCHK((gemm<true, false, EPI_STORE>(g, 1, st)));
+  }
+  return BCNF_OK;
+}
+
+int wide_inverse(const WideLayout& L, const float* prm, const float* pk, const float* z, const float* h, long long hrows,
+                 const int64_t* cidx, long long n, float* y, bool training, const uint64_t* rng, float* scratch,
+                 hipStream_t st) {
+  if (n == 0) return BCNF_OK;
+  ensure_lds_attrs();
+  const bool drop = training && L.p > 0.f && rng;
+  // scratch: P (hrows x nb*HP) | A ping-pong (2 x n x HP) | X (n x XP)
+  float* P = scratch;
+  float* A = P + pad4l(hrows * (long long)L.nb * L.HP) + 64;
+  float* X = A + pad4l(2 * n * (long long)L.HP) + 64;
+  const long long slab = n * L.HP;
+  WCHK(projection(L, pk, h, hrows, P, st));
+  auto Ap = [&](int l) { return A + (l & 1) * slab; };
+  // blocks in reverse (cnf.py:499-506)
+  for (int k = L.nb; k >= 0; --k) {
+    if (k < L.nb)
+      for (int l = 1; l < L.NH; ++l)
+        WCHK(hidden_fwd(L, prm, pk, k, l, n, Ap(l - 1), Ap(l), nullptr, drop ? rng : nullptr, st));
+    LinkArgs a;
+    memset(&a, 0, sizeof(a));
+    a.B = n;
+    a.kt = (k < L.nb) ? k : -1;
+    a.kh = k - 1;
+    a.prm = prm;
+    a.pk = pk;
+    a.Alast = Ap(L.NH - 1);
+    a.Xt = X;
+    a.z = y;
+    a.xin = z;
+    a.Xh = X;
+    a.P = P;
+    a.ldP = (long long)L.nb * L.HP;
+    a.cidx = cidx;
+    a.A0 = Ap(0);
+    a.rng = drop ? rng : nullptr;
+    WCHK(link_launch(L, a, true, st));
+  }
+  return BCNF_OK;
+}
+
+}  // namespace
+
+// ================================================================================================
+// C-ABI (include/bcnf_amd.h)
+// ================================================================================================
+extern "C" {
+
+int bcnf_wide_supported(const BcnfStackDesc* desc) {
+  WideLayout L;
+  return wide_layout(desc, &L) == BCNF_OK ? 1 : 0;
+}
+
+int bcnf_wide_packed_bytes(const BcnfStackDesc* desc, int64_t* bytes) {
+  WideLayout L;
+  WCHK(wide_layout(desc, &L));
+  if (!bytes) return BCNF_ERR_ARG;
+  *bytes = L.total * 4;
+  return BCNF_OK;
+}
+
+int bcnf_wide_workspace_bytes(const BcnfStackDesc* desc, int64_t batch, int32_t save, int64_t* bytes) {
+  WideLayout L;
+  WCHK(wide_layout(desc, &L));
+  if (!bytes || batch < 0) return BCNF_ERR_ARG;
+  *bytes = carve(L, batch, save != 0, nullptr).total * 4;
+  return BCNF_OK;
+}
+
+int bcnf_wide_inverse_scratch_bytes(const BcnfStackDesc* desc, int64_t h_rows, int64_t n_rows, int64_t* bytes) {
+  WideLayout L;
+  WCHK(wide_layout(desc, &L));
+  if (!bytes || h_rows < 0 || n_rows < 0) return BCNF_ERR_ARG;
+  *bytes = (pad4l(h_rows * (long long)L.nb * L.HP) + 64 + pad4l(2 * n_rows * (long long)L.HP) + 64 +
+            n_rows * (long long)L.XP + 64) * 4;
+  return BCNF_OK;
+}
+
+int bcnf_wide_pack(const BcnfStackDesc* desc, const float* params, const float* qmats, void* packed, void* stream) {
+  WideLayout L;
+  WCHK(wide_layout(desc, &L));
+  if (!params || !packed || (L.nb > 1 && !qmats) || !aligned16(packed)) return BCNF_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const long long n = L.pk_ldc;
+  const int grid = (int)std::min<long long>((n + WWG - 1) / WWG, 4096);
+  hipLaunchKernelGGL(k_wpack, dim3(grid), dim3(WWG), 0, st, L, params, qmats, (float*)packed);
+  WCHK(bcnf_rt::launched());
+  hipLaunchKernelGGL(k_wpack_ldc, dim3(1), dim3(((L.nb + 63) / 64) * 64), 0, st, L, params, (float*)packed);
+  return bcnf_rt::launched();
+}
+
+int bcnf_wide_forward(const BcnfStackDesc* desc, const float* params, const void* packed, const float* y,
+                      const float* h, int64_t batch, float* z, float* ldj, float* nll_part, int32_t training,
+                      const uint64_t* rng_state, void* workspace, int32_t save, void* stream) {
+  WideLayout L;
+  WCHK(wide_layout(desc, &L));
+  if (batch < 0) return BCNF_ERR_ARG;
+  if (batch == 0) return BCNF_OK;
+  if (!params || !packed || !y || !h || !z || !ldj || !workspace || !aligned16(h) || !aligned16(workspace))
+    return BCNF_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  WCHK(wide_forward(L, params, (const float*)packed, y, h, batch, z, ldj, training != 0, rng_state, (float*)workspace,
+                    save != 0, st));
+  if (nll_part) {
+    const WideWs w = carve(L, batch, save != 0, (float*)workspace);
+    if (hipMemcpyAsync(nll_part, w.nllp, batch * sizeof(float), hipMemcpyDeviceToDevice, st) != hipSuccess)
+      return bcnf_rt::launched() ? BCNF_ERR_HIP : BCNF_ERR_HIP;
+  }
+  return BCNF_OK;
+}
+
+int bcnf_wide_nll_finalize(const BcnfStackDesc* desc, const void* workspace, int64_t batch, int32_t save,
+                           float* loss_out, uint64_t* rng_state, int32_t* guard, void* stream) {
+  WideLayout L;
+  WCHK(wide_layout(desc, &L));
+  if (batch <= 0 || !workspace || !loss_out) return BCNF_ERR_ARG;
+  const WideWs w = carve(L, batch, save != 0, (float*)workspace);
+  hipLaunchKernelGGL(k_wnll_finalize, dim3(1), dim3(WWG), 0, (hipStream_t)stream, w.nllp, (long long)batch, loss_out,
+                     rng_state, guard);
+  return bcnf_rt::launched();
+}
+
+int bcnf_wide_backward(const BcnfStackDesc* desc, const float* params, const void* packed, const float* h,
+                       const float* z, const float* dz, const float* dldj, const float* dloss, int32_t nll,
+                       int64_t batch, void* workspace, float* dy, float* dh, float* dparams, void* stream) {
+  WideLayout L;
+  WCHK(wide_layout(desc, &L));
+  if (batch < 0) return BCNF_ERR_ARG;
+  if (!params || !packed || !h || !workspace || (nll && !z)) return BCNF_ERR_ARG;
+  if (batch == 0) {
+    if (dparams) (void)hipMemsetAsync(dparams, 0, L.n_trainable * 4, (hipStream_t)stream);
+    return BCNF_OK;
+  }
+  return wide_backward(L, params, (const float*)packed, h, z, dz, dldj, dloss, nll, batch, (float*)workspace, dy, dh,
+                       dparams, (hipStream_t)stream);
+}
+
+int bcnf_wide_inverse(const BcnfStackDesc* desc, const float* params, const void* packed, const float* z,
+                      const float* h, int64_t h_rows, const int64_t* cond_index, int64_t n_rows, float* y,
+                      int32_t training, const uint64_t* rng_state, void* scratch, void* stream) {
+  WideLayout L;
+  WCHK(wide_layout(desc, &L));
+  if (n_rows < 0 || h_rows < 0) return BCNF_ERR_ARG;
+  if (n_rows == 0) return BCNF_OK;
+  if (!params || !packed || !z || !h || !y || !scratch || !aligned16(h) || !aligned16(scratch)) return BCNF_ERR_ARG;
+  if (!cond_index && h_rows != n_rows) return BCNF_ERR_ARG;
+  return wide_inverse(L, params, (const float*)packed, z, h, h_rows, cond_index, n_rows, y, training != 0, rng_state,
+                      (float*)scratch, (hipStream_t)stream);
+}
+
+// Test hook: one plain GEMM through the tile machinery. layout: 0 = NT (A[m][k], B[n][k]), 1 = NN (A[m][k], B[k][n]),
+// 2 = TN (A[k][m], B[k][n]).
+int bcnf_wide_gemm_test(int32_t layout, int32_t M, int32_t N, int32_t K, const float* A, int64_t lda, const float* B,
+                        int64_t ldb, float* C, int64_t ldc, void* stream) {
+  GemmArgs g = gemm_args(M, N, K, A, lda, B, ldb, C, ldc);
+  hipStream_t st = (hipStream_t)stream;
+  if (layout == 0) return gemm<true, true, EPI_STORE>(g, 1, st);
+  if (layout == 1) return gemm<true, false, EPI_STORE>(g, 1, st);
+  if (layout == 2) return gemm<false, false, EPI_STORE>(g, 1, st);
+  return BCNF_ERR_ARG;
+}
+
+}  // extern "C"

@@ -1,0 +1,210 @@
+"""Host runtime of the wide-MLP coupling stack (trajectory_FC_large / trajectory_LSTM_large class).
+
+Same contract as `FusedStack` (bcnf_amd/fused.py): one flat fp32 buffer of the trainable coupling parameters in
+state_dict order with every nn.Parameter a view into it, the frozen orthonormal matrices in a second buffer, the
+same autograd Functions (`_StackForward`, `_StackNLL`, `_StackInverse`) and the same launch_* methods, so
+CondRealNVP_v2, TrainStep and the optimizer do not know which family runs. The arithmetic is in
+libbcnf_amd.so (bcnf_amd/csrc/bcnf_wide.hip): fp32-MFMA GEMMs with fused bias/GELU/dropout/gradient epilogues
+and per-sample link kernels; the condition projection h W0h^T of all blocks is one GEMM per pass.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from bcnf_amd import _native as N
+from bcnf_amd.fused import FusedStack
+
+_LOG2PI = math.log(2.0 * math.pi)
+
+
+class WideStack(FusedStack):
+    """Owns the flat parameter buffers of one wide-MLP coupling stack and drives the wide HIP kernels."""
+
+    @property
+    def supported(self) -> bool:
+        return bool(N.lib().bcnf_wide_supported(self._pdesc))
+
+    def _pack_into(self, out):
+        N.check(N.lib().bcnf_wide_pack(self._pdesc, N.ptr(self.flat), N.ptr(self.qflat), N.ptr(out),
+                                       N.stream_handle(self.flat.device)), "bcnf_wide_pack")
+
+    def packed(self, fresh: bool = False):
+        """Padded weight copies (bcnf_wide_pack). Re-packed on every call unless inside reuse_pack(); with
+        fresh=True a private copy that a later forward cannot overwrite before this one's backward runs."""
+        nbytes = N.query_i64(N.lib().bcnf_wide_packed_bytes, self._pdesc)
+        if fresh and not self._pack_frozen:
+            out = torch.empty(nbytes // 4, dtype=torch.float32, device=self.flat.device)
+            self._pack_into(out)
+            return out
+        if self._packed is None:
+            self._packed = torch.empty(nbytes // 4, dtype=torch.float32, device=self.flat.device)
+        if not self._pack_frozen:
+            self._pack_into(self._packed)
+        return self._packed
+
+    def workspace_bytes(self, batch: int, save: bool):
+        return N.query_i64(N.lib().bcnf_wide_workspace_bytes, self._pdesc, ctypes.c_int64(batch),
+                           ctypes.c_int32(int(save))), 0
+
+    def _workspace(self, batch, save, dev):
+        wb, _ = self.workspace_bytes(batch, save)
+        return torch.empty(max(wb // 4, 1), dtype=torch.float32, device=dev)
+
+    def _timed(self, name, fn):
+        tm = self.timers
+        if tm is None:
+            return fn()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = fn()
+        e1.record()
+        tm.setdefault(name, []).append((e0, e1))
+        return out
+
+    # ------------------------------------------------------------------ launches
+    def _forward(self, y, h, training, save, nll_part=None):
+        self._check_inputs(y, h, "forward")
+        if h.shape[0] != y.shape[0]:
+            raise ValueError(f"bcnf_amd forward: {y.shape[0]} samples but {h.shape[0]} feature rows")
+        B = y.shape[0]
+        dev = y.device
+        z = torch.empty_like(y)
+        ldj = torch.empty(B, dtype=torch.float32, device=dev)
+        drop = training and self.cfg.dropout > 0.0
+        rng = self.rng_state() if drop else None
+        ws = self._workspace(B, save, dev)
+        pk = self.packed(fresh=save)
+        rc = self._timed("k_forward", lambda: N.lib().bcnf_wide_forward(
+            self._pdesc, N.ptr(self.flat), N.ptr(pk), N.ptr(y), N.ptr(h), ctypes.c_int64(B), N.ptr(z), N.ptr(ldj),
+            N.ptr(nll_part), ctypes.c_int32(int(training)), N.ptr(rng), N.ptr(ws), ctypes.c_int32(int(save)),
+            N.stream_handle(dev)))
+        N.check(rc, "bcnf_wide_forward")
+        return z, ldj, rng, (ws, pk)
+
+    def launch_forward(self, y, h, training: bool, save: bool, want_logp: bool = False):
+        B = y.shape[0]
+        part = torch.empty(B, dtype=torch.float32, device=y.device) if want_logp else None
+        z, ldj, rng, saved = self._forward(y, h, training, save, part)
+        if rng is not None:
+            rng[1:2].add_(1)
+        logp = None
+        if want_logp:
+            logp = -part - 0.5 * self.cfg.size * _LOG2PI
+        return z, ldj, logp, saved
+
+    def launch_backward(self, h, dz, dldj, training: bool, saved, want_dy: bool, want_dh: bool):
+        return self._backward(h, None, dz, dldj, None, False, saved, want_dy, want_dh)
+
+    def _backward(self, h, z, dz, dldj, dvals, nll, saved, want_dy, want_dh):
+        ws, pk = saved
+        B = h.shape[0]
+        dev = h.device
+        dparams = torch.empty_like(self.flat)
+        dh = torch.empty_like(h) if want_dh else None
+        dy = torch.empty((B, self.cfg.size), dtype=torch.float32, device=dev) if want_dy else None
+        rc = self._timed("k_backward", lambda: N.lib().bcnf_wide_backward(
+            self._pdesc, N.ptr(self.flat), N.ptr(pk), N.ptr(h), N.ptr(z), N.ptr(dz), N.ptr(dldj), N.ptr(dvals),
+            ctypes.c_int32(int(nll)), ctypes.c_int64(B), N.ptr(ws), N.ptr(dy), N.ptr(dh), N.ptr(dparams),
+            N.stream_handle(dev)))
+        N.check(rc, "bcnf_wide_backward")
+        return dy, dh, dparams
+
+    def _finalize(self, ws, B, vals, training, save=True):
+        drop = training and self.cfg.dropout > 0.0
+        rng = self.rng_state() if drop else None
+        N.check(N.lib().bcnf_wide_nll_finalize(self._pdesc, N.ptr(ws), ctypes.c_int64(B), ctypes.c_int32(int(save)),
+                                               N.ptr(vals), N.ptr(rng), N.ptr(self.guard),
+                                               N.stream_handle(vals.device)), "bcnf_wide_nll_finalize")
+
+    def launch_nll_forward(self, y, h, training: bool, finalize: bool = True):
+        B = y.shape[0]
+        if B == 0:
+            raise ValueError("bcnf_amd: the NLL of an empty batch is undefined")
+        z, ldj, _, saved = self._forward(y, h, training, True)
+        vals = torch.empty(3, dtype=torch.float32, device=y.device)
+        if finalize:
+            self._finalize(saved[0], B, vals, training)
+        return z, ldj, vals, saved
+
+    def launch_nll_backward(self, h, z, dvals, training: bool, saved, want_dy: bool, want_dh: bool,
+                            finalize_into=None):
+        if finalize_into is not None:
+            self._finalize(saved[0], h.shape[0], finalize_into, training)
+        return self._backward(h, z, None, None, dvals, True, saved, want_dy, want_dh)
+
+    @torch.no_grad()
+    def time_kernels(self, y, h, training: bool = True, iters: int = 20):
+        """Average device time (us) of the wide forward (save on) and backward launches, HIP events on the launch
+        stream around `iters` back-to-back calls."""
+        L = N.lib()
+        dev = y.device
+        stream = N.stream_handle(dev)
+        B = y.shape[0]
+        z, _, vals, (ws, pk) = self.launch_nll_forward(y, h, training, finalize=False)
+        ldj = torch.empty(B, dtype=torch.float32, device=dev)
+        dparams = torch.empty_like(self.flat)
+        dh = torch.empty_like(h)
+        rng = self.rng_state() if (training and self.cfg.dropout > 0.0) else None
+        calls = {
+            "forward": lambda: L.bcnf_wide_forward(self._pdesc, N.ptr(self.flat), N.ptr(pk), N.ptr(y), N.ptr(h),
+                                                   ctypes.c_int64(B), N.ptr(z), N.ptr(ldj), None,
+                                                   ctypes.c_int32(int(training)), N.ptr(rng), N.ptr(ws),
+                                                   ctypes.c_int32(1), stream),
+            "backward": lambda: L.bcnf_wide_backward(self._pdesc, N.ptr(self.flat), N.ptr(pk), N.ptr(h), N.ptr(z),
+                                                     None, None, None, ctypes.c_int32(1), ctypes.c_int64(B),
+                                                     N.ptr(ws), None, N.ptr(dh), N.ptr(dparams), stream),
+        }
+        out = {}
+        for name, fn in calls.items():
+            N.check(fn(), name)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(iters):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            out[name] = e0.elapsed_time(e1) * 1e3 / iters
+        return out
+
+    def launch_inverse(self, z, h, cond_index=None, training: bool = False):
+        self._check_inputs(z, h, "inverse")
+        n = z.shape[0]
+        if cond_index is None and h.shape[0] != n:
+            raise ValueError(f"bcnf_amd inverse: {n} latents but {h.shape[0]} feature rows and no cond_index")
+        y = torch.empty_like(z)
+        drop = training and self.cfg.dropout > 0.0
+        rng = self.rng_state() if drop else None
+        if cond_index is not None:
+            cond_index = cond_index.to(device=z.device, dtype=torch.int64).contiguous()
+        hr = h.shape[0]
+        sb = N.query_i64(N.lib().bcnf_wide_inverse_scratch_bytes, self._pdesc, ctypes.c_int64(hr), ctypes.c_int64(n))
+        scratch = torch.empty(max(sb // 4, 1), dtype=torch.float32, device=z.device)
+        rc = N.lib().bcnf_wide_inverse(self._pdesc, N.ptr(self.flat), N.ptr(self.packed()), N.ptr(z), N.ptr(h),
+                                       ctypes.c_int64(hr), N.ptr(cond_index), ctypes.c_int64(n), N.ptr(y),
+                                       ctypes.c_int32(int(training)), N.ptr(rng), N.ptr(scratch),
+                                       N.stream_handle(z.device))
+        N.check(rc, "bcnf_wide_inverse")
+        if drop:
+            rng[1:2].add_(1)
+        return y
+
+
+def make_stack(cfg, trainable, frozen, bind: bool = True) -> FusedStack:
+    """The register-resident small family when the shape fits it (FC_small), else the wide-MLP family."""
+    st = FusedStack(cfg, trainable, frozen, bind=False)
+    if not st.supported:
+        wd = WideStack(cfg, trainable, frozen, bind=False)
+        if wd.supported:
+            st = wd
+    if bind:
+        st.bind = True
+        st.flatten()
+    return st
+
+
+__all__ = ["WideStack", "make_stack"]

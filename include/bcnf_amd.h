@@ -218,6 +218,46 @@ int64_t bcnf_linear_work_bytes(int64_t rows, int32_t in_features, int32_t out_fe
 int bcnf_linear_backward(const float* x, const float* weight, const float* dy, int64_t rows, int32_t in_features,
                          int32_t out_features, float* dx, float* dweight, float* dbias, void* work, void* stream);
 
+/* ---- Wide-MLP family (trajectory_FC_large / trajectory_LSTM_large class: nested_sizes = [H] * NH with H too
+ * wide for the register-resident kernels above, e.g. [526] * 5, C = 1360, 26 blocks) ----------------------------
+ * Same BcnfStackDesc, same canonical flat parameter layout (state_dict order) and the same reference interfaces
+ * as bcnf_stack_forward / _backward / _inverse / bcnf_nll_* above (cnf.py:49-107, 165-213, 312-354, 467-508;
+ * utils.py:40-53; trainer.py:260-268), built from fp32-MFMA GEMMs (v_mfma_f32_32x32x2_f32) with fused
+ * bias / GELU / dropout / gradient epilogues and per-sample link kernels (coupling, log|det J|, orthonormal mix,
+ * ActNorm). Requirements: equal nested sizes, n_conditions % 4 == 0, size <= 32, two_way == 0.
+ * The wide family takes the canonical flat params directly plus its own packed buffer (padded weight copies,
+ * bcnf_wide_pack after every parameter update). */
+int bcnf_wide_supported(const BcnfStackDesc* desc);
+int bcnf_wide_packed_bytes(const BcnfStackDesc* desc, int64_t* bytes);
+/* save != 0: the forward keeps every activation, GELU-derivative factor and block input for the backward. */
+int bcnf_wide_workspace_bytes(const BcnfStackDesc* desc, int64_t batch, int32_t save, int64_t* bytes);
+int bcnf_wide_inverse_scratch_bytes(const BcnfStackDesc* desc, int64_t h_rows, int64_t n_rows, int64_t* bytes);
+int bcnf_wide_pack(const BcnfStackDesc* desc, const float* params, const float* qmats, void* packed, void* stream);
+/* z (B x D), ldj (B); nll_part (nullable) receives 0.5 |z_b|^2 - ldj_b per sample (the per-sample inn_nll_loss,
+ * utils.py:49-53 with reduction 'none'). Dropout as bcnf_stack_forward (device rng_state; the caller advances the
+ * offset, or bcnf_wide_nll_finalize does). */
+int bcnf_wide_forward(const BcnfStackDesc* desc, const float* params, const void* packed, const float* y,
+                      const float* h, int64_t batch, float* z, float* ldj, float* nll_part, int32_t training,
+                      const uint64_t* rng_state, void* workspace, int32_t save, void* stream);
+/* loss_out[0..2] = [loss, nll, mse = 0] from the forward's per-sample NLL terms (workspace of that forward), plus
+ * the dropout RNG advance and the divergence guard, as bcnf_nll_forward's finalize. */
+int bcnf_wide_nll_finalize(const BcnfStackDesc* desc, const void* workspace, int64_t batch, int32_t save,
+                           float* loss_out, uint64_t* rng_state, int32_t* guard, void* stream);
+/* Backward of a save != 0 forward. nll == 0: cotangents dz (B x D) / dldj (B), either nullable. nll != 0: through
+ * the NLL, dz = z g / B and dldj = -g / B with g = dloss[0] + dloss[1] (dloss nullable = 1), z = the forward's
+ * output. Writes dy, dh (nullable) and dparams (canonical flat, every element overwritten; nullable). */
+int bcnf_wide_backward(const BcnfStackDesc* desc, const float* params, const void* packed, const float* h,
+                       const float* z, const float* dz, const float* dldj, const float* dloss, int32_t nll,
+                       int64_t batch, void* workspace, float* dy, float* dh, float* dparams, void* stream);
+/* Inverse: as bcnf_stack_inverse (cond_index selects feature rows; scratch = bcnf_wide_inverse_scratch_bytes). */
+int bcnf_wide_inverse(const BcnfStackDesc* desc, const float* params, const void* packed, const float* z,
+                      const float* h, int64_t h_rows, const int64_t* cond_index, int64_t n_rows, float* y,
+                      int32_t training, const uint64_t* rng_state, void* scratch, void* stream);
+/* Test hook for the GEMM tiles: C (M x N) = A B with layout 0 = A[m][k] B[n][k], 1 = A[m][k] B[k][n],
+ * 2 = A[k][m] B[k][n]; leading dimensions and K multiples of 4, 16-byte aligned bases. */
+int bcnf_wide_gemm_test(int32_t layout, int32_t M, int32_t N, int32_t K, const float* A, int64_t lda, const float* B,
+                        int64_t ldb, float* C, int64_t ldc, void* stream);
+
 const char* bcnf_status_string(int status);
 int bcnf_last_hip_error(void);
 

@@ -1,0 +1,363 @@
+"""GPU parity of the wide-MLP coupling family (trajectory_FC_large / trajectory_LSTM_large class, bcnf_wide.hip)
+against the reference's own outputs (fixture g7: FC_large-shaped proxy, C = 1360, nested_sizes = [526] * 5, made by
+running psaegert/bcnf, tests/golden/make_golden.py) and against the CPU oracle (oracle/cnf_oracle.py).
+
+Tolerances as tests/test_gpu_parity.py: values |got - ref| <= 1e-5 |ref| + 1e-5 max(1, max|ref|); gradients
+1e-4 (fp64 oracle as the reference there, since fp32 rounding of a 1,370-term sum is itself ~1e-6 relative).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import close, load_golden
+from oracle import cnf_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+SEED = 2024_03_25
+
+
+def _lib():
+    from bcnf_amd import _native as N
+    return N
+
+
+# ------------------------------------------------------------------------------------------ GEMM tiles
+@pytest.mark.parametrize("layout", [0, 1, 2])
+@pytest.mark.parametrize("mnk", [(64, 64, 32), (100, 70, 36), (2048, 528, 528), (18, 527, 300), (4096, 4096, 64),
+                                 (3, 5, 4)])
+def test_wide_gemm_layouts_vs_fp64(layout, mnk):
+    """C = A B through the MFMA tile machinery (both tile configs, ragged M / N / K tails) vs fp64."""
+    import ctypes
+    N = _lib()
+    M, Nn, K = mnk
+    g = torch.Generator().manual_seed(M * 7 + Nn + K + layout)
+    A = torch.randn(M, K, generator=g, dtype=torch.float64)
+    B = torch.randn(K, Nn, generator=g, dtype=torch.float64)
+    ref = A @ B
+    pad = lambda n: (n + 3) // 4 * 4  # noqa: E731
+    if layout == 0:      # A[m][k], B[n][k]
+        Ad = torch.zeros(M, pad(K), dtype=torch.float32)
+        Ad[:, :K] = A.float()
+        Bd = torch.zeros(Nn, pad(K), dtype=torch.float32)
+        Bd[:, :K] = B.t().float()
+    elif layout == 1:    # A[m][k], B[k][n]
+        Ad = torch.zeros(M, pad(K), dtype=torch.float32)
+        Ad[:, :K] = A.float()
+        Bd = torch.zeros(K, pad(Nn), dtype=torch.float32)
+        Bd[:, :Nn] = B.float()
+    else:                # A[k][m], B[k][n]
+        Ad = torch.zeros(K, pad(M), dtype=torch.float32)
+        Ad[:, :M] = A.t().float()
+        Bd = torch.zeros(K, pad(Nn), dtype=torch.float32)
+        Bd[:, :Nn] = B.float()
+    Ad, Bd = Ad.to(DEV), Bd.to(DEV)
+    C = torch.full((M, pad(Nn)), float("nan"), device=DEV)
+    Kp = pad(K) if layout != 2 else K
+    rc = N.lib().bcnf_wide_gemm_test(layout, M, Nn, Kp, N.ptr(Ad), Ad.shape[1], N.ptr(Bd), Bd.shape[1], N.ptr(C),
+                                     C.shape[1], N.stream_handle(C.device))
+    N.check(rc, "bcnf_wide_gemm_test")
+    torch.cuda.synchronize()
+    got = C[:, :Nn].double().cpu()
+    tol = 2e-6 * (A.abs() @ B.abs()) + 1e-6
+    assert bool(((got - ref).abs() <= tol).all()), float((got - ref).abs().max())
+    assert torch.isnan(C[:, Nn:]).all() or Nn == C.shape[1]      # nothing written past N
+
+
+# ------------------------------------------------------------------------------------------ model builders
+def _model(shape, seed=7, fsizes=None):
+    from bcnf_amd import CondRealNVP_v2
+    C = shape["n_conditions"]
+    torch.manual_seed(seed)
+    if fsizes is None:
+        fnets = [{"type": "ConcatenateCondition", "kwargs": {"input_size": None, "output_size": C}}]
+    else:
+        fnets = [{"type": "ConcatenateCondition", "kwargs": {"input_size": None, "output_size": fsizes[0]}},
+                 {"type": "FullyConnected", "kwargs": {"sizes": fsizes, "dropout": 0.0}}]
+    cfg = {"global": {"parameter_selection": [f"p{i}" for i in range(shape["size"])]},
+           "model": {"kwargs": shape}, "feature_networks": fnets}
+    m = CondRealNVP_v2.from_config(cfg)
+    assert type(m.fused).__name__ == "WideStack"
+    return m
+
+
+def _perturb(m):
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if n.endswith("scale"):
+                p.copy_(0.5 + torch.rand_like(p))
+            elif n.endswith("bias") and n.count(".") == 2:
+                p.copy_(0.1 * torch.randn_like(p))
+
+
+def _spec(shape, fsizes=()):
+    return O.StackSpec(size=shape["size"], nested_sizes=shape["nested_sizes"], n_blocks=shape["n_blocks"],
+                       n_conditions=shape["n_conditions"], dropout=shape["dropout"], act_norm=shape["act_norm"],
+                       feature_sizes=list(fsizes))
+
+
+WIDE_SHAPES = [
+    dict(size=19, nested_sizes=[40] * 3, n_blocks=3, n_conditions=24, dropout=0.2, act_norm=True),
+    dict(size=7, nested_sizes=[33] * 2, n_blocks=2, n_conditions=8, dropout=0.0, act_norm=False),
+    dict(size=19, nested_sizes=[20], n_blocks=3, n_conditions=4, dropout=0.1, act_norm=True),      # one hidden layer
+    dict(size=32, nested_sizes=[64] * 4, n_blocks=2, n_conditions=300, dropout=0.0, act_norm=True),
+    dict(size=19, nested_sizes=[526] * 5, n_blocks=2, n_conditions=1360, dropout=0.407, act_norm=True),  # FC_large
+]
+
+
+@pytest.mark.parametrize("shape", WIDE_SHAPES)
+@pytest.mark.parametrize("B", [1, 37, 300])
+def test_wide_shapes_vs_oracle(shape, B):
+    """Forward / log-det / inverse / eval gradients of the wide family vs the oracle (fp64 for gradients)."""
+    from bcnf_amd import inn_nll_loss
+    m = _model(shape)
+    _perturb(m)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    spec = _spec(shape)
+    m.to(DEV).eval()
+    C = shape["n_conditions"]
+    gen = torch.Generator().manual_seed(B)
+    y = torch.randn(B, shape["size"], generator=gen)
+    c = torch.randn(B, C, generator=gen)
+    zr, lr = O.model_forward(sd, spec, y, c)
+    z = m.forward(y.to(DEV), c.to(DEV), log_det_J=True)
+    ok, err = close(z.detach().cpu(), zr)
+    assert ok, ("z", err)
+    ok, err = close(m.log_det_J.detach().cpu(), lr)
+    assert ok, ("ldj", err)
+    with torch.no_grad():
+        lp = m.log_prob(y.to(DEV), c.to(DEV))
+    assert close(lp.cpu(), O.log_prob(zr, lr))[0]
+    zl = torch.randn(B, shape["size"], generator=gen)
+    inv_r = O.model_inverse(sd, spec, zl, c)
+    with torch.no_grad():
+        inv = m.inverse(zl.to(DEV), c.to(DEV))
+    ok, err = close(inv.cpu(), inv_r)
+    assert ok, ("inverse", err)
+    # eval-mode gradients (parameters, dL/dh, dL/dy) vs fp64 oracle autograd
+    sdg = {k: v.double().clone().requires_grad_(not k.endswith("orthonormal_matrix")) for k, v in sd.items()}
+    cg = c.double().clone().requires_grad_(True)
+    yg = y.double().clone().requires_grad_(True)
+    zo, lo = O.model_forward(sdg, spec, yg, cg)
+    O.inn_nll_loss(zo, lo).backward()
+    m.zero_grad(set_to_none=True)
+    cd = c.to(DEV).requires_grad_(True)
+    yd = y.to(DEV).requires_grad_(True)
+    zg = m.forward(yd, cd, log_det_J=True)
+    inn_nll_loss(zg, m.log_det_J).backward()
+    assert close(cd.grad.cpu(), cg.grad, rtol=1e-4, floor=1e-4)[0]
+    assert close(yd.grad.cpu(), yg.grad, rtol=1e-4, floor=1e-4)[0]
+    n = 0
+    for name, p in m.named_parameters():
+        if p.grad is None:
+            continue
+        ok, err = close(p.grad.cpu(), sdg[name].grad, rtol=1e-4, floor=1e-4)
+        assert ok, (name, err)
+        n += 1
+    assert n == len([k for k in sd if not k.endswith("orthonormal_matrix")])
+
+
+def _large_proxy_sd(model, seed=SEED):
+    """tests/golden/make_golden.py:large_proxy_state (numpy PCG64 weights in state_dict order)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    sd = {}
+    for k, v in model.state_dict().items():
+        if k.endswith("orthonormal_matrix"):
+            sd[k] = v.numpy()
+            continue
+        shape = tuple(v.shape)
+        if k.endswith(".scale"):
+            a = rng.uniform(0.7, 1.3, size=shape)
+        elif len(shape) == 2:
+            a = rng.uniform(-1.0, 1.0, size=shape) / np.sqrt(shape[1])
+        else:
+            a = rng.uniform(-0.05, 0.05, size=shape)
+        sd[k] = a.astype(np.float32)
+    return sd
+
+
+@pytest.fixture(scope="module")
+def g7_model():
+    d = load_golden("g7_large_proxy.npz")
+    shape = dict(size=19, nested_sizes=[526] * 5, n_blocks=2, n_conditions=1360, dropout=0.407, act_norm=True)
+    m = _model(shape, fsizes=[90, 1360])
+    sd = _large_proxy_sd(m)
+    sd["layers.2.orthonormal_matrix"] = d["q/layers.2.orthonormal_matrix"]
+    m.load_state_dict({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in sd.items()})
+    m.to(DEV).eval()
+    return m, d, {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in sd.items()}
+
+
+def test_wide_g7_matches_reference(g7_model):
+    """FC_large-shaped proxy (C = 1360, [526] * 5): z, log|det J|, log_prob and inverse vs the reference's outputs."""
+    m, d, _ = g7_model
+    y, traj = torch.from_numpy(d["y"]).to(DEV), torch.from_numpy(d["traj"]).to(DEV)
+    with torch.no_grad():
+        z = m.forward(y, traj, log_det_J=True)
+        ldj = m.log_det_J.clone()
+        lp = m.log_prob(y, traj)
+        inv = m.inverse(torch.from_numpy(d["z"]).to(DEV), traj)
+    ok, err = close(z.cpu(), d["z"])
+    assert ok, ("z", err)
+    ok, err = close(ldj.cpu(), d["ldj"])
+    assert ok, ("ldj", err)
+    ref_lp = -(0.5 * (d["z"].astype(np.float64) ** 2).sum(1) - d["ldj"]) - 0.5 * 19 * math.log(2 * math.pi)
+    ok, err = close(lp.cpu(), ref_lp)
+    assert ok, ("log_prob", err)
+    ok, err = close(inv.cpu(), d["inv"])
+    assert ok, ("inverse", err)
+
+
+def test_wide_g7_grads_vs_oracle(g7_model):
+    """FC_large-shaped proxy: every parameter gradient and dL/dy against the fp64 oracle."""
+    from bcnf_amd import inn_nll_loss
+    m, d, sd = g7_model
+    spec = _spec(dict(size=19, nested_sizes=[526] * 5, n_blocks=2, n_conditions=1360, dropout=0.407,
+                      act_norm=True), fsizes=[90, 1360])
+    sdg = {k: v.double().clone().requires_grad_(not k.endswith("orthonormal_matrix")) for k, v in sd.items()}
+    y = torch.from_numpy(d["y"]).double().requires_grad_(True)
+    h = O.feature_forward(sdg, spec, torch.from_numpy(d["traj"]).double())
+    zo, lo = O.model_forward(sdg, spec, y, h)
+    O.inn_nll_loss(zo, lo).backward()
+    m.zero_grad(set_to_none=True)
+    yd = torch.from_numpy(d["y"]).to(DEV).requires_grad_(True)
+    z = m.forward(yd, torch.from_numpy(d["traj"]).to(DEV), log_det_J=True)
+    inn_nll_loss(z, m.log_det_J).backward()
+    assert close(yd.grad.cpu(), y.grad, rtol=1e-4, floor=1e-4)[0]
+    for name, p in m.named_parameters():
+        if p.grad is None:
+            continue
+        ok, err = close(p.grad.cpu(), sdg[name].grad, rtol=1e-4, floor=1e-4)
+        assert ok, (name, err)
+
+
+def _train_model(shape=None):
+    shape = shape or dict(size=19, nested_sizes=[96] * 3, n_blocks=3, n_conditions=80, dropout=0.3, act_norm=True)
+    m = _model(shape, fsizes=[90, 80])
+    _perturb(m)
+    return m.to(DEV).train()
+
+
+def test_wide_nll_fused_equals_unfused_with_dropout():
+    """Training mode: nll_loss (forward + per-sample NLL + finalize; backward through the NLL) == forward +
+    inn_nll_loss + autograd on the same dropout stream; the finalize advances the RNG offset once."""
+    from bcnf_amd import inn_nll_loss
+    m = _train_model()
+    m.flat_parameters()
+    gen = torch.Generator().manual_seed(3)
+    y = torch.randn(257, 19, generator=gen).to(DEV)
+    traj = torch.randn(257, 30, 3, generator=gen).to(DEV)
+    m.fused.set_seed(99)
+    vals = m.nll_loss(y, traj)
+    torch.autograd.backward(vals, torch.tensor([1.0, 0.0, 0.0], device=DEV))
+    g_fused = m.fused.flat_param.grad.clone()
+    assert int(m.fused.rng_state()[1].item()) == 1
+    m.zero_grad(set_to_none=True)
+    m.fused.flat_param.grad = None
+    m.fused.set_seed(99)
+    z = m(y, traj, log_det_J=True)
+    loss = inn_nll_loss(z, m.log_det_J)
+    loss.backward()
+    assert abs(loss.item() - vals[0].item()) <= 1e-6 * abs(loss.item())
+    assert torch.allclose(m.fused.flat_param.grad, g_fused, rtol=1e-5, atol=1e-6)
+
+
+def test_wide_dropout_statistics_and_fd_consistency():
+    """Philox dropout keeps ~(1 - p) of the hidden units (from the saved derivative factors), fresh masks per
+    call, and the backward is the exact gradient of the forward that drew them (central differences at a fixed
+    RNG offset)."""
+    from bcnf_amd import inn_nll_loss
+    m = _train_model()
+    st = m.fused
+    st.set_seed(1234)
+    gen = torch.Generator().manual_seed(5)
+    y = torch.randn(512, 19, generator=gen).to(DEV)
+    traj = torch.randn(512, 30, 3, generator=gen).to(DEV)
+    with torch.no_grad():
+        z1 = m(y, traj)
+        z2 = m(y, traj)
+        assert not torch.allclose(z1, z2)
+        h = m.feature_network_stack(traj)
+        _, _, _, (ws, _) = st.launch_forward(y, h, True, save=True)
+    # G factors: region after P (B x nb x HP) and nllp (B) and A (nb x NH x B x HP); see carve() in bcnf_wide.hip
+    B, nb, NH, H, HP = 512, 3, 3, 96, 100
+    off = (B * nb * HP + 3) // 4 * 4 + 64
+    off += (B + 3) // 4 * 4 + 64
+    off += (nb * NH * B * HP + 3) // 4 * 4 + 64
+    G = ws[off: off + nb * NH * B * HP].view(nb, NH, B, HP)[..., :H]
+    keep = (G != 0).double().mean().item()
+    assert abs(keep - 0.7) < 0.01, keep
+
+    def loss_at(offset):
+        st.rng_state()[1] = offset
+        zz = m(y, traj, log_det_J=True)
+        return inn_nll_loss(zz, m.log_det_J)
+
+    m.zero_grad(set_to_none=True)
+    L0 = loss_at(77)
+    L0.backward()
+    g = torch.cat([p.grad.reshape(-1) for p in st.trainable])
+    gn = g.norm().item()
+    v = g / gn
+    eps = 1e-3 / max(1.0, gn / 100.0)
+    with torch.no_grad():
+        st.flat.add_(eps * v)
+        Lp = loss_at(77).double().item()
+        st.flat.add_(-2 * eps * v)
+        Lm = loss_at(77).double().item()
+        st.flat.add_(eps * v)
+    fd = (Lp - Lm) / (2 * eps)
+    assert abs(fd - gn) <= 2e-2 * gn, (fd, gn)
+    with torch.no_grad():
+        assert loss_at(78).item() != loss_at(77).item()
+
+
+def test_wide_trainstep_graph_replay_equals_eager():
+    """HIP-graph TrainStep on the wide family == eager TrainStep over 3 dropout steps, bit for bit, and the loss
+    goes down over a few steps."""
+    from bcnf_amd.train import TrainStep
+    gen = torch.Generator().manual_seed(11)
+    pool_y = torch.randn(1024, 19, generator=gen).to(DEV)
+    pool_t = torch.randn(1024, 30, 3, generator=gen).to(DEV)
+    idxs = [torch.randperm(1024, generator=gen)[:256].to(DEV) for _ in range(3)]
+    res = []
+    for capture in (False, True):
+        torch.manual_seed(0)
+        m = _train_model()
+        m.fused.set_seed(77)
+        st = TrainStep(m, lr=2e-4, capture=capture)
+        st.set_pool(pool_y, pool_t)
+        losses = [st.step_indexed(i) for i in idxs]
+        res.append((losses, [p.detach().clone() for p in m.parameters()], int(m.fused.rng_state()[1].item())))
+    (l0, p0, r0), (l1, p1, r1) = res
+    assert l0 == l1 and r0 == r1 == 3
+    for a, b in zip(p0, p1):
+        assert torch.equal(a, b)
+    torch.manual_seed(0)
+    m = _train_model()
+    st = TrainStep(m, lr=1e-3, capture=True)
+    y, t = pool_y[:256], pool_t[:256]
+    first = st.step(y, t)[0]
+    for _ in range(20):
+        last = st.step(y, t)[0]
+    assert last < first, (first, last)
+
+
+def test_wide_sample_matches_oracle():
+    """sample(outer=True): the reference's CPU z stream and chunking, features once per condition (cond_index)."""
+    shape = dict(size=19, nested_sizes=[48] * 2, n_blocks=3, n_conditions=80, dropout=0.2, act_norm=True)
+    m = _model(shape, fsizes=[90, 80])
+    _perturb(m)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m.to(DEV).eval()
+    traj = torch.randn(7, 30, 3, generator=torch.Generator().manual_seed(2))
+    torch.manual_seed(123)
+    got = m.sample(50, traj, outer=True, batch_size=3, sample_batch_size=16)
+    torch.manual_seed(123)
+    ref = O.sample(sd, _spec(shape, fsizes=[90, 80]), 50, traj, outer=True, batch_size=3, sample_batch_size=16)
+    assert got.shape == ref.shape == (50, 7, 19)
+    ok, err = close(got, ref)
+    assert ok, err
