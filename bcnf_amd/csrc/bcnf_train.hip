@@ -362,11 +362,27 @@ int split_rows(long long M) {        // rows per split-K chunk of the weight gra
   return (int)((r + 31) & ~31LL);
 }
 
+inline int64_t n_partials(int64_t total_numel) { return total_numel <= 0 ? 1 : (total_numel + CHUNK - 1) / CHUNK; }
+
+// Sum of many partials by one workgroup (fixed order), so that every clip workgroup then reads one value
+// instead of re-reducing all partials (quadratic in the parameter count otherwise).
+constexpr int CLIP_DIRECT_PARTIALS = 2048;
+__global__ __launch_bounds__(BCNF_WG) void k_sum_partials(const float* __restrict__ part, int nparts,
+                                                          float* __restrict__ out, const int32_t* __restrict__ guard) {
+  __shared__ float red[BCNF_WG];
+  if (guard && guard[BCNF_GUARD_HALTED]) return;
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += BCNF_WG) acc += part[i];
+  const float s = wg_sum(acc, red);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
 }  // namespace
 
 extern "C" {
 
-int64_t bcnf_grad_partials(int64_t total_numel) { return total_numel <= 0 ? 1 : (total_numel + CHUNK - 1) / CHUNK; }
+// one partial per workgroup of k_adam / k_sumsq, plus one slot for the pre-reduced total of large sets
+int64_t bcnf_grad_partials(int64_t total_numel) { return n_partials(total_numel) + 1; }
 
 int bcnf_adam_step(int32_t n_tensors, float* const* params, float* const* grads, float* const* exp_avg,
                    float* const* exp_avg_sq, const int64_t* numel, float* step, double lr, double beta1,
@@ -379,7 +395,7 @@ int bcnf_adam_step(int32_t n_tensors, float* const* params, float* const* grads,
   for (int i = 0; i < n_tensors; ++i)
     if (!T.p[i] || !T.m[i] || !T.v[i]) return BCNF_ERR_ARG;
   const long long total = T.start[T.n];
-  const unsigned nwg = (unsigned)bcnf_grad_partials(total);
+  const unsigned nwg = (unsigned)n_partials(total);
   hipLaunchKernelGGL(k_adam, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, step, lr, beta1, beta2, eps,
                      weight_decay, grad_partials, guard);
   if ((rc = launched()) || !advance_step) return rc;
@@ -392,7 +408,7 @@ int bcnf_grad_sumsq(int32_t n_tensors, float* const* grads, const int64_t* numel
   int rc = make_tlist(n_tensors, nullptr, grads, nullptr, nullptr, numel, &T);
   if (rc) return rc;
   if (!grad_partials) return BCNF_ERR_ARG;
-  const unsigned nwg = (unsigned)bcnf_grad_partials(T.start[T.n]);
+  const unsigned nwg = (unsigned)n_partials(T.start[T.n]);
   hipLaunchKernelGGL(k_sumsq, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, grad_partials);
   return launched();
 }
@@ -405,9 +421,17 @@ int bcnf_clip_grad_norm(int32_t n_tensors, float* const* grads, const int64_t* n
   int rc = make_tlist(n_tensors, nullptr, grads, nullptr, nullptr, numel, &T);
   if (rc) return rc;
   if (!grad_partials) return BCNF_ERR_ARG;
-  const long long np = bcnf_grad_partials(T.start[T.n]);
+  const long long np = n_partials(T.start[T.n]);
   if (advance_cursor && cursor_modulo < 1) return BCNF_ERR_ARG;
-  hipLaunchKernelGGL(k_clip, dim3((unsigned)np), dim3(BCNF_WG), 0, (hipStream_t)stream, T, grad_partials, (int)np,
+  const float* part = grad_partials;
+  int nread = (int)np;
+  if (np > CLIP_DIRECT_PARTIALS) {      // pre-reduce into the extra slot
+    hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(BCNF_WG), 0, (hipStream_t)stream, grad_partials, (int)np,
+                       const_cast<float*>(grad_partials) + np, guard);
+    part = grad_partials + np;
+    nread = 1;
+  }
+  hipLaunchKernelGGL(k_clip, dim3((unsigned)np), dim3(BCNF_WG), 0, (hipStream_t)stream, T, part, nread,
                      max_norm, total_norm, advance_step, (long long*)advance_cursor, (long long)cursor_modulo,
                      log_values, log_history, guard);
   return launched();

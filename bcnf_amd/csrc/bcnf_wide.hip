@@ -38,10 +38,9 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 namespace {
 
 constexpr int WWG = 256;      // threads per workgroup of every wide kernel
-constexpr int LINK_ROWS = 2;  // samples per wavefront in the link kernels
 constexpr int DM = 32;        // max D of the wide family (register arrays of the link kernels)
 
-inline int pad4(int x) { return (x + 3) & ~3; }
+__host__ __device__ inline int pad4(int x) { return (x + 3) & ~3; }
 inline long long pad4l(long long x) { return (x + 3) & ~3LL; }
 
 struct WideLayout {
@@ -60,6 +59,7 @@ struct WideLayout {
   long long pk_wl;              // [nb][2 Db][HP]   last Linear, zero beyond H
   long long pk_q;               // [nb-1][D][D]
   long long pk_ldc;             // [nb]             sum_i log|scale_k,i| (0 without ActNorm)
+  long long pk_b0;              // [nb][HP]         Linear-1 bias, zero beyond H
   long long total;
 };
 
@@ -116,6 +116,7 @@ int wide_layout(const BcnfStackDesc* d, WideLayout* L) {
   L->pk_wl = o;  o += pad4l((long long)L->nb * 2 * L->Db * L->HP);
   L->pk_q = o;   o += pad4l((long long)(L->nb - 1) * L->D * L->D);
   L->pk_ldc = o; o += pad4l(L->nb);
+  L->pk_b0 = o;  o += (long long)L->nb * L->HP;
   L->total = o;
   return BCNF_OK;
 }
@@ -175,6 +176,12 @@ __global__ void k_wpack_ldc(const WideLayout L, const float* __restrict__ prm, f
   pk[L.pk_ldc + k] = s;
 }
 
+__global__ __launch_bounds__(WWG) void k_wpack_b0(const WideLayout L, const float* __restrict__ prm, float* __restrict__ pk) {
+  const int k = blockIdx.x;
+  for (int n = threadIdx.x; n < L.HP; n += WWG)
+    pk[L.pk_b0 + (long long)k * L.HP + n] = n < L.H ? prm[wcb(L, k) + L.lin_b[0] + n] : 0.f;
+}
+
 // ------------------------------------------------------------------------------------------------
 // fp32-MFMA GEMM  C[m][n] = sum_k A(m, k) B(k, n), v_mfma_f32_32x32x2_f32.
 //   A(m, k): AKC ? A[m * lda + k] : A[k * lda + m]      B(k, n): BKC ? B[n * ldb + k] : B[k * ldb + n]
@@ -208,90 +215,160 @@ struct GemmArgs {
 __device__ __forceinline__ floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
 __device__ __forceinline__ void st4(float* p, floatx4 v) { *reinterpret_cast<floatx4*>(p) = v; }
 
+// Global -> register -> LDS staging of one BM x BK (A) and BK x BN (B) tile pair, shared by both MFMA tilings.
+template <int BM, int BN, int BK, bool AKC, bool BKC>
+struct TileIO {
+  static constexpr int ASZ = AKC ? BM * (BK + 4) : BK * (BM + 4);
+  static constexpr int BSZ = BKC ? BN * (BK + 4) : BK * (BN + 4);
+  static constexpr int AV = (BM * BK / 4 + WWG - 1) / WWG, BV = (BN * BK / 4 + WWG - 1) / WWG;
+  floatx4 ra[AV], rb[BV];
+
+  template <int ROWS, bool KC>
+  __device__ __forceinline__ static floatx4 fetch(const float* __restrict__ X, long long ld, int e, int mn0, int k0,
+                                                  int MN, int K) {
+    floatx4 v = {0.f, 0.f, 0.f, 0.f};
+    if (e >= ROWS * BK / 4) return v;
+    if (KC) {
+      const int row = e / (BK / 4), kq = e % (BK / 4);
+      const int gm = mn0 + row, gk = k0 + 4 * kq;
+      if (gm < MN && gk < K) v = ld4(X + (long long)gm * ld + gk);
+    } else {
+      const int kr = e / (ROWS / 4), mq = e % (ROWS / 4);
+      const int gk = k0 + kr, gm = mn0 + 4 * mq;
+      if (gk < K) {
+        const float* p = X + (long long)gk * ld + gm;
+        if (gm + 3 < MN) v = ld4(p);
+        else {
+          if (gm < MN) v.x = p[0];
+          if (gm + 1 < MN) v.y = p[1];
+          if (gm + 2 < MN) v.z = p[2];
+        }
+      }
+    }
+    return v;
+  }
+  template <int ROWS, bool KC>
+  __device__ __forceinline__ static void put(float* S, int e, floatx4 v) {
+    if (e >= ROWS * BK / 4) return;
+    if (KC) st4(S + (e / (BK / 4)) * (BK + 4) + 4 * (e % (BK / 4)), v);
+    else st4(S + (e / (ROWS / 4)) * (ROWS + 4) + 4 * (e % (ROWS / 4)), v);
+  }
+  __device__ __forceinline__ void load(const GemmArgs& g, const float* A, const float* B, int m0, int n0, int k0) {
+#pragma unroll
+    for (int i = 0; i < AV; ++i) ra[i] = fetch<BM, AKC>(A, g.lda, threadIdx.x + WWG * i, m0, k0, g.M, g.K);
+#pragma unroll
+    for (int i = 0; i < BV; ++i) rb[i] = fetch<BN, BKC>(B, g.ldb, threadIdx.x + WWG * i, n0, k0, g.N, g.K);
+  }
+  __device__ __forceinline__ void store(float* As, float* Bs) const {
+#pragma unroll
+    for (int i = 0; i < AV; ++i) put<BM, AKC>(As, threadIdx.x + WWG * i, ra[i]);
+#pragma unroll
+    for (int i = 0; i < BV; ++i) put<BN, BKC>(Bs, threadIdx.x + WWG * i, rb[i]);
+  }
+  // four consecutive-k operand values of row / column mn at k offset kb of the staged tile
+  template <int ROWS, bool KC>
+  __device__ __forceinline__ static floatx4 frag(const float* S, int mn, int kb) {
+    if (KC) return ld4(S + mn * (BK + 4) + kb);
+    return floatx4{S[(kb + 0) * (ROWS + 4) + mn], S[(kb + 1) * (ROWS + 4) + mn], S[(kb + 2) * (ROWS + 4) + mn],
+                   S[(kb + 3) * (ROWS + 4) + mn]};
+  }
+};
+
+// Epilogue of four consecutive output rows rbase..rbase+3 at column col (both MFMA tilings hold their
+// accumulators in such groups). rnd: the group's Philox draw (EPI_ACT with dropout).
+template <int EPI>
+__device__ __forceinline__ void epi4(const GemmArgs& g, float* __restrict__ Cg, float* __restrict__ Xg, int rbase,
+                                     int col, const float v[4], uint4 rnd) {
+  const int M = g.M, N = g.N;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int row = rbase + rr;
+    if (row >= M || col >= N) continue;
+    if (EPI == EPI_STORE) {
+      Cg[(long long)row * g.ldc + col] = v[rr];
+    } else if (EPI == EPI_ACT) {
+      float a = 0.f, gd = 0.f;
+      if (col < g.n_real) {
+        float ge, dg;
+        gelu_fg(v[rr] + g.bias[col], ge, dg);
+        if (g.rng) {
+          const uint32_t u = rr == 0 ? rnd.x : rr == 1 ? rnd.y : rr == 2 ? rnd.z : rnd.w;
+          const float m = u >= g.thresh ? g.keep_scale : 0.f;
+          a = ge * m;
+          gd = dg * m;
+        } else {
+          a = ge;
+          gd = dg;
+        }
+      } else if (col == g.n_real) {
+        a = 1.f;
+      }
+      Cg[(long long)row * g.ldc + col] = a;
+      if (Xg) Xg[(long long)row * g.ldaux + col] = gd;
+    } else if (EPI == EPI_GRAD) {
+      Cg[(long long)row * g.ldc + col] = v[rr] * Xg[(long long)row * g.ldaux + col];
+    } else if (EPI == EPI_LINGRAD) {
+      if (col < g.wcols) Cg[(long long)row * g.ldc + col] = v[rr];
+      else if (col == g.wcols) Cg[g.boff + row] = v[rr];
+    } else {   // EPI_ROWMAP
+      const int blk = row / g.rm_hp, n = row - blk * g.rm_hp;
+      if (n < g.rm_h)
+        Cg[(long long)blk * g.cb_stride + ((blk < g.cb_nb - 1) ? g.cb_an : 0) + g.rm_off + (long long)n * g.ldc + col] =
+            v[rr];
+    }
+  }
+}
+
+struct EpiCtx {
+  float* C;
+  float* X;
+  uint64_t seed, offs;
+  uint32_t tag;
+};
+
+template <int EPI>
+__device__ __forceinline__ EpiCtx epi_ctx(const GemmArgs& g, int g1, int g0) {
+  EpiCtx e;
+  e.C = g.C;
+  if (EPI == EPI_LINGRAD || EPI == EPI_ROWMAP) {
+    if (g.use_cb) e.C += g1 * g.cb_stride + ((g1 < g.cb_nb - 1) ? g.cb_an : 0) + g0 * g.sC0;
+  } else {
+    e.C += g1 * g.sC1 + g0 * g.sC0;
+  }
+  e.X = (EPI == EPI_ACT || EPI == EPI_GRAD) && g.aux ? g.aux + g1 * g.saux1 + g0 * g.saux0 : nullptr;
+  e.seed = 0;
+  e.offs = 0;
+  if (EPI == EPI_ACT && g.rng) {
+    e.seed = g.rng[0];
+    e.offs = g.rng[1];
+  }
+  e.tag = g.tag + (uint32_t)g1 * g.tag_s1;
+  return e;
+}
+
+template <int EPI>
+__device__ __forceinline__ uint4 epi_rnd(const GemmArgs& g, const EpiCtx& e, int rbase, int col) {
+  if (EPI == EPI_ACT && g.rng)
+    return philox4x32_10(make_uint4((uint32_t)rbase, (uint32_t)col, e.tag, (uint32_t)e.offs),
+                         make_uint2((uint32_t)e.seed, (uint32_t)(e.seed >> 32) ^ (uint32_t)(e.offs >> 32)));
+  return make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+}
+
+// Tiling A: v_mfma_f32_32x32x2_f32, 2 x 2 waves, each (BM/2) x (BN/2) as 32x32 accumulators. Inside a K tile
+// lane half h consumes k = h*BK/2 + s at MFMA step s.
 template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI>
 __global__ __launch_bounds__(WWG, 2) void k_wgemm(const GemmArgs g) {
+  using IO = TileIO<BM, BN, BK, AKC, BKC>;
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TI = WM / 32, TJ = WN / 32;
-  constexpr int ASZ = AKC ? BM * (BK + 4) : BK * (BM + 4);
-  constexpr int BSZ = BKC ? BN * (BK + 4) : BK * (BN + 4);
-  constexpr int AV = BM * BK / 4 / WWG, BV = BN * BK / 4 / WWG;
-  static_assert(AV >= 1 && BV >= 1, "tile too small for 256 threads");
-  __shared__ __attribute__((aligned(16))) float lds[2 * (ASZ + BSZ)];
-
+  __shared__ __attribute__((aligned(16))) float lds[2 * (IO::ASZ + IO::BSZ)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, c32 = lane & 31, hh = lane >> 5;
   const int z = blockIdx.z, g1 = z / g.G0, g0 = z - g1 * g.G0;
   const float* __restrict__ A = g.A + g1 * g.sA1 + g0 * g.sA0;
   const float* __restrict__ B = g.B + g1 * g.sB1 + g0 * g.sB0;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int M = g.M, N = g.N, K = g.K;
-
-  floatx4 ra[AV], rb[BV];
-  auto load_a = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < AV; ++i) {
-      const int e = tid + WWG * i;
-      floatx4 v = {0.f, 0.f, 0.f, 0.f};
-      if (AKC) {
-        const int row = e / (BK / 4), kq = e % (BK / 4);
-        const int gm = m0 + row, gk = k0 + 4 * kq;
-        if (gm < M && gk < K) v = ld4(A + (long long)gm * g.lda + gk);
-      } else {
-        const int kr = e / (BM / 4), mq = e % (BM / 4);
-        const int gk = k0 + kr, gm = m0 + 4 * mq;
-        if (gk < K) {
-          const float* p = A + (long long)gk * g.lda + gm;
-          if (gm + 3 < M) v = ld4(p);
-          else {
-            if (gm < M) v.x = p[0];
-            if (gm + 1 < M) v.y = p[1];
-            if (gm + 2 < M) v.z = p[2];
-          }
-        }
-      }
-      ra[i] = v;
-    }
-  };
-  auto load_b = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < BV; ++i) {
-      const int e = tid + WWG * i;
-      floatx4 v = {0.f, 0.f, 0.f, 0.f};
-      if (BKC) {
-        const int row = e / (BK / 4), kq = e % (BK / 4);
-        const int gn = n0 + row, gk = k0 + 4 * kq;
-        if (gn < N && gk < K) v = ld4(B + (long long)gn * g.ldb + gk);
-      } else {
-        const int kr = e / (BN / 4), nq = e % (BN / 4);
-        const int gk = k0 + kr, gn = n0 + 4 * nq;
-        if (gk < K) {
-          const float* p = B + (long long)gk * g.ldb + gn;
-          if (gn + 3 < N) v = ld4(p);
-          else {
-            if (gn < N) v.x = p[0];
-            if (gn + 1 < N) v.y = p[1];
-            if (gn + 2 < N) v.z = p[2];
-          }
-        }
-      }
-      rb[i] = v;
-    }
-  };
-  auto store_tiles = [&](float* As, float* Bs) {
-#pragma unroll
-    for (int i = 0; i < AV; ++i) {
-      const int e = tid + WWG * i;
-      if (AKC) st4(As + (e / (BK / 4)) * (BK + 4) + 4 * (e % (BK / 4)), ra[i]);
-      else st4(As + (e / (BM / 4)) * (BM + 4) + 4 * (e % (BM / 4)), ra[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < BV; ++i) {
-      const int e = tid + WWG * i;
-      if (BKC) st4(Bs + (e / (BK / 4)) * (BK + 4) + 4 * (e % (BK / 4)), rb[i]);
-      else st4(Bs + (e / (BN / 4)) * (BN + 4) + 4 * (e % (BN / 4)), rb[i]);
-    }
-  };
-
+  IO io;
   floatx16 acc[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; ++i)
@@ -299,38 +376,23 @@ __global__ __launch_bounds__(WWG, 2) void k_wgemm(const GemmArgs g) {
     for (int j = 0; j < TJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int nk = (K + BK - 1) / BK;
-  load_a(0);
-  load_b(0);
-  store_tiles(lds, lds + ASZ);
+  const int nk = (g.K + BK - 1) / BK;
+  io.load(g, A, B, m0, n0, 0);
+  io.store(lds, lds + IO::ASZ);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
-    float* As = lds + (kt & 1) * (ASZ + BSZ);
-    float* Bs = As + ASZ;
+    const float* As = lds + (kt & 1) * (IO::ASZ + IO::BSZ);
+    const float* Bs = As + IO::ASZ;
     const bool more = kt + 1 < nk;
-    if (more) {
-      load_a((kt + 1) * BK);
-      load_b((kt + 1) * BK);
-    }
+    if (more) io.load(g, A, B, m0, n0, (kt + 1) * BK);
 #pragma unroll
     for (int sq = 0; sq < BK / 8; ++sq) {
       const int kb = hh * (BK / 2) + 4 * sq;
       floatx4 af[TI], bf[TJ];
 #pragma unroll
-      for (int i = 0; i < TI; ++i) {
-        const int row = wm * WM + 32 * i + c32;
-        if (AKC) af[i] = ld4(As + row * (BK + 4) + kb);
-        else af[i] = floatx4{As[(kb + 0) * (BM + 4) + row], As[(kb + 1) * (BM + 4) + row],
-                             As[(kb + 2) * (BM + 4) + row], As[(kb + 3) * (BM + 4) + row]};
-      }
+      for (int i = 0; i < TI; ++i) af[i] = IO::template frag<BM, AKC>(As, wm * WM + 32 * i + c32, kb);
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int col = wn * WN + 32 * j + c32;
-        if (BKC) bf[j] = ld4(Bs + col * (BK + 4) + kb);
-        else bf[j] = floatx4{Bs[(kb + 0) * (BN + 4) + col], Bs[(kb + 1) * (BN + 4) + col],
-                             Bs[(kb + 2) * (BN + 4) + col], Bs[(kb + 3) * (BN + 4) + col]};
-      }
+      for (int j = 0; j < TJ; ++j) bf[j] = IO::template frag<BN, BKC>(Bs, wn * WN + 32 * j + c32, kb);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -340,26 +402,13 @@ __global__ __launch_bounds__(WWG, 2) void k_wgemm(const GemmArgs g) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
     }
     if (more) {
-      float* An = lds + ((kt + 1) & 1) * (ASZ + BSZ);
-      store_tiles(An, An + ASZ);
+      float* An = lds + ((kt + 1) & 1) * (IO::ASZ + IO::BSZ);
+      io.store(An, An + IO::ASZ);
     }
     __syncthreads();
   }
-
-  // ---------------------------------------------------------------- epilogue
   // accumulator element r of lane (c32, hh): row = (r & 3) + 8 (r >> 2) + 4 hh, col = c32
-  float* __restrict__ Cg = g.C;
-  if (EPI == EPI_LINGRAD || EPI == EPI_ROWMAP) {
-    if (g.use_cb) Cg += g1 * g.cb_stride + ((g1 < g.cb_nb - 1) ? g.cb_an : 0) + g0 * g.sC0;
-  } else {
-    Cg += g1 * g.sC1 + g0 * g.sC0;
-  }
-  float* __restrict__ Xg = (EPI == EPI_ACT || EPI == EPI_GRAD) && g.aux ? g.aux + g1 * g.saux1 + g0 * g.saux0 : nullptr;
-  uint64_t seed = 0, offs = 0;
-  if (EPI == EPI_ACT && g.rng) {
-    seed = g.rng[0];
-    offs = g.rng[1];
-  }
+  const EpiCtx e = epi_ctx<EPI>(g, g1, g0);
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -368,70 +417,111 @@ __global__ __launch_bounds__(WWG, 2) void k_wgemm(const GemmArgs g) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int rbase = m0 + wm * WM + 32 * i + 8 * q + 4 * hh;
-        uint4 rnd = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
-        if (EPI == EPI_ACT && g.rng) {
-          const uint32_t tag = g.tag + (uint32_t)g1 * g.tag_s1;
-          rnd = philox4x32_10(make_uint4((uint32_t)rbase, (uint32_t)col, tag, (uint32_t)offs),
-                              make_uint2((uint32_t)seed, (uint32_t)(seed >> 32) ^ (uint32_t)(offs >> 32)));
-        }
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int row = rbase + rr;
-          const float v = acc[i][j][4 * q + rr];
-          if (row >= M || col >= N) continue;
-          if (EPI == EPI_STORE) {
-            Cg[(long long)row * g.ldc + col] = v;
-          } else if (EPI == EPI_ACT) {
-            float a = 0.f, gd = 0.f;
-            if (col < g.n_real) {
-              float ge, dg;
-              gelu_fg(v + g.bias[col], ge, dg);
-              if (g.rng) {
-                const uint32_t u = rr == 0 ? rnd.x : rr == 1 ? rnd.y : rr == 2 ? rnd.z : rnd.w;
-                const float m = u >= g.thresh ? g.keep_scale : 0.f;
-                a = ge * m;
-                gd = dg * m;
-              } else {
-                a = ge;
-                gd = dg;
-              }
-            } else if (col == g.n_real) {
-              a = 1.f;
-            }
-            Cg[(long long)row * g.ldc + col] = a;
-            if (Xg) Xg[(long long)row * g.ldaux + col] = gd;
-          } else if (EPI == EPI_GRAD) {
-            Cg[(long long)row * g.ldc + col] = v * Xg[(long long)row * g.ldaux + col];
-          } else if (EPI == EPI_LINGRAD) {
-            if (col < g.wcols) Cg[(long long)row * g.ldc + col] = v;
-            else if (col == g.wcols) Cg[g.boff + row] = v;
-          } else {   // EPI_ROWMAP
-            const int blk = row / g.rm_hp, n = row - blk * g.rm_hp;
-            if (n < g.rm_h)
-              Cg[(long long)blk * g.cb_stride + ((blk < g.cb_nb - 1) ? g.cb_an : 0) + g.rm_off + (long long)n * g.ldc + col] = v;
-          }
-        }
+        const float v[4] = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+        epi4<EPI>(g, e.C, e.X, rbase, col, v, epi_rnd<EPI>(g, e, rbase, col));
       }
     }
 }
 
+// Tiling B: v_mfma_f32_16x16x4_f32, 4 waves stacked along M, each (BM/4) x BN as 16x16 accumulators (>= 2
+// independent chains cover the 40-cycle dependent latency). Inside a 16-k chunk lane group q = lane >> 4 consumes
+// k = 4q + s at MFMA step s. Finer N granularity than tiling A: e.g. BN = 48 tiles N = 528 exactly.
+template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI>
+__global__ __launch_bounds__(WWG, 2) void k_wgemm16(const GemmArgs g) {
+  using IO = TileIO<BM, BN, BK, AKC, BKC>;
+  constexpr int WM = BM / 4;
+  constexpr int TI = WM / 16, TJ = BN / 16;
+  __shared__ __attribute__((aligned(16))) float lds[2 * (IO::ASZ + IO::BSZ)];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c16 = lane & 15, qq = lane >> 4;
+  const int z = blockIdx.z, g1 = z / g.G0, g0 = z - g1 * g.G0;
+  const float* __restrict__ A = g.A + g1 * g.sA1 + g0 * g.sA0;
+  const float* __restrict__ B = g.B + g1 * g.sB1 + g0 * g.sB0;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  IO io;
+  floatx4 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (g.K + BK - 1) / BK;
+  io.load(g, A, B, m0, n0, 0);
+  io.store(lds, lds + IO::ASZ);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const float* As = lds + (kt & 1) * (IO::ASZ + IO::BSZ);
+    const float* Bs = As + IO::ASZ;
+    const bool more = kt + 1 < nk;
+    if (more) io.load(g, A, B, m0, n0, (kt + 1) * BK);
+#pragma unroll
+    for (int kc = 0; kc < BK / 16; ++kc) {
+      const int kb = 16 * kc + 4 * qq;
+      floatx4 af[TI], bf[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) af[i] = IO::template frag<BM, AKC>(As, wave * WM + 16 * i + c16, kb);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) bf[j] = IO::template frag<BN, BKC>(Bs, 16 * j + c16, kb);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      float* An = lds + ((kt + 1) & 1) * (IO::ASZ + IO::BSZ);
+      io.store(An, An + IO::ASZ);
+    }
+    __syncthreads();
+  }
+  // accumulator element r of lane (c16, qq): row = 4 qq + r, col = c16
+  const EpiCtx e = epi_ctx<EPI>(g, g1, g0);
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int col = n0 + 16 * j + c16;
+      const int rbase = m0 + wave * WM + 16 * i + 4 * qq;
+      const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      epi4<EPI>(g, e.C, e.X, rbase, col, v, epi_rnd<EPI>(g, e, rbase, col));
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
-// Link kernels: one wavefront per LINK_ROWS samples, 4 wavefronts per workgroup.
-// Cross-lane sums: DPP rotations inside each 16-lane row, then the four row sums via readlane.
+// Link kernels: one 32-lane half-wavefront per sample, 8 samples per 256-thread workgroup.
+//   * The sample's D-vector is lane-distributed (lane i < D holds element i); vectors every lane needs (u_a, v,
+//     dO) go through LDS, so no register array is ever indexed by a runtime value.
+//   * The long dot products (last Linear: 2 Db outputs over HP inputs; Linear-1 y-part backward: Da outputs) are
+//     lane-split over float4 chunks, then reduced through an LDS transpose: lane j sums the 32 partials of
+//     output j.
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ float wave_sum(float v) {
+constexpr int LR = 8;          // samples per link workgroup
+
+// Global -> LDS copy of n4 float4 by the whole workgroup with 8 loads in flight per thread (a plain copy loop
+// serialises one L2 round trip per iteration).
+__device__ __forceinline__ void stage4(float* __restrict__ dst, const float* __restrict__ src, int n4) {
+  for (int e0 = 0; e0 < n4; e0 += 8 * WWG) {
+    floatx4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * WWG + (int)threadIdx.x;
+      if (e < n4) v[u] = ld4(src + 4 * e);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * WWG + (int)threadIdx.x;
+      if (e < n4) st4(dst + 4 * e, v[u]);
+    }
+  }
+}
+
+__device__ __forceinline__ float half_sum(float v) {      // sum over the 32 lanes of a half-wavefront
   v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xf, 0xf, true));  // row_ror:8
   v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xf, 0xf, true));  // row_ror:4
   v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x122, 0xf, 0xf, true));  // row_ror:2
   v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x121, 0xf, 0xf, true));  // row_ror:1
-  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
-  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
-  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
-  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
-  return (r0 + r1) + (r2 + r3);
-}
-__device__ __forceinline__ float bcast(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+  return v + __shfl_xor(v, 16);
 }
 
 struct LinkArgs {
@@ -456,232 +546,197 @@ struct LinkArgs {
 };
 
 // Dropout mask for a float4 group (4 consecutive columns n..n+3 of one row).
-__device__ __forceinline__ uint4 drop4(const uint64_t* rng, uint64_t seed, uint64_t offs, long long row, int n,
-                                       uint32_t tag) {
+__device__ __forceinline__ uint4 drop4(uint64_t seed, uint64_t offs, long long row, int n, uint32_t tag) {
   return philox4x32_10(make_uint4((uint32_t)row, (uint32_t)n | 0x80000000u, tag, (uint32_t)offs),
                        make_uint2((uint32_t)seed, (uint32_t)(seed >> 32) ^ (uint32_t)(offs >> 32)));
+}
+
+__host__ __device__ inline int link_ps(const WideLayout& L) { return (2 * L.Db > L.Da ? 2 * L.Db : L.Da) + 1; }
+
+// LDS floats of a link launch: [tail / bwd-head weights][head / bwd-tail weights][Q][partials][8 x 3 x 32 vectors]
+__host__ __device__ inline int link_lds_floats(const WideLayout& L, bool w_last, bool w_first) {
+  return (w_last ? 2 * L.Db * L.HP : 0) + (w_first ? L.Da * L.HP : 0) + pad4(L.D * L.D) + pad4(LR * 32 * link_ps(L)) +
+         LR * 96;
 }
 
 // Forward (INV = false): tail(kt) = last Linear, t / tanh(s), z_b = exp(s) u_b + t, ldj += sum s, x Q_kt;
 //                        head(kh) = ActNorm, Linear-1 from P + u_a W0y^T + b0, GELU, dropout.
 // Inverse (INV = true):  tail(kt) = last Linear, y_b = (z_b - t) exp(-s), ActNorm^-1;
 //                        head(kh) = v = x Q_kh^T, Linear-1 as above.   (cnf.py:198-213, 337-339, 353-354)
-template <bool INV>
+// DD > 0: the sample dimension D as a compile-time constant (every loop over D, Da, 2 Db fully unrolled, loads
+// batched); DD = 0: runtime D (any D <= 32).
+template <bool INV, int DD>
 __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int HP = L.HP, H = L.H, D = L.D, Da = L.Da, Db = L.Db, O2 = 2 * Db;
-  float* Wl = sm;                       // [2Db][HP] last Linear of block kt
-  float* W0 = sm + (a.kt >= 0 ? O2 * HP : 0);   // [Da][HP] W0y^T of block kh
-  if (a.kt >= 0) {
-    const float* src = a.pk + L.pk_wl + (long long)a.kt * O2 * HP;
-    for (int e = tid; e < O2 * HP / 4; e += WWG) st4(Wl + 4 * e, ld4(src + 4 * e));
-  }
-  if (a.kh >= 0) {
-    const float* src = a.pk + L.pk_w0y + (long long)a.kh * Da * HP;
-    for (int e = tid; e < Da * HP / 4; e += WWG) st4(W0 + 4 * e, ld4(src + 4 * e));
-  }
+  const int tid = threadIdx.x, ln = tid & 31, r = tid >> 5;
+  const int HP = L.HP, H = L.H;
+  const int D = DD ? DD : L.D, Da = DD ? (DD + 1) / 2 : L.Da, Db = DD ? DD / 2 : L.Db, O2 = 2 * Db;
+  const int PS = link_ps(L);
+  const int nq = HP / 4;
+  float* Wl = sm;
+  float* W0 = Wl + (a.kt >= 0 ? O2 * HP : 0);
+  float* Qs = W0 + (a.kh >= 0 ? Da * HP : 0);
+  float* part = Qs + pad4(D * D);
+  float* Os = part + pad4(LR * 32 * PS) + r * 96;
+  float* vs = Os + 32;
+  float* us = vs + 32;
+  const int kq = INV ? a.kh : a.kt;                 // the orthonormal matrix this launch applies
+  if (a.kt >= 0) stage4(Wl, a.pk + L.pk_wl + (long long)a.kt * O2 * HP, O2 * HP / 4);
+  if (a.kh >= 0) stage4(W0, a.pk + L.pk_w0y + (long long)a.kh * Da * HP, Da * HP / 4);
+  if (kq >= 0 && kq < L.nb - 1)
+    for (int e = tid; e < D * D; e += WWG) Qs[e] = a.pk[L.pk_q + (long long)kq * D * D + e];
   __syncthreads();
 
-  const long long row0 = ((long long)blockIdx.x * 4 + wave) * LINK_ROWS;
-  if (row0 >= a.B) return;
-  const int nq = HP / 4;                // float4 groups per activation row
+  const long long row = (long long)blockIdx.x * LR + r;
+  const bool valid = row < a.B;
+  const bool lv = valid && ln < D;
   uint64_t seed = 0, offs = 0;
   if (a.rng) {
     seed = a.rng[0];
     offs = a.rng[1];
   }
-
-  for (int rr = 0; rr < LINK_ROWS; ++rr) {
-    const long long row = row0 + rr;
-    if (row >= a.B) break;
-    float x[DM];                          // the sample's D-vector (wave-uniform)
-    // ------------------------------------------------------------ tail of block kt
-    if (a.kt >= 0) {
-      const int k = a.kt;
-      float o[DM];
+  float xi = 0.f;                                   // element ln of the sample's D-vector
+  // ------------------------------------------------------------ tail of block kt
+  if (a.kt >= 0) {
+    const int k = a.kt;
+    float acc[DM];
 #pragma unroll
-      for (int j = 0; j < DM; ++j) o[j] = 0.f;
+    for (int j = 0; j < DM; ++j) acc[j] = 0.f;
+    if (valid) {
       const float* arow = a.Alast + row * HP;
-      for (int q = lane; q < nq; q += 64) {
+      for (int q = ln; q < nq; q += 32) {
         const floatx4 av = ld4(arow + 4 * q);
 #pragma unroll
         for (int j = 0; j < DM; ++j) {
           if (j < O2) {
             const floatx4 w = ld4(Wl + j * HP + 4 * q);
-            o[j] = fmaf(av.x, w.x, fmaf(av.y, w.y, fmaf(av.z, w.z, fmaf(av.w, w.w, o[j]))));
+            acc[j] = fmaf(av.x, w.x, fmaf(av.y, w.y, fmaf(av.z, w.z, fmaf(av.w, w.w, acc[j]))));
           }
         }
       }
-      const float* bl = a.prm + wcb(L, k) + L.lin_b[L.NH];
+    }
 #pragma unroll
-      for (int j = 0; j < DM; ++j)
-        if (j < O2) o[j] = wave_sum(o[j]) + bl[j];
-      // block kt's input row as the coupling sees it
-      const float* xt = a.Xt + row * L.XP;
+    for (int j = 0; j < DM; ++j)
+      if (j < O2) part[(r * 32 + ln) * PS + j] = acc[j];
+    __syncthreads();
+    if (ln < O2) {
+      float s = 0.f;
 #pragma unroll
-      for (int i = 0; i < DM; ++i)
-        if (i < D) x[i] = xt[i];
-      float ssum = 0.f;
+      for (int l = 0; l < 32; ++l) s += part[(r * 32 + l) * PS + ln];
+      Os[ln] = s + a.prm[wcb(L, k) + L.lin_b[L.NH] + ln];
+    }
+    __syncthreads();
+    float sj = 0.f;
+    const bool anb = L.an && k < L.nb - 1;
+    const float* sc = a.prm + (long long)k * L.blk_stride;
+    if (lv) {
+      xi = a.Xt[row * L.XP + ln];
       if (!INV) {
-        if (L.an && k < L.nb - 1) {
-          const float* sc = a.prm + (long long)k * L.blk_stride;
-#pragma unroll
-          for (int i = 0; i < DM; ++i)
-            if (i < D) x[i] = sc[i] * x[i] + sc[D + i];        // ActNorm (cnf.py:350)
-        }
-#pragma unroll
-        for (int i = 0; i < DM / 2; ++i) {
-          if (i < Db) {
-            const float s = tanh_bf(o[Db + i]);
-            ssum += s;
-            x[Da + i] = fmaf(exp_fast(s), x[Da + i], o[i]);    // z_b = exp(s) y_b + t (cnf.py:179)
-            if (a.S && lane == 0) a.S[row * L.SP + i] = s;
-          }
-        }
-        float lj = a.ldj[row] + ssum;
-        if (k < L.nb - 1) {
-          // x <- x Q_k (cnf.py:333-335): lane j computes column j, then broadcast
-          const float* Q = a.pk + L.pk_q + (long long)k * D * D;
-          float cj = 0.f;
-          const int lj_ = lane < D ? lane : 0;
-#pragma unroll
-          for (int i = 0; i < DM; ++i)
-            if (i < D) cj = fmaf(x[i], Q[i * D + lj_], cj);
-#pragma unroll
-          for (int j = 0; j < DM; ++j)
-            if (j < D) x[j] = bcast(cj, j);
-          if (lane == 0) a.ldj[row] = lj;
-        } else {
-          // z and the per-sample NLL term 0.5 |z|^2 - ldj (utils.py:40-46)
-          float zz = 0.f;
-#pragma unroll
-          for (int i = 0; i < DM; ++i)
-            if (i < D) zz = fmaf(x[i], x[i], zz);
-          if (lane == 0) {
-            a.ldj[row] = lj;
-            if (a.nllp) a.nllp[row] = 0.5f * zz - lj;
-          }
+        if (anb) xi = sc[ln] * xi + sc[D + ln];                    // ActNorm (cnf.py:350)
+        if (ln >= Da) {
+          const int j = ln - Da;
+          sj = tanh_bf(Os[Db + j]);
+          xi = fmaf(exp_fast(sj), xi, Os[j]);                     // z_b = exp(s) y_b + t (cnf.py:179)
+          if (a.S) a.S[row * L.SP + j] = sj;
         }
       } else {
-#pragma unroll
-        for (int i = 0; i < DM / 2; ++i) {
-          if (i < Db) {
-            const float s = tanh_bf(o[Db + i]);
-            x[Da + i] = (x[Da + i] - o[i]) * exp_fast(-s);    // y_b = (z_b - t) exp(-s) (cnf.py:201)
-          }
+        if (ln >= Da) {
+          const int j = ln - Da;
+          xi = (xi - Os[j]) * exp_fast(-tanh_bf(Os[Db + j]));     // y_b = (z_b - t) exp(-s) (cnf.py:201)
         }
-        if (L.an && k < L.nb - 1) {
-          const float* sc = a.prm + (long long)k * L.blk_stride;
+        if (anb) xi = (xi - sc[D + ln]) / sc[ln];                 // ActNorm inverse (cnf.py:354)
+      }
+    }
+    if (!INV) {
+      const float ssum = half_sum(sj);
+      if (k < L.nb - 1) {                                         // x Q_k (cnf.py:333-335)
+        vs[ln] = xi;
+        __syncthreads();
+        float c = 0.f;
+        if (ln < D) {
 #pragma unroll
           for (int i = 0; i < DM; ++i)
-            if (i < D) x[i] = (x[i] - sc[D + i]) / sc[i];      // ActNorm inverse (cnf.py:354)
+            if (i < D) c = fmaf(vs[i], Qs[i * D + ln], c);
         }
-        if (k == 0) {
-          float mine = 0.f;
-#pragma unroll
-          for (int i = 0; i < DM; ++i)
-            if (i == lane) mine = x[i];
-          if (lane < D) a.z[row * D + lane] = mine;
+        xi = c;
+        if (valid && ln == 0) a.ldj[row] += ssum;
+      } else {
+        const float zz = half_sum(xi * xi);
+        if (lv) a.z[row * D + ln] = xi;
+        if (valid && ln == 0) {
+          const float lj = a.ldj[row] + ssum;
+          a.ldj[row] = lj;
+          if (a.nllp) a.nllp[row] = 0.5f * zz - lj;               // per-sample inn_nll_loss (utils.py:49-53)
         }
+      }
+    } else if (k == 0 && lv) {
+      a.z[row * D + ln] = xi;
+    }
+  } else {
+    if (lv) xi = a.xin[row * D + ln];
+    if (!INV && valid && ln == 0) a.ldj[row] = 0.f;
+  }
+  // ------------------------------------------------------------ head of block kh
+  if (a.kh >= 0) {
+    const int k = a.kh;
+    if (!INV) {
+      if (lv) a.Xh[row * L.XP + ln] = xi;                         // saved pre-ActNorm input
+      if (L.an && k < L.nb - 1) {
+        const float* sc = a.prm + (long long)k * L.blk_stride;
+        if (ln < D) xi = sc[ln] * xi + sc[D + ln];
+        if (valid && ln == 0) a.ldj[row] += a.pk[L.pk_ldc + k];   // ActNorm log|det J| (cnf.py:349)
       }
     } else {
-      const float* xr = a.xin + row * D;
+      if (k < L.nb - 1) {                                         // v = x Q_k^T (cnf.py:337-339)
+        vs[ln] = xi;
+        __syncthreads();
+        float c = 0.f;
+        if (ln < D) {
 #pragma unroll
-      for (int i = 0; i < DM; ++i)
-        if (i < D) x[i] = xr[i];
-      if (!INV && lane == 0) a.ldj[row] = 0.f;
-    }
-    // the last-block store above used x[lane]: redo it with a register select (no dynamic indexing)
-    if (!INV && a.kt == L.nb - 1) {
-      float mine = 0.f;
-#pragma unroll
-      for (int i = 0; i < DM; ++i)
-        if (i == lane) mine = x[i];
-      if (lane < D) a.z[row * D + lane] = mine;
-    }
-    // ------------------------------------------------------------ head of block kh
-    if (a.kh >= 0) {
-      const int k = a.kh;
-      float u[DM / 2];
-      {
-        float mine = 0.f;
-#pragma unroll
-        for (int i = 0; i < DM; ++i)
-          if (i == lane) mine = x[i];
-        if (!INV) {
-          if (lane < D) a.Xh[row * L.XP + lane] = mine;        // saved pre-ActNorm input
-          if (L.an && k < L.nb - 1) {
-            const float* sc = a.prm + (long long)k * L.blk_stride;
-#pragma unroll
-            for (int i = 0; i < DM; ++i)
-              if (i < D) x[i] = sc[i] * x[i] + sc[D + i];
-            if (lane == 0) a.ldj[row] += a.pk[L.pk_ldc + k];  // ActNorm log|det J| (cnf.py:349)
-          }
-        } else {
-          if (k < L.nb - 1) {
-            // v = x Q_k^T (cnf.py:337-339): lane i computes v_i = sum_j x_j Q[i][j]
-            const float* Q = a.pk + L.pk_q + (long long)k * D * D;
-            float ci = 0.f;
-            const int li_ = lane < D ? lane : 0;
-#pragma unroll
-            for (int j = 0; j < DM; ++j)
-              if (j < D) ci = fmaf(x[j], Q[li_ * D + j], ci);
-#pragma unroll
-            for (int j = 0; j < DM; ++j)
-              if (j < D) x[j] = bcast(ci, j);
-            mine = 0.f;
-#pragma unroll
-            for (int i = 0; i < DM; ++i)
-              if (i == lane) mine = x[i];
-          }
-          if (lane < D) a.Xh[row * L.XP + lane] = mine;        // v, read back by this block's tail
+          for (int j = 0; j < DM; ++j)
+            if (j < D) c = fmaf(vs[j], Qs[ln * D + j], c);
         }
-#pragma unroll
-        for (int i = 0; i < DM / 2; ++i) u[i] = i < Da ? x[i] : 0.f;
-        if (a.U && lane < L.UP) {
-          float uv = 0.f;
-#pragma unroll
-          for (int i = 0; i < DM / 2; ++i)
-            if (i == lane) uv = u[i];
-          a.U[row * L.UP + lane] = lane < Da ? uv : (lane == Da ? 1.f : 0.f);
-        }
+        xi = c;
       }
-      const float* b0 = a.prm + wcb(L, k) + L.lin_b[0];
+      if (lv) a.Xh[row * L.XP + ln] = xi;                         // v, read back by this block's tail
+    }
+    us[ln] = xi;
+    __syncthreads();
+    float ua[DM / 2];
+#pragma unroll
+    for (int j = 0; j < DM / 2; ++j) ua[j] = j < Da ? us[j] : 0.f;
+    if (a.U && valid && ln < L.UP) a.U[row * L.UP + ln] = ln < Da ? us[ln] : (ln == Da ? 1.f : 0.f);
+    if (valid) {
+      const float* b0 = a.pk + L.pk_b0 + (long long)k * HP;
       const long long prow = a.cidx ? a.cidx[row] : row;
       const float* Pr = a.P + prow * a.ldP + (long long)k * HP;
       const uint32_t tag = (uint32_t)k * 16u;
-      for (int q = lane; q < nq; q += 64) {
+      for (int q = ln; q < nq; q += 32) {
         const int n = 4 * q;
-        floatx4 pre = ld4(Pr + n);
+        floatx4 pre = ld4(Pr + n) + ld4(b0 + n);
 #pragma unroll
         for (int j = 0; j < DM / 2; ++j) {
           if (j < Da) {
             const floatx4 w = ld4(W0 + j * HP + n);
-            pre.x = fmaf(u[j], w.x, pre.x);
-            pre.y = fmaf(u[j], w.y, pre.y);
-            pre.z = fmaf(u[j], w.z, pre.z);
-            pre.w = fmaf(u[j], w.w, pre.w);
+            pre.x = fmaf(ua[j], w.x, pre.x);
+            pre.y = fmaf(ua[j], w.y, pre.y);
+            pre.z = fmaf(ua[j], w.z, pre.z);
+            pre.w = fmaf(ua[j], w.w, pre.w);
           }
         }
         uint4 rnd = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
-        if (a.rng) rnd = drop4(a.rng, seed, offs, row, n, tag);
+        if (a.rng) rnd = drop4(seed, offs, row, n, tag);
         float av[4], gv[4];
         const float pv[4] = {pre.x, pre.y, pre.z, pre.w};
         const uint32_t rv[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int c = n + e;
-          if (c < H) {
-            float ge, dg;
-            gelu_fg(pv[e] + b0[c], ge, dg);
-            const float m = a.rng ? (rv[e] >= L.thresh ? L.keep_scale : 0.f) : 1.f;
-            av[e] = ge * m;
-            gv[e] = dg * m;
-          } else {
-            av[e] = c == H ? 1.f : 0.f;
-            gv[e] = 0.f;
-          }
+          float ge, dg;
+          gelu_fg(pv[e], ge, dg);
+          const float m = (c < H) ? (a.rng ? (rv[e] >= L.thresh ? L.keep_scale : 0.f) : 1.f) : 0.f;
+          av[e] = c == H ? 1.f : ge * m;
+          gv[e] = dg * m;
         }
         st4(a.A0 + row * HP + n, floatx4{av[0], av[1], av[2], av[3]});
         if (a.G0) st4(a.G0 + row * HP + n, floatx4{gv[0], gv[1], gv[2], gv[3]});
@@ -714,152 +769,115 @@ struct LinkBArgs {
   float* dZl;  long long ldZl;        // dZ_{NH-1} of block kh
 };
 
+template <int DD>
 __global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const LinkBArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int HP = L.HP, H = L.H, D = L.D, Da = L.Da, Db = L.Db, O2 = 2 * Db;
-  float* W0 = sm;                                   // [Da][HP] W0y^T of block kt
-  float* Wl = sm + (a.kt >= 0 ? Da * HP : 0);       // [2Db][HP] last Linear of block kh
-  if (a.kt >= 0) {
-    const float* src = a.pk + L.pk_w0y + (long long)a.kt * Da * HP;
-    for (int e = tid; e < Da * HP / 4; e += WWG) st4(W0 + 4 * e, ld4(src + 4 * e));
-  }
+  const int tid = threadIdx.x, ln = tid & 31, r = tid >> 5;
+  const int HP = L.HP;
+  const int D = DD ? DD : L.D, Da = DD ? (DD + 1) / 2 : L.Da, Db = DD ? DD / 2 : L.Db, O2 = 2 * Db;
+  const int PS = link_ps(L);
+  const int nq = HP / 4;
+  float* Wl = sm;                                   // [2Db][HP] last Linear of block kh
+  float* W0 = Wl + (a.kh >= 0 ? O2 * HP : 0);       // [Da][HP] W0y^T of block kt
+  float* Qs = W0 + (a.kt >= 0 ? Da * HP : 0);
+  float* part = Qs + pad4(D * D);
+  float* Os = part + pad4(LR * 32 * PS) + r * 96;
+  float* vs = Os + 32;
+  if (a.kt >= 0) stage4(W0, a.pk + L.pk_w0y + (long long)a.kt * Da * HP, Da * HP / 4);
   if (a.kh >= 0) {
-    const float* src = a.pk + L.pk_wl + (long long)a.kh * O2 * HP;
-    for (int e = tid; e < O2 * HP / 4; e += WWG) st4(Wl + 4 * e, ld4(src + 4 * e));
+    stage4(Wl, a.pk + L.pk_wl + (long long)a.kh * O2 * HP, O2 * HP / 4);
+    if (a.kh < L.nb - 1)
+      for (int e = tid; e < D * D; e += WWG) Qs[e] = a.pk[L.pk_q + (long long)a.kh * D * D + e];
   }
   __syncthreads();
-  const long long row0 = ((long long)blockIdx.x * 4 + wave) * LINK_ROWS;
-  if (row0 >= a.B) return;
-  const int nq = HP / 4;
-  float gscale = 1.f;
-  if (a.nll) gscale = (a.dvals ? a.dvals[0] + a.dvals[1] : 1.f) / (float)a.B;
-
-  for (int rr = 0; rr < LINK_ROWS; ++rr) {
-    const long long row = row0 + rr;
-    if (row >= a.B) break;
-    float dx[DM];
-    // ------------------------------------------------------------ tail-B of block kt
-    if (a.kt >= 0) {
-      const int k = a.kt;
-      float da[DM / 2];
+  const long long row = (long long)blockIdx.x * LR + r;
+  const bool valid = row < a.B;
+  const bool lv = valid && ln < D;
+  const float gscale = a.nll ? (a.dvals ? a.dvals[0] + a.dvals[1] : 1.f) / (float)a.B : 0.f;
+  float dxi = 0.f;                                  // element ln of the gradient w.r.t. the current D-vector
+  // ------------------------------------------------------------ tail-B of block kt
+  if (a.kt >= 0) {
+    const int k = a.kt;
+    float acc[DM / 2];
 #pragma unroll
-      for (int j = 0; j < DM / 2; ++j) da[j] = 0.f;
+    for (int j = 0; j < DM / 2; ++j) acc[j] = 0.f;
+    if (valid) {
       const float* zr = a.dZ0 + row * a.ldZ0;
-      for (int q = lane; q < nq; q += 64) {
+      for (int q = ln; q < nq; q += 32) {
         const floatx4 dzv = ld4(zr + 4 * q);
 #pragma unroll
         for (int j = 0; j < DM / 2; ++j) {
           if (j < Da) {
             const floatx4 w = ld4(W0 + j * HP + 4 * q);
-            da[j] = fmaf(dzv.x, w.x, fmaf(dzv.y, w.y, fmaf(dzv.z, w.z, fmaf(dzv.w, w.w, da[j]))));
+            acc[j] = fmaf(dzv.x, w.x, fmaf(dzv.y, w.y, fmaf(dzv.z, w.z, fmaf(dzv.w, w.w, acc[j]))));
           }
         }
-      }
-      const float* dvr = a.DV + row * L.XP;
-#pragma unroll
-      for (int i = 0; i < DM; ++i) dx[i] = 0.f;
-#pragma unroll
-      for (int j = 0; j < DM / 2; ++j)
-        if (j < Da) dx[j] = wave_sum(da[j]) + dvr[j];
-#pragma unroll
-      for (int i = 0; i < DM / 2; ++i)
-        if (i < Db) dx[Da + i] = dvr[Da + i];
-      if (L.an && k < L.nb - 1) {
-        const float* sc = a.prm + (long long)k * L.blk_stride;
-        const float* xr = a.X + k * a.sX + row * L.XP;
-        float mine_s = 0.f, mine_b = 0.f;
-#pragma unroll
-        for (int i = 0; i < DM; ++i) {
-          if (i < D) {
-            if (i == lane) {
-              mine_s = dx[i] * xr[i];
-              mine_b = dx[i];
-            }
-            dx[i] *= sc[i];                                     // d x = d u * scale
-          }
-        }
-        if (lane < D) {
-          a.ANP[row * L.AP + lane] = mine_s;
-          a.ANP[row * L.AP + D + lane] = mine_b;
-        }
-      }
-      if (k == 0 && a.dy) {
-        float mine = 0.f;
-#pragma unroll
-        for (int i = 0; i < DM; ++i)
-          if (i == lane) mine = dx[i];
-        if (lane < D) a.dy[row * D + lane] = mine;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < DM; ++i) dx[i] = 0.f;
-      if (a.nll) {
-        const float* zr = a.zn + row * D;
-#pragma unroll
-        for (int i = 0; i < DM; ++i)
-          if (i < D) dx[i] = zr[i] * gscale;
-      } else if (a.dz) {
-        const float* zr = a.dz + row * D;
-#pragma unroll
-        for (int i = 0; i < DM; ++i)
-          if (i < D) dx[i] = zr[i];
       }
     }
-    // ------------------------------------------------------------ head-B of block kh
-    if (a.kh >= 0) {
-      const int k = a.kh;
-      if (k < L.nb - 1) {
-        const float* Q = a.pk + L.pk_q + (long long)k * D * D;
-        float ci = 0.f;
-        const int li_ = lane < D ? lane : 0;
 #pragma unroll
-        for (int j = 0; j < DM; ++j)
-          if (j < D) ci = fmaf(dx[j], Q[li_ * D + j], ci);
+    for (int j = 0; j < DM / 2; ++j)
+      if (j < Da) part[(r * 32 + ln) * PS + j] = acc[j];
+    __syncthreads();
+    if (lv) {
+      float du = a.DV[row * L.XP + ln];
+      if (ln < Da) {
+        float t = 0.f;
 #pragma unroll
-        for (int j = 0; j < DM; ++j)
-          if (j < D) dx[j] = bcast(ci, j);
+        for (int l = 0; l < 32; ++l) t += part[(r * 32 + l) * PS + ln];
+        du += t;                                                  // du_a = dv_a + dZ_0 W0y
       }
-      float dl = a.nll ? -gscale : (a.dldj ? a.dldj[row] : 0.f);
-      const float* xr = a.X + k * a.sX + row * L.XP;
-      const float* sr = a.S + k * a.sS + row * L.SP;
-      const bool anb = L.an && k < L.nb - 1;
-      const float* sc = a.prm + (long long)k * L.blk_stride;
+      if (L.an && k < L.nb - 1) {
+        const float* sc = a.prm + (long long)k * L.blk_stride;
+        const float xk = a.X[k * a.sX + row * L.XP + ln];
+        a.ANP[row * L.AP + ln] = du * xk;                        // dscale partial
+        a.ANP[row * L.AP + D + ln] = du;                         // dbias partial
+        du *= sc[ln];
+      }
+      dxi = du;
+      if (k == 0 && a.dy) a.dy[row * D + ln] = dxi;
+    }
+  } else if (lv) {
+    dxi = a.nll ? a.zn[row * D + ln] * gscale : (a.dz ? a.dz[row * D + ln] : 0.f);
+  }
+  // ------------------------------------------------------------ head-B of block kh
+  if (a.kh >= 0) {
+    const int k = a.kh;
+    if (k < L.nb - 1) {                                           // dv = dX Q_k^T
+      vs[ln] = dxi;
+      __syncthreads();
+      float c = 0.f;
+      if (ln < D) {
+#pragma unroll
+        for (int j = 0; j < DM; ++j)
+          if (j < D) c = fmaf(vs[j], Qs[ln * D + j], c);
+      }
+      dxi = c;
+    }
+    float dvo = dxi;
+    if (lv && ln >= Da) {
+      const int j = ln - Da;
+      const float dl = a.nll ? -gscale : (a.dldj ? a.dldj[row] : 0.f);
+      float ub = a.X[k * a.sX + row * L.XP + ln];
+      if (L.an && k < L.nb - 1) {
+        const float* sc = a.prm + (long long)k * L.blk_stride;
+        ub = sc[ln] * ub + sc[D + ln];
+      }
+      const float s = a.S[k * a.sS + row * L.SP + j];
+      const float es = exp_fast(s);
+      dvo = dxi * es;                                             // du_b
+      Os[j] = dxi;                                                // dt
+      Os[Db + j] = fmaf(dxi * ub, es, dl) * (1.f - s * s);        // d s' (through tanh and the log-det)
+    }
+    if (valid && ln < L.XP) a.DV[row * L.XP + ln] = ln < D ? dvo : 0.f;
+    __syncthreads();
+    if (valid) {
+      if (ln < L.OP) a.Ob[row * L.OP + ln] = ln < O2 ? Os[ln] : 0.f;
       float dO[DM];
 #pragma unroll
-      for (int j = 0; j < DM; ++j) dO[j] = 0.f;
-      float dub[DM / 2];
-#pragma unroll
-      for (int i = 0; i < DM / 2; ++i) {
-        dub[i] = 0.f;
-        if (i < Db) {
-          float ub = xr[Da + i];
-          if (anb) ub = sc[Da + i] * ub + sc[D + Da + i];
-          const float s = sr[i];
-          const float es = exp_fast(s);
-          const float dvb = dx[Da + i];
-          dub[i] = dvb * es;
-          const float ds = fmaf(dvb * ub, es, dl);
-          dO[i] = dvb;                                   // dt
-          dO[Db + i] = ds * (1.f - s * s);               // d s' through tanh
-        }
-      }
-      {
-        float mo = 0.f, mv = 0.f;
-#pragma unroll
-        for (int j = 0; j < DM; ++j)
-          if (j == lane) mo = dO[j];
-#pragma unroll
-        for (int i = 0; i < DM / 2; ++i) {
-          if (i == lane && i < Da) mv = dx[i];
-          if (i < Db && lane == Da + i) mv = dub[i];
-        }
-        if (lane < L.OP) a.Ob[row * L.OP + lane] = lane < O2 ? mo : 0.f;
-        if (lane < L.XP) a.DV[row * L.XP + lane] = lane < D ? mv : 0.f;
-      }
+      for (int j = 0; j < DM; ++j) dO[j] = j < O2 ? Os[j] : 0.f;
       const float* gr = a.Gl + row * HP;
       float* out = a.dZl + row * a.ldZl;
-      for (int q = lane; q < nq; q += 64) {
+      for (int q = ln; q < nq; q += 32) {
         const int n = 4 * q;
         floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -872,12 +890,10 @@ __global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const Lin
             s4.w = fmaf(dO[j], w.w, s4.w);
           }
         }
-        const floatx4 gv = ld4(gr + n);
-        st4(out + n, floatx4{s4.x * gv.x, s4.y * gv.y, s4.z * gv.z, s4.w * gv.w});
+        st4(out + n, s4 * ld4(gr + n));
       }
     }
   }
-  (void)H;
 }
 
 // ActNorm gradients of every block: dscale_i = sum_b du_i x_i + (sum_b dldj_b) / scale_i  (the log|scale| term of
@@ -910,8 +926,15 @@ __global__ __launch_bounds__(WWG) void k_wactnorm_grad(const WideLayout L, const
   // columns: 4 row phases x 64 columns
   const int c = tid & 63, ph = tid >> 6;
   float s = 0.f;
-  if (c < ncol)
-    for (long long r = ph; r < B; r += 4) s += P[r * L.AP + c];
+  if (c < ncol) {                      // 8 independent chains per thread keep 8 loads in flight
+    float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    long long r = ph;
+    for (; r + 28 < B; r += 32)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s8[u] += P[(r + 4 * u) * L.AP + c];
+    for (; r < B; r += 4) s8[0] += P[r * L.AP + c];
+    s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
+  }
   __syncthreads();
   red[tid] = s;
   __syncthreads();
@@ -985,15 +1008,39 @@ int launch_cfg(const GemmArgs& g, int groups, hipStream_t st) {
   return bcnf_rt::launched();
 }
 
-// Tile choice: 128x128 when that still gives >= 2 workgroups per CU (256 CUs), else 64x64.
+template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI>
+int launch_cfg16(const GemmArgs& g, int groups, hipStream_t st) {
+  dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, groups);
+  hipLaunchKernelGGL((k_wgemm16<BM, BN, BK, AKC, BKC, EPI>), grid, dim3(WWG), 0, st, g);
+  return bcnf_rt::launched();
+}
+
+constexpr int N_CU = 256;
+// Modelled time of a tiling: rounds of one workgroup per CU (MI355X: 256 CUs) x tile area / relative efficiency.
+double tile_cost(const GemmArgs& g, int groups, int BM, int BN, double eff) {
+  const long long wgs = (long long)((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN) * groups;
+  return (double)((wgs + N_CU - 1) / N_CU) * BM * BN / eff;
+}
+
+int g_force_tiling = -1;   // test hook: 0 = 128x128, 1 = 64x64, 2 = 128x48 (16x16 MFMA)
+
 template <bool AKC, bool BKC, int EPI>
 int gemm(const GemmArgs& g, int groups, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0 || groups <= 0) return BCNF_OK;
   if ((g.lda & 3) || (g.ldb & 3) || (!aligned16(g.A)) || (!aligned16(g.B))) return BCNF_ERR_ARG;
   if ((AKC || BKC) && (g.K & 3)) return BCNF_ERR_ARG;
-  const long long t128 = (long long)((g.M + 127) / 128) * ((g.N + 127) / 128) * groups;
-  if (t128 >= 512) return launch_cfg<128, 128, 16, AKC, BKC, EPI>(g, groups, st);
-  return launch_cfg<64, 64, 32, AKC, BKC, EPI>(g, groups, st);
+  int pick = g_force_tiling;
+  if (pick < 0) {
+    // relative efficiencies per operand layout, measured at 4096^3 on MI355X (tools/gemm_bench.py)
+    const double e1 = AKC ? (BKC ? 1.06 : 0.88) : 0.78, e2 = AKC ? (BKC ? 0.86 : 0.70) : 0.60;
+    const double c0 = tile_cost(g, groups, 128, 128, 1.0);
+    const double c1 = tile_cost(g, groups, 64, 64, e1);
+    const double c2 = tile_cost(g, groups, 128, 48, e2);
+    pick = (c0 <= c1 && c0 <= c2) ? 0 : (c2 <= c1 ? 2 : 1);
+  }
+  if (pick == 0) return launch_cfg<128, 128, 16, AKC, BKC, EPI>(g, groups, st);
+  if (pick == 2) return launch_cfg16<128, 48, 64, AKC, BKC, EPI>(g, groups, st);
+  return launch_cfg<64, 64, 64, AKC, BKC, EPI>(g, groups, st);
 }
 
 struct WideWs {       // workspace carve-up (floats)
@@ -1032,33 +1079,33 @@ WideWs carve(const WideLayout& L, long long B, bool train, float* base) {
   return w;
 }
 
-size_t link_lds(const WideLayout& L, bool tail, bool head) {
-  return (size_t)((tail ? 2 * L.Db * L.HP : 0) + (head ? L.Da * L.HP : 0)) * sizeof(float);
-}
-
 int link_launch(const WideLayout& L, const LinkArgs& a, bool inv, hipStream_t st) {
-  const int rows_per_wg = 4 * LINK_ROWS;
-  dim3 grid((unsigned)((a.B + rows_per_wg - 1) / rows_per_wg));
-  const size_t lds = link_lds(L, a.kt >= 0, a.kh >= 0);
-  if (inv) hipLaunchKernelGGL(k_wlink<true>, grid, dim3(WWG), lds, st, L, a);
-  else hipLaunchKernelGGL(k_wlink<false>, grid, dim3(WWG), lds, st, L, a);
+  dim3 grid((unsigned)((a.B + LR - 1) / LR));
+  const size_t lds = (size_t)link_lds_floats(L, a.kt >= 0, a.kh >= 0) * sizeof(float);
+  if (L.D == 19) {                       // every shipped trajectory config (19 physical parameters)
+    if (inv) hipLaunchKernelGGL((k_wlink<true, 19>), grid, dim3(WWG), lds, st, L, a);
+    else hipLaunchKernelGGL((k_wlink<false, 19>), grid, dim3(WWG), lds, st, L, a);
+  } else {
+    if (inv) hipLaunchKernelGGL((k_wlink<true, 0>), grid, dim3(WWG), lds, st, L, a);
+    else hipLaunchKernelGGL((k_wlink<false, 0>), grid, dim3(WWG), lds, st, L, a);
+  }
   return bcnf_rt::launched();
 }
 
 int linkb_launch(const WideLayout& L, const LinkBArgs& a, hipStream_t st) {
-  const int rows_per_wg = 4 * LINK_ROWS;
-  dim3 grid((unsigned)((a.B + rows_per_wg - 1) / rows_per_wg));
-  const size_t lds = (size_t)((a.kt >= 0 ? L.Da * L.HP : 0) + (a.kh >= 0 ? 2 * L.Db * L.HP : 0)) * sizeof(float);
-  hipLaunchKernelGGL(k_wlink_bwd, grid, dim3(WWG), lds, st, L, a);
+  dim3 grid((unsigned)((a.B + LR - 1) / LR));
+  const size_t lds = (size_t)link_lds_floats(L, a.kh >= 0, a.kt >= 0) * sizeof(float);
+  if (L.D == 19) hipLaunchKernelGGL((k_wlink_bwd<19>), grid, dim3(WWG), lds, st, L, a);
+  else hipLaunchKernelGGL((k_wlink_bwd<0>), grid, dim3(WWG), lds, st, L, a);
   return bcnf_rt::launched();
 }
 
 bool lds_attr_done = false;
 void ensure_lds_attrs() {
   if (lds_attr_done) return;
-  (void)hipFuncSetAttribute((const void*)k_wlink<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute((const void*)k_wlink<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute((const void*)k_wlink_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  const void* fns[] = {(const void*)k_wlink<true, 0>, (const void*)k_wlink<false, 0>, (const void*)k_wlink<true, 19>,
+                       (const void*)k_wlink<false, 19>, (const void*)k_wlink_bwd<0>, (const void*)k_wlink_bwd<19>};
+  for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   lds_attr_done = true;
 }
 
@@ -1351,6 +1398,8 @@ int bcnf_wide_pack(const BcnfStackDesc* desc, const float* params, const float* 
   hipLaunchKernelGGL(k_wpack, dim3(grid), dim3(WWG), 0, st, L, params, qmats, (float*)packed);
   WCHK(bcnf_rt::launched());
   hipLaunchKernelGGL(k_wpack_ldc, dim3(1), dim3(((L.nb + 63) / 64) * 64), 0, st, L, params, (float*)packed);
+  WCHK(bcnf_rt::launched());
+  hipLaunchKernelGGL(k_wpack_b0, dim3(L.nb), dim3(WWG), 0, st, L, params, (float*)packed);
   return bcnf_rt::launched();
 }
 
@@ -1413,11 +1462,25 @@ int bcnf_wide_inverse(const BcnfStackDesc* desc, const float* params, const void
                       (float*)scratch, (hipStream_t)stream);
 }
 
+// Tiling override for every wide GEMM launch (-1 = the cost model's choice; 0 = 128x128, 1 = 64x64, 2 = 128x48).
+int bcnf_wide_force_tiling(int32_t tiling) {
+  const int prev = g_force_tiling;
+  g_force_tiling = (tiling >= 0 && tiling <= 2) ? tiling : -1;
+  return prev;
+}
+
 // Test hook: one plain GEMM through the tile machinery. layout: 0 = NT (A[m][k], B[n][k]), 1 = NN (A[m][k], B[k][n]),
 // 2 = TN (A[k][m], B[k][n]).
 int bcnf_wide_gemm_test(int32_t layout, int32_t M, int32_t N, int32_t K, const float* A, int64_t lda, const float* B,
                         int64_t ldb, float* C, int64_t ldc, void* stream) {
   GemmArgs g = gemm_args(M, N, K, A, lda, B, ldb, C, ldc);
+  const int prev = g_force_tiling;
+  if (layout >> 4) g_force_tiling = (layout >> 4) - 1;      // layout bits 4..: tiling + 1 (0 = current choice)
+  layout &= 15;
+  struct Reset {
+    int p;
+    ~Reset() { g_force_tiling = p; }
+  } reset{prev};
   hipStream_t st = (hipStream_t)stream;
   if (layout == 0) return gemm<true, true, EPI_STORE>(g, 1, st);
   if (layout == 1) return gemm<true, false, EPI_STORE>(g, 1, st);

@@ -44,6 +44,32 @@ BWD_FLOP_PER_SAMPLE = 2 * 220_087
 # Minimal HBM bytes per sample of the fused kernels (inputs + outputs + saved block inputs / masks):
 #   forward (train): y 76 + h 320 + z 76 + ldj 4 + ysave 32*128 + masks 8*64        = 5,164 B
 #   backward       : h 320 + dz 76 + dldj 4 + ysave 4,096 + masks 512 + dh 320 + slab share = 5,328 B + slab
+# trajectory_FC_large / trajectory_LSTM_large (configs/runs/old/*.yaml): the wide-MLP family (bcnf_wide.hip)
+FC_LARGE = {
+    "global": FC_SMALL["global"],
+    "model": {"kwargs": {"size": 19, "nested_sizes": [526] * 5, "n_conditions": 1360, "n_blocks": 26,
+                         "dropout": 0.407, "act_norm": True}},
+    "feature_networks": [
+        {"type": "ConcatenateCondition", "kwargs": {"input_size": None, "output_size": 90}},
+        {"type": "FullyConnected", "kwargs": {"sizes": [90] + [310] * 7 + [1360], "dropout": 0.111}},
+    ],
+}
+LSTM_LARGE = {
+    "global": FC_SMALL["global"],
+    "model": {"kwargs": {"size": 19, "nested_sizes": [526] * 5, "n_conditions": 1360, "n_blocks": 26,
+                         "dropout": 0.407, "act_norm": True, "random_state": 2024_03_25}},
+    "feature_networks": [
+        {"type": "ConcatenateCondition", "kwargs": {"input_size": None, "output_size": 3}},
+        {"type": "LSTM", "kwargs": {"input_size": 3, "hidden_size": 140, "output_size": 1360, "num_layers": 2,
+                                    "dropout": 0.111, "bidirectional": True, "pooling": "mean", "pool_dim": 1}},
+    ],
+}
+# training FLOPs per sample (2 x MAC, forward + dX + dW of every Linear of the flow; feature net excluded)
+#   flow forward = 26 * (1370*526 + 4*526*526 + 526*18) + 25 * 19*19 = 47,765,617 MAC
+WIDE_FWD_FLOP_PER_SAMPLE = 2 * 47_765_617
+WIDE_TRAIN_FLOP_PER_SAMPLE = 3 * WIDE_FWD_FLOP_PER_SAMPLE
+WIDE_NAMES = {"fc_large": "trajectory_FC_large", "lstm_large": "trajectory_LSTM_large"}
+WORKLOADS = {"fc_small": (FC_SMALL, 4096), "fc_large": (FC_LARGE, 2048), "lstm_large": (LSTM_LARGE, 1024)}
 PEAK_FP32_TFLOPS = 157.3       # MI355X fp32 (vector = MFMA f32), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
 
@@ -53,7 +79,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=4096, help="samples per GPU (weak scaling)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="fc_small",
+                    help="fc_small = the headline metric (configs[1]); fc_large / lstm_large = configs[2] / [3] per GPU")
+    ap.add_argument("--batch", type=int, default=None, help="samples per GPU (weak scaling; default per workload)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=12)
@@ -135,6 +163,10 @@ def kernel_timing(model, data, args):
 
 def main():
     args = parse()
+    if args.batch is None:
+        args.batch = WORKLOADS[args.workload][1]
+    if args.workload != "fc_small":
+        return main_wide(args)
     world, rank, local = init_dist(args)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
@@ -217,6 +249,103 @@ def main():
         }
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline_wide(args, cfg, batch=256, steps=4):
+    """CPU oracle training step of the wide workload (FC_large shapes) on this host, bounded: B=256, a few steps."""
+    from oracle import cnf_oracle as O
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(2024_03_25)
+    from bcnf_amd import CondRealNVP_v2
+    m = CondRealNVP_v2.from_config(cfg)
+    kw = cfg["model"]["kwargs"]
+    fs = cfg["feature_networks"][1]["kwargs"]
+    spec = O.StackSpec(size=19, nested_sizes=kw["nested_sizes"], n_blocks=kw["n_blocks"],
+                       n_conditions=kw["n_conditions"], dropout=kw["dropout"], act_norm=kw["act_norm"],
+                       feature_sizes=fs["sizes"], feature_dropout=fs["dropout"])
+    sd = {k: v.detach().clone().requires_grad_(not k.endswith("orthonormal_matrix")) for k, v in m.state_dict().items()}
+    opt = torch.optim.Adam([v for v in sd.values() if v.requires_grad], lr=2e-4)
+    g = torch.Generator().manual_seed(7)
+    y = torch.randn(batch, 19, generator=g)
+    traj = torch.randn(batch, 30, 3, generator=g)
+    times = []
+    for _ in range(1 + steps):
+        t0 = time.perf_counter()
+        O.train_step_cpu(sd, spec, y, traj, opt, training=True)
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times[1:])
+    return {"value": round(batch / med, 1), "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/cnf_oracle.train_step_cpu, {args.workload} B={batch}, dropout on, median of {steps} "
+                      f"steps after 1 warmup, {threads} threads, {med * 1e3:.0f} ms/step"}
+
+
+def main_wide(args):
+    """NLL-training samples/s of the wide workloads (trajectory_FC_large = configs[2], trajectory_LSTM_large =
+    configs[3]) per GPU, same step definition and timing contract as main()."""
+    world, rank, local = init_dist(args)
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    from bcnf_amd import CondRealNVP_v2
+    from bcnf_amd.data import DeviceBatches
+    from bcnf_amd.train import TrainStep
+    cfg = WORKLOADS[args.workload][0]
+    torch.manual_seed(2024_03_25)
+    model = CondRealNVP_v2.from_config(cfg).to(device)
+    model.train()
+    model.fused.set_seed(2024_03_25 + 7919 * rank)
+    data = DeviceBatches(max(16384, 4 * args.batch), args.batch, device, seed=2024_03_25 + rank)
+    step = TrainStep(model, lr=2e-4, capture=not args.no_graph)
+    step.broadcast_parameters()
+    step.set_pool(data.y, data.traj)
+    batches = [data.next_indices() for _ in range(args.warmup + args.steps)]
+    step.set_epoch(torch.cat(batches), args.batch)
+    step.run_epoch(args.warmup)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    vals = step.run_epoch(args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    value = world * args.batch * args.steps / dt
+    kern = kernel_timing(model, data, args) if rank == 0 else {}
+    if rank == 0:
+        B = args.batch
+        flop_step = WIDE_TRAIN_FLOP_PER_SAMPLE * B
+        achieved = flop_step / (dt / args.steps) / 1e12
+        fb_us = kern.get("forward", float("nan")) + kern.get("backward", float("nan"))
+        kw = cfg["model"]["kwargs"]
+        line = {
+            "metric": f"NLL-training samples/sec, {WIDE_NAMES[args.workload]}",
+            "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic ballistic trajectories (bcnf_amd/data.py), device-resident",
+            "config": {"workload": f"trajectory_{args.workload} NLL training step", "batch_per_gpu": B,
+                       "global_batch": B * world, "parallelism": f"dp{world}", "hip_graph": not args.no_graph,
+                       "n_blocks": kw["n_blocks"], "nested_sizes": kw["nested_sizes"],
+                       "n_conditions": kw["n_conditions"], "dropout": kw["dropout"]},
+            "last_loss": vals[-1][0] if vals else None,
+            "roofline": {"bound": "mfma", "kernel": "coupling stack forward+backward (all launches)",
+                         "achieved": round(WIDE_TRAIN_FLOP_PER_SAMPLE * B / (fb_us * 1e-6) / 1e12, 3),
+                         "achieved_whole_step": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(WIDE_TRAIN_FLOP_PER_SAMPLE * B / (fb_us * 1e-6) / 1e12 / PEAK_FP32_TFLOPS, 4),
+                         "traffic": None, "flop_per_step": flop_step},
+            "kernels_us": {k: round(v, 2) for k, v in kern.items()},
+        }
+        if not args.no_cpu_baseline and args.workload == "fc_large":
+            line["cpu_baseline"] = cpu_baseline_wide(args, cfg)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -41,7 +41,7 @@ extern "C" {
 #endif
 
 #define BCNF_MAX_HIDDEN 8
-#define BCNF_MAX_TENSORS 16
+#define BCNF_MAX_TENSORS 48
 
 enum {
   BCNF_OK = 0,
@@ -153,8 +153,8 @@ int bcnf_nll_backward(const BcnfStackDesc* desc, const void* packed, const float
 
 /* ---- Optimizer ------------------------------------------------------------------------------------
  * Tensors are passed as arrays of n_tensors (<= BCNF_MAX_TENSORS) device pointers + element counts and
- * treated as one concatenated index space. bcnf_grad_partials(total) = number of per-workgroup partial
- * sums of squared gradients the kernels below write / read. */
+ * treated as one concatenated index space. bcnf_grad_partials(total) = floats of the partials buffer the kernels
+ * below write / read: one sum of squared gradients per workgroup, plus one slot for their pre-reduced total. */
 int64_t bcnf_grad_partials(int64_t total_numel);
 
 /* One torch.optim.Adam step (amsgrad = maximize = False) over every tensor; hyper-parameters are
@@ -253,8 +253,13 @@ int bcnf_wide_backward(const BcnfStackDesc* desc, const float* params, const voi
 int bcnf_wide_inverse(const BcnfStackDesc* desc, const float* params, const void* packed, const float* z,
                       const float* h, int64_t h_rows, const int64_t* cond_index, int64_t n_rows, float* y,
                       int32_t training, const uint64_t* rng_state, void* scratch, void* stream);
-/* Test hook for the GEMM tiles: C (M x N) = A B with layout 0 = A[m][k] B[n][k], 1 = A[m][k] B[k][n],
- * 2 = A[k][m] B[k][n]; leading dimensions and K multiples of 4, 16-byte aligned bases. */
+/* Debug / test knob: force the tiling of every wide GEMM launch (-1 = the cost model's choice, 0 = 128x128 and
+ * 1 = 64x64 with v_mfma_f32_32x32x2_f32, 2 = 128x48 with v_mfma_f32_16x16x4_f32). Returns the previous setting.
+ * Process-wide; not for concurrent use. */
+int bcnf_wide_force_tiling(int32_t tiling);
+/* Test hook for the GEMM tiles: C (M x N) = A B with (layout & 15) 0 = A[m][k] B[n][k], 1 = A[m][k] B[k][n],
+ * 2 = A[k][m] B[k][n]; layout >> 4 forces a tiling (0 = the dispatcher's choice, 1 = 128x128, 2 = 64x64,
+ * 3 = 128x48); leading dimensions and K multiples of 4, 16-byte aligned bases. */
 int bcnf_wide_gemm_test(int32_t layout, int32_t M, int32_t N, int32_t K, const float* A, int64_t lda, const float* B,
                         int64_t ldb, float* C, int64_t ldc, void* stream);
 

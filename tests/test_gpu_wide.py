@@ -26,11 +26,13 @@ def _lib():
 
 
 # ------------------------------------------------------------------------------------------ GEMM tiles
+@pytest.mark.parametrize("tiling", [0, 1, 2, 3])
 @pytest.mark.parametrize("layout", [0, 1, 2])
-@pytest.mark.parametrize("mnk", [(64, 64, 32), (100, 70, 36), (2048, 528, 528), (18, 527, 300), (4096, 4096, 64),
+@pytest.mark.parametrize("mnk", [(64, 64, 32), (100, 70, 36), (2048, 528, 528), (18, 527, 300), (1030, 1360, 64),
                                  (3, 5, 4)])
-def test_wide_gemm_layouts_vs_fp64(layout, mnk):
-    """C = A B through the MFMA tile machinery (both tile configs, ragged M / N / K tails) vs fp64."""
+def test_wide_gemm_layouts_vs_fp64(layout, mnk, tiling):
+    """C = A B through the MFMA tile machinery (tiling 0 = the dispatcher's choice, 1 = 128x128 32x32-MFMA,
+    2 = 64x64, 3 = 128x48 16x16-MFMA; ragged M / N / K tails) vs fp64."""
     import ctypes
     N = _lib()
     M, Nn, K = mnk
@@ -57,7 +59,7 @@ def test_wide_gemm_layouts_vs_fp64(layout, mnk):
     Ad, Bd = Ad.to(DEV), Bd.to(DEV)
     C = torch.full((M, pad(Nn)), float("nan"), device=DEV)
     Kp = pad(K) if layout != 2 else K
-    rc = N.lib().bcnf_wide_gemm_test(layout, M, Nn, Kp, N.ptr(Ad), Ad.shape[1], N.ptr(Bd), Bd.shape[1], N.ptr(C),
+    rc = N.lib().bcnf_wide_gemm_test(layout | (tiling << 4), M, Nn, Kp, N.ptr(Ad), Ad.shape[1], N.ptr(Bd), Bd.shape[1], N.ptr(C),
                                      C.shape[1], N.stream_handle(C.device))
     N.check(rc, "bcnf_wide_gemm_test")
     torch.cuda.synchronize()
@@ -108,11 +110,22 @@ WIDE_SHAPES = [
 ]
 
 
+@pytest.fixture(params=[-1, 0, 1, 2], ids=["auto", "t128x128", "t64x64", "t128x48"])
+def tiling(request):
+    N = _lib()
+    prev = N.lib().bcnf_wide_force_tiling(request.param)
+    yield request.param
+    N.lib().bcnf_wide_force_tiling(prev)
+
+
 @pytest.mark.parametrize("shape", WIDE_SHAPES)
 @pytest.mark.parametrize("B", [1, 37, 300])
-def test_wide_shapes_vs_oracle(shape, B):
-    """Forward / log-det / inverse / eval gradients of the wide family vs the oracle (fp64 for gradients)."""
+def test_wide_shapes_vs_oracle(shape, B, tiling):
+    """Forward / log-det / inverse / eval gradients of the wide family vs the oracle (fp64 for gradients), with every
+    GEMM tiling (all epilogues: activation, gradient, Linear-gradient, row-mapped, plain)."""
     from bcnf_amd import inn_nll_loss
+    if tiling >= 0 and B == 1:
+        pytest.skip("B = 1 covered by the auto tiling")
     m = _model(shape)
     _perturb(m)
     sd = {k: v.detach().clone() for k, v in m.state_dict().items()}

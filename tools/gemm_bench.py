@@ -1,0 +1,56 @@
+"""Time the wide-family GEMM tilings (bcnf_wide_gemm_test) against torch.matmul (hipBLASLt) on the FC_large shapes.
+Usage (GPU box): python tools/gemm_bench.py"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bcnf_amd import _native as N  # noqa: E402
+
+
+def bench(fn, iters=50):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / iters
+
+
+def main():
+    dev = torch.device("cuda")
+    L = N.lib()
+    shapes = [(2048, 528, 528), (16384, 528, 528), (2048, 13728, 1360), (2048, 1360, 13728), (528, 528, 2048),
+              (4096, 4096, 4096)]
+    for (M, Nn, K) in shapes:
+        for layout in (0, 1, 2):
+            if layout == 2:
+                A = torch.randn(K, M, device=dev)
+            else:
+                A = torch.randn(M, K, device=dev)
+            B = torch.randn(Nn, K, device=dev) if layout == 0 else torch.randn(K, Nn, device=dev)
+            C = torch.empty(M, Nn, device=dev)
+            st = N.stream_handle(dev)
+            res = []
+            for t in (1, 2, 3):
+                def f():
+                    L.bcnf_wide_gemm_test(layout | (t << 4), M, Nn, K, N.ptr(A), A.shape[1], N.ptr(B), B.shape[1],
+                                          N.ptr(C), Nn, st)
+                us = bench(f)
+                res.append(f"t{t}={us:7.1f}us {2 * M * Nn * K / us / 1e6:6.1f}TF")
+            if layout == 0:
+                ref = bench(lambda: torch.matmul(A, B.t(), out=C))
+            elif layout == 1:
+                ref = bench(lambda: torch.matmul(A, B, out=C))
+            else:
+                ref = bench(lambda: torch.matmul(A.t(), B, out=C))
+            res.append(f"torch={ref:7.1f}us {2 * M * Nn * K / ref / 1e6:6.1f}TF")
+            print(f"M={M:6d} N={Nn:6d} K={K:6d} layout={layout}: " + "  ".join(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
