@@ -69,7 +69,8 @@ LSTM_LARGE = {
 WIDE_FWD_FLOP_PER_SAMPLE = 2 * 47_765_617
 WIDE_TRAIN_FLOP_PER_SAMPLE = 3 * WIDE_FWD_FLOP_PER_SAMPLE
 WIDE_NAMES = {"fc_large": "trajectory_FC_large", "lstm_large": "trajectory_LSTM_large"}
-WORKLOADS = {"fc_small": (FC_SMALL, 4096), "fc_large": (FC_LARGE, 2048), "lstm_large": (LSTM_LARGE, 1024)}
+WORKLOADS = {"fc_small": (FC_SMALL, 4096), "fc_large": (FC_LARGE, 2048), "lstm_large": (LSTM_LARGE, 1024),
+             "sample": (FC_SMALL, 1024)}
 PEAK_FP32_TFLOPS = 157.3       # MI355X fp32 (vector = MFMA f32), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
 
@@ -165,6 +166,8 @@ def main():
     args = parse()
     if args.batch is None:
         args.batch = WORKLOADS[args.workload][1]
+    if args.workload == "sample":
+        return main_sample(args)
     if args.workload != "fc_small":
         return main_wide(args)
     world, rank, local = init_dist(args)
@@ -350,6 +353,97 @@ def main_wide(args):
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def main_sample(args, n_draws=500):
+    """Posterior draws/s (BASELINE configs[4]): 500 draws for each of 1024 conditions (--batch) with trajectory_FC_small,
+    the conditions sharded over the ranks (strong scaling of a fixed job; bcnf_amd/sampling.py), gathered at the end.
+    One step = draw_sharded(500, all conditions) incl. feature net, device z draw, inverse, all-gather."""
+    world, rank, local = init_dist(args)
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    from bcnf_amd import CondRealNVP_v2
+    from bcnf_amd.data import simulate
+    from bcnf_amd.sampling import draw_sharded, shard_range
+    torch.manual_seed(2024_03_25)
+    model = CondRealNVP_v2.from_config(FC_SMALL).to(device).eval()
+    _, traj = simulate(args.batch, seed=2024_03_25)
+    traj = torch.from_numpy(traj)
+    traj = ((traj - traj.mean((0, 1))) / (traj.std((0, 1)) + 1e-6)).to(device)
+    gen = torch.Generator(device=device).manual_seed(17 + rank)
+    with model.fused.reuse_pack():
+        for _ in range(args.warmup):
+            draw_sharded(model, n_draws, traj, generator=gen)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = draw_sharded(model, n_draws, traj, generator=gen)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([dt], device=device)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = float(tt.item())
+        # dominant kernel: the inverse of this rank's n_draws x N_local rows, HIP events on the launch stream
+        a, b = shard_range(args.batch, rank, world)
+        with torch.no_grad():
+            h = model.feature_network_stack(traj[a:b]).contiguous()
+            rows = n_draws * (b - a)
+            z = torch.randn(rows, 19, device=device, generator=gen)
+            idx = torch.arange(rows, device=device) % (b - a)
+            model._inverse_indexed(z, h, idx)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                model._inverse_indexed(z, h, idx)
+            e1.record()
+            torch.cuda.synchronize()
+            inv_us = e0.elapsed_time(e1) * 1e3 / 5
+    value = n_draws * args.batch * args.steps / dt
+    if rank == 0:
+        flop = FWD_FLOP_PER_SAMPLE * rows
+        achieved = flop / (inv_us * 1e-6) / 1e12
+        line = {
+            "metric": "posterior draws/sec (inverse sampling, 500 draws x 1024 conditions), trajectory_FC_small",
+            "value": round(value, 1), "unit": "draws/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic ballistic trajectories as conditions, device z",
+            "config": {"workload": "CondRealNVP_v2.sample-equivalent draw (configs[4])", "conditions": args.batch,
+                       "draws_per_condition": n_draws, "parallelism": f"condition shards x{world}",
+                       "output": tuple(out.shape)},
+            "roofline": {"bound": "mfma", "kernel": "k_inverse (this rank's rows)", "achieved": round(achieved, 3),
+                         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                         "traffic": None, "avg_us": round(inv_us, 2), "flop_per_launch": flop},
+        }
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline_sample()
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline_sample(n_draws=500, n_cond=1024):
+    """The oracle's sample(outer=True, batch_size=100) (CPU restatement of cnf.py:510-588) on the host, bounded."""
+    from oracle import cnf_oracle as O
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(2024_03_25)
+    from bcnf_amd import CondRealNVP_v2
+    m = CondRealNVP_v2.from_config(FC_SMALL)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    cond = torch.randn(n_cond, 30, 3, generator=torch.Generator().manual_seed(3))
+    O.sample(sd, O.FC_SMALL_SPEC, 10, cond[:16], outer=True, batch_size=100)
+    t0 = time.perf_counter()
+    O.sample(sd, O.FC_SMALL_SPEC, n_draws, cond, outer=True, batch_size=100)
+    dt = time.perf_counter() - t0
+    return {"value": round(n_draws * n_cond / dt, 1), "unit": "draws/s", "cores": threads, "kind": "port",
+            "sample": f"oracle.sample(outer=True, batch_size=100), {n_draws} draws x {n_cond} conditions, "
+                      f"{threads} threads, {dt:.2f} s"}
 
 
 if __name__ == "__main__":
