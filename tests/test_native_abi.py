@@ -94,3 +94,42 @@ def test_state_dict_roundtrip_keeps_flat_views():
     assert p0.data_ptr() == b.fused.flat.data_ptr() + 2 * 19 * 4
     assert list(a.state_dict().keys())[2:6] == ["layers.0.scale", "layers.0.bias", "layers.1.nn_a.nn.0.weight",
                                                 "layers.1.nn_a.nn.0.bias"]
+
+
+def test_wide_family_routing_and_layout_queries():
+    """FC_large / LSTM_large shapes route to the wide-MLP family (bcnf_wide.hip); its size queries follow the
+    carve-up documented in DESIGN.md (padded activation rows HP = round_up(H + 1, 4))."""
+    from bcnf_amd import CondRealNVP_v2
+    from bcnf_amd import _native as N
+    from bcnf_amd.wide import WideStack
+    lib = N.lib()
+    big = N.make_desc(19, [526] * 5, 26, 1360, 0.407, True)
+    assert lib.bcnf_wide_supported(ctypes.byref(big)) == 1
+    for bad in (N.make_desc(19, [526, 500], 2, 1360, 0.0, True),          # unequal nested sizes
+                N.make_desc(19, [526] * 2, 2, 1361, 0.0, True),           # C % 4 != 0
+                N.make_desc(40, [526] * 2, 2, 1360, 0.0, True),           # D > 32
+                N.make_desc(19, [526] * 2, 2, 1360, 0.0, True, two_way=True)):
+        assert lib.bcnf_wide_supported(ctypes.byref(bad)) == 0
+    cfg = {"global": {"parameter_selection": [str(i) for i in range(19)]},
+           "model": {"kwargs": {"size": 19, "nested_sizes": [526] * 5, "n_conditions": 1360, "n_blocks": 26,
+                                "dropout": 0.407, "act_norm": True}},
+           "feature_networks": [{"type": "ConcatenateCondition", "kwargs": {"input_size": None, "output_size": 90}},
+                                {"type": "FullyConnected", "kwargs": {"sizes": [90] + [310] * 7 + [1360],
+                                                                      "dropout": 0.111}}]}
+    m = CondRealNVP_v2.from_config(cfg)
+    assert isinstance(m.fused, WideStack)
+    assert m.n_params == 48_865_045                       # SURVEY §8a-1 [measured]
+    assert m.fused.flat.numel() == m.fused.counts()[0] == 47_826_390
+    HP, nb, NH, B = 528, 26, 5, 2048
+    pk = N.query_i64(lib.bcnf_wide_packed_bytes, ctypes.byref(big))
+    r4 = lambda n: (n + 3) // 4 * 4  # noqa: E731
+    assert pk == 4 * (r4(nb * HP * 1360) + r4(nb * (NH - 1) * HP * HP) + r4(nb * 10 * HP) + r4(nb * 18 * HP)
+                      + r4(25 * 19 * 19) + r4(nb) + nb * HP)
+    ws = N.query_i64(lib.bcnf_wide_workspace_bytes, ctypes.byref(big), ctypes.c_int64(B), ctypes.c_int32(1))
+    slab = B * HP
+    regions = [B * nb * HP, B, nb * NH * slab, nb * NH * slab, nb * (NH - 1) * slab, B * nb * HP, (nb + 1) * B * 20,
+               nb * B * 12, nb * B * 12, nb * B * 20, B * 20, nb * B * 40]
+    assert ws == 4 * sum(r4(n) + 64 for n in regions)
+    # the small family keeps FC_small
+    small = N.make_desc(19, [16] * 7, 32, 80, 0.383, True)
+    assert lib.bcnf_stack_supported(ctypes.byref(small)) == 1
