@@ -30,6 +30,8 @@
  *                           (trainer.py:272, after the step)
  *   bcnf_linear_forward / bcnf_linear_backward
  *                        <- nn.Linear of FullyConnectedFeatureNetwork (feature_network.py:114-145)
+ *   bcnf_wide_*          <- the same stack interfaces for the wide-MLP shapes (FC_large / LSTM_large)
+ *   bcnf_rank_count      <- the rank count of compute_y_hat_ranks (eval/calibration.py:42-46)
  */
 #ifndef BCNF_AMD_H
 #define BCNF_AMD_H
@@ -253,6 +255,12 @@ int bcnf_wide_backward(const BcnfStackDesc* desc, const float* params, const voi
 int bcnf_wide_inverse(const BcnfStackDesc* desc, const float* params, const void* packed, const float* z,
                       const float* h, int64_t h_rows, const int64_t* cond_index, int64_t n_rows, float* y,
                       int32_t training, const uint64_t* rng_state, void* scratch, void* stream);
+/* ---- Calibration (eval/calibration.py:20-48, compute_y_hat_ranks) -----------------------------------------------
+ * counts[i * dim + d] += #{ s < n_draws : y_hat[(s * n_rows + i) * dim + d] < y[i * dim + d] } for the (n_draws, n_rows,
+ * dim) draws of sample(outer=True); counts is uint32 and accumulates, so draws can be fed in chunks. */
+int bcnf_rank_count(const float* y_hat, const float* y, int64_t n_draws, int64_t n_rows, int32_t dim, uint32_t* counts,
+                    void* stream);
+
 /* Debug / test knob: force the tiling of every wide GEMM launch (-1 = the cost model's choice, 0 = 128x128 and
  * 1 = 64x64 with v_mfma_f32_32x32x2_f32, 2 = 128x48 with v_mfma_f32_16x16x4_f32). Returns the previous setting.
  * Process-wide; not for concurrent use. */
