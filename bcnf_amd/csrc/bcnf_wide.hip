@@ -330,11 +330,10 @@ template <int EPI>
 __device__ __forceinline__ EpiCtx epi_ctx(const GemmArgs& g, int g1, int g0) {
   EpiCtx e;
   e.C = g.C;
-  if (EPI == EPI_LINGRAD || EPI == EPI_ROWMAP) {
-    if (g.use_cb) e.C += g1 * g.cb_stride + ((g1 < g.cb_nb - 1) ? g.cb_an : 0) + g0 * g.sC0;
-  } else {
+  if ((EPI == EPI_LINGRAD || EPI == EPI_ROWMAP) && g.use_cb)
+    e.C += g1 * g.cb_stride + ((g1 < g.cb_nb - 1) ? g.cb_an : 0) + g0 * g.sC0;
+  else
     e.C += g1 * g.sC1 + g0 * g.sC0;
-  }
   e.X = (EPI == EPI_ACT || EPI == EPI_GRAD) && g.aux ? g.aux + g1 * g.saux1 + g0 * g.saux0 : nullptr;
   e.seed = 0;
   e.offs = 0;
@@ -354,6 +353,26 @@ __device__ __forceinline__ uint4 epi_rnd(const GemmArgs& g, const EpiCtx& e, int
   return make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
 }
 
+// XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup
+// dispatch), so linear ids b and b + 8 share an L2. Renumber so that each XCD walks a contiguous run of tiles
+// (N fastest, then M, then group): its L2 then holds one band of A rows plus the B columns that band needs, instead
+// of every XCD streaming all of A and B. Speed only -- any tile order is correct.
+struct TileId {
+  int x, y, z;
+};
+__device__ __forceinline__ TileId tile_id() {
+  const unsigned gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+  const unsigned total = gx * gy * gz;
+  unsigned lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  if (total >= 16 && (total & 7u) == 0) lin = (lin & 7u) * (total >> 3) + (lin >> 3);
+  TileId t;
+  t.x = (int)(lin % gx);
+  lin /= gx;
+  t.y = (int)(lin % gy);
+  t.z = (int)(lin / gy);
+  return t;
+}
+
 // Tiling A: v_mfma_f32_32x32x2_f32, 2 x 2 waves, each (BM/2) x (BN/2) as 32x32 accumulators. Inside a K tile
 // lane half h consumes k = h*BK/2 + s at MFMA step s.
 template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI>
@@ -364,10 +383,11 @@ __global__ __launch_bounds__(WWG, 2) void k_wgemm(const GemmArgs g) {
   __shared__ __attribute__((aligned(16))) float lds[2 * (IO::ASZ + IO::BSZ)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, c32 = lane & 31, hh = lane >> 5;
-  const int z = blockIdx.z, g1 = z / g.G0, g0 = z - g1 * g.G0;
+  const TileId tl = tile_id();
+  const int z = tl.z, g1 = z / g.G0, g0 = z - g1 * g.G0;
   const float* __restrict__ A = g.A + g1 * g.sA1 + g0 * g.sA0;
   const float* __restrict__ B = g.B + g1 * g.sB1 + g0 * g.sB0;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int m0 = tl.y * BM, n0 = tl.x * BN;
   IO io;
   floatx16 acc[TI][TJ];
 #pragma unroll
@@ -434,10 +454,11 @@ __global__ __launch_bounds__(WWG, 2) void k_wgemm16(const GemmArgs g) {
   __shared__ __attribute__((aligned(16))) float lds[2 * (IO::ASZ + IO::BSZ)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c16 = lane & 15, qq = lane >> 4;
-  const int z = blockIdx.z, g1 = z / g.G0, g0 = z - g1 * g.G0;
+  const TileId tl = tile_id();
+  const int z = tl.z, g1 = z / g.G0, g0 = z - g1 * g.G0;
   const float* __restrict__ A = g.A + g1 * g.sA1 + g0 * g.sA0;
   const float* __restrict__ B = g.B + g1 * g.sB1 + g0 * g.sB0;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int m0 = tl.y * BM, n0 = tl.x * BN;
   IO io;
   floatx4 acc[TI][TJ];
 #pragma unroll
@@ -497,6 +518,7 @@ __global__ __launch_bounds__(WWG, 2) void k_wgemm16(const GemmArgs g) {
 //     output j.
 // ------------------------------------------------------------------------------------------------
 constexpr int LR = 8;          // samples per link workgroup
+constexpr int MQ = 5;          // float4 chunks per lane prefetched into registers (rows of up to 640 floats)
 
 // Global -> LDS copy of n4 float4 by the whole workgroup with 8 loads in flight per thread (a plain copy loop
 // serialises one L2 round trip per iteration).
@@ -581,15 +603,31 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
   float* vs = Os + 32;
   float* us = vs + 32;
   const int kq = INV ? a.kh : a.kt;                 // the orthonormal matrix this launch applies
+  const long long row = (long long)blockIdx.x * LR + r;
+  const bool valid = row < a.B;
+  const bool lv = valid && ln < D;
+  // The sample's HBM rows (last activation of block kt, projection row of block kh, saved input) are requested
+  // first, so their latency overlaps the weight staging instead of serialising inside the dot-product loops.
+  floatx4 ach[MQ], pch[MQ];
+  const float* arow = a.kt >= 0 ? a.Alast + row * HP : nullptr;
+  const float* Pr = nullptr;
+  if (a.kh >= 0) Pr = a.P + (a.cidx && valid ? a.cidx[row] : row) * a.ldP + (long long)a.kh * HP;
+#pragma unroll
+  for (int t = 0; t < MQ; ++t) {
+    const int q = ln + 32 * t;
+    if (valid && q < nq) {
+      if (a.kt >= 0) ach[t] = ld4(arow + 4 * q);
+      if (a.kh >= 0) pch[t] = ld4(Pr + 4 * q);
+    }
+  }
+  float xpre = 0.f;
+  if (lv) xpre = a.kt >= 0 ? a.Xt[row * L.XP + ln] : a.xin[row * D + ln];
   if (a.kt >= 0) stage4(Wl, a.pk + L.pk_wl + (long long)a.kt * O2 * HP, O2 * HP / 4);
   if (a.kh >= 0) stage4(W0, a.pk + L.pk_w0y + (long long)a.kh * Da * HP, Da * HP / 4);
   if (kq >= 0 && kq < L.nb - 1)
     for (int e = tid; e < D * D; e += WWG) Qs[e] = a.pk[L.pk_q + (long long)kq * D * D + e];
   __syncthreads();
 
-  const long long row = (long long)blockIdx.x * LR + r;
-  const bool valid = row < a.B;
-  const bool lv = valid && ln < D;
   uint64_t seed = 0, offs = 0;
   if (a.rng) {
     seed = a.rng[0];
@@ -603,9 +641,7 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
 #pragma unroll
     for (int j = 0; j < DM; ++j) acc[j] = 0.f;
     if (valid) {
-      const float* arow = a.Alast + row * HP;
-      for (int q = ln; q < nq; q += 32) {
-        const floatx4 av = ld4(arow + 4 * q);
+      auto chunk = [&](int q, floatx4 av) {
 #pragma unroll
         for (int j = 0; j < DM; ++j) {
           if (j < O2) {
@@ -613,7 +649,11 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
             acc[j] = fmaf(av.x, w.x, fmaf(av.y, w.y, fmaf(av.z, w.z, fmaf(av.w, w.w, acc[j]))));
           }
         }
-      }
+      };
+#pragma unroll
+      for (int t = 0; t < MQ; ++t)
+        if (ln + 32 * t < nq) chunk(ln + 32 * t, ach[t]);
+      for (int q = ln + 32 * MQ; q < nq; q += 32) chunk(q, ld4(arow + 4 * q));
     }
 #pragma unroll
     for (int j = 0; j < DM; ++j)
@@ -630,7 +670,7 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
     const bool anb = L.an && k < L.nb - 1;
     const float* sc = a.prm + (long long)k * L.blk_stride;
     if (lv) {
-      xi = a.Xt[row * L.XP + ln];
+      xi = xpre;
       if (!INV) {
         if (anb) xi = sc[ln] * xi + sc[D + ln];                    // ActNorm (cnf.py:350)
         if (ln >= Da) {
@@ -673,7 +713,7 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
       a.z[row * D + ln] = xi;
     }
   } else {
-    if (lv) xi = a.xin[row * D + ln];
+    xi = xpre;
     if (!INV && valid && ln == 0) a.ldj[row] = 0.f;
   }
   // ------------------------------------------------------------ head of block kh
@@ -708,12 +748,10 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
     if (a.U && valid && ln < L.UP) a.U[row * L.UP + ln] = ln < Da ? us[ln] : (ln == Da ? 1.f : 0.f);
     if (valid) {
       const float* b0 = a.pk + L.pk_b0 + (long long)k * HP;
-      const long long prow = a.cidx ? a.cidx[row] : row;
-      const float* Pr = a.P + prow * a.ldP + (long long)k * HP;
       const uint32_t tag = (uint32_t)k * 16u;
-      for (int q = ln; q < nq; q += 32) {
+      auto chunk = [&](int q, floatx4 pv4) {
         const int n = 4 * q;
-        floatx4 pre = ld4(Pr + n) + ld4(b0 + n);
+        floatx4 pre = pv4 + ld4(b0 + n);
 #pragma unroll
         for (int j = 0; j < DM / 2; ++j) {
           if (j < Da) {
@@ -740,7 +778,11 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
         }
         st4(a.A0 + row * HP + n, floatx4{av[0], av[1], av[2], av[3]});
         if (a.G0) st4(a.G0 + row * HP + n, floatx4{gv[0], gv[1], gv[2], gv[3]});
-      }
+      };
+#pragma unroll
+      for (int t = 0; t < MQ; ++t)
+        if (ln + 32 * t < nq) chunk(ln + 32 * t, pch[t]);
+      for (int q = ln + 32 * MQ; q < nq; q += 32) chunk(q, ld4(Pr + 4 * q));
     }
   }
 }
@@ -783,6 +825,32 @@ __global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const Lin
   float* part = Qs + pad4(D * D);
   float* Os = part + pad4(LR * 32 * PS) + r * 96;
   float* vs = Os + 32;
+  const long long row = (long long)blockIdx.x * LR + r;
+  const bool valid = row < a.B;
+  const bool lv = valid && ln < D;
+  // HBM rows first (dZ_0 of block kt, G of block kh, per-sample vectors), then the weight staging
+  floatx4 zch[MQ], gch[MQ];
+  const float* zr = a.kt >= 0 ? a.dZ0 + row * a.ldZ0 : nullptr;
+  const float* gr = a.kh >= 0 ? a.Gl + row * HP : nullptr;
+#pragma unroll
+  for (int t = 0; t < MQ; ++t) {
+    const int q = ln + 32 * t;
+    if (valid && q < nq) {
+      if (a.kt >= 0) zch[t] = ld4(zr + 4 * q);
+      if (a.kh >= 0) gch[t] = ld4(gr + 4 * q);
+    }
+  }
+  float dvp = 0.f, xkt = 0.f, xkh = 0.f, skh = 0.f;
+  if (lv) {
+    if (a.kt >= 0) {
+      dvp = a.DV[row * L.XP + ln];
+      xkt = a.X[a.kt * a.sX + row * L.XP + ln];
+    }
+    if (a.kh >= 0) {
+      xkh = a.X[a.kh * a.sX + row * L.XP + ln];
+      if (ln >= Da) skh = a.S[a.kh * a.sS + row * L.SP + ln - Da];
+    }
+  }
   if (a.kt >= 0) stage4(W0, a.pk + L.pk_w0y + (long long)a.kt * Da * HP, Da * HP / 4);
   if (a.kh >= 0) {
     stage4(Wl, a.pk + L.pk_wl + (long long)a.kh * O2 * HP, O2 * HP / 4);
@@ -790,9 +858,6 @@ __global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const Lin
       for (int e = tid; e < D * D; e += WWG) Qs[e] = a.pk[L.pk_q + (long long)a.kh * D * D + e];
   }
   __syncthreads();
-  const long long row = (long long)blockIdx.x * LR + r;
-  const bool valid = row < a.B;
-  const bool lv = valid && ln < D;
   const float gscale = a.nll ? (a.dvals ? a.dvals[0] + a.dvals[1] : 1.f) / (float)a.B : 0.f;
   float dxi = 0.f;                                  // element ln of the gradient w.r.t. the current D-vector
   // ------------------------------------------------------------ tail-B of block kt
@@ -802,9 +867,7 @@ __global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const Lin
 #pragma unroll
     for (int j = 0; j < DM / 2; ++j) acc[j] = 0.f;
     if (valid) {
-      const float* zr = a.dZ0 + row * a.ldZ0;
-      for (int q = ln; q < nq; q += 32) {
-        const floatx4 dzv = ld4(zr + 4 * q);
+      auto chunk = [&](int q, floatx4 dzv) {
 #pragma unroll
         for (int j = 0; j < DM / 2; ++j) {
           if (j < Da) {
@@ -812,14 +875,18 @@ __global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const Lin
             acc[j] = fmaf(dzv.x, w.x, fmaf(dzv.y, w.y, fmaf(dzv.z, w.z, fmaf(dzv.w, w.w, acc[j]))));
           }
         }
-      }
+      };
+#pragma unroll
+      for (int t = 0; t < MQ; ++t)
+        if (ln + 32 * t < nq) chunk(ln + 32 * t, zch[t]);
+      for (int q = ln + 32 * MQ; q < nq; q += 32) chunk(q, ld4(zr + 4 * q));
     }
 #pragma unroll
     for (int j = 0; j < DM / 2; ++j)
       if (j < Da) part[(r * 32 + ln) * PS + j] = acc[j];
     __syncthreads();
     if (lv) {
-      float du = a.DV[row * L.XP + ln];
+      float du = dvp;
       if (ln < Da) {
         float t = 0.f;
 #pragma unroll
@@ -828,8 +895,7 @@ __global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const Lin
       }
       if (L.an && k < L.nb - 1) {
         const float* sc = a.prm + (long long)k * L.blk_stride;
-        const float xk = a.X[k * a.sX + row * L.XP + ln];
-        a.ANP[row * L.AP + ln] = du * xk;                        // dscale partial
+        a.ANP[row * L.AP + ln] = du * xkt;                       // dscale partial
         a.ANP[row * L.AP + D + ln] = du;                         // dbias partial
         du *= sc[ln];
       }
@@ -857,12 +923,12 @@ __global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const Lin
     if (lv && ln >= Da) {
       const int j = ln - Da;
       const float dl = a.nll ? -gscale : (a.dldj ? a.dldj[row] : 0.f);
-      float ub = a.X[k * a.sX + row * L.XP + ln];
+      float ub = xkh;
       if (L.an && k < L.nb - 1) {
         const float* sc = a.prm + (long long)k * L.blk_stride;
         ub = sc[ln] * ub + sc[D + ln];
       }
-      const float s = a.S[k * a.sS + row * L.SP + j];
+      const float s = skh;
       const float es = exp_fast(s);
       dvo = dxi * es;                                             // du_b
       Os[j] = dxi;                                                // dt
@@ -875,9 +941,8 @@ __global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const Lin
       float dO[DM];
 #pragma unroll
       for (int j = 0; j < DM; ++j) dO[j] = j < O2 ? Os[j] : 0.f;
-      const float* gr = a.Gl + row * HP;
       float* out = a.dZl + row * a.ldZl;
-      for (int q = ln; q < nq; q += 32) {
+      auto chunk = [&](int q, floatx4 gv) {
         const int n = 4 * q;
         floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -890,8 +955,12 @@ __global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const Lin
             s4.w = fmaf(dO[j], w.w, s4.w);
           }
         }
-        st4(out + n, s4 * ld4(gr + n));
-      }
+        st4(out + n, s4 * gv);
+      };
+#pragma unroll
+      for (int t = 0; t < MQ; ++t)
+        if (ln + 32 * t < nq) chunk(ln + 32 * t, gch[t]);
+      for (int q = ln + 32 * MQ; q < nq; q += 32) chunk(q, ld4(gr + 4 * q));
     }
   }
 }
@@ -1246,7 +1315,7 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
   }
   // ---- parameter gradients (canonical flat, every element written exactly once) ----
   if (dprm) {
-    if (L.NH > 1) {   // hidden Linears: [dW_l | db_l] = dZ_l^T [A_{l-1} | 1]
+    if (L.NH > 1) {   // hidden Linears of every block in one grouped launch: [dW_l | db_l] = dZ_l^T [A_{l-1} | 1]
       GemmArgs g = gemm_args(L.H, L.H + 1, (int)B, w.dZ, L.HP, w.A, L.HP, dprm, L.H);
       g.G0 = L.NH - 1;
       g.sA1 = (long long)(L.NH - 1) * slab;
