@@ -30,7 +30,7 @@ EXPORTS = (
     "bcnf_clip_grad_norm", "bcnf_linear_forward", "bcnf_linear_work_bytes", "bcnf_linear_backward",
     "bcnf_inverse_scratch_bytes", "bcnf_stack_dh", "bcnf_backward_tail", "bcnf_gather_rows2",
     "bcnf_gather_batch", "bcnf_advance_counters",
-    "bcnf_wide_supported", "bcnf_wide_packed_bytes", "bcnf_wide_workspace_bytes", "bcnf_wide_inverse_scratch_bytes",
+    "bcnf_wide_supported", "bcnf_wide_param_count", "bcnf_wide_packed_bytes", "bcnf_wide_workspace_bytes", "bcnf_wide_inverse_scratch_bytes",
     "bcnf_wide_pack", "bcnf_wide_forward", "bcnf_wide_nll_finalize", "bcnf_wide_backward", "bcnf_wide_inverse",
     "bcnf_wide_gemm_test", "bcnf_wide_force_tiling", "bcnf_rank_count",
 )
@@ -107,6 +107,7 @@ def _bind(lib):
         "bcnf_linear_work_bytes": (_i64, [_i64, _i32, _i32]),
         "bcnf_linear_backward": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
         "bcnf_wide_supported": (_i32, [_pdesc]),
+        "bcnf_wide_param_count": (_i32, [_pdesc, _pi64, _pi64]),
         "bcnf_wide_packed_bytes": (_i32, [_pdesc, _pi64]),
         "bcnf_wide_workspace_bytes": (_i32, [_pdesc, _i64, _i32, _pi64]),
         "bcnf_wide_inverse_scratch_bytes": (_i32, [_pdesc, _i64, _i64, _pi64]),

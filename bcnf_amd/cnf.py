@@ -151,15 +151,17 @@ class ConditionalAffineCouplingLayer(ConditionalInvertibleLayer):
 
     def _standalone(self) -> tuple[FusedStack, torch.Tensor]:
         _check_fused_family(*self._fam, self.two_way)
-        if self.two_way:
-            raise NotImplementedError("bcnf_amd: two_way coupling is not implemented by the HIP kernels yet")
-        cfg = StackConfig(self.input_size, tuple(self.nested_sizes), 1, self.n_conditions, self.dropout, False, False)
+        cfg = StackConfig(self.input_size, tuple(self.nested_sizes), 1, self.n_conditions, self.dropout, False,
+                          self.two_way)
         key = (cfg, )
         st = getattr(self, "_solo", None)
         if st is None or st[0] != key:
             st = (key, make_stack(cfg, [], [], bind=False))
             object.__setattr__(self, "_solo", st)
-        flat = torch.cat([p.reshape(-1) for p in self.canonical_params()])
+        if not st[1].supported:
+            raise NotImplementedError(f"bcnf_amd: no HIP kernel family implements this coupling shape ({cfg})")
+        params = self.canonical_params() + (self.nn_b.canonical_params() if self.two_way else [])
+        flat = torch.cat([p.reshape(-1) for p in params])
         return st[1], flat
 
     def forward(self, y: torch.Tensor, x: torch.Tensor, log_det_J: bool = False) -> torch.Tensor:
@@ -316,13 +318,11 @@ class CondRealNVP_v2(ConditionalInvertibleLayer):
             # cnf.py:479-485: with n_conditions == 0 no layer matches and the reference raises
             raise ValueError("Layer must be an instance of ConditionalInvertibleLayer or InvertibleLayer, but got "
                              f"{type(self.layers[0])}")
-        if self.two_way:
-            raise NotImplementedError("bcnf_amd: two_way coupling is not implemented by the HIP kernels yet")
         if not self._fused.supported:
             raise NotImplementedError(
                 "bcnf_amd: this stack shape fits neither HIP kernel family: the register-resident small family "
-                "(hidden sizes <= 16, size <= 32, n_conditions <= 256) nor the wide-MLP MFMA family (equal nested "
-                "sizes, size <= 32, n_conditions % 4 == 0)")
+                "(hidden sizes <= 16, size <= 32, n_conditions <= 256, one-way) nor the wide-MLP MFMA family (equal "
+                "nested sizes, size <= 32; one-way or two_way)")
 
     # ------------------------------------------------------------------ reference API
     def verify(self) -> None:

@@ -43,28 +43,39 @@ constexpr int DM = 32;        // max D of the wide family (register arrays of th
 __host__ __device__ inline int pad4(int x) { return (x + 3) & ~3; }
 inline long long pad4l(long long x) { return (x + 3) & ~3LL; }
 
+// Virtual blocks: a two_way coupling (cnf.py:176-186) is two half-couplings in sequence -- side a (nn_a: input
+// the first Da coordinates, transforms the last Db) then side b (nn_b: input the last Db, transforms the first Da)
+// -- so the stack is nv = nb * S half-couplings (S = 2 for two_way, else 1), each with its own nested MLP. Virtual
+// block v belongs to real block v / S and has side v % S; ActNorm sits before a block's first half, the orthonormal
+// mix after its last half.
 struct WideLayout {
-  int D, Da, Db, C, H, NH, nb, an;
-  int HP, UP, OP, XP, SP, AP;   // row strides: activations, [u_a | 1], dO, block inputs, tanh(s), ActNorm partials
-  int in0;                      // Da + C
-  long long blk_stride;
-  long long lin_w[BCNF_MAX_HIDDEN + 1], lin_b[BCNF_MAX_HIDDEN + 1];
+  int D, Da, Db, C, Cp, H, NH, nb, an, S, nv;
+  int HP, UP, OP, XP, SP, AP;   // row strides: activations, [u_in | 1], dO, block inputs, tanh(s), ActNorm partials
+  int nin[2], nout[2], ioff[2], toff[2], in0[2];   // per side: MLP input width / transformed width / their offsets
+  long long mlp[2];             // floats of nn_a / nn_b
+  long long lin_w[2][BCNF_MAX_HIDDEN + 1], lin_b[2][BCNF_MAX_HIDDEN + 1];   // Linear offsets inside nn_a / nn_b
+  long long blk_stride;         // canonical floats per (ActNorm + coupling) block
   long long n_trainable;
+  int WY, WL;                   // rows per virtual block of the W0y^T and last-Linear copies (max over sides)
   float p, keep_scale;
   uint32_t thresh;              // drop if philox u32 < thresh
   // packed buffer (floats)
-  long long pk_w0h;             // [nb * HP][C]     row k*HP + n = W0_k[n][Da + c], rows n >= H zero
-  long long pk_hid;             // [nb][NH-1][HP][HP]  W_l (l = 1..NH-1), zero beyond H
-  long long pk_w0y;             // [nb][Da][HP]     W0_k[n][j] transposed
-  long long pk_wl;              // [nb][2 Db][HP]   last Linear, zero beyond H
+  long long pk_w0h;             // [nv * HP][Cp]    row v*HP + n = W0_v[n][nin_v + c], rows n >= H and c >= C zero
+  long long pk_hid;             // [nv][NH-1][HP][HP]  W_l (l = 1..NH-1), zero beyond H
+  long long pk_w0y;             // [nv][WY][HP]     W0_v[n][j] transposed
+  long long pk_wl;              // [nv][WL][HP]     last Linear, zero beyond H
   long long pk_q;               // [nb-1][D][D]
   long long pk_ldc;             // [nb]             sum_i log|scale_k,i| (0 without ActNorm)
-  long long pk_b0;              // [nb][HP]         Linear-1 bias, zero beyond H
+  long long pk_b0;              // [nv][HP]         Linear-1 bias, zero beyond H
   long long total;
 };
 
 __host__ __device__ inline long long wcb(const WideLayout& L, int k) {
   return (long long)k * L.blk_stride + ((k < L.nb - 1) ? L.an : 0);
+}
+// first float of virtual block v's nested MLP in the canonical flat parameters
+__host__ __device__ inline long long vbase(const WideLayout& L, int v) {
+  return wcb(L, v / L.S) + (v % L.S ? L.mlp[0] : 0);
 }
 
 int wide_layout(const BcnfStackDesc* d, WideLayout* L) {
@@ -75,48 +86,59 @@ int wide_layout(const BcnfStackDesc* d, WideLayout* L) {
   if (!(d->dropout >= 0.f && d->dropout < 1.f)) return BCNF_ERR_ARG;
   for (int i = 0; i < d->n_hidden; ++i)
     if (d->hidden[i] < 1) return BCNF_ERR_ARG;
-  if (d->two_way) return BCNF_ERR_UNSUPPORTED;
   for (int i = 1; i < d->n_hidden; ++i)
     if (d->hidden[i] != d->hidden[0]) return BCNF_ERR_UNSUPPORTED;     // equal widths (every shipped config)
-  if (d->size > DM || d->n_conditions < 1 || (d->n_conditions & 3) || d->hidden[0] > 8192) return BCNF_ERR_UNSUPPORTED;
+  if (d->size > DM || d->n_conditions < 1 || d->hidden[0] > 8192) return BCNF_ERR_UNSUPPORTED;
   L->D = d->size;
   L->Da = (d->size + 1) / 2;
   L->Db = d->size / 2;
   L->C = d->n_conditions;
+  L->Cp = pad4(L->C);
   L->H = d->hidden[0];
   L->NH = d->n_hidden;
   L->nb = d->n_blocks;
   L->an = d->act_norm ? 2 * d->size : 0;
+  L->S = d->two_way ? 2 : 1;
+  L->nv = L->nb * L->S;
+  L->nin[0] = L->Da;  L->nout[0] = L->Db;  L->ioff[0] = 0;      L->toff[0] = L->Da;
+  L->nin[1] = L->Db;  L->nout[1] = L->Da;  L->ioff[1] = L->Da;  L->toff[1] = 0;
+  const int nout_max = L->S == 2 ? L->Da : L->Db;
+  L->WY = L->Da;
+  L->WL = 2 * nout_max;
   L->HP = pad4(L->H + 1);
   L->UP = pad4(L->Da + 1);
-  L->OP = pad4(2 * L->Db);
+  L->OP = pad4(2 * nout_max);
   L->XP = pad4(L->D);
-  L->SP = pad4(L->Db);
+  L->SP = pad4(nout_max);
   L->AP = pad4(2 * L->D);
-  L->in0 = L->Da + L->C;
-  long long off = 0;
-  for (int l = 0; l <= L->NH; ++l) {
-    const long long in = (l == 0) ? L->in0 : L->H;
-    const long long out = (l == L->NH) ? 2 * L->Db : L->H;
-    L->lin_w[l] = off;
-    off += in * out;
-    L->lin_b[l] = off;
-    off += out;
+  L->blk_stride = L->an;
+  for (int sd = 0; sd < L->S; ++sd) {
+    L->in0[sd] = L->nin[sd] + L->C;
+    long long off = 0;
+    for (int l = 0; l <= L->NH; ++l) {
+      const long long in = (l == 0) ? L->in0[sd] : L->H;
+      const long long out = (l == L->NH) ? 2 * L->nout[sd] : L->H;
+      L->lin_w[sd][l] = off;
+      off += in * out;
+      L->lin_b[sd][l] = off;
+      off += out;
+    }
+    L->mlp[sd] = off;
+    L->blk_stride += off;
   }
-  L->blk_stride = L->an + off;
-  L->n_trainable = (long long)(L->nb - 1) * L->blk_stride + off;
+  L->n_trainable = (long long)L->nb * L->blk_stride - L->an;
   L->p = d->dropout;
   L->keep_scale = 1.0f / (1.0f - d->dropout);
   const double t = (double)d->dropout * 4294967296.0;
   L->thresh = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
   long long o = 0;
-  L->pk_w0h = o; o += pad4l((long long)L->nb * L->HP * L->C);
-  L->pk_hid = o; o += pad4l((long long)L->nb * (L->NH - 1) * L->HP * L->HP);
-  L->pk_w0y = o; o += pad4l((long long)L->nb * L->Da * L->HP);
-  L->pk_wl = o;  o += pad4l((long long)L->nb * 2 * L->Db * L->HP);
+  L->pk_w0h = o; o += pad4l((long long)L->nv * L->HP * L->Cp);
+  L->pk_hid = o; o += pad4l((long long)L->nv * (L->NH - 1) * L->HP * L->HP);
+  L->pk_w0y = o; o += pad4l((long long)L->nv * L->WY * L->HP);
+  L->pk_wl = o;  o += pad4l((long long)L->nv * L->WL * L->HP);
   L->pk_q = o;   o += pad4l((long long)(L->nb - 1) * L->D * L->D);
   L->pk_ldc = o; o += pad4l(L->nb);
-  L->pk_b0 = o;  o += (long long)L->nb * L->HP;
+  L->pk_b0 = o;  o += (long long)L->nv * L->HP;
   L->total = o;
   return BCNF_OK;
 }
@@ -130,34 +152,43 @@ __global__ __launch_bounds__(WWG) void k_wpack(const WideLayout L, const float* 
   for (long long e = (long long)blockIdx.x * WWG + threadIdx.x; e < L.pk_ldc; e += stride) {
     float v = 0.f;
     if (e < L.pk_hid) {
-      const long long r = e / L.C;
-      const int c = (int)(e - r * L.C);
-      const int k = (int)(r / L.HP), n = (int)(r - (long long)k * L.HP);
-      if (k < L.nb && n < L.H) v = prm[wcb(L, k) + L.lin_w[0] + (long long)n * L.in0 + L.Da + c];
+      const long long r = e / L.Cp;
+      const int c = (int)(e - r * L.Cp);
+      const int vb = (int)(r / L.HP), n = (int)(r - (long long)vb * L.HP);
+      if (vb < L.nv && n < L.H && c < L.C) {
+        const int sd = vb % L.S;
+        v = prm[vbase(L, vb) + L.lin_w[sd][0] + (long long)n * L.in0[sd] + L.nin[sd] + c];
+      }
     } else if (e < L.pk_w0y) {
       const long long i = e - L.pk_hid;
       const long long per = (long long)L.HP * L.HP;
       const long long kl = i / per;
       const long long rem = i - kl * per;
       const int n = (int)(rem / L.HP), kk = (int)(rem - (long long)n * L.HP);
-      if (L.NH > 1 && kl < (long long)L.nb * (L.NH - 1) && n < L.H && kk < L.H) {
-        const int k = (int)(kl / (L.NH - 1)), l = (int)(kl % (L.NH - 1)) + 1;
-        v = prm[wcb(L, k) + L.lin_w[l] + (long long)n * L.H + kk];
+      if (L.NH > 1 && kl < (long long)L.nv * (L.NH - 1) && n < L.H && kk < L.H) {
+        const int vb = (int)(kl / (L.NH - 1)), l = (int)(kl % (L.NH - 1)) + 1;
+        v = prm[vbase(L, vb) + L.lin_w[vb % L.S][l] + (long long)n * L.H + kk];
       }
     } else if (e < L.pk_wl) {
       const long long i = e - L.pk_w0y;
-      const long long per = (long long)L.Da * L.HP;
-      const int k = (int)(i / per);
-      const long long rem = i - (long long)k * per;
+      const long long per = (long long)L.WY * L.HP;
+      const int vb = (int)(i / per);
+      const long long rem = i - (long long)vb * per;
       const int j = (int)(rem / L.HP), n = (int)(rem - (long long)j * L.HP);
-      if (k < L.nb && n < L.H) v = prm[wcb(L, k) + L.lin_w[0] + (long long)n * L.in0 + j];
+      if (vb < L.nv) {
+        const int sd = vb % L.S;
+        if (n < L.H && j < L.nin[sd]) v = prm[vbase(L, vb) + L.lin_w[sd][0] + (long long)n * L.in0[sd] + j];
+      }
     } else if (e < L.pk_q) {
       const long long i = e - L.pk_wl;
-      const long long per = (long long)2 * L.Db * L.HP;
-      const int k = (int)(i / per);
-      const long long rem = i - (long long)k * per;
+      const long long per = (long long)L.WL * L.HP;
+      const int vb = (int)(i / per);
+      const long long rem = i - (long long)vb * per;
       const int j = (int)(rem / L.HP), n = (int)(rem - (long long)j * L.HP);
-      if (k < L.nb && n < L.H) v = prm[wcb(L, k) + L.lin_w[L.NH] + (long long)j * L.H + n];
+      if (vb < L.nv) {
+        const int sd = vb % L.S;
+        if (n < L.H && j < 2 * L.nout[sd]) v = prm[vbase(L, vb) + L.lin_w[sd][L.NH] + (long long)j * L.H + n];
+      }
     } else {
       const long long i = e - L.pk_q;
       if (i < (long long)(L.nb - 1) * L.D * L.D) v = q[i];
@@ -177,9 +208,20 @@ __global__ void k_wpack_ldc(const WideLayout L, const float* __restrict__ prm, f
 }
 
 __global__ __launch_bounds__(WWG) void k_wpack_b0(const WideLayout L, const float* __restrict__ prm, float* __restrict__ pk) {
-  const int k = blockIdx.x;
+  const int vb = blockIdx.x;
   for (int n = threadIdx.x; n < L.HP; n += WWG)
-    pk[L.pk_b0 + (long long)k * L.HP + n] = n < L.H ? prm[wcb(L, k) + L.lin_b[0] + n] : 0.f;
+    pk[L.pk_b0 + (long long)vb * L.HP + n] = n < L.H ? prm[vbase(L, vb) + L.lin_b[vb % L.S][0] + n] : 0.f;
+}
+
+// rows of C floats -> rows of Cp floats (zero tail), for condition widths that are not a multiple of 4
+__global__ __launch_bounds__(WWG) void k_wpad_rows(const float* __restrict__ src, int C, long long rows,
+                                                   float* __restrict__ dst, int Cp) {
+  const long long n = rows * Cp;
+  for (long long e = (long long)blockIdx.x * WWG + threadIdx.x; e < n; e += (long long)gridDim.x * WWG) {
+    const long long r = e / Cp;
+    const int c = (int)(e - r * Cp);
+    dst[e] = c < C ? src[r * C + c] : 0.f;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -206,10 +248,12 @@ struct GemmArgs {
   const uint64_t* rng; uint32_t thresh; float keep_scale; uint32_t tag, tag_s1;   // tag of group = tag + g1*tag_s1
   // EPI_LINGRAD: row r, col c: c < wcols -> C[r * ldc + c], c == wcols -> C[boff + r]
   int wcols; long long boff;
-  // flat-gradient group base (EPI_LINGRAD / EPI_ROWMAP): C + g1 * cb_stride + (g1 < cb_nb - 1 ? cb_an : 0) + g0 * sC0
-  long long cb_stride; int cb_an, cb_nb, use_cb;
-  // EPI_ROWMAP: row r -> block r / rm_hp, n = r % rm_hp (skipped when >= rm_h): C + cb(block) + rm_off + n*ldc + col
-  int rm_hp, rm_h; long long rm_off;
+  // flat-gradient group base (EPI_LINGRAD with use_cb, EPI_ROWMAP) of virtual block v = g1 (real block v / cb_S,
+  // side v % cb_S): C + (v / cb_S) * cb_stride + (v / cb_S < cb_nb - 1 ? cb_an : 0) + (v % cb_S) * cb_side + g0 * sC0
+  long long cb_stride, cb_side; int cb_an, cb_nb, cb_S, use_cb;
+  // EPI_ROWMAP: row r -> virtual block v = r / rm_hp, n = r % rm_hp (skipped when >= rm_h):
+  //   C + cb(v) + rm_off[side] + n * rm_ld[side] + col
+  int rm_hp, rm_h; long long rm_off[2], rm_ld[2];
 };
 
 __device__ __forceinline__ floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
@@ -311,10 +355,12 @@ __device__ __forceinline__ void epi4(const GemmArgs& g, float* __restrict__ Cg, 
       if (col < g.wcols) Cg[(long long)row * g.ldc + col] = v[rr];
       else if (col == g.wcols) Cg[g.boff + row] = v[rr];
     } else {   // EPI_ROWMAP
-      const int blk = row / g.rm_hp, n = row - blk * g.rm_hp;
-      if (n < g.rm_h)
-        Cg[(long long)blk * g.cb_stride + ((blk < g.cb_nb - 1) ? g.cb_an : 0) + g.rm_off + (long long)n * g.ldc + col] =
-            v[rr];
+      const int vb = row / g.rm_hp, n = row - vb * g.rm_hp;
+      if (n < g.rm_h) {
+        const int blk = vb / g.cb_S, sd = vb - blk * g.cb_S;
+        Cg[(long long)blk * g.cb_stride + ((blk < g.cb_nb - 1) ? g.cb_an : 0) + sd * g.cb_side + g.rm_off[sd] +
+           (long long)n * g.rm_ld[sd] + col] = v[rr];
+      }
     }
   }
 }
@@ -330,9 +376,12 @@ template <int EPI>
 __device__ __forceinline__ EpiCtx epi_ctx(const GemmArgs& g, int g1, int g0) {
   EpiCtx e;
   e.C = g.C;
-  if ((EPI == EPI_LINGRAD || EPI == EPI_ROWMAP) && g.use_cb)
-    e.C += g1 * g.cb_stride + ((g1 < g.cb_nb - 1) ? g.cb_an : 0) + g0 * g.sC0;
-  else
+  if (EPI == EPI_LINGRAD && g.use_cb) {
+    const int blk = g1 / g.cb_S, sd = g1 - blk * g.cb_S;
+    e.C += blk * g.cb_stride + ((blk < g.cb_nb - 1) ? g.cb_an : 0) + sd * g.cb_side + g0 * g.sC0;
+  } else if (EPI == EPI_ROWMAP) {
+    // the row map carries the whole offset
+  } else
     e.C += g1 * g.sC1 + g0 * g.sC0;
   e.X = (EPI == EPI_ACT || EPI == EPI_GRAD) && g.aux ? g.aux + g1 * g.saux1 + g0 * g.saux0 : nullptr;
   e.seed = 0;
@@ -511,11 +560,12 @@ __global__ __launch_bounds__(WWG, 2) void k_wgemm16(const GemmArgs g) {
 
 // ------------------------------------------------------------------------------------------------
 // Link kernels: one 32-lane half-wavefront per sample, 8 samples per 256-thread workgroup.
-//   * The sample's D-vector is lane-distributed (lane i < D holds element i); vectors every lane needs (u_a, v,
+//   * The sample's D-vector is lane-distributed (lane i < D holds element i); vectors every lane needs (u_in, v,
 //     dO) go through LDS, so no register array is ever indexed by a runtime value.
-//   * The long dot products (last Linear: 2 Db outputs over HP inputs; Linear-1 y-part backward: Da outputs) are
-//     lane-split over float4 chunks, then reduced through an LDS transpose: lane j sums the 32 partials of
-//     output j.
+//   * The long dot products (last Linear: 2 nout outputs over HP inputs; Linear-1 input-part backward: nin outputs)
+//     are lane-split over float4 chunks, then reduced through an LDS transpose: lane j sums the 32 partials of j.
+//   * TS / HS: side of the virtual block whose tail / head the launch runs (0 = nn_a, 1 = nn_b of a two_way
+//     coupling; always 0 for one-way stacks), so every per-side width is a compile-time constant when DD is.
 // ------------------------------------------------------------------------------------------------
 constexpr int LR = 8;          // samples per link workgroup
 constexpr int MQ = 5;          // float4 chunks per lane prefetched into registers (rows of up to 640 floats)
@@ -548,22 +598,22 @@ __device__ __forceinline__ float half_sum(float v) {      // sum over the 32 lan
 
 struct LinkArgs {
   long long B;
-  int kt, kh;                   // tail block (-1: none), head block (-1: none)
+  int vt, vh;                   // virtual block of the tail / of the head (-1: none)
   const float* prm;             // canonical flat parameters
   const float* pk;              // packed
   // tail
-  const float* Alast;           // [B][HP] last hidden activation of block kt
-  const float* Xt;              // block kt's saved input rows (forward: pre-ActNorm x; inverse: v = x Q^T)
-  float* S;                     // forward save: tanh(s) of block kt [B][SP] (nullable)
+  const float* Alast;           // [B][HP] last hidden activation of block vt
+  const float* Xt;              // block vt's saved input rows (forward: pre-ActNorm x or mid-coupling state; inverse: v)
+  float* S;                     // forward save: tanh(s) of block vt [B][SP] (nullable)
   float* z;                     // last block: z / inverse output y [B][D] (ld D)
   float* ldj;                   // [B]
   float* nllp;                  // last block: 0.5 |z|^2 - ldj per row (nullable)
   // head
   const float* xin;             // head-only launch: input rows (ld D): y (forward) or z (inverse)
-  float* Xh;                    // block kh's saved input rows [B][XP]
+  float* Xh;                    // block vh's saved input rows [B][XP]
   const float* P; long long ldP; const int64_t* cidx;   // hoisted projection rows (row r uses cidx[r])
   float* A0; float* G0;         // [B][HP] first hidden activation and its derivative factor (G0 nullable)
-  float* U;                     // forward save: [u_a | 1 | 0] of block kh [B][UP] (nullable)
+  float* U;                     // forward save: [u_in | 1 | 0] of block vh [B][UP] (nullable)
   const uint64_t* rng;          // dropout (nullable = off)
 };
 
@@ -573,70 +623,81 @@ __device__ __forceinline__ uint4 drop4(uint64_t seed, uint64_t offs, long long r
                        make_uint2((uint32_t)seed, (uint32_t)(seed >> 32) ^ (uint32_t)(offs >> 32)));
 }
 
-__host__ __device__ inline int link_ps(const WideLayout& L) { return (2 * L.Db > L.Da ? 2 * L.Db : L.Da) + 1; }
+__host__ __device__ inline int link_ps(const WideLayout& L) { return (L.WL > L.WY ? L.WL : L.WY) + 1; }
 
-// LDS floats of a link launch: [tail / bwd-head weights][head / bwd-tail weights][Q][partials][8 x 3 x 32 vectors]
+// LDS floats of a link launch: [last-Linear rows][W0y^T rows][Q][partials][8 x 3 x 32 vectors]
 __host__ __device__ inline int link_lds_floats(const WideLayout& L, bool w_last, bool w_first) {
-  return (w_last ? 2 * L.Db * L.HP : 0) + (w_first ? L.Da * L.HP : 0) + pad4(L.D * L.D) + pad4(LR * 32 * link_ps(L)) +
+  return (w_last ? L.WL * L.HP : 0) + (w_first ? L.WY * L.HP : 0) + pad4(L.D * L.D) + pad4(LR * 32 * link_ps(L)) +
          LR * 96;
 }
 
-// Forward (INV = false): tail(kt) = last Linear, t / tanh(s), z_b = exp(s) u_b + t, ldj += sum s, x Q_kt;
-//                        head(kh) = ActNorm, Linear-1 from P + u_a W0y^T + b0, GELU, dropout.
-// Inverse (INV = true):  tail(kt) = last Linear, y_b = (z_b - t) exp(-s), ActNorm^-1;
-//                        head(kh) = v = x Q_kh^T, Linear-1 as above.   (cnf.py:198-213, 337-339, 353-354)
-// DD > 0: the sample dimension D as a compile-time constant (every loop over D, Da, 2 Db fully unrolled, loads
-// batched); DD = 0: runtime D (any D <= 32).
-template <bool INV, int DD>
+// Forward (INV = false): tail(vt) = last Linear, t / tanh(s), x_T = exp(s) x_T + t on the half's transformed part,
+//                        ldj += sum s, x Q after a block's last half;
+//                        head(vh) = ActNorm before a block's first half, Linear-1 from P + u_in W0y^T + b0, GELU,
+//                        dropout.   (cnf.py:165-196, 333-335, 348-351)
+// Inverse (INV = true):  head(vh) = v = x Q^T before a block's first processed half; tail(vt) =
+//                        x_T = (x_T - t) exp(-s), ActNorm^-1 after its last half. The reference's two_way inverse
+//                        (cnf.py:198-213) runs nn_a then nn_b, both on the current state -- not the true inverse; the
+//                        processing order of the host loop reproduces exactly that.   (cnf.py:337-339, 353-354)
+// DD > 0: the sample dimension D as a compile-time constant (every loop over D and the per-side widths fully
+// unrolled); DD = 0: runtime D (any D <= 32).
+template <bool INV, int DD, int TS, int HS>
 __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x, ln = tid & 31, r = tid >> 5;
   const int HP = L.HP, H = L.H;
-  const int D = DD ? DD : L.D, Da = DD ? (DD + 1) / 2 : L.Da, Db = DD ? DD / 2 : L.Db, O2 = 2 * Db;
+  const int D = DD ? DD : L.D, Da = DD ? (DD + 1) / 2 : L.Da, Db = DD ? DD / 2 : L.Db;
+  const int nout_t = TS ? Da : Db, toff_t = TS ? 0 : Da, O2 = 2 * nout_t;
+  const int nin_h = HS ? Db : Da, ioff_h = HS ? Da : 0;
   const int PS = link_ps(L);
   const int nq = HP / 4;
+  const int vt = a.vt, vh = a.vh;
+  const int kt = vt >= 0 ? vt / L.S : -1, kh = vh >= 0 ? vh / L.S : -1;
+  const bool t_first = vt >= 0 && vt % L.S == 0, t_last = vt >= 0 && vt % L.S == L.S - 1;
+  const bool h_first = vh >= 0 && vh % L.S == 0;
   float* Wl = sm;
-  float* W0 = Wl + (a.kt >= 0 ? O2 * HP : 0);
-  float* Qs = W0 + (a.kh >= 0 ? Da * HP : 0);
+  float* W0 = Wl + (vt >= 0 ? L.WL * HP : 0);
+  float* Qs = W0 + (vh >= 0 ? L.WY * HP : 0);
   float* part = Qs + pad4(D * D);
   float* Os = part + pad4(LR * 32 * PS) + r * 96;
   float* vs = Os + 32;
   float* us = vs + 32;
-  const int kq = INV ? a.kh : a.kt;                 // the orthonormal matrix this launch applies
+  // the orthonormal matrix this launch applies: forward after the tail block's last half, inverse before the head
+  // block's first processed half
+  const int kq = INV ? (h_first ? kh : -1) : (t_last ? kt : -1);
   const long long row = (long long)blockIdx.x * LR + r;
   const bool valid = row < a.B;
   const bool lv = valid && ln < D;
-  // The sample's HBM rows (last activation of block kt, projection row of block kh, saved input) are requested
+  // The sample's HBM rows (last activation of block vt, projection row of block vh, saved input) are requested
   // first, so their latency overlaps the weight staging instead of serialising inside the dot-product loops.
   floatx4 ach[MQ], pch[MQ];
-  const float* arow = a.kt >= 0 ? a.Alast + row * HP : nullptr;
+  const float* arow = vt >= 0 ? a.Alast + row * HP : nullptr;
   const float* Pr = nullptr;
-  if (a.kh >= 0) Pr = a.P + (a.cidx && valid ? a.cidx[row] : row) * a.ldP + (long long)a.kh * HP;
+  if (vh >= 0) Pr = a.P + (a.cidx && valid ? a.cidx[row] : row) * a.ldP + (long long)vh * HP;
 #pragma unroll
   for (int t = 0; t < MQ; ++t) {
     const int q = ln + 32 * t;
     if (valid && q < nq) {
-      if (a.kt >= 0) ach[t] = ld4(arow + 4 * q);
-      if (a.kh >= 0) pch[t] = ld4(Pr + 4 * q);
+      if (vt >= 0) ach[t] = ld4(arow + 4 * q);
+      if (vh >= 0) pch[t] = ld4(Pr + 4 * q);
     }
   }
   float xpre = 0.f;
-  if (lv) xpre = a.kt >= 0 ? a.Xt[row * L.XP + ln] : a.xin[row * D + ln];
-  if (a.kt >= 0) stage4(Wl, a.pk + L.pk_wl + (long long)a.kt * O2 * HP, O2 * HP / 4);
-  if (a.kh >= 0) stage4(W0, a.pk + L.pk_w0y + (long long)a.kh * Da * HP, Da * HP / 4);
+  if (lv) xpre = vt >= 0 ? a.Xt[row * L.XP + ln] : a.xin[row * D + ln];
+  if (vt >= 0) stage4(Wl, a.pk + L.pk_wl + (long long)vt * L.WL * HP, O2 * HP / 4);
+  if (vh >= 0) stage4(W0, a.pk + L.pk_w0y + (long long)vh * L.WY * HP, nin_h * HP / 4);
   if (kq >= 0 && kq < L.nb - 1)
     for (int e = tid; e < D * D; e += WWG) Qs[e] = a.pk[L.pk_q + (long long)kq * D * D + e];
   __syncthreads();
-
   uint64_t seed = 0, offs = 0;
   if (a.rng) {
     seed = a.rng[0];
     offs = a.rng[1];
   }
   float xi = 0.f;                                   // element ln of the sample's D-vector
-  // ------------------------------------------------------------ tail of block kt
-  if (a.kt >= 0) {
-    const int k = a.kt;
+  // ------------------------------------------------------------ tail of virtual block vt
+  if (vt >= 0) {
+    const int st = vt % L.S;
     float acc[DM];
 #pragma unroll
     for (int j = 0; j < DM; ++j) acc[j] = 0.f;
@@ -663,42 +724,41 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
       float s = 0.f;
 #pragma unroll
       for (int l = 0; l < 32; ++l) s += part[(r * 32 + l) * PS + ln];
-      Os[ln] = s + a.prm[wcb(L, k) + L.lin_b[L.NH] + ln];
+      Os[ln] = s + a.prm[vbase(L, vt) + L.lin_b[st][L.NH] + ln];
     }
     __syncthreads();
     float sj = 0.f;
-    const bool anb = L.an && k < L.nb - 1;
-    const float* sc = a.prm + (long long)k * L.blk_stride;
+    const int jt = ln - toff_t;
+    const bool tl = lv && jt >= 0 && jt < nout_t;             // lane in the transformed part
+    const float* sc = a.prm + (long long)kt * L.blk_stride;
     if (lv) {
       xi = xpre;
       if (!INV) {
-        if (anb) xi = sc[ln] * xi + sc[D + ln];                    // ActNorm (cnf.py:350)
-        if (ln >= Da) {
-          const int j = ln - Da;
-          sj = tanh_bf(Os[Db + j]);
-          xi = fmaf(exp_fast(sj), xi, Os[j]);                     // z_b = exp(s) y_b + t (cnf.py:179)
-          if (a.S) a.S[row * L.SP + j] = sj;
+        if (t_first && L.an && kt < L.nb - 1) xi = sc[ln] * xi + sc[D + ln];       // ActNorm (cnf.py:350)
+        if (tl) {
+          sj = tanh_bf(Os[nout_t + jt]);
+          xi = fmaf(exp_fast(sj), xi, Os[jt]);                    // x_T = exp(s) x_T + t (cnf.py:179, 184)
+          if (a.S) a.S[row * L.SP + jt] = sj;
         }
       } else {
-        if (ln >= Da) {
-          const int j = ln - Da;
-          xi = (xi - Os[j]) * exp_fast(-tanh_bf(Os[Db + j]));     // y_b = (z_b - t) exp(-s) (cnf.py:201)
-        }
-        if (anb) xi = (xi - sc[D + ln]) / sc[ln];                 // ActNorm inverse (cnf.py:354)
+        if (tl) xi = (xi - Os[jt]) * exp_fast(-tanh_bf(Os[nout_t + jt]));   // (x_T - t) exp(-s) (cnf.py:201, 208)
+        if (t_last && L.an && kt < L.nb - 1) xi = (xi - sc[D + ln]) / sc[ln];  // ActNorm inverse (cnf.py:354)
       }
     }
     if (!INV) {
       const float ssum = half_sum(sj);
-      if (k < L.nb - 1) {                                         // x Q_k (cnf.py:333-335)
-        vs[ln] = xi;
-        __syncthreads();
-        float c = 0.f;
-        if (ln < D) {
+      if (vt < L.nv - 1) {
+        if (t_last) {                                             // x Q_k (cnf.py:333-335)
+          vs[ln] = xi;
+          __syncthreads();
+          float c = 0.f;
+          if (ln < D) {
 #pragma unroll
-          for (int i = 0; i < DM; ++i)
-            if (i < D) c = fmaf(vs[i], Qs[i * D + ln], c);
+            for (int i = 0; i < DM; ++i)
+              if (i < D) c = fmaf(vs[i], Qs[i * D + ln], c);
+          }
+          xi = c;
         }
-        xi = c;
         if (valid && ln == 0) a.ldj[row] += ssum;
       } else {
         const float zz = half_sum(xi * xi);
@@ -709,25 +769,24 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
           if (a.nllp) a.nllp[row] = 0.5f * zz - lj;               // per-sample inn_nll_loss (utils.py:49-53)
         }
       }
-    } else if (k == 0 && lv) {
+    } else if (t_last && kt == 0 && lv) {
       a.z[row * D + ln] = xi;
     }
   } else {
     xi = xpre;
     if (!INV && valid && ln == 0) a.ldj[row] = 0.f;
   }
-  // ------------------------------------------------------------ head of block kh
-  if (a.kh >= 0) {
-    const int k = a.kh;
+  // ------------------------------------------------------------ head of virtual block vh
+  if (vh >= 0) {
     if (!INV) {
-      if (lv) a.Xh[row * L.XP + ln] = xi;                         // saved pre-ActNorm input
-      if (L.an && k < L.nb - 1) {
-        const float* sc = a.prm + (long long)k * L.blk_stride;
+      if (lv) a.Xh[row * L.XP + ln] = xi;                         // saved input (pre-ActNorm for a first half)
+      if (h_first && L.an && kh < L.nb - 1) {
+        const float* sc = a.prm + (long long)kh * L.blk_stride;
         if (ln < D) xi = sc[ln] * xi + sc[D + ln];
-        if (valid && ln == 0) a.ldj[row] += a.pk[L.pk_ldc + k];   // ActNorm log|det J| (cnf.py:349)
+        if (valid && ln == 0) a.ldj[row] += a.pk[L.pk_ldc + kh];  // ActNorm log|det J| (cnf.py:349)
       }
     } else {
-      if (k < L.nb - 1) {                                         // v = x Q_k^T (cnf.py:337-339)
+      if (h_first && kh < L.nb - 1) {                             // v = x Q_k^T (cnf.py:337-339)
         vs[ln] = xi;
         __syncthreads();
         float c = 0.f;
@@ -738,23 +797,23 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
         }
         xi = c;
       }
-      if (lv) a.Xh[row * L.XP + ln] = xi;                         // v, read back by this block's tail
+      if (lv) a.Xh[row * L.XP + ln] = xi;                         // read back by this half's tail
     }
     us[ln] = xi;
     __syncthreads();
     float ua[DM / 2];
 #pragma unroll
-    for (int j = 0; j < DM / 2; ++j) ua[j] = j < Da ? us[j] : 0.f;
-    if (a.U && valid && ln < L.UP) a.U[row * L.UP + ln] = ln < Da ? us[ln] : (ln == Da ? 1.f : 0.f);
+    for (int j = 0; j < DM / 2; ++j) ua[j] = j < nin_h ? us[ioff_h + j] : 0.f;
+    if (a.U && valid && ln < L.UP) a.U[row * L.UP + ln] = ln < nin_h ? us[ioff_h + ln] : (ln == nin_h ? 1.f : 0.f);
     if (valid) {
-      const float* b0 = a.pk + L.pk_b0 + (long long)k * HP;
-      const uint32_t tag = (uint32_t)k * 16u;
+      const float* b0 = a.pk + L.pk_b0 + (long long)vh * HP;
+      const uint32_t tag = (uint32_t)vh * 16u;
       auto chunk = [&](int q, floatx4 pv4) {
         const int n = 4 * q;
         floatx4 pre = pv4 + ld4(b0 + n);
 #pragma unroll
         for (int j = 0; j < DM / 2; ++j) {
-          if (j < Da) {
+          if (j < nin_h) {
             const floatx4 w = ld4(W0 + j * HP + n);
             pre.x = fmaf(ua[j], w.x, pre.x);
             pre.y = fmaf(ua[j], w.y, pre.y);
@@ -787,82 +846,91 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
   }
 }
 
-// Backward links.
-//   head-B(k): dv = dX Q_k^T (k < nb-1) or dX = dz (last); coupling backward -> dO = [dt, ds'] (stored),
-//              du_b, dv_a (stored in DV); dZ_{NH-1} = (dO W_NH) * G_{NH-1} (stored).
-//   tail-B(k): du_a = dv_a + dZ_0 W0y; ActNorm backward (per-row partials of dscale, dbias) -> dX_k.
-// One launch = tail-B(kt) then head-B(kt - 1) (kt = -1: head-B(nb-1) only).
+// Backward links (forward order reversed, one virtual block = one half-coupling).
+//   head-B(v): dv = dX Q_k^T after a block's last half (k < nb-1), or dX = dz (final half); half-coupling backward on
+//              the transformed part -> dO = [dt, ds'] (stored), d x_T and the untouched input part (stored in DV);
+//              dZ_{NH-1} = (dO W_NH) * G_{NH-1} (stored).
+//   tail-B(v): d x_in = DV_in + dZ_0 W0y on the input part; ActNorm backward before a block's first half (per-row
+//              partials of dscale, dbias) -> dX of the previous half.
+// One launch = tail-B(vt) then head-B(vt - 1) (vt = -1: head-B(nv-1) only).
 struct LinkBArgs {
   long long B;
-  int kt, kh;
+  int vt, vh;
   const float* prm; const float* pk;
-  const float* X;  long long sX;      // saved block inputs, block k at X + k * sX
+  const float* X;  long long sX;      // saved half inputs, virtual block v at X + v * sX
   const float* S;  long long sS;      // saved tanh(s)
-  const float* dz; const float* dldj; // head-B(nb-1) input (dz nullable in NLL mode), dldj nullable
+  const float* dz; const float* dldj; // head-B(nv-1) input (dz nullable in NLL mode), dldj nullable
   const float* zn; const float* dvals; int nll;   // NLL mode: dz = z g / B, dldj = -g / B, g = dvals[0] + dvals[1]
-  // tail-B(kt)
-  const float* dZ0; long long ldZ0;   // dZ_0 of block kt (row stride ldZ0)
-  float* DV;                          // [B][XP]: dv_a (Da) | du_b (Db)  (written by head-B, read by tail-B)
-  float* ANP;                         // [B][AP] ActNorm partials of block kt (du*x | du)
-  float* dy;                          // kt == 0: dL/dy (nullable)
-  // head-B(kh)
-  float* Ob;                          // [B][OP] dO of block kh
-  const float* Gl;                    // [B][HP] G_{NH-1} of block kh
-  float* dZl;  long long ldZl;        // dZ_{NH-1} of block kh
+  // tail-B(vt)
+  const float* dZ0; long long ldZ0;   // dZ_0 of block vt (row stride ldZ0)
+  float* DV;                          // [B][XP]: d(input part) | d(transformed part)  (head-B -> tail-B)
+  float* ANP;                         // [B][AP] ActNorm partials of real block vt / S (du*x | du)
+  float* dy;                          // vt == 0: dL/dy (nullable)
+  // head-B(vh)
+  float* Ob;                          // [B][OP] dO of block vh
+  const float* Gl;                    // [B][HP] G_{NH-1} of block vh
+  float* dZl;  long long ldZl;        // dZ_{NH-1} of block vh
 };
 
-template <int DD>
+template <int DD, int TS, int HS>
 __global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const LinkBArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x, ln = tid & 31, r = tid >> 5;
   const int HP = L.HP;
-  const int D = DD ? DD : L.D, Da = DD ? (DD + 1) / 2 : L.Da, Db = DD ? DD / 2 : L.Db, O2 = 2 * Db;
+  const int D = DD ? DD : L.D, Da = DD ? (DD + 1) / 2 : L.Da, Db = DD ? DD / 2 : L.Db;
+  const int nin_t = TS ? Db : Da, ioff_t = TS ? Da : 0;
+  const int nout_h = HS ? Da : Db, toff_h = HS ? 0 : Da, O2 = 2 * nout_h;
   const int PS = link_ps(L);
   const int nq = HP / 4;
-  float* Wl = sm;                                   // [2Db][HP] last Linear of block kh
-  float* W0 = Wl + (a.kh >= 0 ? O2 * HP : 0);       // [Da][HP] W0y^T of block kt
-  float* Qs = W0 + (a.kt >= 0 ? Da * HP : 0);
+  const int vt = a.vt, vh = a.vh;
+  const int kt = vt >= 0 ? vt / L.S : -1, kh = vh >= 0 ? vh / L.S : -1;
+  const bool t_first = vt >= 0 && vt % L.S == 0;
+  const bool h_first = vh >= 0 && vh % L.S == 0, h_last = vh >= 0 && vh % L.S == L.S - 1;
+  float* Wl = sm;                                   // [2 nout][HP] last Linear of block vh
+  float* W0 = Wl + (vh >= 0 ? L.WL * HP : 0);       // [nin][HP] W0y^T of block vt
+  float* Qs = W0 + (vt >= 0 ? L.WY * HP : 0);
   float* part = Qs + pad4(D * D);
   float* Os = part + pad4(LR * 32 * PS) + r * 96;
   float* vs = Os + 32;
   const long long row = (long long)blockIdx.x * LR + r;
   const bool valid = row < a.B;
   const bool lv = valid && ln < D;
-  // HBM rows first (dZ_0 of block kt, G of block kh, per-sample vectors), then the weight staging
+  // HBM rows first (dZ_0 of block vt, G of block vh, per-sample vectors), then the weight staging
   floatx4 zch[MQ], gch[MQ];
-  const float* zr = a.kt >= 0 ? a.dZ0 + row * a.ldZ0 : nullptr;
-  const float* gr = a.kh >= 0 ? a.Gl + row * HP : nullptr;
+  const float* zr = vt >= 0 ? a.dZ0 + row * a.ldZ0 : nullptr;
+  const float* gr = vh >= 0 ? a.Gl + row * HP : nullptr;
 #pragma unroll
   for (int t = 0; t < MQ; ++t) {
     const int q = ln + 32 * t;
     if (valid && q < nq) {
-      if (a.kt >= 0) zch[t] = ld4(zr + 4 * q);
-      if (a.kh >= 0) gch[t] = ld4(gr + 4 * q);
+      if (vt >= 0) zch[t] = ld4(zr + 4 * q);
+      if (vh >= 0) gch[t] = ld4(gr + 4 * q);
     }
   }
+  const int jh = ln - toff_h;
+  const bool hl = lv && vh >= 0 && jh >= 0 && jh < nout_h;  // lane in head block's transformed part
   float dvp = 0.f, xkt = 0.f, xkh = 0.f, skh = 0.f;
   if (lv) {
-    if (a.kt >= 0) {
+    if (vt >= 0) {
       dvp = a.DV[row * L.XP + ln];
-      xkt = a.X[a.kt * a.sX + row * L.XP + ln];
+      xkt = a.X[vt * a.sX + row * L.XP + ln];
     }
-    if (a.kh >= 0) {
-      xkh = a.X[a.kh * a.sX + row * L.XP + ln];
-      if (ln >= Da) skh = a.S[a.kh * a.sS + row * L.SP + ln - Da];
+    if (vh >= 0) {
+      xkh = a.X[vh * a.sX + row * L.XP + ln];
+      if (hl) skh = a.S[vh * a.sS + row * L.SP + jh];
     }
   }
-  if (a.kt >= 0) stage4(W0, a.pk + L.pk_w0y + (long long)a.kt * Da * HP, Da * HP / 4);
-  if (a.kh >= 0) {
-    stage4(Wl, a.pk + L.pk_wl + (long long)a.kh * O2 * HP, O2 * HP / 4);
-    if (a.kh < L.nb - 1)
-      for (int e = tid; e < D * D; e += WWG) Qs[e] = a.pk[L.pk_q + (long long)a.kh * D * D + e];
+  if (vt >= 0) stage4(W0, a.pk + L.pk_w0y + (long long)vt * L.WY * HP, nin_t * HP / 4);
+  if (vh >= 0) {
+    stage4(Wl, a.pk + L.pk_wl + (long long)vh * L.WL * HP, O2 * HP / 4);
+    if (h_last && kh < L.nb - 1)
+      for (int e = tid; e < D * D; e += WWG) Qs[e] = a.pk[L.pk_q + (long long)kh * D * D + e];
   }
   __syncthreads();
   const float gscale = a.nll ? (a.dvals ? a.dvals[0] + a.dvals[1] : 1.f) / (float)a.B : 0.f;
   float dxi = 0.f;                                  // element ln of the gradient w.r.t. the current D-vector
-  // ------------------------------------------------------------ tail-B of block kt
-  if (a.kt >= 0) {
-    const int k = a.kt;
+  // ------------------------------------------------------------ tail-B of virtual block vt
+  if (vt >= 0) {
     float acc[DM / 2];
 #pragma unroll
     for (int j = 0; j < DM / 2; ++j) acc[j] = 0.f;
@@ -870,7 +938,7 @@ __global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const Lin
       auto chunk = [&](int q, floatx4 dzv) {
 #pragma unroll
         for (int j = 0; j < DM / 2; ++j) {
-          if (j < Da) {
+          if (j < nin_t) {
             const floatx4 w = ld4(W0 + j * HP + 4 * q);
             acc[j] = fmaf(dzv.x, w.x, fmaf(dzv.y, w.y, fmaf(dzv.z, w.z, fmaf(dzv.w, w.w, acc[j]))));
           }
@@ -883,32 +951,32 @@ __global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const Lin
     }
 #pragma unroll
     for (int j = 0; j < DM / 2; ++j)
-      if (j < Da) part[(r * 32 + ln) * PS + j] = acc[j];
+      if (j < nin_t) part[(r * 32 + ln) * PS + j] = acc[j];
     __syncthreads();
     if (lv) {
       float du = dvp;
-      if (ln < Da) {
+      const int ji = ln - ioff_t;
+      if (ji >= 0 && ji < nin_t) {
         float t = 0.f;
 #pragma unroll
-        for (int l = 0; l < 32; ++l) t += part[(r * 32 + l) * PS + ln];
-        du += t;                                                  // du_a = dv_a + dZ_0 W0y
+        for (int l = 0; l < 32; ++l) t += part[(r * 32 + l) * PS + ji];
+        du += t;                                                  // d x_in = dv_in + dZ_0 W0y
       }
-      if (L.an && k < L.nb - 1) {
-        const float* sc = a.prm + (long long)k * L.blk_stride;
+      if (t_first && L.an && kt < L.nb - 1) {
+        const float* sc = a.prm + (long long)kt * L.blk_stride;
         a.ANP[row * L.AP + ln] = du * xkt;                       // dscale partial
         a.ANP[row * L.AP + D + ln] = du;                         // dbias partial
         du *= sc[ln];
       }
       dxi = du;
-      if (k == 0 && a.dy) a.dy[row * D + ln] = dxi;
+      if (vt == 0 && a.dy) a.dy[row * D + ln] = dxi;
     }
   } else if (lv) {
     dxi = a.nll ? a.zn[row * D + ln] * gscale : (a.dz ? a.dz[row * D + ln] : 0.f);
   }
-  // ------------------------------------------------------------ head-B of block kh
-  if (a.kh >= 0) {
-    const int k = a.kh;
-    if (k < L.nb - 1) {                                           // dv = dX Q_k^T
+  // ------------------------------------------------------------ head-B of virtual block vh
+  if (vh >= 0) {
+    if (h_last && kh < L.nb - 1) {                                // dv = dX Q_k^T
       vs[ln] = dxi;
       __syncthreads();
       float c = 0.f;
@@ -920,19 +988,18 @@ __global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const Lin
       dxi = c;
     }
     float dvo = dxi;
-    if (lv && ln >= Da) {
-      const int j = ln - Da;
+    if (hl) {
       const float dl = a.nll ? -gscale : (a.dldj ? a.dldj[row] : 0.f);
       float ub = xkh;
-      if (L.an && k < L.nb - 1) {
-        const float* sc = a.prm + (long long)k * L.blk_stride;
+      if (h_first && L.an && kh < L.nb - 1) {
+        const float* sc = a.prm + (long long)kh * L.blk_stride;
         ub = sc[ln] * ub + sc[D + ln];
       }
       const float s = skh;
       const float es = exp_fast(s);
-      dvo = dxi * es;                                             // du_b
-      Os[j] = dxi;                                                // dt
-      Os[Db + j] = fmaf(dxi * ub, es, dl) * (1.f - s * s);        // d s' (through tanh and the log-det)
+      dvo = dxi * es;                                             // d x_T before the affine
+      Os[jh] = dxi;                                               // dt
+      Os[nout_h + jh] = fmaf(dxi * ub, es, dl) * (1.f - s * s);   // d s' (through tanh and the log-det)
     }
     if (valid && ln < L.XP) a.DV[row * L.XP + ln] = ln < D ? dvo : 0.f;
     __syncthreads();
@@ -1067,6 +1134,7 @@ GemmArgs gemm_args(int M, int N, int K, const float* A, long long lda, const flo
   g.C = C;
   g.ldc = ldc;
   g.keep_scale = 1.f;
+  g.cb_S = 1;
   return g;
 }
 
@@ -1113,7 +1181,7 @@ int gemm(const GemmArgs& g, int groups, hipStream_t st) {
 }
 
 struct WideWs {       // workspace carve-up (floats)
-  float *P, *A, *G, *dZ, *dZ0, *X, *S, *U, *O, *DV, *ANP, *nllp;
+  float *P, *A, *G, *dZ, *dZ0, *X, *S, *U, *O, *DV, *ANP, *nllp, *Hp;
   long long total;
 };
 
@@ -1127,53 +1195,80 @@ WideWs carve(const WideLayout& L, long long B, bool train, float* base) {
     return p;
   };
   const long long slab = B * L.HP;
-  w.P = take(B * (long long)L.nb * L.HP);
+  w.P = take(B * (long long)L.nv * L.HP);
   w.nllp = take(B);
   if (train) {
-    w.A = take((long long)L.nb * L.NH * slab);
-    w.G = take((long long)L.nb * L.NH * slab);
-    w.dZ = take((long long)L.nb * (L.NH - 1) * slab);
-    w.dZ0 = take(B * (long long)L.nb * L.HP);
-    w.X = take((long long)(L.nb + 1) * B * L.XP);
-    w.S = take((long long)L.nb * B * L.SP);
-    w.U = take((long long)L.nb * B * L.UP);
-    w.O = take((long long)L.nb * B * L.OP);
+    w.A = take((long long)L.nv * L.NH * slab);
+    w.G = take((long long)L.nv * L.NH * slab);
+    w.dZ = take((long long)L.nv * (L.NH - 1) * slab);
+    w.dZ0 = take(B * (long long)L.nv * L.HP);
+    w.X = take((long long)(L.nv + 1) * B * L.XP);
+    w.S = take((long long)L.nv * B * L.SP);
+    w.U = take((long long)L.nv * B * L.UP);
+    w.O = take((long long)L.nv * B * L.OP);
     w.DV = take(B * (long long)L.XP);
     w.ANP = take((long long)L.nb * B * L.AP);
   } else {
     w.A = take(2 * slab);     // ping-pong
     w.X = take(B * (long long)L.XP);
   }
+  if (L.Cp != L.C) w.Hp = take(B * (long long)L.Cp);   // h re-laid to rows of Cp floats
   w.total = o;
   return w;
 }
 
+// (tail side, head side) of a link launch -> kernel instantiation; the unused side of a head-only / tail-only
+// launch is free, so every launch maps onto (0,0) [one-way], (0,1) or (1,0) [two_way].
+template <bool INV, int DD>
+void link_dispatch(int ts, int hs, dim3 grid, size_t lds, hipStream_t st, const WideLayout& L, const LinkArgs& a) {
+  if (L.S == 1) hipLaunchKernelGGL((k_wlink<INV, DD, 0, 0>), grid, dim3(WWG), lds, st, L, a);
+  else if (ts == 0 && hs == 1) hipLaunchKernelGGL((k_wlink<INV, DD, 0, 1>), grid, dim3(WWG), lds, st, L, a);
+  else hipLaunchKernelGGL((k_wlink<INV, DD, 1, 0>), grid, dim3(WWG), lds, st, L, a);
+}
+
 int link_launch(const WideLayout& L, const LinkArgs& a, bool inv, hipStream_t st) {
   dim3 grid((unsigned)((a.B + LR - 1) / LR));
-  const size_t lds = (size_t)link_lds_floats(L, a.kt >= 0, a.kh >= 0) * sizeof(float);
+  const size_t lds = (size_t)link_lds_floats(L, a.vt >= 0, a.vh >= 0) * sizeof(float);
+  const int ts = a.vt >= 0 ? a.vt % L.S : 1 - (a.vh % L.S);
+  const int hs = a.vh >= 0 ? a.vh % L.S : 1 - ts;
   if (L.D == 19) {                       // every shipped trajectory config (19 physical parameters)
-    if (inv) hipLaunchKernelGGL((k_wlink<true, 19>), grid, dim3(WWG), lds, st, L, a);
-    else hipLaunchKernelGGL((k_wlink<false, 19>), grid, dim3(WWG), lds, st, L, a);
+    if (inv) link_dispatch<true, 19>(ts, hs, grid, lds, st, L, a);
+    else link_dispatch<false, 19>(ts, hs, grid, lds, st, L, a);
   } else {
-    if (inv) hipLaunchKernelGGL((k_wlink<true, 0>), grid, dim3(WWG), lds, st, L, a);
-    else hipLaunchKernelGGL((k_wlink<false, 0>), grid, dim3(WWG), lds, st, L, a);
+    if (inv) link_dispatch<true, 0>(ts, hs, grid, lds, st, L, a);
+    else link_dispatch<false, 0>(ts, hs, grid, lds, st, L, a);
   }
   return bcnf_rt::launched();
 }
 
+template <int DD>
+void linkb_dispatch(int ts, int hs, dim3 grid, size_t lds, hipStream_t st, const WideLayout& L, const LinkBArgs& a) {
+  if (L.S == 1) hipLaunchKernelGGL((k_wlink_bwd<DD, 0, 0>), grid, dim3(WWG), lds, st, L, a);
+  else if (ts == 0 && hs == 1) hipLaunchKernelGGL((k_wlink_bwd<DD, 0, 1>), grid, dim3(WWG), lds, st, L, a);
+  else hipLaunchKernelGGL((k_wlink_bwd<DD, 1, 0>), grid, dim3(WWG), lds, st, L, a);
+}
+
 int linkb_launch(const WideLayout& L, const LinkBArgs& a, hipStream_t st) {
   dim3 grid((unsigned)((a.B + LR - 1) / LR));
-  const size_t lds = (size_t)link_lds_floats(L, a.kh >= 0, a.kt >= 0) * sizeof(float);
-  if (L.D == 19) hipLaunchKernelGGL((k_wlink_bwd<19>), grid, dim3(WWG), lds, st, L, a);
-  else hipLaunchKernelGGL((k_wlink_bwd<0>), grid, dim3(WWG), lds, st, L, a);
+  const size_t lds = (size_t)link_lds_floats(L, a.vh >= 0, a.vt >= 0) * sizeof(float);
+  const int ts = a.vt >= 0 ? a.vt % L.S : 1 - (a.vh % L.S);
+  const int hs = a.vh >= 0 ? a.vh % L.S : 1 - ts;
+  if (L.D == 19) linkb_dispatch<19>(ts, hs, grid, lds, st, L, a);
+  else linkb_dispatch<0>(ts, hs, grid, lds, st, L, a);
   return bcnf_rt::launched();
 }
 
 bool lds_attr_done = false;
 void ensure_lds_attrs() {
   if (lds_attr_done) return;
-  const void* fns[] = {(const void*)k_wlink<true, 0>, (const void*)k_wlink<false, 0>, (const void*)k_wlink<true, 19>,
-                       (const void*)k_wlink<false, 19>, (const void*)k_wlink_bwd<0>, (const void*)k_wlink_bwd<19>};
+  const void* fns[] = {
+      (const void*)k_wlink<true, 0, 0, 0>,  (const void*)k_wlink<true, 0, 0, 1>,  (const void*)k_wlink<true, 0, 1, 0>,
+      (const void*)k_wlink<false, 0, 0, 0>, (const void*)k_wlink<false, 0, 0, 1>, (const void*)k_wlink<false, 0, 1, 0>,
+      (const void*)k_wlink<true, 19, 0, 0>, (const void*)k_wlink<true, 19, 0, 1>, (const void*)k_wlink<true, 19, 1, 0>,
+      (const void*)k_wlink<false, 19, 0, 0>, (const void*)k_wlink<false, 19, 0, 1>,
+      (const void*)k_wlink<false, 19, 1, 0>, (const void*)k_wlink_bwd<0, 0, 0>, (const void*)k_wlink_bwd<0, 0, 1>,
+      (const void*)k_wlink_bwd<0, 1, 0>,    (const void*)k_wlink_bwd<19, 0, 0>, (const void*)k_wlink_bwd<19, 0, 1>,
+      (const void*)k_wlink_bwd<19, 1, 0>};
   for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   lds_attr_done = true;
 }
@@ -1184,25 +1279,36 @@ void ensure_lds_attrs() {
     if (_rc) return _rc;   \
   } while (0)
 
-// P = h W0h_all^T  (rows x nb*HP)
-int projection(const WideLayout& L, const float* pk, const float* h, long long rows, float* P, hipStream_t st) {
-  GemmArgs g = gemm_args((int)rows, L.nb * L.HP, L.C, h, L.C, pk + L.pk_w0h, L.C, P, (long long)L.nb * L.HP);
+// h (rows x C) as rows of Cp floats: h itself when C % 4 == 0, else a padded copy in `pad`
+const float* padded_h(const WideLayout& L, const float* h, long long rows, float* pad, hipStream_t st, int* rc) {
+  *rc = BCNF_OK;
+  if (L.Cp == L.C || rows == 0) return h;
+  const long long n = rows * L.Cp;
+  const int grid = (int)std::min<long long>((n + WWG - 1) / WWG, 4096);
+  hipLaunchKernelGGL(k_wpad_rows, dim3(grid), dim3(WWG), 0, st, h, L.C, rows, pad, L.Cp);
+  *rc = bcnf_rt::launched();
+  return pad;
+}
+
+// P = h W0h_all^T  (rows x nv*HP), h with row stride Cp
+int projection(const WideLayout& L, const float* pk, const float* hp, long long rows, float* P, hipStream_t st) {
+  GemmArgs g = gemm_args((int)rows, L.nv * L.HP, L.Cp, hp, L.Cp, pk + L.pk_w0h, L.Cp, P, (long long)L.nv * L.HP);
   return gemm<true, true, EPI_STORE>(g, 1, st);
 }
 
-// hidden Linear l (1..NH-1) of block k: A_l = dropout(GELU(A_{l-1} W_l^T + b_l)), G_l
-int hidden_fwd(const WideLayout& L, const float* prm, const float* pk, int k, int l, long long B, const float* Ain,
+// hidden Linear l (1..NH-1) of virtual block v: A_l = dropout(GELU(A_{l-1} W_l^T + b_l)), G_l
+int hidden_fwd(const WideLayout& L, const float* prm, const float* pk, int v, int l, long long B, const float* Ain,
                float* Aout, float* Gout, const uint64_t* rng, hipStream_t st) {
-  GemmArgs g = gemm_args((int)B, L.HP, L.HP, Ain, L.HP, pk + L.pk_hid + ((long long)k * (L.NH - 1) + (l - 1)) * L.HP * L.HP,
+  GemmArgs g = gemm_args((int)B, L.HP, L.HP, Ain, L.HP, pk + L.pk_hid + ((long long)v * (L.NH - 1) + (l - 1)) * L.HP * L.HP,
                          L.HP, Aout, L.HP);
-  g.bias = prm + wcb(L, k) + L.lin_b[l];
+  g.bias = prm + vbase(L, v) + L.lin_b[v % L.S][l];
   g.aux = Gout;
   g.ldaux = L.HP;
   g.n_real = L.H;
   g.rng = rng;
   g.thresh = L.thresh;
   g.keep_scale = L.keep_scale;
-  g.tag = (uint32_t)k * 16u + (uint32_t)l;
+  g.tag = (uint32_t)v * 16u + (uint32_t)l;
   return gemm<true, true, EPI_ACT>(g, 1, st);
 }
 
@@ -1213,36 +1319,39 @@ int wide_forward(const WideLayout& L, const float* prm, const float* pk, const f
   const bool drop = training && L.p > 0.f && rng;
   const WideWs w = carve(L, B, save, ws);
   const long long slab = B * L.HP;
-  WCHK(projection(L, pk, h, B, w.P, st));
-  auto Aptr = [&](int k, int l) -> float* { return save ? w.A + ((long long)k * L.NH + l) * slab : w.A + (l & 1) * slab; };
-  auto Gptr = [&](int k, int l) -> float* { return save ? w.G + ((long long)k * L.NH + l) * slab : nullptr; };
-  for (int k = -1; k < L.nb; ++k) {
-    if (k >= 0)
+  int rc;
+  const float* hp = padded_h(L, h, B, w.Hp, st, &rc);
+  WCHK(rc);
+  WCHK(projection(L, pk, hp, B, w.P, st));
+  auto Aptr = [&](int v, int l) -> float* { return save ? w.A + ((long long)v * L.NH + l) * slab : w.A + (l & 1) * slab; };
+  auto Gptr = [&](int v, int l) -> float* { return save ? w.G + ((long long)v * L.NH + l) * slab : nullptr; };
+  for (int v = -1; v < L.nv; ++v) {
+    if (v >= 0)
       for (int l = 1; l < L.NH; ++l)
-        WCHK(hidden_fwd(L, prm, pk, k, l, B, Aptr(k, l - 1), Aptr(k, l), Gptr(k, l), drop ? rng : nullptr, st));
+        WCHK(hidden_fwd(L, prm, pk, v, l, B, Aptr(v, l - 1), Aptr(v, l), Gptr(v, l), drop ? rng : nullptr, st));
     LinkArgs a;
     memset(&a, 0, sizeof(a));
     a.B = B;
-    a.kt = k;
-    a.kh = (k + 1 < L.nb) ? k + 1 : -1;
+    a.vt = v;
+    a.vh = (v + 1 < L.nv) ? v + 1 : -1;
     a.prm = prm;
     a.pk = pk;
-    if (k >= 0) {
-      a.Alast = Aptr(k, L.NH - 1);
-      a.Xt = save ? w.X + (long long)k * B * L.XP : w.X;
-      a.S = save ? w.S + (long long)k * B * L.SP : nullptr;
+    if (v >= 0) {
+      a.Alast = Aptr(v, L.NH - 1);
+      a.Xt = save ? w.X + (long long)v * B * L.XP : w.X;
+      a.S = save ? w.S + (long long)v * B * L.SP : nullptr;
     }
     a.z = z;
     a.ldj = ldj;
     a.nllp = w.nllp;
     a.xin = y;
-    if (a.kh >= 0) {
-      a.Xh = save ? w.X + (long long)a.kh * B * L.XP : w.X;
+    if (a.vh >= 0) {
+      a.Xh = save ? w.X + (long long)a.vh * B * L.XP : w.X;
       a.P = w.P;
-      a.ldP = (long long)L.nb * L.HP;
-      a.A0 = Aptr(a.kh, 0);
-      a.G0 = Gptr(a.kh, 0);
-      a.U = save ? w.U + (long long)a.kh * B * L.UP : nullptr;
+      a.ldP = (long long)L.nv * L.HP;
+      a.A0 = Aptr(a.vh, 0);
+      a.G0 = Gptr(a.vh, 0);
+      a.U = save ? w.U + (long long)a.vh * B * L.UP : nullptr;
     }
     a.rng = drop ? rng : nullptr;
     WCHK(link_launch(L, a, false, st));
@@ -1257,25 +1366,24 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
   ensure_lds_attrs();
   const WideWs w = carve(L, B, true, ws);
   const long long slab = B * L.HP;
-  const long long ld0 = (long long)L.nb * L.HP;
-  auto Aptr = [&](int k, int l) -> float* { return w.A + ((long long)k * L.NH + l) * slab; };
-  auto Gptr = [&](int k, int l) -> float* { return w.G + ((long long)k * L.NH + l) * slab; };
-  // dZ_l (l = 1..NH-1) of block k; dZ_0 of block k is the column slice k*HP of dZ0_all
-  auto dZptr = [&](int k, int l, long long* ld) -> float* {
+  const long long ld0 = (long long)L.nv * L.HP;
+  auto Gptr = [&](int v, int l) -> float* { return w.G + ((long long)v * L.NH + l) * slab; };
+  // dZ_l (l = 1..NH-1) of virtual block v; dZ_0 of v is the column slice v*HP of dZ0_all
+  auto dZptr = [&](int v, int l, long long* ld) -> float* {
     if (l == 0) {
       *ld = ld0;
-      return w.dZ0 + (long long)k * L.HP;
+      return w.dZ0 + (long long)v * L.HP;
     }
     *ld = L.HP;
-    return w.dZ + ((long long)k * (L.NH - 1) + (l - 1)) * slab;
+    return w.dZ + ((long long)v * (L.NH - 1) + (l - 1)) * slab;
   };
-  for (int k = L.nb; k >= 0; --k) {
-    // link: tail-B(k) (k < nb), head-B(k-1)
+  for (int v = L.nv; v >= 0; --v) {
+    // link: tail-B(v) (v < nv), head-B(v-1)
     LinkBArgs a;
     memset(&a, 0, sizeof(a));
     a.B = B;
-    a.kt = (k < L.nb) ? k : -1;
-    a.kh = k - 1;
+    a.vt = (v < L.nv) ? v : -1;
+    a.vh = v - 1;
     a.prm = prm;
     a.pk = pk;
     a.X = w.X;
@@ -1289,83 +1397,94 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
     a.nll = nll;
     a.DV = w.DV;
     a.dy = dy;
-    if (a.kt >= 0) {
-      a.dZ0 = dZptr(k, 0, &a.ldZ0);
-      a.ANP = w.ANP + (long long)k * B * L.AP;
+    if (a.vt >= 0) {
+      a.dZ0 = dZptr(v, 0, &a.ldZ0);
+      a.ANP = w.ANP + (long long)(v / L.S) * B * L.AP;
     }
-    if (a.kh >= 0) {
-      a.Ob = w.O + (long long)a.kh * B * L.OP;
-      a.Gl = Gptr(a.kh, L.NH - 1);
-      a.dZl = dZptr(a.kh, L.NH - 1, &a.ldZl);
+    if (a.vh >= 0) {
+      a.Ob = w.O + (long long)a.vh * B * L.OP;
+      a.Gl = Gptr(a.vh, L.NH - 1);
+      a.dZl = dZptr(a.vh, L.NH - 1, &a.ldZl);
     }
     WCHK(linkb_launch(L, a, st));
-    if (a.kh < 0) break;
-    const int kb = a.kh;
+    if (a.vh < 0) break;
+    const int vb = a.vh;
     // dZ_{l-1} = (dZ_l W_l) * G_{l-1}, l = NH-1 .. 1
     for (int l = L.NH - 1; l >= 1; --l) {
       long long ldi, ldo;
-      const float* din = dZptr(kb, l, &ldi);
-      float* dout = dZptr(kb, l - 1, &ldo);
+      const float* din = dZptr(vb, l, &ldi);
+      float* dout = dZptr(vb, l - 1, &ldo);
       GemmArgs g = gemm_args((int)B, L.HP, L.HP, din, ldi,
-                             pk + L.pk_hid + ((long long)kb * (L.NH - 1) + (l - 1)) * L.HP * L.HP, L.HP, dout, ldo);
-      g.aux = Gptr(kb, l - 1);
+                             pk + L.pk_hid + ((long long)vb * (L.NH - 1) + (l - 1)) * L.HP * L.HP, L.HP, dout, ldo);
+      g.aux = Gptr(vb, l - 1);
       g.ldaux = L.HP;
       WCHK((gemm<true, false, EPI_GRAD>(g, 1, st)));
     }
   }
+  int rc;
+  const float* hp = padded_h(L, h, B, w.Hp, st, &rc);
+  WCHK(rc);
   // ---- parameter gradients (canonical flat, every element written exactly once) ----
   if (dprm) {
-    if (L.NH > 1) {   // hidden Linears of every block in one grouped launch: [dW_l | db_l] = dZ_l^T [A_{l-1} | 1]
-      GemmArgs g = gemm_args(L.H, L.H + 1, (int)B, w.dZ, L.HP, w.A, L.HP, dprm, L.H);
+    auto flat_groups = [&](GemmArgs& g) {   // group g1 = virtual block (or real block with S = 1 semantics)
+      g.use_cb = 1;
+      g.cb_stride = L.blk_stride;
+      g.cb_an = L.an;
+      g.cb_nb = L.nb;
+    };
+    if (L.NH > 1) {   // hidden Linears of every virtual block in one grouped launch: [dW_l | db_l] = dZ_l^T [A_{l-1} | 1]
+      GemmArgs g = gemm_args(L.H, L.H + 1, (int)B, w.dZ, L.HP, w.A, L.HP, dprm + L.lin_w[0][1], L.H);
       g.G0 = L.NH - 1;
       g.sA1 = (long long)(L.NH - 1) * slab;
       g.sA0 = slab;
       g.sB1 = (long long)L.NH * slab;
       g.sB0 = slab;
-      g.use_cb = 1;
-      g.cb_stride = L.blk_stride;
-      g.cb_an = L.an;
-      g.cb_nb = L.nb;
-      g.C = dprm + L.lin_w[1];
-      g.sC0 = (L.NH > 2) ? (L.lin_w[2] - L.lin_w[1]) : 0;
+      flat_groups(g);
+      g.cb_S = L.S;
+      g.cb_side = L.mlp[0] + (L.S == 2 ? L.lin_w[1][1] - L.lin_w[0][1] : 0);
+      g.sC0 = (L.NH > 2) ? (L.lin_w[0][2] - L.lin_w[0][1]) : 0;
       g.wcols = L.H;
       g.boff = (long long)L.H * L.H;
-      WCHK((gemm<false, false, EPI_LINGRAD>(g, L.nb * (L.NH - 1), st)));
+      WCHK((gemm<false, false, EPI_LINGRAD>(g, L.nv * (L.NH - 1), st)));
     }
-    {   // last Linear: [dW | db] = dO^T [A_{NH-1} | 1]
-      GemmArgs g = gemm_args(2 * L.Db, L.H + 1, (int)B, w.O, L.OP, w.A + (long long)(L.NH - 1) * slab, L.HP, dprm, L.H);
-      g.sA1 = B * L.OP;
-      g.sB1 = (long long)L.NH * slab;
-      g.use_cb = 1;
+    for (int sd = 0; sd < L.S; ++sd) {
+      {   // last Linear of every block's side-sd half: [dW | db] = dO^T [A_{NH-1} | 1]
+        GemmArgs g = gemm_args(2 * L.nout[sd], L.H + 1, (int)B, w.O + (long long)sd * B * L.OP, L.OP,
+                               w.A + ((long long)sd * L.NH + L.NH - 1) * slab, L.HP,
+                               dprm + (sd ? L.mlp[0] : 0) + L.lin_w[sd][L.NH], L.H);
+        g.sA1 = (long long)L.S * B * L.OP;
+        g.sB1 = (long long)L.S * L.NH * slab;
+        flat_groups(g);
+        g.wcols = L.H;
+        g.boff = (long long)2 * L.nout[sd] * L.H;
+        WCHK((gemm<false, false, EPI_LINGRAD>(g, L.nb, st)));
+      }
+      {   // Linear-1, input columns + bias: [dW0[:, :nin] | db0] = dZ_0^T [u_in | 1]
+        GemmArgs g = gemm_args(L.H, L.nin[sd] + 1, (int)B, w.dZ0 + (long long)sd * L.HP, ld0,
+                               w.U + (long long)sd * B * L.UP, L.UP, dprm + (sd ? L.mlp[0] : 0) + L.lin_w[sd][0],
+                               L.in0[sd]);
+        g.sA1 = (long long)L.S * L.HP;
+        g.sB1 = (long long)L.S * B * L.UP;
+        flat_groups(g);
+        g.wcols = L.nin[sd];
+        g.boff = (long long)L.H * L.in0[sd];
+        WCHK((gemm<false, false, EPI_LINGRAD>(g, L.nb, st)));
+      }
+    }
+    {   // Linear-1, condition columns of every virtual block in one GEMM: dW0h_all = dZ0_all^T h
+      GemmArgs g = gemm_args(L.nv * L.HP, L.C, (int)B, w.dZ0, ld0, hp, L.Cp, dprm, 0);
       g.cb_stride = L.blk_stride;
       g.cb_an = L.an;
       g.cb_nb = L.nb;
-      g.C = dprm + L.lin_w[L.NH];
-      g.wcols = L.H;
-      g.boff = (long long)2 * L.Db * L.H;
-      WCHK((gemm<false, false, EPI_LINGRAD>(g, L.nb, st)));
-    }
-    {   // Linear-1, y columns + bias: [dW0[:, :Da] | db0] = dZ_0^T [u_a | 1]
-      GemmArgs g = gemm_args(L.H, L.Da + 1, (int)B, w.dZ0, ld0, w.U, L.UP, dprm, L.in0);
-      g.sA1 = L.HP;
-      g.sB1 = B * L.UP;
-      g.use_cb = 1;
-      g.cb_stride = L.blk_stride;
-      g.cb_an = L.an;
-      g.cb_nb = L.nb;
-      g.C = dprm + L.lin_w[0];
-      g.wcols = L.Da;
-      g.boff = (long long)L.H * L.in0;
-      WCHK((gemm<false, false, EPI_LINGRAD>(g, L.nb, st)));
-    }
-    {   // Linear-1, condition columns of every block in one GEMM: dW0h_all = dZ0_all^T h
-      GemmArgs g = gemm_args(L.nb * L.HP, L.C, (int)B, w.dZ0, ld0, h, L.C, dprm, L.in0);
-      g.cb_stride = L.blk_stride;
-      g.cb_an = L.an;
-      g.cb_nb = L.nb;
+      g.cb_S = L.S;
+      g.cb_side = L.mlp[0];
       g.rm_hp = L.HP;
       g.rm_h = L.H;
-      g.rm_off = L.lin_w[0] + L.Da;
+      for (int sd = 0; sd < 2; ++sd) {
+        const int ss = sd < L.S ? sd : 0;
+        g.rm_off[sd] = L.lin_w[ss][0] + L.nin[ss];
+        g.rm_ld[sd] = L.in0[ss];
+      }
       WCHK((gemm<false, false, EPI_ROWMAP>(g, 1, st)));
     }
     if (L.an && L.nb > 1) {
@@ -1374,10 +1493,15 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
     }
   }
   if (dh) {   // dh = dZ0_all W0h_all
-    GemmArgs g = gemm_args((int)B, L.C, L.nb * L.HP, w.dZ0, ld0, pk + L.pk_w0h, L.C, dh, L.C);
+    GemmArgs g = gemm_args((int)B, L.C, L.nv * L.HP, w.dZ0, ld0, pk + L.pk_w0h, L.Cp, dh, L.C);
     WCHK((gemm<true, false, EPI_STORE>(g, 1, st)));
   }
   return BCNF_OK;
+}
+
+long long inverse_scratch_floats(const WideLayout& L, long long hrows, long long n) {
+  return pad4l(hrows * (long long)L.nv * L.HP) + 64 + pad4l(2 * n * (long long)L.HP) + 64 + pad4l(n * (long long)L.XP) +
+         64 + (L.Cp != L.C ? pad4l(hrows * (long long)L.Cp) + 64 : 0);
 }
 
 int wide_inverse(const WideLayout& L, const float* prm, const float* pk, const float* z, const float* h, long long hrows,
@@ -1386,23 +1510,30 @@ int wide_inverse(const WideLayout& L, const float* prm, const float* pk, const f
   if (n == 0) return BCNF_OK;
   ensure_lds_attrs();
   const bool drop = training && L.p > 0.f && rng;
-  // scratch: P (hrows x nb*HP) | A ping-pong (2 x n x HP) | X (n x XP)
+  // scratch: P (hrows x nv*HP) | A ping-pong (2 x n x HP) | X (n x XP) | padded h
   float* P = scratch;
-  float* A = P + pad4l(hrows * (long long)L.nb * L.HP) + 64;
+  float* A = P + pad4l(hrows * (long long)L.nv * L.HP) + 64;
   float* X = A + pad4l(2 * n * (long long)L.HP) + 64;
+  float* Hp = X + pad4l(n * (long long)L.XP) + 64;
   const long long slab = n * L.HP;
-  WCHK(projection(L, pk, h, hrows, P, st));
+  int rc;
+  const float* hp = padded_h(L, h, hrows, Hp, st, &rc);
+  WCHK(rc);
+  WCHK(projection(L, pk, hp, hrows, P, st));
   auto Ap = [&](int l) { return A + (l & 1) * slab; };
-  // blocks in reverse (cnf.py:499-506)
-  for (int k = L.nb; k >= 0; --k) {
-    if (k < L.nb)
+  // processing order (cnf.py:499-506 with the coupling inverse cnf.py:198-213): real blocks in reverse, and inside a
+  // two_way block nn_a's half before nn_b's (the reference's order)
+  auto order = [&](int i) { return i < 0 ? -1 : (L.nb - 1 - i / L.S) * L.S + i % L.S; };
+  for (int i = -1; i < L.nv; ++i) {
+    const int vt = order(i), vh = (i + 1 < L.nv) ? order(i + 1) : -1;
+    if (vt >= 0)
       for (int l = 1; l < L.NH; ++l)
-        WCHK(hidden_fwd(L, prm, pk, k, l, n, Ap(l - 1), Ap(l), nullptr, drop ? rng : nullptr, st));
+        WCHK(hidden_fwd(L, prm, pk, vt, l, n, Ap(l - 1), Ap(l), nullptr, drop ? rng : nullptr, st));
     LinkArgs a;
     memset(&a, 0, sizeof(a));
     a.B = n;
-    a.kt = (k < L.nb) ? k : -1;
-    a.kh = k - 1;
+    a.vt = vt;
+    a.vh = vh;
     a.prm = prm;
     a.pk = pk;
     a.Alast = Ap(L.NH - 1);
@@ -1411,7 +1542,7 @@ int wide_inverse(const WideLayout& L, const float* prm, const float* pk, const f
     a.xin = z;
     a.Xh = X;
     a.P = P;
-    a.ldP = (long long)L.nb * L.HP;
+    a.ldP = (long long)L.nv * L.HP;
     a.cidx = cidx;
     a.A0 = Ap(0);
     a.rng = drop ? rng : nullptr;
@@ -1430,6 +1561,14 @@ extern "C" {
 int bcnf_wide_supported(const BcnfStackDesc* desc) {
   WideLayout L;
   return wide_layout(desc, &L) == BCNF_OK ? 1 : 0;
+}
+
+int bcnf_wide_param_count(const BcnfStackDesc* desc, int64_t* n_trainable, int64_t* n_frozen) {
+  WideLayout L;
+  WCHK(wide_layout(desc, &L));
+  if (n_trainable) *n_trainable = L.n_trainable;
+  if (n_frozen) *n_frozen = (int64_t)(L.nb - 1) * L.D * L.D;
+  return BCNF_OK;
 }
 
 int bcnf_wide_packed_bytes(const BcnfStackDesc* desc, int64_t* bytes) {
@@ -1452,8 +1591,7 @@ int bcnf_wide_inverse_scratch_bytes(const BcnfStackDesc* desc, int64_t h_rows, i
   WideLayout L;
   WCHK(wide_layout(desc, &L));
   if (!bytes || h_rows < 0 || n_rows < 0) return BCNF_ERR_ARG;
-  *bytes = (pad4l(h_rows * (long long)L.nb * L.HP) + 64 + pad4l(2 * n_rows * (long long)L.HP) + 64 +
-            n_rows * (long long)L.XP + 64) * 4;
+  *bytes = inverse_scratch_floats(L, h_rows, n_rows) * 4;
   return BCNF_OK;
 }
 
@@ -1468,7 +1606,7 @@ int bcnf_wide_pack(const BcnfStackDesc* desc, const float* params, const float* 
   WCHK(bcnf_rt::launched());
   hipLaunchKernelGGL(k_wpack_ldc, dim3(1), dim3(((L.nb + 63) / 64) * 64), 0, st, L, params, (float*)packed);
   WCHK(bcnf_rt::launched());
-  hipLaunchKernelGGL(k_wpack_b0, dim3(L.nb), dim3(WWG), 0, st, L, params, (float*)packed);
+  hipLaunchKernelGGL(k_wpack_b0, dim3(L.nv), dim3(WWG), 0, st, L, params, (float*)packed);
   return bcnf_rt::launched();
 }
 
@@ -1479,7 +1617,8 @@ int bcnf_wide_forward(const BcnfStackDesc* desc, const float* params, const void
   WCHK(wide_layout(desc, &L));
   if (batch < 0) return BCNF_ERR_ARG;
   if (batch == 0) return BCNF_OK;
-  if (!params || !packed || !y || !h || !z || !ldj || !workspace || !aligned16(h) || !aligned16(workspace))
+  if (!params || !packed || !y || !h || !z || !ldj || !workspace || !aligned16(workspace) ||
+      (L.Cp == L.C && !aligned16(h)))
     return BCNF_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   WCHK(wide_forward(L, params, (const float*)packed, y, h, batch, z, ldj, training != 0, rng_state, (float*)workspace,
@@ -1525,7 +1664,8 @@ int bcnf_wide_inverse(const BcnfStackDesc* desc, const float* params, const void
   WCHK(wide_layout(desc, &L));
   if (n_rows < 0 || h_rows < 0) return BCNF_ERR_ARG;
   if (n_rows == 0) return BCNF_OK;
-  if (!params || !packed || !z || !h || !y || !scratch || !aligned16(h) || !aligned16(scratch)) return BCNF_ERR_ARG;
+  if (!params || !packed || !z || !h || !y || !scratch || !aligned16(scratch) || (L.Cp == L.C && !aligned16(h)))
+    return BCNF_ERR_ARG;
   if (!cond_index && h_rows != n_rows) return BCNF_ERR_ARG;
   return wide_inverse(L, params, (const float*)packed, z, h, h_rows, cond_index, n_rows, y, training != 0, rng_state,
                       (float*)scratch, (hipStream_t)stream);

@@ -27,6 +27,11 @@ class WideStack(FusedStack):
     def supported(self) -> bool:
         return bool(N.lib().bcnf_wide_supported(self._pdesc))
 
+    def counts(self):
+        a, b = ctypes.c_int64(0), ctypes.c_int64(0)
+        N.check(N.lib().bcnf_wide_param_count(self._pdesc, ctypes.byref(a), ctypes.byref(b)), "bcnf_wide_param_count")
+        return int(a.value), int(b.value)
+
     def _pack_into(self, out):
         N.check(N.lib().bcnf_wide_pack(self._pdesc, N.ptr(self.flat), N.ptr(self.qflat), N.ptr(out),
                                        N.stream_handle(self.flat.device)), "bcnf_wide_pack")

@@ -60,7 +60,7 @@ typedef struct BcnfStackDesc {
   int32_t hidden[BCNF_MAX_HIDDEN];   /* nested_sizes                           */
   int32_t n_blocks;                  /* n_blocks                               */
   int32_t act_norm;                  /* 0/1                                    */
-  int32_t two_way;                   /* 0/1 (the fused family requires 0)      */
+  int32_t two_way;                   /* 0/1 (small family: 0 only; wide: both) */
   float dropout;                     /* p of every nn.Dropout in the nested MLP */
 } BcnfStackDesc;
 
@@ -226,10 +226,13 @@ int bcnf_linear_backward(const float* x, const float* weight, const float* dy, i
  * as bcnf_stack_forward / _backward / _inverse / bcnf_nll_* above (cnf.py:49-107, 165-213, 312-354, 467-508;
  * utils.py:40-53; trainer.py:260-268), built from fp32-MFMA GEMMs (v_mfma_f32_32x32x2_f32) with fused
  * bias / GELU / dropout / gradient epilogues and per-sample link kernels (coupling, log|det J|, orthonormal mix,
- * ActNorm). Requirements: equal nested sizes, n_conditions % 4 == 0, size <= 32, two_way == 0.
+ * ActNorm). Requirements: equal nested sizes, size <= 32. two_way couplings (cnf.py:176-186) run as two
+ * half-couplings per block (nn_a then nn_b), with the reference's inverse (cnf.py:198-213).
  * The wide family takes the canonical flat params directly plus its own packed buffer (padded weight copies,
  * bcnf_wide_pack after every parameter update). */
 int bcnf_wide_supported(const BcnfStackDesc* desc);
+/* Canonical flat sizes as bcnf_param_count, for the wide family (two_way: nn_a then nn_b per block). */
+int bcnf_wide_param_count(const BcnfStackDesc* desc, int64_t* n_trainable, int64_t* n_frozen);
 int bcnf_wide_packed_bytes(const BcnfStackDesc* desc, int64_t* bytes);
 /* save != 0: the forward keeps every activation, GELU-derivative factor and block input for the backward. */
 int bcnf_wide_workspace_bytes(const BcnfStackDesc* desc, int64_t batch, int32_t save, int64_t* bytes);

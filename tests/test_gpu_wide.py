@@ -98,7 +98,7 @@ def _perturb(m):
 def _spec(shape, fsizes=()):
     return O.StackSpec(size=shape["size"], nested_sizes=shape["nested_sizes"], n_blocks=shape["n_blocks"],
                        n_conditions=shape["n_conditions"], dropout=shape["dropout"], act_norm=shape["act_norm"],
-                       feature_sizes=list(fsizes))
+                       two_way=shape.get("two_way", False), feature_sizes=list(fsizes))
 
 
 WIDE_SHAPES = [
@@ -107,6 +107,11 @@ WIDE_SHAPES = [
     dict(size=19, nested_sizes=[20], n_blocks=3, n_conditions=4, dropout=0.1, act_norm=True),      # one hidden layer
     dict(size=32, nested_sizes=[64] * 4, n_blocks=2, n_conditions=300, dropout=0.0, act_norm=True),
     dict(size=19, nested_sizes=[526] * 5, n_blocks=2, n_conditions=1360, dropout=0.407, act_norm=True),  # FC_large
+    # two_way couplings (nn_a then nn_b per block, cnf.py:176-186; the reference's non-inverse inverse, :198-213)
+    dict(size=19, nested_sizes=[40] * 2, n_blocks=3, n_conditions=24, dropout=0.2, act_norm=True, two_way=True),
+    dict(size=7, nested_sizes=[33] * 3, n_blocks=2, n_conditions=6, dropout=0.0, act_norm=False, two_way=True),
+    # n_conditions not a multiple of 4 (rows re-laid to 4-float multiples inside the library)
+    dict(size=19, nested_sizes=[24] * 2, n_blocks=2, n_conditions=13, dropout=0.0, act_norm=True),
 ]
 
 
@@ -374,3 +379,63 @@ def test_wide_sample_matches_oracle():
     assert got.shape == ref.shape == (50, 7, 19)
     ok, err = close(got, ref)
     assert ok, err
+
+
+# ------------------------------------------------------------------------------------------ two_way vs the reference
+def test_wide_two_way_coupling_layer_matches_reference():
+    """Standalone two_way coupling (D = 7, nested [19] * 5, C = 5: fixture g6 from the reference) and the one-way
+    layer at the reference test's shapes (tests/test_cnf.py:18-32): z, log|det J|, and the reference's inverse."""
+    from bcnf_amd import ConditionalAffineCouplingLayer
+    d = load_golden("g6_two_way.npz")
+    x, c = torch.from_numpy(d["x"]).to(DEV), torch.from_numpy(d["c"]).to(DEV)
+    for prefix, two_way, zk, lk, ik in (("layer_sd/", True, "z", "ldj", "inv"), ("l1_sd/", False, "z1", "ldj1", "inv1")):
+        layer = ConditionalAffineCouplingLayer(input_size=7, nested_sizes=[19] * 5, n_conditions=5, two_way=two_way)
+        layer.load_state_dict({k[len(prefix):]: torch.from_numpy(d[k]) for k in d.keys() if k.startswith(prefix)})
+        layer.to(DEV).eval()
+        with torch.no_grad():
+            z = layer(x, c, log_det_J=True)
+            inv = layer.inverse(z, c)
+        for got, key in ((z, zk), (layer.log_det_J, lk), (inv, ik)):
+            ok, err = close(got.cpu(), d[key])
+            assert ok, (prefix, key, err)
+
+
+def test_wide_two_way_model_matches_reference():
+    """two_way CondRealNVP_v2 (D = 19, [16] * 3, C = 80, 4 blocks, ActNorm; fixture g6 from the reference): z, ldj,
+    inverse; and every gradient vs the fp64 oracle."""
+    from bcnf_amd import CondRealNVP_v2, inn_nll_loss
+    from conftest import FC_SMALL_CFG
+    d = load_golden("g6_two_way.npz")
+    cfg = {"global": FC_SMALL_CFG["global"], "feature_networks": FC_SMALL_CFG["feature_networks"],
+           "model": {"kwargs": {"size": 19, "nested_sizes": [16] * 3, "n_conditions": 80, "n_blocks": 4,
+                                "dropout": 0.0, "act_norm": True, "two_way": True}}}
+    m = CondRealNVP_v2.from_config(cfg)
+    assert type(m.fused).__name__ == "WideStack"
+    sd = {k[len("m_sd/"):]: torch.from_numpy(d[k]) for k in d.keys() if k.startswith("m_sd/")}
+    m.load_state_dict(sd)
+    m.to(DEV).eval()
+    y, traj = torch.from_numpy(d["m_y"]).to(DEV), torch.from_numpy(d["m_traj"]).to(DEV)
+    with torch.no_grad():
+        z = m(y, traj, log_det_J=True)
+        ldj = m.log_det_J.clone()
+        inv = m.inverse(z, traj)
+    for got, key in ((z, "m_z"), (ldj, "m_ldj"), (inv, "m_inv")):
+        ok, err = close(got.cpu(), d[key])
+        assert ok, (key, err)
+    spec = O.StackSpec(size=19, nested_sizes=[16] * 3, n_blocks=4, n_conditions=80, act_norm=True, two_way=True,
+                       feature_sizes=[90, 80], feature_dropout=0.244)
+    sdg = {k: v.double().clone().requires_grad_(not k.endswith("orthonormal_matrix")) for k, v in sd.items()}
+    h = O.feature_forward(sdg, spec, torch.from_numpy(d["m_traj"]).double())
+    zo, lo = O.model_forward(sdg, spec, torch.from_numpy(d["m_y"]).double(), h)
+    O.inn_nll_loss(zo, lo).backward()
+    m.zero_grad(set_to_none=True)
+    zg = m(y, traj, log_det_J=True)
+    inn_nll_loss(zg, m.log_det_J).backward()
+    n = 0
+    for name, p in m.named_parameters():
+        if p.grad is None:
+            continue
+        ok, err = close(p.grad.cpu(), sdg[name].grad, rtol=1e-4, floor=1e-4)
+        assert ok, (name, err)
+        n += 1
+    assert n == len([k for k in sd if not k.endswith("orthonormal_matrix")])

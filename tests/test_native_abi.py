@@ -106,10 +106,11 @@ def test_wide_family_routing_and_layout_queries():
     big = N.make_desc(19, [526] * 5, 26, 1360, 0.407, True)
     assert lib.bcnf_wide_supported(ctypes.byref(big)) == 1
     for bad in (N.make_desc(19, [526, 500], 2, 1360, 0.0, True),          # unequal nested sizes
-                N.make_desc(19, [526] * 2, 2, 1361, 0.0, True),           # C % 4 != 0
-                N.make_desc(40, [526] * 2, 2, 1360, 0.0, True),           # D > 32
-                N.make_desc(19, [526] * 2, 2, 1360, 0.0, True, two_way=True)):
+                N.make_desc(40, [526] * 2, 2, 1360, 0.0, True)):          # D > 32
         assert lib.bcnf_wide_supported(ctypes.byref(bad)) == 0
+    for good in (N.make_desc(19, [526] * 2, 2, 1361, 0.0, True),          # C % 4 != 0 (rows re-laid inside)
+                 N.make_desc(19, [336] * 5, 26, 1360, 0.407, True, two_way=True)):   # trajectory_LSTM_2_large
+        assert lib.bcnf_wide_supported(ctypes.byref(good)) == 1
     cfg = {"global": {"parameter_selection": [str(i) for i in range(19)]},
            "model": {"kwargs": {"size": 19, "nested_sizes": [526] * 5, "n_conditions": 1360, "n_blocks": 26,
                                 "dropout": 0.407, "act_norm": True}},
@@ -133,3 +134,25 @@ def test_wide_family_routing_and_layout_queries():
     # the small family keeps FC_small
     small = N.make_desc(19, [16] * 7, 32, 80, 0.383, True)
     assert lib.bcnf_stack_supported(ctypes.byref(small)) == 1
+
+
+def test_two_way_parameter_layout_matches_module_tree():
+    """two_way: each block's nn_b parameters follow its nn_a parameters in the flat buffer (state_dict order), and the
+    library's count agrees (dev config trajectory_LSTM_2_large shapes, FC feature net stand-in)."""
+    from bcnf_amd import CondRealNVP_v2
+    from bcnf_amd.wide import WideStack
+    cfg = {"global": {"parameter_selection": [str(i) for i in range(19)]},
+           "model": {"kwargs": {"size": 19, "nested_sizes": [336] * 5, "n_conditions": 1360, "n_blocks": 3,
+                                "dropout": 0.407, "act_norm": True, "two_way": True}},
+           "feature_networks": [{"type": "ConcatenateCondition", "kwargs": {"input_size": None, "output_size": 90}},
+                                {"type": "FullyConnected", "kwargs": {"sizes": [90, 1360]}}]}
+    m = CondRealNVP_v2.from_config(cfg)
+    assert isinstance(m.fused, WideStack) and m.fused.supported
+    names = [n for n, _ in m.named_parameters() if n.startswith("layers.")]
+    assert names[:4] == ["layers.0.scale", "layers.0.bias", "layers.1.nn_a.nn.0.weight", "layers.1.nn_a.nn.0.bias"]
+    assert names[2 + 12] == "layers.1.nn_b.nn.0.weight"
+    mlp_a = (10 + 1360) * 336 + 336 + 4 * (336 * 336 + 336) + 336 * 18 + 18
+    mlp_b = (9 + 1360) * 336 + 336 + 4 * (336 * 336 + 336) + 336 * 20 + 20
+    assert m.fused.flat.numel() == m.fused.counts()[0] == 3 * (mlp_a + mlp_b) + 2 * 38
+    w_b = m.layers[1].nn_b.nn[0].weight
+    assert w_b.data_ptr() == m.fused.flat.data_ptr() + (38 + mlp_a) * 4
