@@ -320,9 +320,24 @@ struct TileIO {
 
 // Epilogue of four consecutive output rows rbase..rbase+3 at column col (both MFMA tilings hold their
 // accumulators in such groups). rnd: the group's Philox draw (EPI_ACT with dropout).
+// Operands the epilogue of a 4-row group needs from memory (EPI_GRAD: the G factors; EPI_ACT: the column's bias),
+// fetched before the K loop so their latency hides behind it.
+template <int EPI>
+__device__ __forceinline__ void epi_pre(const GemmArgs& g, const float* __restrict__ Xg, int rbase, int col, float pre[4]) {
+  pre[0] = pre[1] = pre[2] = pre[3] = 0.f;
+  if (col >= g.N) return;
+  if (EPI == EPI_GRAD) {
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr)
+      if (rbase + rr < g.M) pre[rr] = Xg[(long long)(rbase + rr) * g.ldaux + col];
+  } else if (EPI == EPI_ACT) {
+    if (col < g.n_real) pre[0] = g.bias[col];
+  }
+}
+
 template <int EPI>
 __device__ __forceinline__ void epi4(const GemmArgs& g, float* __restrict__ Cg, float* __restrict__ Xg, int rbase,
-                                     int col, const float v[4], uint4 rnd) {
+                                     int col, const float v[4], uint4 rnd, const float pre[4]) {
   const int M = g.M, N = g.N;
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
@@ -334,7 +349,7 @@ __device__ __forceinline__ void epi4(const GemmArgs& g, float* __restrict__ Cg, 
       float a = 0.f, gd = 0.f;
       if (col < g.n_real) {
         float ge, dg;
-        gelu_fg(v[rr] + g.bias[col], ge, dg);
+        gelu_fg(v[rr] + pre[0], ge, dg);
         if (g.rng) {
           const uint32_t u = rr == 0 ? rnd.x : rr == 1 ? rnd.y : rr == 2 ? rnd.z : rnd.w;
           const float m = u >= g.thresh ? g.keep_scale : 0.f;
@@ -350,7 +365,7 @@ __device__ __forceinline__ void epi4(const GemmArgs& g, float* __restrict__ Cg, 
       Cg[(long long)row * g.ldc + col] = a;
       if (Xg) Xg[(long long)row * g.ldaux + col] = gd;
     } else if (EPI == EPI_GRAD) {
-      Cg[(long long)row * g.ldc + col] = v[rr] * Xg[(long long)row * g.ldaux + col];
+      Cg[(long long)row * g.ldc + col] = v[rr] * pre[rr];
     } else if (EPI == EPI_LINGRAD) {
       if (col < g.wcols) Cg[(long long)row * g.ldc + col] = v[rr];
       else if (col == g.wcols) Cg[g.boff + row] = v[rr];
@@ -438,6 +453,15 @@ __global__ __launch_bounds__(WWG, 2) void k_wgemm(const GemmArgs g) {
   const float* __restrict__ B = g.B + g1 * g.sB1 + g0 * g.sB0;
   const int m0 = tl.y * BM, n0 = tl.x * BN;
   IO io;
+  const EpiCtx e = epi_ctx<EPI>(g, g1, g0);
+  float pre[TI][TJ][4][4];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        epi_pre<EPI>(g, e.X, m0 + wm * WM + 32 * i + 8 * q + 4 * hh, n0 + wn * WN + 32 * j + c32, pre[i][j][q]);
   floatx16 acc[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; ++i)
@@ -477,7 +501,6 @@ __global__ __launch_bounds__(WWG, 2) void k_wgemm(const GemmArgs g) {
     __syncthreads();
   }
   // accumulator element r of lane (c32, hh): row = (r & 3) + 8 (r >> 2) + 4 hh, col = c32
-  const EpiCtx e = epi_ctx<EPI>(g, g1, g0);
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -487,7 +510,7 @@ __global__ __launch_bounds__(WWG, 2) void k_wgemm(const GemmArgs g) {
       for (int q = 0; q < 4; ++q) {
         const int rbase = m0 + wm * WM + 32 * i + 8 * q + 4 * hh;
         const float v[4] = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
-        epi4<EPI>(g, e.C, e.X, rbase, col, v, epi_rnd<EPI>(g, e, rbase, col));
+        epi4<EPI>(g, e.C, e.X, rbase, col, v, epi_rnd<EPI>(g, e, rbase, col), pre[i][j][q]);
       }
     }
 }
@@ -509,6 +532,12 @@ __global__ __launch_bounds__(WWG, 2) void k_wgemm16(const GemmArgs g) {
   const float* __restrict__ B = g.B + g1 * g.sB1 + g0 * g.sB0;
   const int m0 = tl.y * BM, n0 = tl.x * BN;
   IO io;
+  const EpiCtx e = epi_ctx<EPI>(g, g1, g0);
+  float pre[TI][TJ][4];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) epi_pre<EPI>(g, e.X, m0 + wave * WM + 16 * i + 4 * qq, n0 + 16 * j + c16, pre[i][j]);
   floatx4 acc[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; ++i)
@@ -546,7 +575,6 @@ __global__ __launch_bounds__(WWG, 2) void k_wgemm16(const GemmArgs g) {
     __syncthreads();
   }
   // accumulator element r of lane (c16, qq): row = 4 qq + r, col = c16
-  const EpiCtx e = epi_ctx<EPI>(g, g1, g0);
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -554,7 +582,7 @@ __global__ __launch_bounds__(WWG, 2) void k_wgemm16(const GemmArgs g) {
       const int col = n0 + 16 * j + c16;
       const int rbase = m0 + wave * WM + 16 * i + 4 * qq;
       const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      epi4<EPI>(g, e.C, e.X, rbase, col, v, epi_rnd<EPI>(g, e, rbase, col));
+      epi4<EPI>(g, e.C, e.X, rbase, col, v, epi_rnd<EPI>(g, e, rbase, col), pre[i][j]);
     }
 }
 
