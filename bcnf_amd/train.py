@@ -9,7 +9,7 @@
     nll = inn_nll_loss(z, model.log_det_J)
     loss = (nll + mse * w) / (1 + w)
     loss.backward()
-    [data parallel: RCCL all-reduce (sum / world) of every gradient]
+    [data parallel: every gradient packed into one bucket, ONE RCCL all-reduce (mean), grads = bucket views]
     optimizer.step()                                   # Adam
     clip_grad_norm_(parameters, max_norm=1.0)          # after the step, as the reference does
     loss.item(), nll.item(), mse.item()
@@ -61,6 +61,7 @@ class TrainStep:
         self._static = None
         self._pool = None
         self._epoch = None      # (order, cursor, n_batches, batch) for the device-cursor batch walk
+        self._bucket = None     # data parallel: every gradient in one buffer, one all-reduce per step
         self._host_cursor = 0   # host mirror of the epoch cursor (the history row of the next step)
         dev = self.params[0].device
         self._guard = None
@@ -86,13 +87,40 @@ class TrainStep:
         loss.backward()
         return torch.stack([loss.detach(), nll.detach(), mse.detach()])
 
+    def _pack_grads(self):
+        """All gradients -> one contiguous bucket (one launch), so the data-parallel exchange is ONE collective
+        per step whatever the number of feature-network tensors (FC_large: 17, LSTM_large: 19)."""
+        grads = [p.grad for p in self.params]
+        if any(g is None for g in grads):
+            raise RuntimeError("bcnf_amd TrainStep: a parameter received no gradient")
+        if self._bucket is None:
+            n = sum(g.numel() for g in grads)
+            self._bucket = torch.empty(n, dtype=torch.float32, device=grads[0].device)
+        torch.cat([g.reshape(-1) for g in grads], out=self._bucket)
+
+    def _bind_grads(self):
+        """Every .grad becomes a view of the (reduced) bucket: Adam and the clip read it in place."""
+        off = 0
+        for p in self.params:
+            n = p.numel()
+            p.grad = self._bucket[off:off + n].view_as(p)
+            off += n
+
+    def _reduce_bucket(self):
+        """Sum over ranks of the gradient bucket: ONE RCCL all-reduce per step (the 1/world scaling runs inside
+        the captured update segment, _scale_bucket)."""
+        dist.all_reduce(self._bucket, op=dist.ReduceOp.SUM, group=self.pg)
+
+    def _scale_bucket(self):
+        self._bucket.mul_(1.0 / self.world)
+
     def _allreduce(self):
         if self.world == 1:
             return
-        for p in self.params:
-            if p.grad is not None:
-                dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, group=self.pg)
-                p.grad.mul_(1.0 / self.world)
+        self._pack_grads()
+        self._reduce_bucket()
+        self._scale_bucket()
+        self._bind_grads()
 
     def _update(self, vals=None):
         """Adam, then clip_grad_norm_ after the step (trainer.py:270-272); the clip launch also advances the
@@ -187,10 +215,14 @@ class TrainStep:
             vals = self._forward_backward(sy, st)
             if self.world == 1:
                 self._update(vals)
+            else:
+                self._pack_grads()          # the bucket copy is part of the captured step
         g2 = None
         if self.world > 1:
+            self._bind_grads()              # the update reads the reduced bucket
             g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g2):
+                self._scale_bucket()
                 self._update(vals)
         self._graphs = (g1, g2, vals)
 
@@ -327,7 +359,7 @@ class TrainStep:
         g1, g2, vals = self._graphs
         g1.replay()
         if g2 is not None:
-            self._allreduce()
+            self._reduce_bucket()           # the one collective of the step, between the two graph segments
             g2.replay()
         return vals
 
