@@ -32,7 +32,7 @@ EXPORTS = (
     "bcnf_gather_batch", "bcnf_advance_counters",
     "bcnf_wide_supported", "bcnf_wide_param_count", "bcnf_wide_packed_bytes", "bcnf_wide_workspace_bytes", "bcnf_wide_inverse_scratch_bytes",
     "bcnf_wide_pack", "bcnf_wide_forward", "bcnf_wide_nll_finalize", "bcnf_wide_backward", "bcnf_wide_inverse",
-    "bcnf_wide_gemm_test", "bcnf_wide_force_tiling", "bcnf_rank_count",
+    "bcnf_wide_gemm_test", "bcnf_wide_force_tiling", "bcnf_wide_debug_phases", "bcnf_rank_count",
 )
 MAX_TENSORS = 48
 
@@ -118,6 +118,7 @@ def _bind(lib):
                                       _vp]),
         "bcnf_wide_inverse": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i32, _vp, _vp, _vp]),
         "bcnf_wide_force_tiling": (_i32, [_i32]),
+        "bcnf_wide_debug_phases": (_i32, [_vp]),
         "bcnf_rank_count": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _vp]),
         "bcnf_wide_gemm_test": (_i32, [_i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp]),
         "bcnf_status_string": (ctypes.c_char_p, [_i32]),

@@ -616,6 +616,27 @@ __device__ __forceinline__ void stage4(float* __restrict__ dst, const float* __r
   }
 }
 
+// Two regions staged with every load in flight at once (one memory round trip for up to 16 float4 per thread).
+__device__ __forceinline__ void stage4x2(float* __restrict__ d1, const float* __restrict__ s1, int n1,
+                                         float* __restrict__ d2, const float* __restrict__ s2, int n2) {
+  const int n = n1 + n2;
+  for (int e0 = 0; e0 < n; e0 += 16 * WWG) {
+    floatx4 v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = e0 + u * WWG + (int)threadIdx.x;
+      if (e < n1) v[u] = ld4(s1 + 4 * e);
+      else if (e < n) v[u] = ld4(s2 + 4 * (e - n1));
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = e0 + u * WWG + (int)threadIdx.x;
+      if (e < n1) st4(d1 + 4 * e, v[u]);
+      else if (e < n) st4(d2 + 4 * (e - n1), v[u]);
+    }
+  }
+}
+
 __device__ __forceinline__ float half_sum(float v) {      // sum over the 32 lanes of a half-wavefront
   v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xf, 0xf, true));  // row_ror:8
   v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xf, 0xf, true));  // row_ror:4
@@ -643,7 +664,14 @@ struct LinkArgs {
   float* A0; float* G0;         // [B][HP] first hidden activation and its derivative factor (G0 nullable)
   float* U;                     // forward save: [u_in | 1 | 0] of block vh [B][UP] (nullable)
   const uint64_t* rng;          // dropout (nullable = off)
+  unsigned long long* dbg;      // phase timestamps of workgroup 0 (bcnf_wide_debug_phases), nullable
 };
+
+#define LINK_STAMP(i)                                                                          \
+  do {                                                                                         \
+    if (a.dbg && a.vt >= 0 && a.vh >= 0 && blockIdx.x == 0 && threadIdx.x == 0)                \
+      a.dbg[i] = __builtin_amdgcn_s_memtime();                                                 \
+  } while (0)
 
 // Dropout mask for a float4 group (4 consecutive columns n..n+3 of one row).
 __device__ __forceinline__ uint4 drop4(uint64_t seed, uint64_t offs, long long row, int n, uint32_t tag) {
@@ -683,6 +711,7 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
   const int kt = vt >= 0 ? vt / L.S : -1, kh = vh >= 0 ? vh / L.S : -1;
   const bool t_first = vt >= 0 && vt % L.S == 0, t_last = vt >= 0 && vt % L.S == L.S - 1;
   const bool h_first = vh >= 0 && vh % L.S == 0;
+  LINK_STAMP(0);
   float* Wl = sm;
   float* W0 = Wl + (vt >= 0 ? L.WL * HP : 0);
   float* Qs = W0 + (vh >= 0 ? L.WY * HP : 0);
@@ -712,11 +741,45 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
   }
   float xpre = 0.f;
   if (lv) xpre = vt >= 0 ? a.Xt[row * L.XP + ln] : a.xin[row * D + ln];
-  if (vt >= 0) stage4(Wl, a.pk + L.pk_wl + (long long)vt * L.WL * HP, O2 * HP / 4);
-  if (vh >= 0) stage4(W0, a.pk + L.pk_w0y + (long long)vh * L.WY * HP, nin_h * HP / 4);
-  if (kq >= 0 && kq < L.nb - 1)
-    for (int e = tid; e < D * D; e += WWG) Qs[e] = a.pk[L.pk_q + (long long)kq * D * D + e];
+  // every other global operand of the launch, also up front (a load behind a global store in a loop cannot be
+  // hoisted by the compiler, and each one left in the body is a full memory round trip on the critical path)
+  floatx4 bch[MQ];
+  if (vh >= 0) {
+    const float* b0 = a.pk + L.pk_b0 + (long long)vh * HP;
+#pragma unroll
+    for (int t = 0; t < MQ; ++t)
+      if (valid && ln + 32 * t < nq) bch[t] = ld4(b0 + 4 * (ln + 32 * t));
+  }
+  const bool has_q = kq >= 0 && kq < L.nb - 1;
+  float qv[4] = {0.f, 0.f, 0.f, 0.f};       // D * D <= 1024 = 4 per thread
+  if (has_q)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (tid + u * WWG < D * D) qv[u] = a.pk[L.pk_q + (long long)kq * D * D + tid + u * WWG];
+  const float blast = (vt >= 0 && ln < O2) ? a.prm[vbase(L, vt) + L.lin_b[vt % L.S][L.NH] + ln] : 0.f;
+  float sct = 1.f, bct = 0.f, sch = 1.f, bch_an = 0.f, ldj0 = 0.f, ldc_h = 0.f;
+  if (ln < D) {
+    if (vt >= 0 && L.an && kt < L.nb - 1) {
+      sct = a.prm[(long long)kt * L.blk_stride + ln];
+      bct = a.prm[(long long)kt * L.blk_stride + D + ln];
+    }
+    if (vh >= 0 && L.an && kh < L.nb - 1) {
+      sch = a.prm[(long long)kh * L.blk_stride + ln];
+      bch_an = a.prm[(long long)kh * L.blk_stride + D + ln];
+    }
+  }
+  if (!INV && valid && ln == 0) {
+    if (vt >= 0) ldj0 = a.ldj[row];
+    if (vh >= 0 && L.an && kh < L.nb - 1) ldc_h = a.pk[L.pk_ldc + kh];
+  }
+  stage4x2(Wl, a.pk + L.pk_wl + (long long)(vt >= 0 ? vt : 0) * L.WL * HP, vt >= 0 ? O2 * HP / 4 : 0,
+           W0, a.pk + L.pk_w0y + (long long)(vh >= 0 ? vh : 0) * L.WY * HP, vh >= 0 ? nin_h * HP / 4 : 0);
+  if (has_q)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (tid + u * WWG < D * D) Qs[tid + u * WWG] = qv[u];
   __syncthreads();
+  LINK_STAMP(1);
   uint64_t seed = 0, offs = 0;
   if (a.rng) {
     seed = a.rng[0];
@@ -747,22 +810,23 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
 #pragma unroll
     for (int j = 0; j < DM; ++j)
       if (j < O2) part[(r * 32 + ln) * PS + j] = acc[j];
+    LINK_STAMP(2);
     __syncthreads();
     if (ln < O2) {
       float s = 0.f;
 #pragma unroll
       for (int l = 0; l < 32; ++l) s += part[(r * 32 + l) * PS + ln];
-      Os[ln] = s + a.prm[vbase(L, vt) + L.lin_b[st][L.NH] + ln];
+      Os[ln] = s + blast;
     }
     __syncthreads();
+    LINK_STAMP(3);
     float sj = 0.f;
     const int jt = ln - toff_t;
     const bool tl = lv && jt >= 0 && jt < nout_t;             // lane in the transformed part
-    const float* sc = a.prm + (long long)kt * L.blk_stride;
     if (lv) {
       xi = xpre;
       if (!INV) {
-        if (t_first && L.an && kt < L.nb - 1) xi = sc[ln] * xi + sc[D + ln];       // ActNorm (cnf.py:350)
+        if (t_first && L.an && kt < L.nb - 1) xi = sct * xi + bct;                 // ActNorm (cnf.py:350)
         if (tl) {
           sj = tanh_bf(Os[nout_t + jt]);
           xi = fmaf(exp_fast(sj), xi, Os[jt]);                    // x_T = exp(s) x_T + t (cnf.py:179, 184)
@@ -770,7 +834,7 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
         }
       } else {
         if (tl) xi = (xi - Os[jt]) * exp_fast(-tanh_bf(Os[nout_t + jt]));   // (x_T - t) exp(-s) (cnf.py:201, 208)
-        if (t_last && L.an && kt < L.nb - 1) xi = (xi - sc[D + ln]) / sc[ln];  // ActNorm inverse (cnf.py:354)
+        if (t_last && L.an && kt < L.nb - 1) xi = (xi - bct) / sct;            // ActNorm inverse (cnf.py:354)
       }
     }
     if (!INV) {
@@ -787,12 +851,12 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
           }
           xi = c;
         }
-        if (valid && ln == 0) a.ldj[row] += ssum;
+        ldj0 += ssum;
       } else {
         const float zz = half_sum(xi * xi);
         if (lv) a.z[row * D + ln] = xi;
         if (valid && ln == 0) {
-          const float lj = a.ldj[row] + ssum;
+          const float lj = ldj0 + ssum;
           a.ldj[row] = lj;
           if (a.nllp) a.nllp[row] = 0.5f * zz - lj;               // per-sample inn_nll_loss (utils.py:49-53)
         }
@@ -802,16 +866,15 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
     }
   } else {
     xi = xpre;
-    if (!INV && valid && ln == 0) a.ldj[row] = 0.f;
+    ldj0 = 0.f;
   }
   // ------------------------------------------------------------ head of virtual block vh
   if (vh >= 0) {
     if (!INV) {
       if (lv) a.Xh[row * L.XP + ln] = xi;                         // saved input (pre-ActNorm for a first half)
       if (h_first && L.an && kh < L.nb - 1) {
-        const float* sc = a.prm + (long long)kh * L.blk_stride;
-        if (ln < D) xi = sc[ln] * xi + sc[D + ln];
-        if (valid && ln == 0) a.ldj[row] += a.pk[L.pk_ldc + kh];  // ActNorm log|det J| (cnf.py:349)
+        if (ln < D) xi = sch * xi + bch_an;
+        ldj0 += ldc_h;                                            // ActNorm log|det J| (cnf.py:349)
       }
     } else {
       if (h_first && kh < L.nb - 1) {                             // v = x Q_k^T (cnf.py:337-339)
@@ -827,8 +890,11 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
       }
       if (lv) a.Xh[row * L.XP + ln] = xi;                         // read back by this half's tail
     }
+    if (!INV && valid && ln == 0) a.ldj[row] = ldj0;             // the running log|det J| of the sample
+    LINK_STAMP(4);
     us[ln] = xi;
     __syncthreads();
+    LINK_STAMP(5);
     float ua[DM / 2];
 #pragma unroll
     for (int j = 0; j < DM / 2; ++j) ua[j] = j < nin_h ? us[ioff_h + j] : 0.f;
@@ -836,9 +902,9 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
     if (valid) {
       const float* b0 = a.pk + L.pk_b0 + (long long)vh * HP;
       const uint32_t tag = (uint32_t)vh * 16u;
-      auto chunk = [&](int q, floatx4 pv4) {
+      auto chunk = [&](int q, floatx4 pv4, floatx4 bv4) {
         const int n = 4 * q;
-        floatx4 pre = pv4 + ld4(b0 + n);
+        floatx4 pre = pv4 + bv4;
 #pragma unroll
         for (int j = 0; j < DM / 2; ++j) {
           if (j < nin_h) {
@@ -868,10 +934,11 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
       };
 #pragma unroll
       for (int t = 0; t < MQ; ++t)
-        if (ln + 32 * t < nq) chunk(ln + 32 * t, pch[t]);
-      for (int q = ln + 32 * MQ; q < nq; q += 32) chunk(q, ld4(Pr + 4 * q));
+        if (ln + 32 * t < nq) chunk(ln + 32 * t, pch[t], bch[t]);
+      for (int q = ln + 32 * MQ; q < nq; q += 32) chunk(q, ld4(Pr + 4 * q), ld4(b0 + 4 * q));
     }
   }
+  LINK_STAMP(6);
 }
 
 // Backward links (forward order reversed, one virtual block = one half-coupling).
@@ -948,14 +1015,30 @@ __global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const Lin
       if (hl) skh = a.S[vh * a.sS + row * L.SP + jh];
     }
   }
-  if (vt >= 0) stage4(W0, a.pk + L.pk_w0y + (long long)vt * L.WY * HP, nin_t * HP / 4);
-  if (vh >= 0) {
-    stage4(Wl, a.pk + L.pk_wl + (long long)vh * L.WL * HP, O2 * HP / 4);
-    if (h_last && kh < L.nb - 1)
-      for (int e = tid; e < D * D; e += WWG) Qs[e] = a.pk[L.pk_q + (long long)kh * D * D + e];
+  // the remaining global operands, up front as well
+  const bool has_q = vh >= 0 && h_last && kh < L.nb - 1;
+  float qv[4] = {0.f, 0.f, 0.f, 0.f};       // D * D <= 1024 = 4 per thread
+  if (has_q)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (tid + u * WWG < D * D) qv[u] = a.pk[L.pk_q + (long long)kh * D * D + tid + u * WWG];
+  float sct = 1.f, sch = 1.f, bch_an = 0.f, dlp = 0.f;
+  if (ln < D) {
+    if (vt >= 0 && L.an && kt < L.nb - 1) sct = a.prm[(long long)kt * L.blk_stride + ln];
+    if (vh >= 0 && L.an && kh < L.nb - 1) {
+      sch = a.prm[(long long)kh * L.blk_stride + ln];
+      bch_an = a.prm[(long long)kh * L.blk_stride + D + ln];
+    }
   }
-  __syncthreads();
   const float gscale = a.nll ? (a.dvals ? a.dvals[0] + a.dvals[1] : 1.f) / (float)a.B : 0.f;
+  if (hl && !a.nll && a.dldj) dlp = a.dldj[row];
+  stage4x2(W0, a.pk + L.pk_w0y + (long long)(vt >= 0 ? vt : 0) * L.WY * HP, vt >= 0 ? nin_t * HP / 4 : 0,
+           Wl, a.pk + L.pk_wl + (long long)(vh >= 0 ? vh : 0) * L.WL * HP, vh >= 0 ? O2 * HP / 4 : 0);
+  if (has_q)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (tid + u * WWG < D * D) Qs[tid + u * WWG] = qv[u];
+  __syncthreads();
   float dxi = 0.f;                                  // element ln of the gradient w.r.t. the current D-vector
   // ------------------------------------------------------------ tail-B of virtual block vt
   if (vt >= 0) {
@@ -991,10 +1074,9 @@ __global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const Lin
         du += t;                                                  // d x_in = dv_in + dZ_0 W0y
       }
       if (t_first && L.an && kt < L.nb - 1) {
-        const float* sc = a.prm + (long long)kt * L.blk_stride;
         a.ANP[row * L.AP + ln] = du * xkt;                       // dscale partial
         a.ANP[row * L.AP + D + ln] = du;                         // dbias partial
-        du *= sc[ln];
+        du *= sct;
       }
       dxi = du;
       if (vt == 0 && a.dy) a.dy[row * D + ln] = dxi;
@@ -1017,12 +1099,9 @@ __global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const Lin
     }
     float dvo = dxi;
     if (hl) {
-      const float dl = a.nll ? -gscale : (a.dldj ? a.dldj[row] : 0.f);
+      const float dl = a.nll ? -gscale : dlp;
       float ub = xkh;
-      if (h_first && L.an && kh < L.nb - 1) {
-        const float* sc = a.prm + (long long)kh * L.blk_stride;
-        ub = sc[ln] * ub + sc[D + ln];
-      }
+      if (h_first && L.an && kh < L.nb - 1) ub = sch * ub + bch_an;
       const float s = skh;
       const float es = exp_fast(s);
       dvo = dxi * es;                                             // d x_T before the affine
@@ -1254,7 +1333,11 @@ void link_dispatch(int ts, int hs, dim3 grid, size_t lds, hipStream_t st, const 
   else hipLaunchKernelGGL((k_wlink<INV, DD, 1, 0>), grid, dim3(WWG), lds, st, L, a);
 }
 
-int link_launch(const WideLayout& L, const LinkArgs& a, bool inv, hipStream_t st) {
+unsigned long long* g_link_dbg = nullptr;   // bcnf_wide_debug_phases
+
+int link_launch(const WideLayout& L, const LinkArgs& a_in, bool inv, hipStream_t st) {
+  LinkArgs a = a_in;
+  a.dbg = g_link_dbg;
   dim3 grid((unsigned)((a.B + LR - 1) / LR));
   const size_t lds = (size_t)link_lds_floats(L, a.vt >= 0, a.vh >= 0) * sizeof(float);
   const int ts = a.vt >= 0 ? a.vt % L.S : 1 - (a.vh % L.S);
@@ -1697,6 +1780,12 @@ int bcnf_wide_inverse(const BcnfStackDesc* desc, const float* params, const void
   if (!cond_index && h_rows != n_rows) return BCNF_ERR_ARG;
   return wide_inverse(L, params, (const float*)packed, z, h, h_rows, cond_index, n_rows, y, training != 0, rng_state,
                       (float*)scratch, (hipStream_t)stream);
+}
+
+// Debug: phase timestamps (s_memtime) of workgroup 0 of every forward link launch into dbg[0..6] (nullptr = off).
+int bcnf_wide_debug_phases(unsigned long long* dbg) {
+  g_link_dbg = dbg;
+  return BCNF_OK;
 }
 
 // Tiling override for every wide GEMM launch (-1 = the cost model's choice; 0 = 128x128, 1 = 64x64, 2 = 128x48).

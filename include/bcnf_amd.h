@@ -264,6 +264,10 @@ int bcnf_wide_inverse(const BcnfStackDesc* desc, const float* params, const void
 int bcnf_rank_count(const float* y_hat, const float* y, int64_t n_draws, int64_t n_rows, int32_t dim, uint32_t* counts,
                     void* stream);
 
+/* Debug knob: device buffer of 8 uint64 receiving s_memtime stamps of workgroup 0's phases in every forward link
+ * launch (0 start, 1 staged, 2 tail dot products, 3 tail reduction, 4 coupling, 5 head vector, 6 end); NULL = off. */
+int bcnf_wide_debug_phases(unsigned long long* dbg);
+
 /* Debug / test knob: force the tiling of every wide GEMM launch (-1 = the cost model's choice, 0 = 128x128 and
  * 1 = 64x64 with v_mfma_f32_32x32x2_f32, 2 = 128x48 with v_mfma_f32_16x16x4_f32). Returns the previous setting.
  * Process-wide; not for concurrent use. */
