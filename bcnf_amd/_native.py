@@ -29,7 +29,8 @@ EXPORTS = (
     "bcnf_nll_forward", "bcnf_nll_backward", "bcnf_grad_partials", "bcnf_adam_step", "bcnf_grad_sumsq",
     "bcnf_clip_grad_norm", "bcnf_linear_forward", "bcnf_linear_work_bytes", "bcnf_linear_backward",
     "bcnf_inverse_scratch_bytes", "bcnf_stack_dh", "bcnf_backward_tail", "bcnf_gather_rows2",
-    "bcnf_gather_batch", "bcnf_advance_counters",
+    "bcnf_gather_batch", "bcnf_advance_counters", "bcnf_fold_bytes", "bcnf_fold_slab_bytes",
+    "bcnf_pack_params_fold", "bcnf_fold_nll_forward", "bcnf_fold_backward_tail",
     "bcnf_wide_supported", "bcnf_wide_param_count", "bcnf_wide_packed_bytes", "bcnf_wide_workspace_bytes", "bcnf_wide_inverse_scratch_bytes",
     "bcnf_wide_pack", "bcnf_wide_forward", "bcnf_wide_nll_finalize", "bcnf_wide_backward", "bcnf_wide_inverse",
     "bcnf_wide_gemm_test", "bcnf_wide_force_tiling", "bcnf_wide_debug_phases", "bcnf_rank_count",
@@ -97,6 +98,13 @@ def _bind(lib):
         "bcnf_nll_forward": (_i32, [_pdesc, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _i32, _vp, _vp, _vp]),
         "bcnf_nll_backward": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                      _vp, _vp]),
+        "bcnf_fold_bytes": (_i32, [_pdesc, _i32, _pi64]),
+        "bcnf_fold_slab_bytes": (_i32, [_pdesc, _i32, _i64, _pi64]),
+        "bcnf_pack_params_fold": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
+        "bcnf_fold_nll_forward": (_i32, [_pdesc, _vp, _vp, _i32, _vp, _vp, _i32, _i64, _vp, _vp, _i32, _vp, _vp,
+                                         _i32, _vp, _vp, _vp]),
+        "bcnf_fold_backward_tail": (_i32, [_pdesc, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _i64, _i32, _vp, _vp,
+                                           _vp, _vp]),
         "bcnf_grad_partials": (_i64, [_i64]),
         "bcnf_adam_step": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double,
                                   ctypes.c_double, ctypes.c_double, ctypes.c_double, _vp, _i32, _vp, _vp]),

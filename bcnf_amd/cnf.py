@@ -24,8 +24,9 @@ import torch
 import torch.nn as nn
 
 from bcnf_amd.factories import FeatureNetworkFactory, LayerFactory
-from bcnf_amd.feature_network import FeatureNetwork, FeatureNetworkStack
-from bcnf_amd.fused import FusedStack, StackConfig, stack_forward, stack_inverse, stack_nll
+from bcnf_amd.feature_network import (ConcatenateCondition, FeatureNetwork, FeatureNetworkStack,
+                                      FullyConnectedFeatureNetwork)
+from bcnf_amd.fused import FusedStack, StackConfig, stack_forward, stack_inverse, stack_nll, stack_nll_fold
 from bcnf_amd.wide import make_stack
 from bcnf_amd.utils import ParameterIndexMapping, log_prob_from_latent
 
@@ -391,10 +392,64 @@ class CondRealNVP_v2(ConditionalInvertibleLayer):
         kernels with no dz / dldj tensors in between. defer_reduction=True (a backward certainly follows)
         moves the loss reduction into the backward launch; vals is then valid only after backward."""
         self._check_supported()
-        condition = self._features(conditions)
         if y.dim() == 1:
             y = y.unsqueeze(0)
+        fold = self._foldable_linear(y, conditions)
+        if fold is not None:
+            x, lin = fold
+            return stack_nll_fold(self._fused, y, x, lin.weight, lin.bias, self.training, defer=defer_reduction)
+        condition = self._features(conditions)
         return stack_nll(self._fused, y, condition, self.training, defer=defer_reduction)
+
+    # The training fast path for a feature stack that is ONE nn.Linear (ConcatenateCondition ->
+    # FullyConnected(sizes=[X, C]), trajectory_FC_small): h = x Wf^T + bf only enters the stack through the
+    # condition projection, so the Linear is folded into it (include/bcnf_amd.h, bcnf_pack_params_fold) and the
+    # feature GEMM, dL/dh and the feature dW split-K leave the step. Same sums, reassociated.
+    fold_features = True
+
+    def _fold_linear(self):
+        """The feature stack's single nn.Linear when the fold applies to this model's structure, else None."""
+        if not self.fold_features or type(self._fused) is not FusedStack:
+            return None
+        fns = list(self.feature_network_stack.feature_networks)
+        if len(fns) != 2 or not isinstance(fns[0], ConcatenateCondition) \
+                or not isinstance(fns[1], FullyConnectedFeatureNetwork):
+            return None
+        mods = list(fns[1].nn)
+        if len(mods) != 1 or not isinstance(mods[0], nn.Linear):
+            return None
+        lin = mods[0]
+        if lin.weight.dtype != torch.float32 or not lin.weight.is_cuda:
+            return None
+        if not self._fused.fold_supported(lin.in_features):
+            return None
+        return lin
+
+    def _foldable_linear(self, y, conditions):
+        if len(conditions) != 1:
+            return None
+        lin = self._fold_linear()
+        if lin is None:
+            return None
+        c = conditions[0]
+        if not c.is_cuda or c.dtype != torch.float32 or c.requires_grad or y.requires_grad or c.dim() < 1:
+            return None
+        x = c.reshape(c.shape[0], -1)       # a view for TrainStep's padded rows (stride(0) = padded width)
+        if x.shape[1] != lin.in_features:
+            return None
+        return x, lin
+
+    def fold_pool_width(self, cond_pool: torch.Tensor):
+        """Row width to zero-pad a device-resident condition pool to (TrainStep.set_pool) so the folded path
+        reads its batches with float4 loads: the per-sample size rounded up to 4, or None when the fold does not
+        apply or the rows are already aligned."""
+        lin = self._fold_linear()
+        if lin is None or not cond_pool.is_cuda or cond_pool.dim() < 1 or cond_pool.shape[0] == 0:
+            return None
+        X = cond_pool[0].numel()
+        if X != lin.in_features or X % 4 == 0:
+            return None
+        return (X + 3) // 4 * 4
 
     def log_prob(self, y: torch.Tensor, *conditions: torch.Tensor) -> torch.Tensor:
         """log p(y | conditions) = -0.5 |z|^2 + log|det J| - D/2 log(2 pi). The reference has no such

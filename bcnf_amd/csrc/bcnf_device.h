@@ -51,6 +51,7 @@ struct BcnfLayout {
   //   W1hC [Cp][NKp]  (c, k*16+j)   W1hR [NKp][Cp]  (k*16+j, c)   b1c [NKp]
   int NKp;
   long long pf_off, pb_off, pi_off, w1c_off, w1r_off, b1c_off, ldc_off, total;
+  int ldh;              // row stride (floats) of the projection input: C for h, ldx for the folded path's x
 };
 
 __device__ __forceinline__ int coupling_base(const BcnfLayout& L, int k) {

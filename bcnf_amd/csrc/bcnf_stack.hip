@@ -8,7 +8,7 @@
 //   k_inverse   whole-stack inverse, one launch                              (cnf.py:499-506)
 //   k_backward  whole-stack backward with per-block recompute, one launch; dW via fp32 MFMA on LDS
 //               tiles of the workgroup's 16 samples; per-workgroup slabs
-//   k_reduce    deterministic slab sum -> canonical flat gradient
+//   k_bwd_tail  deterministic slab sum -> canonical flat gradient
 //
 // Reference: psaegert/bcnf src/bcnf/models/cnf.py. See DESIGN.md for layouts and rooflines.
 #include "bcnf_device.h"
@@ -60,6 +60,7 @@ int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
   L->Da = (d->size + 1) / 2;
   L->Db = d->size / 2;
   L->C = d->n_conditions;
+  L->ldh = d->n_conditions;
   L->Cp = ((d->n_conditions + 15) / 16) * 16;
   if (L->Cp == 0) L->Cp = 16;
   L->NH = d->n_hidden;
@@ -232,10 +233,10 @@ __device__ float rec_b(const BcnfLayout& L, const float* P, const float* Q, int 
 // the ActNorm log|det| constant  sum_k sum_i log|scale_k,i|  (cnf.py:350) in a fixed order.
 constexpr int PACK_WG = 512;
 
-__global__ __launch_bounds__(BCNF_WG) void k_pack(BcnfLayout L, const float* __restrict__ P,
-                                                  const float* __restrict__ Q, float* __restrict__ out) {
-  if (blockIdx.x == PACK_WG) {
-    __shared__ float part[BCNF_WG];
+__device__ __forceinline__ void pack_body(const BcnfLayout& L, const float* __restrict__ P,
+                                          const float* __restrict__ Q, float* __restrict__ out, int bx,
+                                          float* __restrict__ part) {
+  if (bx == PACK_WG) {
     float acc = 0.f;
     if (L.act_norm) {
       const int n = (L.nb - 1) * L.D;
@@ -258,7 +259,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_pack(BcnfLayout L, const float* __r
   const int n_pb = L.nb * 16 * L.RB;
   const int n_w = L.Cp * L.NKp;                       // each of W1hC, W1hR
   const int total = 2 * n_pf + n_pb + 2 * n_w + L.NKp;
-  for (int i = blockIdx.x * BCNF_WG + threadIdx.x; i < total; i += PACK_WG * BCNF_WG) {
+  for (int i = bx * BCNF_WG + threadIdx.x; i < total; i += PACK_WG * BCNF_WG) {
     float v;
     long long o;
     if (i < n_pf) {                                   // PF
@@ -292,6 +293,94 @@ __global__ __launch_bounds__(BCNF_WG) void k_pack(BcnfLayout L, const float* __r
     }
     out[o] = v;
   }
+}
+
+__global__ __launch_bounds__(BCNF_WG) void k_pack(BcnfLayout L, const float* __restrict__ P,
+                                                  const float* __restrict__ Q, float* __restrict__ out) {
+  __shared__ float part[BCNF_WG];
+  pack_body(L, P, Q, out, blockIdx.x, part);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Folded linear feature network (training fast path when the feature stack is ONE nn.Linear,
+// feature_network.py:114-145 with sizes [X, C] — trajectory_FC_small). h = x Wf^T + bf reaches the stack
+// only through the condition projection, so with kj = k*16 + j and W1h_k[j][c] = W1_k[j][Da + c]:
+//   HP[k][r][j] = sum_xc x[r][xc] Wc[xc][kj] + bc[kj],  Wc[xc][kj] = sum_c W1h_k[j][c] Wf[c][xc],
+//                                                       bc[kj]     = b1_k[j] + sum_c W1h_k[j][c] bf[c]
+// and with Gx[kj][xc] = sum_b D1[k][b][j] x1[b][xc]  (x1 = [x | 1], D1 = dL/d pre-activation of Linear 1):
+//   dW1h_k[j][c] = sum_{xc<X} Gx[kj][xc] Wf[c][xc] + Gx[kj][X] bf[c]
+//   dWf[c][xc]   = sum_kj W1h_k[j][c] Gx[kj][xc],       dbf[c] = sum_kj W1h_k[j][c] Gx[kj][X]
+// h and dL/dh are never formed: the feature Linear's forward GEMM, the dL/dh GEMM and the feature dW split-K
+// disappear from the step (same sums, reassociated: fp32 rounding differs from the unfolded path at ~1e-6).
+// The fold buffer: Wc [Xp][NKp] then bc [NKp], Xp = 16-multiple > X (row X, the ones column, is zero).
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ inline int fold_xp(int X) { return ((X + 1 + 15) / 16) * 16; }
+
+// Layout seen by the projection kernels (k_hp, the split-K dW1h body) when they run on x instead of h.
+BcnfLayout fold_layout(const BcnfLayout& L, int X, int ldx) {
+  BcnfLayout F = L;
+  F.C = X;
+  F.ldh = ldx;
+  F.Cp = fold_xp(X);
+  F.w1c_off = 0;
+  F.b1c_off = (long long)F.Cp * L.NKp;
+  return F;
+}
+
+// Fold workgroup f: block k = f / 4, rows j0 = 4 (f % 4) .. j0 + 3; thread xc < Xp computes column xc of
+// W1h_k[j0:j0+4] [Wf | bf | 0]: Wc[xc][kj] for xc < X, the bias dot for xc == X, zero rows X..Xp-1. One staging
+// round trip (the 4 W1h rows, [c][4] in LDS, read as broadcast float4), then C independent L2-resident loads of Wf
+// per thread, coalesced across the lanes.
+constexpr int FOLD_SPLIT = 4;
+
+__device__ __forceinline__ void fold_body(const BcnfLayout& L, const float* __restrict__ P,
+                                          const float* __restrict__ wf, const float* __restrict__ bf, int X,
+                                          float* __restrict__ fold, int f, float* __restrict__ w1s) {
+  const int Xp = fold_xp(X), k = f / FOLD_SPLIT, j0 = (f % FOLD_SPLIT) * 4, tid = threadIdx.x;
+  const bool kval = k < L.nb;
+  for (int i = tid; i < 4 * L.C; i += BCNF_WG) {
+    const int c = i >> 2, jj = i & 3, j = j0 + jj;
+    w1s[i] = (kval && j < L.H[1]) ? cW(L, P, k, 1, j, L.Da + c) : 0.f;
+  }
+  __syncthreads();
+  if (tid >= Xp) return;
+  const int xc = tid;
+  const bool isw = xc < X, live = isw || (xc == X && bf != nullptr);
+  const float* src = isw ? wf + xc : bf;
+  const int stride = isw ? X : 1;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+  for (int c = 0; c < L.C; ++c) {
+    const float v = live ? src[(long long)c * stride] : 0.f;
+    const floatx4 w = *reinterpret_cast<const floatx4*>(w1s + 4 * c);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) acc[jj] = fmaf(w[jj], v, acc[jj]);
+  }
+  const int kj = k * 16 + j0;
+  if (xc == X) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int j = j0 + jj;
+      fold[(long long)Xp * L.NKp + kj + jj] = (kval && j < L.H[1]) ? cB(L, P, k, 1, j) + acc[jj] : 0.f;
+    }
+    acc = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+  *reinterpret_cast<floatx4*>(fold + (long long)xc * L.NKp + kj) = acc;
+}
+
+// NKp / 4 fold workgroups first (they start before the record workgroups), then k_pack's grid. The fold reads
+// the canonical parameters, not k_pack's output.
+__global__ __launch_bounds__(BCNF_WG) void k_pack_fold(BcnfLayout L, const float* __restrict__ P,
+                                                       const float* __restrict__ Q, float* __restrict__ out,
+                                                       const float* __restrict__ wf, const float* __restrict__ bf,
+                                                       int X, float* __restrict__ fold) {
+  __shared__ __attribute__((aligned(16))) float smem[4 * 16 * NC16_MAX];
+  const int n_fold = L.NKp / 16 * FOLD_SPLIT, bx = blockIdx.x;
+  if (bx < n_fold) {
+    fold_body(L, P, wf, bf, X, fold, bx, smem);
+    return;
+  }
+  pack_body(L, P, Q, out, bx - n_fold, smem);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -332,7 +421,7 @@ struct Stage {
 // bound by load issue / round trips rather than MFMA, so: operands come from contiguous packed copies
 // (W1hC, W1hR) with float4 loads, a workgroup stages a K-chunk of up to 128 of both operands in LDS per
 // round trip (next chunk in flight), and the K loops issue all LDS reads of 4-8 steps before their MFMAs.
-// VEC: C % 4 == 0 (h rows are float4-aligned).
+// VEC: float4 row loads (vec_rows: the row stride ld and the base are 16-byte aligned).
 constexpr int KC = 128;                // K-chunk
 // LDS strides for the MFMA operand reads: [row = lane&15][k = 4t + lane>>4] wants stride = 4 (mod 32),
 // [k = 4t + lane>>4][col = lane&15] wants stride = 16 (mod 32): 64 lanes then hit every bank exactly twice.
@@ -341,17 +430,19 @@ constexpr int BNS = 80;                // k_hp B tile [KC][64]
 __host__ __device__ constexpr int bstride16(int n) { return n + ((16 - (n & 31)) & 31); }   // >= n, = 16 mod 32
 
 // Stage rows [r0, r0 + 64) x cols [c0, c0 + KC) of a row-major (nrows x ncols, ld) matrix into regs
-// (8 float4 per thread: row = i4 / 32, col = 4 (i4 % 32)), zero outside.
+// (8 float4 per thread: row = i4 / 32, col = 4 (i4 % 32)), zero outside; column `ones` (>= ncols, or -1 for
+// none) of every valid row reads 1.0 (the bias column of the folded feature Linear).
 template <bool VEC>
 __device__ __forceinline__ void load_rows64(const float* __restrict__ M, long long nrows, int ncols, long long ld,
-                                            long long r0, int c0, floatx4* reg) {
+                                            long long r0, int c0, floatx4* reg, int ones = -1) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int i4 = threadIdx.x + 256 * e, row = i4 >> 5, col = c0 + (i4 & 31) * 4;
     const long long r = r0 + row < nrows ? r0 + row : nrows - 1;
     if (VEC) {
       const floatx4 v = *reinterpret_cast<const floatx4*>(M + r * ld + (col < ncols ? col : 0));
-      reg[e] = v * ((r0 + row < nrows && col < ncols) ? 1.f : 0.f);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) reg[e][q] = (r0 + row < nrows && col + q < ncols) ? v[q] : 0.f;
     } else {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -359,6 +450,11 @@ __device__ __forceinline__ void load_rows64(const float* __restrict__ M, long lo
         const float v = M[r * ld + (cq < ncols ? cq : ncols - 1)];
         reg[e][q] = (r0 + row < nrows && cq < ncols) ? v : 0.f;
       }
+    }
+    if (ones >= 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (col + q == ones && r0 + row < nrows) reg[e][q] = 1.f;
     }
   }
 }
@@ -377,7 +473,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_hp(BcnfLayout L, const float* __res
   const float* w1c = pk + L.w1c_off;
   floatx4 ra[8], rb[8];
   auto load = [&](int c0) {
-    load_rows64<VEC>(h, R, L.C, L.C, b0, c0, ra);
+    load_rows64<VEC>(h, R, L.C, L.ldh, b0, c0, ra);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {                    // B: [KC rows c][64 cols]: row = i4 / 16, col4
       const int i4 = tid + 256 * e, row = c0 + (i4 >> 4), col = n0 + (i4 & 15) * 4;
@@ -507,7 +603,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_dh(BcnfLayout L, const float* __res
 template <bool VEC>
 __device__ __forceinline__ void dw1h_body(const BcnfLayout& L, const float* __restrict__ d1, const float* __restrict__ h,
                                           long long B, int rows_per_split, float* __restrict__ work, int bx, int by,
-                                          float* __restrict__ smem) {
+                                          float* __restrict__ smem, int ones = -1) {
   const int hs = bstride16(L.Cp);
   float* As = smem;                    // [64][KCP] (kj, b)
   float* Bs = smem + 64 * KCP;         // [KC][hs]  (b, c)
@@ -539,7 +635,7 @@ __device__ __forceinline__ void dw1h_body(const BcnfLayout& L, const float* __re
     for (int half = 0; half < 2; ++half) {
       for (int c0 = 0; c0 < L.Cp; c0 += KC) {
         floatx4 rv[8];
-        load_rows64<VEC>(h, m1, L.C, L.C, m0 + 64 * half, c0, rv);
+        load_rows64<VEC>(h, m1, L.C, L.ldh, m0 + 64 * half, c0, rv, ones);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const int i4 = tid + 256 * e, row = 64 * half + (i4 >> 5), col = c0 + (i4 & 31) * 4;
@@ -606,6 +702,127 @@ __global__ __launch_bounds__(BCNF_WG) void k_dw1h_reduce(BcnfLayout L, const flo
   }
   for (; s < splits; ++s) acc += work[(long long)s * total + i];
   dparams[coupling_base(L, k) + L.lin_w[1] + j * L.lin_in[1] + L.Da + c] = acc;
+}
+
+// Folded path: Gx[kj][xc] = sum of the split-K partials work[s][kj][xc] (fixed order), dense [nb*16][Xp].
+__global__ __launch_bounds__(BCNF_WG) void k_gx_reduce(long long total, const float* __restrict__ work, int splits,
+                                                       float* __restrict__ gx) {
+  const long long i = (long long)blockIdx.x * BCNF_WG + threadIdx.x;
+  if (i >= total) return;
+  float acc = 0.f;
+  int s = 0;
+  for (; s + 8 <= splits; s += 8) {
+    float v[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = work[(long long)(s + t) * total + i];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc += v[t];
+  }
+  for (; s < splits; ++s) acc += work[(long long)s * total + i];
+  gx[i] = acc;
+}
+
+// Folded path, last launch of the backward: two small GEMMs as 16 x 16 output tiles, each operand K-chunk staged
+// in LDS as [k][16] in one memory round trip (every load of a chunk issued together: the operands were written by
+// other XCDs, so each access is an L2 miss and a streaming K loop of dependent round trips is what costs).
+//   role a, workgroups [0, nb * nct): dW1h_k[j][c] = sum_{xc<=X} Gx[k*16+j][xc] Wf1[c][xc]   (Wf1 = [Wf | bf])
+//   role b, the rest:               [dWf | dbf][c][xc] = sum_kj W1hR[kj][c] Gx[kj][xc], K = nb*16
+// Tile product: thread (ks = lane & 15, rb = lane >> 4, cb = wave) accumulates the 4 x 4 block rows 4rb.., cols
+// 4cb.. over k = ks + 16 i (conflict-free ds_read_b128: 16 consecutive rows x 4 float4 per wave), then the 16
+// k-slices are summed in a fixed order through LDS.
+constexpr int FIN_KC = 256;                           // K chunk (role a: Xp <= 256 fits one)
+constexpr int FIN_SMEM = 2 * FIN_KC * 16;             // As + Bs; the 16 x 256 reduction aliases them
+
+__device__ __forceinline__ void tile16_accum(const float* __restrict__ As, const float* __restrict__ Bs, int kn,
+                                             floatx4 (&acc)[4]) {
+  const int lane = threadIdx.x & 63, ks = lane & 15, rb = lane >> 4, cb = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int k = ks; k < kn; k += 16) {
+    const floatx4 a = *reinterpret_cast<const floatx4*>(As + k * 16 + 4 * rb);
+    const floatx4 b = *reinterpret_cast<const floatx4*>(Bs + k * 16 + 4 * cb);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(a[r], b[c], acc[r][c]);
+  }
+}
+
+// Fixed-order sum of the 16 k-slices; returns element (row = tid / 16, col = tid % 16) of the tile.
+__device__ __forceinline__ float tile16_reduce(float* __restrict__ red, const floatx4 (&acc)[4]) {
+  const int lane = threadIdx.x & 63, ks = lane & 15, rb = lane >> 4, cb = threadIdx.x >> 6;
+  __syncthreads();                                    // the staging buffers are reused
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) red[ks * 256 + (4 * rb + r) * 16 + 4 * cb + c] = acc[r][c];
+  __syncthreads();
+  float v = 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) v += red[q * 256 + threadIdx.x];
+  return v;
+}
+
+__global__ __launch_bounds__(BCNF_WG) void k_fold_finish(BcnfLayout L, const float* __restrict__ pk,
+                                                         const float* __restrict__ gx, const float* __restrict__ wf,
+                                                         const float* __restrict__ bf, int X,
+                                                         float* __restrict__ dparams, float* __restrict__ dwf,
+                                                         float* __restrict__ dbf) {
+  __shared__ __attribute__((aligned(16))) float smem[FIN_SMEM];
+  float* As = smem;
+  float* Bs = smem + FIN_KC * 16;
+  const int Xp = fold_xp(X), tid = threadIdx.x, nct = L.Cp >> 4;
+  floatx4 acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if ((int)blockIdx.x < L.nb * nct) {
+    const int k = blockIdx.x / nct, c0 = (blockIdx.x % nct) * 16;
+    const float* g = gx + (long long)k * 16 * Xp;     // [16][Xp], contiguous
+    for (int i = tid; i < 16 * Xp; i += BCNF_WG) {
+      const int j = i / Xp, xc = i - j * Xp;
+      As[xc * 16 + j] = g[i];
+      const int cc = j, c = c0 + cc;                  // the same (row, xc) walk over Wf1[c0 + cc][xc]
+      float v = 0.f;
+      if (c < L.C) v = xc < X ? wf[(long long)c * X + xc] : ((xc == X && bf) ? bf[c] : 0.f);
+      Bs[xc * 16 + cc] = v;
+    }
+    __syncthreads();
+    tile16_accum(As, Bs, Xp, acc);
+    const float v = tile16_reduce(smem, acc);
+    const int j = tid >> 4, c = c0 + (tid & 15);
+    if (j < L.H[1] && c < L.C) dparams[coupling_base(L, k) + L.lin_w[1] + j * L.lin_in[1] + L.Da + c] = v;
+    return;
+  }
+  const int tile = blockIdx.x - L.nb * nct, c0 = (tile % nct) * 16, x0 = (tile / nct) * 16;
+  const int K = L.nb * 16;
+  const float* w1r = pk + L.w1r_off + c0;             // W1hR [NKp][Cp], zero beyond C
+  for (int k0 = 0; k0 < K; k0 += FIN_KC) {
+    const int kn = min(FIN_KC, K - k0);
+    if (k0) __syncthreads();
+    floatx4 va[FIN_KC * 4 / BCNF_WG], vb[FIN_KC * 4 / BCNF_WG];
+#pragma unroll
+    for (int e = 0; e < FIN_KC * 4 / BCNF_WG; ++e) {   // row = i4 / 4, float4 q = i4 % 4
+      const int i4 = tid + BCNF_WG * e, r = i4 >> 2, q = i4 & 3, kj = k0 + (r < kn ? r : 0);
+      va[e] = *reinterpret_cast<const floatx4*>(w1r + (long long)kj * L.Cp + 4 * q);
+      vb[e] = *reinterpret_cast<const floatx4*>(gx + (long long)kj * Xp + x0 + 4 * q);
+    }
+#pragma unroll
+    for (int e = 0; e < FIN_KC * 4 / BCNF_WG; ++e) {
+      const int i4 = tid + BCNF_WG * e;
+      reinterpret_cast<floatx4*>(As)[i4] = va[e];
+      reinterpret_cast<floatx4*>(Bs)[i4] = vb[e];
+    }
+    __syncthreads();
+    tile16_accum(As, Bs, kn, acc);
+  }
+  const float v = tile16_reduce(smem, acc);
+  const int c = c0 + (tid >> 4), x = x0 + (tid & 15);
+  if (c < L.C) {
+    if (x < X) {
+      if (dwf) dwf[(long long)c * X + x] = v;
+    } else if (x == X && dbf) {
+      dbf[c] = v;
+    }
+  }
 }
 
 // Compile-time mirror of the forward / backward record layouts of make_layout (checked on the host).
@@ -1285,40 +1502,40 @@ __device__ __forceinline__ long long compact_to_canonical(const BcnfLayout& L, i
   return (long long)m * L.blk_stride + rel;
 }
 
-// 64 output float4 per workgroup x 4 slab groups (group g sums workgroups g, g+4, ...; 8 loads in flight),
-// combined in a fixed order through LDS.
+// RED_O4 output float4 per workgroup x RED_G slab groups (group g sums workgroups g, g+RED_G, ...; RED_T loads
+// in flight per lane), combined in a fixed order through LDS. The slab stream is latency-bound on bytes in
+// flight: 32 lanes x 16 B x 16 loads per group keeps ~35 MB in flight over the ~580-workgroup grid at B=4096.
+constexpr int RED_G = 8, RED_O4 = 32, RED_T = 16;
+
 __device__ __forceinline__ void reduce_body(const BcnfLayout& L, const float* __restrict__ slab, long long stride,
                                             int nwg, float* __restrict__ out, int bx, float* __restrict__ smem) {
-  floatx4 (*part)[64] = reinterpret_cast<floatx4 (*)[64]>(smem);   // [4][64]
-  const int g = threadIdx.x >> 6, o4 = threadIdx.x & 63;
-  const long long i = ((long long)bx * 64 + o4) * 4;
+  floatx4 (*part)[RED_O4] = reinterpret_cast<floatx4 (*)[RED_O4]>(smem);   // [RED_G][RED_O4]
+  const int g = threadIdx.x / RED_O4, o4 = threadIdx.x % RED_O4;
+  const long long i = ((long long)bx * RED_O4 + o4) * 4;
   const bool live = i < stride;
   const long long ic = live ? i : 0;
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
   int w = g;
-  for (; w + 28 < nwg; w += 32) {
-    floatx4 v[8];
+  for (; w + RED_G * (RED_T - 1) < nwg; w += RED_G * RED_T) {
+    floatx4 v[RED_T];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) v[t] = *reinterpret_cast<const floatx4*>(slab + (long long)(w + 4 * t) * stride + ic);
+    for (int t = 0; t < RED_T; ++t)
+      v[t] = *reinterpret_cast<const floatx4*>(slab + (long long)(w + RED_G * t) * stride + ic);
 #pragma unroll
-    for (int t = 0; t < 8; ++t) acc += v[t];
+    for (int t = 0; t < RED_T; ++t) acc += v[t];
   }
-  for (; w < nwg; w += 4) acc += *reinterpret_cast<const floatx4*>(slab + (long long)w * stride + ic);
+  for (; w < nwg; w += RED_G) acc += *reinterpret_cast<const floatx4*>(slab + (long long)w * stride + ic);
   part[g][o4] = acc;
   __syncthreads();
   if (g != 0 || !live) return;
-  const floatx4 tot = ((part[0][o4] + part[1][o4]) + part[2][o4]) + part[3][o4];
+  floatx4 tot = part[0][o4];
+#pragma unroll
+  for (int q = 1; q < RED_G; ++q) tot += part[q][o4];
   const int m = (int)(i / L.blk_pad), o = (int)(i - (long long)m * L.blk_pad);
   const int size_m = L.cblk - ((m < L.nb - 1) ? 0 : L.an_size);
 #pragma unroll
   for (int e = 0; e < 4; ++e)
     if (o + e < size_m) out[compact_to_canonical(L, m, o + e)] = tot[e];
-}
-
-__global__ __launch_bounds__(BCNF_WG) void k_reduce(BcnfLayout L, const float* __restrict__ slab, long long stride,
-                                                    int nwg, float* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) float smem[4 * 64 * 4];
-  reduce_body(L, slab, stride, nwg, out, blockIdx.x, smem);
 }
 
 // The backward's tail in ONE launch: dL/dh tiles, the slab reduction and the W1 condition-part split-K
@@ -1328,10 +1545,12 @@ struct TailGrid {
   int n_dh, gx_dh;      // dh tiles: (gx_dh x Cp/16), 0 if dh is not requested
   int n_red;            // slab-reduce workgroups
   int gx_dw;            // dW1h: (gx_dw x splits)
+  int ones;             // folded path: the split-K runs on x1 = [x | 1] (ones column index), else -1
 };
 
+// Lw: the split-K role's layout (L itself, or fold_layout(L, X) with h = x on the folded path).
 template <bool VEC>
-__global__ __launch_bounds__(BCNF_WG) void k_bwd_tail(BcnfLayout L, TailGrid G, const float* __restrict__ pk,
+__global__ __launch_bounds__(BCNF_WG) void k_bwd_tail(BcnfLayout L, BcnfLayout Lw, TailGrid G, const float* __restrict__ pk,
                                                       const float* __restrict__ d1, const float* __restrict__ h,
                                                       long long B, float* __restrict__ dh,
                                                       const float* __restrict__ slab, long long stride, int nwg,
@@ -1349,7 +1568,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_bwd_tail(BcnfLayout L, TailGrid G, 
     return;
   }
   i -= G.n_red;
-  dw1h_body<VEC>(L, d1, h, B, rows_per_split, work, i % G.gx_dw, i / G.gx_dw, smem);
+  dw1h_body<VEC>(Lw, d1, h, B, rows_per_split, work, i % G.gx_dw, i / G.gx_dw, smem, G.ones);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1372,6 +1591,16 @@ size_t lds_floor_bytes() {
   static size_t v = [] {
     const char* e = getenv("BCNF_LDS_MIN_KB");
     return e ? (size_t)atoi(e) * 1024 : (size_t)0;
+  }();
+  return v;
+}
+
+// Experiment knob (env BCNF_TAIL_ROLES, bit mask, default all): 1 dh, 2 slab reduce, 4 W1h split-K, 8 its reduce.
+// Timing only (tools/tail_bench.py); results are incomplete with any bit cleared. Read once.
+int tail_roles() {
+  static int v = [] {
+    const char* e = getenv("BCNF_TAIL_ROLES");
+    return e ? atoi(e) : 15;
   }();
   return v;
 }
@@ -1412,11 +1641,15 @@ struct NllOut {
   float* part = nullptr;
 };
 
+// float4 row loads: the row stride and the base are 16-byte aligned (columns >= C of a loaded float4 are
+// discarded by select, so a padded row's tail may hold anything).
+bool vec_rows(const BcnfLayout& L, const float* h) { return L.ldh % 4 == 0 && ((uintptr_t)h & 15) == 0; }
+
 int launch_hp(const BcnfLayout& L, const float* pk, const float* h, long long R, float* hp, hipStream_t st) {
   size_t lds = hp_lds_bytes();
   const dim3 grid((unsigned)((R + 63) / 64), (unsigned)(L.NKp / 64));
   int rc;
-  if (L.C % 4 == 0) {
+  if (vec_rows(L, h)) {
     if ((rc = launch_lds(k_hp<true>, lds))) return rc;
     hipLaunchKernelGGL(k_hp<true>, grid, dim3(BCNF_WG), lds, st, L, pk, h, R, hp);
   } else {
@@ -1508,7 +1741,8 @@ long long ws_floats(const BcnfLayout& L, long long B, bool drop) {
 
 int forward_impl(const BcnfStackDesc* desc, const void* packed, const float* y, const float* h, int64_t batch,
                  float* z, float* ldj, float* log_prob, int32_t training, const uint64_t* rng_state, void* workspace,
-                 bool save, bool nll, bool finalize, float* loss_out, int32_t* guard, void* stream) {
+                 bool save, bool nll, bool finalize, float* loss_out, int32_t* guard, void* stream,
+                 const float* fold = nullptr, int X = 0, int ldx = 0) {
   BcnfLayout L;
   int rc = make_layout(desc, &L);
   if (rc) return rc;
@@ -1526,7 +1760,12 @@ int forward_impl(const BcnfStackDesc* desc, const void* packed, const float* y, 
   if (nll) no.part = ws + ws_part_off(L, batch, drop);
   const float* pk = (const float*)packed;
   hipStream_t st = (hipStream_t)stream;
-  if ((rc = launch_hp(L, pk, h, batch, hp, st))) return rc;
+  // h, or x with the folded feature Linear (fold_layout: Wc / bc instead of W1h^T / b1)
+  if (fold) {
+    if ((rc = launch_hp(fold_layout(L, X, ldx), fold, h, batch, hp, st))) return rc;
+  } else if ((rc = launch_hp(L, pk, h, batch, hp, st))) {
+    return rc;
+  }
   switch (L.NH) {
 #define BCNF_CASE(N) case N: rc = fwd_dispatch<N>(L, pk, y, hp, batch, z, ldj, log_prob, drop, rng_state, arec, no, st); break;
     BCNF_CASE(1) BCNF_CASE(2) BCNF_CASE(3) BCNF_CASE(4) BCNF_CASE(5) BCNF_CASE(6) BCNF_CASE(7) BCNF_CASE(8)
@@ -1662,25 +1901,135 @@ int bcnf_backward_tail(const BcnfStackDesc* desc, const void* packed, const void
   TailGrid G;
   G.gx_dh = (int)((batch + 63) / 64);
   G.n_dh = dh ? G.gx_dh * (L.Cp >> 4) : 0;
-  G.n_red = (int)((S / 4 + 63) / 64);
+  G.n_red = (int)((S / 4 + RED_O4 - 1) / RED_O4);
   G.gx_dw = (L.nb + 3) / 4;
+  G.ones = -1;
   const long long n_dw = (long long)G.gx_dw * splits;
   size_t lds = dw1h_lds_bytes(L);
   if (dh_lds_bytes() > lds) lds = dh_lds_bytes();
-  const dim3 grid((unsigned)(G.n_dh + G.n_red + n_dw));
-  if (L.C % 4 == 0) {
+  const int roles = tail_roles();
+  if (!(roles & 1)) G.n_dh = 0;
+  if (!(roles & 2)) G.n_red = 0;
+  const long long n_dw_run = (roles & 4) ? n_dw : 0;
+  const dim3 grid((unsigned)(G.n_dh + G.n_red + n_dw_run));
+  if (vec_rows(L, h)) {
     if ((rc = launch_lds(k_bwd_tail<true>, lds))) return rc;
-    hipLaunchKernelGGL(k_bwd_tail<true>, grid, dim3(BCNF_WG), lds, st, L, G, (const float*)packed, d1, h,
+    hipLaunchKernelGGL(k_bwd_tail<true>, grid, dim3(BCNF_WG), lds, st, L, L, G, (const float*)packed, d1, h,
                        (long long)batch, dh, (const float*)slab, S, nwg, dparams, rps, work);
   } else {
     if ((rc = launch_lds(k_bwd_tail<false>, lds))) return rc;
-    hipLaunchKernelGGL(k_bwd_tail<false>, grid, dim3(BCNF_WG), lds, st, L, G, (const float*)packed, d1, h,
+    hipLaunchKernelGGL(k_bwd_tail<false>, grid, dim3(BCNF_WG), lds, st, L, L, G, (const float*)packed, d1, h,
                        (long long)batch, dh, (const float*)slab, S, nwg, dparams, rps, work);
   }
   if ((rc = check_launch())) return rc;
+  if (!(roles & 8)) return BCNF_OK;
   const long long outs = (long long)L.nb * 16 * L.Cp;
   hipLaunchKernelGGL(k_dw1h_reduce, dim3((unsigned)((outs + BCNF_WG - 1) / BCNF_WG)), dim3(BCNF_WG), 0, st, L,
                      (const float*)work, (int)splits, dparams);
+  return check_launch();
+}
+
+// ---- folded linear feature network (see fold_body) ----
+namespace {
+int fold_setup(const BcnfStackDesc* desc, int32_t X, BcnfLayout* L) {
+  int rc = make_layout(desc, L);
+  if (rc) return rc;
+  if (!layout_supported(*L, desc)) return BCNF_ERR_UNSUPPORTED;
+  if (X < 1 || fold_xp(X) > 16 * NC16_MAX) return BCNF_ERR_UNSUPPORTED;
+  if (dw1h_lds_bytes(fold_layout(*L, X, X)) > LDS_MAX) return BCNF_ERR_UNSUPPORTED;
+  return BCNF_OK;
+}
+long long fold_floats(const BcnfLayout& L, int X) { return (long long)(fold_xp(X) + 1) * L.NKp; }
+}  // namespace
+
+int bcnf_fold_bytes(const BcnfStackDesc* desc, int32_t in_features, int64_t* bytes) {
+  BcnfLayout L;
+  const int rc = fold_setup(desc, in_features, &L);
+  if (rc) return rc;
+  if (!bytes) return BCNF_ERR_ARG;
+  *bytes = fold_floats(L, in_features) * 4;
+  return BCNF_OK;
+}
+
+int bcnf_fold_slab_bytes(const BcnfStackDesc* desc, int32_t in_features, int64_t batch, int64_t* bytes) {
+  BcnfLayout L;
+  const int rc = fold_setup(desc, in_features, &L);
+  if (rc) return rc;
+  if (!bytes || batch < 0) return BCNF_ERR_ARG;
+  const BcnfLayout F = fold_layout(L, in_features, in_features);
+  *bytes = ((int64_t)((batch + 15) / 16) * slab_stride_of(L) + w1h_work_floats(F, batch) +
+            (int64_t)L.nb * 16 * F.Cp) * 4;
+  return BCNF_OK;
+}
+
+int bcnf_pack_params_fold(const BcnfStackDesc* desc, const float* params, const float* qmats,
+                          const float* feat_weight, const float* feat_bias, int32_t in_features, void* packed,
+                          float* fold, void* stream) {
+  BcnfLayout L;
+  int rc = fold_setup(desc, in_features, &L);
+  if (rc) return rc;
+  if (!params || !packed || !fold || !feat_weight || (L.nb > 1 && !qmats)) return BCNF_ERR_ARG;
+  hipLaunchKernelGGL(k_pack_fold, dim3(L.NKp / 16 * FOLD_SPLIT + PACK_WG + 1), dim3(BCNF_WG), 0, (hipStream_t)stream, L, params,
+                     qmats, (float*)packed, feat_weight, feat_bias, (int)in_features, fold);
+  return check_launch();
+}
+
+int bcnf_fold_nll_forward(const BcnfStackDesc* desc, const void* packed, const float* fold, int32_t in_features,
+                          const float* y, const float* x, int32_t ldx, int64_t batch, float* z, float* ldj, int32_t training,
+                          uint64_t* rng_state, void* workspace, int32_t finalize, float* loss_out, int32_t* guard,
+                          void* stream) {
+  BcnfLayout L;
+  const int rc = fold_setup(desc, in_features, &L);
+  if (rc) return rc;
+  if (!fold || ldx < in_features) return BCNF_ERR_ARG;
+  return forward_impl(desc, packed, y, x, batch, z, ldj, nullptr, training, rng_state, workspace, true, true,
+                      finalize != 0, loss_out, guard, stream, fold, in_features, ldx);
+}
+
+int bcnf_fold_backward_tail(const BcnfStackDesc* desc, const void* packed, const void* slab, const float* x,
+                            int32_t ldx, int32_t in_features, const float* feat_weight, const float* feat_bias,
+                            const void* workspace, int64_t batch, int32_t training, float* dparams,
+                            float* dfeat_weight, float* dfeat_bias, void* stream) {
+  BcnfLayout L;
+  int rc = fold_setup(desc, in_features, &L);
+  if (rc) return rc;
+  if (!packed || !slab || !x || !feat_weight || !workspace || !dparams || batch < 1 || ldx < in_features)
+    return BCNF_ERR_ARG;
+  const BcnfLayout F = fold_layout(L, in_features, ldx);
+  hipStream_t st = (hipStream_t)stream;
+  const long long S = slab_stride_of(L);
+  const int nwg = (int)((batch + 15) / 16);
+  const bool drop = training && L.p > 0.f;
+  const float* d1 = (const float*)workspace + ws_d1_off(L, batch, drop);
+  float* work = (float*)slab + (long long)nwg * S;
+  float* gx = work + w1h_work_floats(F, batch);
+  const int rps = w1h_rows_per_split(batch);
+  const long long splits = w1h_splits(batch);
+  TailGrid G;
+  G.gx_dh = 1;
+  G.n_dh = 0;
+  G.n_red = (int)((S / 4 + RED_O4 - 1) / RED_O4);
+  G.gx_dw = (L.nb + 3) / 4;
+  G.ones = in_features;
+  const dim3 grid((unsigned)(G.n_red + (long long)G.gx_dw * splits));
+  size_t lds = dw1h_lds_bytes(F);
+  if (vec_rows(F, x)) {
+    if ((rc = launch_lds(k_bwd_tail<true>, lds))) return rc;
+    hipLaunchKernelGGL(k_bwd_tail<true>, grid, dim3(BCNF_WG), lds, st, L, F, G, (const float*)packed, d1, x,
+                       (long long)batch, (float*)nullptr, (const float*)slab, S, nwg, dparams, rps, work);
+  } else {
+    if ((rc = launch_lds(k_bwd_tail<false>, lds))) return rc;
+    hipLaunchKernelGGL(k_bwd_tail<false>, grid, dim3(BCNF_WG), lds, st, L, F, G, (const float*)packed, d1, x,
+                       (long long)batch, (float*)nullptr, (const float*)slab, S, nwg, dparams, rps, work);
+  }
+  if ((rc = check_launch())) return rc;
+  const long long total = (long long)L.nb * 16 * F.Cp;
+  hipLaunchKernelGGL(k_gx_reduce, dim3((unsigned)((total + BCNF_WG - 1) / BCNF_WG)), dim3(BCNF_WG), 0, st, total,
+                     (const float*)work, (int)splits, gx);
+  if ((rc = check_launch())) return rc;
+  const int n_fin = (L.nb + (F.Cp >> 4)) * (L.Cp >> 4);
+  hipLaunchKernelGGL(k_fold_finish, dim3((unsigned)n_fin), dim3(BCNF_WG), 0, st, L, (const float*)packed,
+                     (const float*)gx, feat_weight, feat_bias, (int)in_features, dparams, dfeat_weight, dfeat_bias);
   return check_launch();
 }
 

@@ -327,6 +327,68 @@ class FusedStack:
         self._backward_tail(h, ws, pk, slab, dh, dparams, B, training, stream, tm, e0)
         return dy, dh, dparams
 
+    # ------------------------------------------------------------------ folded linear feature network
+    def fold_supported(self, in_features: int) -> bool:
+        """Whether a single nn.Linear [in_features -> n_conditions] feature network can be folded into the
+        condition projection (bcnf_pack_params_fold; include/bcnf_amd.h)."""
+        out = ctypes.c_int64(0)
+        return N.lib().bcnf_fold_bytes(self._pdesc, ctypes.c_int32(int(in_features)), ctypes.byref(out)) == N.OK
+
+    def launch_fold_nll_forward(self, y, x, wf, bf, training: bool, finalize: bool = True):
+        """launch_nll_forward with h = x Wf^T + bf never formed: the pack launch also folds the Linear into
+        the projection weights (Wc = W1h Wf, bc = b1 + W1h bf) and the projection runs on x."""
+        self._check_device(y, x, wf, bf)
+        B, X = x.shape
+        if y.dim() != 2 or y.shape != (B, self.cfg.size):
+            raise ValueError(f"bcnf_amd folded forward: y {tuple(y.shape)} vs x {tuple(x.shape)}")
+        if B == 0:
+            raise ValueError("bcnf_amd: the NLL of an empty batch is undefined")
+        L = N.lib()
+        dev = y.device
+        stream = N.stream_handle(dev)
+        pk = torch.empty(N.query_i64(L.bcnf_packed_bytes, self._pdesc) // 4, dtype=torch.float32, device=dev)
+        fold = torch.empty(N.query_i64(L.bcnf_fold_bytes, self._pdesc, ctypes.c_int32(X)) // 4, dtype=torch.float32,
+                           device=dev)
+        N.check(L.bcnf_pack_params_fold(self._pdesc, N.ptr(self.flat), N.ptr(self.qflat), N.ptr(wf), N.ptr(bf),
+                                        ctypes.c_int32(X), N.ptr(pk), N.ptr(fold), stream), "bcnf_pack_params_fold")
+        z = torch.empty_like(y)
+        ldj = torch.empty(B, dtype=torch.float32, device=dev)
+        vals = torch.empty(3, dtype=torch.float32, device=dev)
+        rng = self.rng_state() if (training and self.cfg.dropout > 0.0) else None
+        wb, _ = self.workspace_bytes(B, training)
+        ws = torch.empty(max(wb // 4, 1), dtype=torch.float32, device=dev)
+        rc = L.bcnf_fold_nll_forward(self._pdesc, N.ptr(pk), N.ptr(fold), ctypes.c_int32(X), N.ptr(y), N.ptr(x),
+                                     ctypes.c_int32(x.stride(0)), ctypes.c_int64(B), N.ptr(z), N.ptr(ldj), ctypes.c_int32(int(training)),
+                                     N.ptr(rng), N.ptr(ws), ctypes.c_int32(int(finalize)), N.ptr(vals),
+                                     N.ptr(self.guard if finalize else None), stream)
+        N.check(rc, "bcnf_fold_nll_forward")
+        return z, ldj, vals, (ws, pk)
+
+    def launch_fold_nll_backward(self, x, z, dvals, wf, bf, training: bool, saved, want_feat: bool,
+                                 finalize_into=None):
+        """Fused NLL backward of the folded pass: (dparams, dWf, dbf); no dL/dh, no dL/dx."""
+        ws, pk = saved
+        B, X = x.shape
+        L = N.lib()
+        dev = x.device
+        stream = N.stream_handle(dev)
+        sb = N.query_i64(L.bcnf_fold_slab_bytes, self._pdesc, ctypes.c_int32(X), ctypes.c_int64(B))
+        slab = torch.empty(max(sb // 4, 1), dtype=torch.float32, device=dev)
+        dparams = torch.empty_like(self.flat)
+        dwf = torch.empty_like(wf) if want_feat else None
+        dbf = torch.empty_like(bf) if (want_feat and bf is not None) else None
+        rng = self.rng_state() if (finalize_into is not None and training and self.cfg.dropout > 0.0) else None
+        rc = L.bcnf_nll_backward(self._pdesc, N.ptr(pk), N.ptr(x), N.ptr(z), N.ptr(dvals), ctypes.c_int64(B),
+                                 ctypes.c_int32(int(training)), N.ptr(ws), None, None, None, N.ptr(slab),
+                                 N.ptr(finalize_into), N.ptr(rng),
+                                 N.ptr(self.guard if finalize_into is not None else None), stream)
+        N.check(rc, "bcnf_nll_backward")
+        N.check(L.bcnf_fold_backward_tail(self._pdesc, N.ptr(pk), N.ptr(slab), N.ptr(x), ctypes.c_int32(x.stride(0)),
+                                          ctypes.c_int32(X), N.ptr(wf),
+                                          N.ptr(bf), N.ptr(ws), ctypes.c_int64(B), ctypes.c_int32(int(training)),
+                                          N.ptr(dparams), N.ptr(dwf), N.ptr(dbf), stream), "bcnf_fold_backward_tail")
+        return dparams, dwf, dbf
+
     @torch.no_grad()
     def time_kernels(self, y, h, training: bool = True, iters: int = 20):
         """Average device time (us) of each launch of one NLL training pass, measured with HIP events on the
@@ -454,6 +516,45 @@ def stack_nll(stack: FusedStack, y, h, training: bool, defer: bool = False):
     if torch.is_grad_enabled() and (params_grad or y.requires_grad or h.requires_grad):
         return _StackNLL.apply(y, h, fp if params_grad else fp.detach(), stack, training, defer)
     return stack.launch_nll_forward(y, h, training)[2]
+
+
+class _FoldNLL(torch.autograd.Function):
+    """_StackNLL with the feature network's single nn.Linear folded into the condition projection: inputs
+    (y, x, Wf, bf, flat_param); gradients for Wf, bf and flat_param (not for y or x)."""
+
+    @staticmethod
+    def forward(ctx, y, x, wf, bf, flat_param, stack: FusedStack, training: bool, defer: bool):
+        z, _, vals, saved = stack.launch_fold_nll_forward(y, x, wf, bf, training, finalize=not defer)
+        ctx.stack = stack
+        ctx.training = training
+        ctx.saved = saved
+        ctx.defer = defer
+        ctx.save_for_backward(x, wf, bf, z, vals)
+        return vals
+
+    @staticmethod
+    def backward(ctx, dvals):
+        x, wf, bf, z, vals = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        dparams, dwf, dbf = ctx.stack.launch_fold_nll_backward(x, z, dvals.contiguous(), wf, bf, ctx.training,
+                                                               ctx.saved, want_feat=need[2] or need[3],
+                                                               finalize_into=vals if ctx.defer else None)
+        return (None, None, dwf if need[2] else None, dbf if need[3] else None, dparams if need[4] else None,
+                None, None, None)
+
+
+def stack_nll_fold(stack: FusedStack, y, x, wf, bf, training: bool, defer: bool = False):
+    """stack_nll(stack, y, x Wf^T + bf) without forming the features (see launch_fold_nll_forward)."""
+    y = y.contiguous()
+    if x.stride(1) != 1 or x.stride(0) < x.shape[1]:
+        x = x.contiguous()              # rows may be padded (ldx = stride(0) > X: TrainStep's zero-padded pool)
+    stack.sync_grad_state()
+    params_grad = stack.trainable[0].requires_grad
+    fp = stack.flat_param
+    feat_grad = wf.requires_grad or (bf is not None and bf.requires_grad)
+    if torch.is_grad_enabled() and (params_grad or feat_grad):
+        return _FoldNLL.apply(y, x, wf, bf, fp if params_grad else fp.detach(), stack, training, defer)
+    return stack.launch_fold_nll_forward(y, x, wf, bf, training)[2]
 
 
 class _StackInverse(torch.autograd.Function):

@@ -60,6 +60,7 @@ class TrainStep:
         self._graphs = None
         self._static = None
         self._pool = None
+        self._cond_shape = None  # (per-sample condition shape, its size) when the pool rows are padded
         self._epoch = None      # (order, cursor, n_batches, batch) for the device-cursor batch walk
         self._bucket = None     # data parallel: every gradient in one buffer, one all-reduce per step
         self._host_cursor = 0   # host mirror of the epoch cursor (the history row of the next step)
@@ -164,7 +165,19 @@ class TrainStep:
         else:
             N.check(N.lib().bcnf_gather_rows2(N.ptr(self._static[2]), n, N.ptr(py), cy, N.ptr(y), N.ptr(pt), ct,
                                               N.ptr(t), st), "bcnf_gather_rows2")
-        return y, t
+        return y, self._unpad(t)
+
+    def _unpad(self, t):
+        """A batch of the padded condition pool as the (n, *cond_shape) view the model expects (row stride = the
+        padded width; the folded path reads it in place with float4 loads)."""
+        if self._cond_shape is None:
+            return t
+        shape, X = self._cond_shape
+        return t[:, :X].view((t.shape[0],) + shape)
+
+    def _pool_rows(self, idx):
+        py, pt = self._pool
+        return py.index_select(0, idx), self._unpad(pt.index_select(0, idx))
 
     def _snapshot(self):
         with torch.no_grad():
@@ -257,6 +270,16 @@ class TrainStep:
         for t in (y_pool, traj_pool):
             if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
                 raise ValueError("set_pool: contiguous fp32 device tensors required")
+        # the folded feature Linear (cnf.py fold_pool_width) reads x rows with float4 loads when they are 16-byte
+        # aligned: zero-pad the pool's rows (90 -> 92 floats for FC_small) once, here
+        self._cond_shape = None
+        w = self.model.fold_pool_width(traj_pool) if hasattr(self.model, "fold_pool_width") else None
+        if w is not None:
+            X = traj_pool[0].numel()
+            padded = torch.zeros((traj_pool.shape[0], w), dtype=traj_pool.dtype, device=traj_pool.device)
+            padded[:, :X] = traj_pool.reshape(traj_pool.shape[0], X)
+            self._cond_shape = (tuple(traj_pool.shape[1:]), X)
+            traj_pool = padded
         self._pool = (y_pool, traj_pool)
 
     def step_indexed(self, idx):
@@ -268,8 +291,7 @@ class TrainStep:
             self._static = (None, None, idx)
             return tuple(self.eager_step(*self._gather()).tolist())
         if self._graphs is None:
-            py, pt = self._pool
-            self._build_graphs(py.index_select(0, idx), pt.index_select(0, idx), idx=idx)
+            self._build_graphs(*self._pool_rows(idx), idx=idx)
         self._static[2].copy_(idx, non_blocking=True)
         self._replay()
         return self._host_values()

@@ -119,6 +119,30 @@ int bcnf_backward_tail(const BcnfStackDesc* desc, const void* packed, const void
                        const void* workspace, int64_t batch, int32_t training, float* dh, float* dparams,
                        void* stream);
 
+/* ---- Folded linear feature network (training fast path; no reference counterpart as a function: it
+ * computes the same sums as feature_network.py:114-145's single nn.Linear [X -> C] feeding cnf.py:74-107's
+ * condition input, reassociated). With Wf (C x X, row-major) and bf (C, nullable) of that Linear:
+ *   Wc = W1h Wf, bc = b1 + W1h bf  (bcnf_pack_params_fold, alongside the regular pack, one launch)
+ *   HP = x Wc^T + bc               (bcnf_fold_nll_forward: bcnf_nll_forward with x (B x X) in place of h)
+ *   dW1h, dWf, dbf from Gx = D1^T [x | 1]  (bcnf_fold_backward_tail, after bcnf_nll_backward(dh = dparams
+ *   = NULL) wrote `slab` sized by bcnf_fold_slab_bytes). h and dL/dh are never formed. X + 1 <= 256.
+ * x rows are ldx >= X floats apart; ldx % 4 == 0 with a 16-byte aligned x selects float4 row loads (TrainStep's
+ * padded pool, bcnf_amd/train.py); the padding columns are never used. */
+int bcnf_fold_bytes(const BcnfStackDesc* desc, int32_t in_features, int64_t* bytes);
+int bcnf_fold_slab_bytes(const BcnfStackDesc* desc, int32_t in_features, int64_t batch, int64_t* bytes);
+int bcnf_pack_params_fold(const BcnfStackDesc* desc, const float* params, const float* qmats,
+                          const float* feat_weight, const float* feat_bias, int32_t in_features, void* packed,
+                          float* fold, void* stream);
+int bcnf_fold_nll_forward(const BcnfStackDesc* desc, const void* packed, const float* fold, int32_t in_features,
+                          const float* y, const float* x, int32_t ldx, int64_t batch, float* z, float* ldj,
+                          int32_t training,
+                          uint64_t* rng_state, void* workspace, int32_t finalize, float* loss_out, int32_t* guard,
+                          void* stream);
+int bcnf_fold_backward_tail(const BcnfStackDesc* desc, const void* packed, const void* slab, const float* x,
+                            int32_t ldx, int32_t in_features, const float* feat_weight, const float* feat_bias,
+                            const void* workspace, int64_t batch, int32_t training, float* dparams,
+                            float* dfeat_weight, float* dfeat_bias, void* stream);
+
 /* Deterministic (fixed-order) reduction of a backward's gradient scratch into dparams, including the
  * W1 condition columns (split-K GEMM of D1 with h). Replaces autograd's implicit batch reduction. */
 int bcnf_grad_reduce(const BcnfStackDesc* desc, const void* slab, const float* h, const void* workspace,

@@ -148,6 +148,7 @@ def test_nll_loss_equals_unfused_path_with_dropout(g1):
     y, traj = t(g1["y"]), t(g1["traj"])
     m = fresh_model(g1, train=True)
     m.flat_parameters()
+    m.fold_features = False        # the fused NLL kernel itself; the folded feature Linear: test_gpu_fold.py
     m.fused.set_seed(1234)
     vals = m.nll_loss(y, traj)
     torch.autograd.backward(vals, torch.tensor([1.0, 0.0, 0.0], device=DEV))
