@@ -60,6 +60,9 @@ class TrainStep:
         self._graphs = None
         self._static = None
         self._pool = None
+        self._multi = None      # (graph, steps, grads): run_epoch's multi-step graph (world 1)
+        self._single_grads = None
+        self._multi_bound = False
         self._cond_shape = None  # (per-sample condition shape, its size) when the pool rows are padded
         self._epoch = None      # (order, cursor, n_batches, batch) for the device-cursor batch walk
         self._bucket = None     # data parallel: every gradient in one buffer, one all-reduce per step
@@ -238,6 +241,7 @@ class TrainStep:
                 self._scale_bucket()
                 self._update(vals)
         self._graphs = (g1, g2, vals)
+        self._single_grads = [p.grad for p in self.params]   # what .grad shows after a g1 replay
 
     def step(self, y, traj):
         """One training step; returns (loss, nll, mse) as Python floats (the Trainer's three .item())."""
@@ -364,8 +368,17 @@ class TrainStep:
         self._guard.zero_()
         if check_divergence:
             self._guard[GUARD_CHECK] = 1
-        for _ in range(n):
+        i = 0
+        if self.world == 1 and self.epoch_unroll > 1 and n >= self.epoch_unroll:
+            g, k, grads = self._multi_graph()
+            while n - i >= k:
+                g.replay()
+                i += k
+            self._bind(grads)
+            self._multi_bound = True
+        while i < n:
             self._replay()
+            i += 1
         torch.cuda.current_stream().synchronize()
         vals = [tuple(r) for r in self._hist[start:start + n].tolist()]
         self._host_cursor = (start + n) % nb
@@ -377,7 +390,36 @@ class TrainStep:
                     raise TrainingDivergedError(f"Loss exploded to {v[0]} at batch {start + i}")
         return vals
 
+    # Steps per captured graph in run_epoch: a graph boundary costs ~9 us of idle GPU between two replays
+    # (measured, r01j), so run_epoch replays `epoch_unroll` device-driven steps (cursor, RNG offset, Adam step,
+    # history row all advance on the device) per launch and the remainder one by one.
+    epoch_unroll = 8
+
+    def _multi_graph(self):
+        if self._multi is None or self._multi[1] != self.epoch_unroll:
+            k = self.epoch_unroll
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(k):
+                    sy, st = self._gather()
+                    vals = self._forward_backward(sy, st)
+                    self._update(vals)
+            self._multi = (g, k, [p.grad for p in self.params])
+            self._bind(self._single_grads)
+            self._multi_bound = False
+        return self._multi
+
+    def _bind(self, grads):
+        """.grad = the gradient buffers of the graph that ran last (each captured graph owns its own)."""
+        if grads is None:
+            return
+        for p, gr in zip(self.params, grads):
+            p.grad = gr
+
     def _replay(self):
+        if self._multi_bound:
+            self._bind(self._single_grads)
+            self._multi_bound = False
         g1, g2, vals = self._graphs
         g1.replay()
         if g2 is not None:

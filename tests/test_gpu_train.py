@@ -222,9 +222,10 @@ def _epoch_pool(gen, n=768, blow_up=None):
     return y.to(DEV), traj.to(DEV)
 
 
-def test_run_epoch_equals_per_step_loop(g1):
-    """run_epoch (back-to-back replays, one sync) == step_epoch per step: same logged values, parameters,
-    Adam state, RNG offset and cursor, bit for bit."""
+@pytest.mark.parametrize("unroll", [8, 2, 3])
+def test_run_epoch_equals_per_step_loop(g1, unroll):
+    """run_epoch (back-to-back replays, one sync; `unroll` steps per captured graph) == step_epoch per step: same
+    logged values, parameters, Adam state, RNG offset, cursor and .grad (the last step's), bit for bit."""
     from bcnf_amd.train import TrainStep
     gen = torch.Generator().manual_seed(21)
     py, pt = _epoch_pool(gen)
@@ -234,6 +235,7 @@ def test_run_epoch_equals_per_step_loop(g1):
         m = fresh_model(g1, train=True)
         m.fused.set_seed(5)
         st = TrainStep(m, lr=2e-4)
+        st.epoch_unroll = unroll
         st.set_pool(py, pt)
         st.set_epoch(order, 192)
         if batched:
@@ -242,11 +244,11 @@ def test_run_epoch_equals_per_step_loop(g1):
             vals = [st.step_epoch() for _ in range(4)]
         state = [v.clone() for s in st.opt.state.values() for v in s.values()]
         res.append((vals, [p.detach().clone() for p in m.parameters()], state,
-                    m.fused.rng_state().clone(), st._epoch[1].item()))
-    (v0, p0, s0, r0, c0), (v1, p1, s1, r1, c1) = res
+                    m.fused.rng_state().clone(), st._epoch[1].item(), [p.grad.clone() for p in st.params]))
+    (v0, p0, s0, r0, c0, g0), (v1, p1, s1, r1, c1, gr1) = res
     assert v0 == v1 and len(v1) == 4
     assert c0 == c1 == 0 and torch.equal(r0, r1)
-    for a, b in zip(p0 + s0, p1 + s1):
+    for a, b in zip(p0 + s0 + g0, p1 + s1 + gr1):
         assert torch.equal(a, b)
 
 
@@ -265,6 +267,7 @@ def test_run_epoch_divergence_halts_like_the_trainer(g1):
         m = fresh_model(g1, train=True)
         m.fused.set_seed(9)
         st = TrainStep(m, lr=2e-4)
+        st.epoch_unroll = 2                                   # the halt lands inside a multi-step graph
         st.set_pool(py, pt)
         st.set_epoch(order, 128)
         if mode == "per_step":
