@@ -390,11 +390,15 @@ class FusedStack:
         return dparams, dwf, dbf
 
     @torch.no_grad()
-    def time_kernels(self, y, h, training: bool = True, iters: int = 20):
+    def time_kernels(self, y, h, training: bool = True, iters: int = 20, fold=None):
         """Average device time (us) of each launch of one NLL training pass, measured with HIP events on the
         launch stream around `iters` back-to-back launches of the same (idempotent) call, so host launch
         latency is amortised: 'forward' (k_hp + k_forward), 'k_backward' (the backward kernel alone) and
-        'tail' (dh + slab reduce + W1 condition part)."""
+        'tail' (dh + slab reduce + W1 condition part). fold = (x, Wf, bf): the folded path instead -- 'pack'
+        (pack + fold), 'forward' (k_hp on x + k_forward), 'k_backward', 'tail' (slab reduce + split-K on x,
+        Gx reduce, dW1h / dWf / dbf)."""
+        if fold is not None:
+            return self._time_fold_kernels(y, *fold, training=training, iters=iters)
         L = N.lib()
         dev = y.device
         stream = N.stream_handle(dev)
@@ -417,6 +421,10 @@ class FusedStack:
                                                  ctypes.c_int64(B), ctypes.c_int32(int(training)), N.ptr(dh),
                                                  N.ptr(dparams), stream),
         }
+        return self._event_times(calls, iters)
+
+    @staticmethod
+    def _event_times(calls, iters):
         out = {}
         for name, fn in calls.items():
             N.check(fn(), name)                       # warm (code object, LDS attributes)
@@ -429,6 +437,40 @@ class FusedStack:
             torch.cuda.synchronize()
             out[name] = e0.elapsed_time(e1) * 1e3 / iters
         return out
+
+    def _time_fold_kernels(self, y, x, wf, bf, training: bool, iters: int):
+        L = N.lib()
+        dev = y.device
+        stream = N.stream_handle(dev)
+        B, X = x.shape
+        ldx = ctypes.c_int32(x.stride(0))
+        z, _, vals, (ws, pk) = self.launch_fold_nll_forward(y, x, wf, bf, training, finalize=False)
+        fold = torch.empty(N.query_i64(L.bcnf_fold_bytes, self._pdesc, ctypes.c_int32(X)) // 4, dtype=torch.float32,
+                           device=dev)
+        N.check(L.bcnf_pack_params_fold(self._pdesc, N.ptr(self.flat), N.ptr(self.qflat), N.ptr(wf), N.ptr(bf),
+                                        ctypes.c_int32(X), N.ptr(pk), N.ptr(fold), stream), "pack_fold")
+        sb = N.query_i64(L.bcnf_fold_slab_bytes, self._pdesc, ctypes.c_int32(X), ctypes.c_int64(B))
+        slab = torch.empty(max(sb // 4, 1), dtype=torch.float32, device=dev)
+        dparams = torch.empty_like(self.flat)
+        dwf, dbf = torch.empty_like(wf), (torch.empty_like(bf) if bf is not None else None)
+        ldj = torch.empty(B, dtype=torch.float32, device=dev)
+        rng = self.rng_state() if (training and self.cfg.dropout > 0.0) else None
+        calls = {
+            "pack": lambda: L.bcnf_pack_params_fold(self._pdesc, N.ptr(self.flat), N.ptr(self.qflat), N.ptr(wf),
+                                                    N.ptr(bf), ctypes.c_int32(X), N.ptr(pk), N.ptr(fold), stream),
+            "forward": lambda: L.bcnf_fold_nll_forward(self._pdesc, N.ptr(pk), N.ptr(fold), ctypes.c_int32(X),
+                                                       N.ptr(y), N.ptr(x), ldx, ctypes.c_int64(B), N.ptr(z),
+                                                       N.ptr(ldj), ctypes.c_int32(int(training)), N.ptr(rng),
+                                                       N.ptr(ws), ctypes.c_int32(0), N.ptr(vals), None, stream),
+            "k_backward": lambda: L.bcnf_nll_backward(self._pdesc, N.ptr(pk), N.ptr(x), N.ptr(z), None,
+                                                      ctypes.c_int64(B), ctypes.c_int32(int(training)), N.ptr(ws),
+                                                      None, None, None, N.ptr(slab), None, None, None, stream),
+            "tail": lambda: L.bcnf_fold_backward_tail(self._pdesc, N.ptr(pk), N.ptr(slab), N.ptr(x), ldx,
+                                                      ctypes.c_int32(X), N.ptr(wf), N.ptr(bf), N.ptr(ws),
+                                                      ctypes.c_int64(B), ctypes.c_int32(int(training)),
+                                                      N.ptr(dparams), N.ptr(dwf), N.ptr(dbf), stream),
+        }
+        return self._event_times(calls, iters)
 
     def launch_inverse(self, z, h, cond_index=None, training: bool = False):
         self._check_inputs(z, h, "inverse")

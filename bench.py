@@ -159,6 +159,14 @@ def kernel_timing(model, data, args):
     y, traj = data.y[idx], data.traj[idx]
     with torch.no_grad():
         h = model.feature_network_stack(traj).contiguous()
+        w = model.fold_pool_width(traj) if hasattr(model, "fold_pool_width") else None
+        lin = model._fold_linear() if hasattr(model, "_fold_linear") else None
+    if lin is not None:                 # the folded step: x rows padded like TrainStep's pool
+        X = traj[0].numel()
+        xp = torch.zeros((traj.shape[0], w or X), dtype=traj.dtype, device=traj.device)
+        xp[:, :X] = traj.reshape(traj.shape[0], X)
+        fold = (xp[:, :X], lin.weight.detach(), None if lin.bias is None else lin.bias.detach())
+        return model.fused.time_kernels(y, h, training=True, iters=args.kernel_iters, fold=fold)
     return model.fused.time_kernels(y, h, training=True, iters=args.kernel_iters)
 
 
