@@ -51,6 +51,21 @@ class BcnfStackDesc(ctypes.Structure):
     ]
 
 
+class BcnfGather2(ctypes.Structure):
+    """include/bcnf_amd.h BcnfGather2: a batch gather run inside bcnf_pack_params_fold's launch."""
+    _fields_ = [
+        ("idx", ctypes.c_void_p),
+        ("cursor", ctypes.c_void_p),
+        ("n", ctypes.c_int64),
+        ("src0", ctypes.c_void_p),
+        ("cols0", ctypes.c_int32),
+        ("dst0", ctypes.c_void_p),
+        ("src1", ctypes.c_void_p),
+        ("cols1", ctypes.c_int32),
+        ("dst1", ctypes.c_void_p),
+    ]
+
+
 def make_desc(size, nested_sizes, n_blocks, n_conditions, dropout=0.0, act_norm=False, two_way=False):
     d = BcnfStackDesc()
     d.size = int(size)
@@ -100,7 +115,7 @@ def _bind(lib):
                                      _vp, _vp]),
         "bcnf_fold_bytes": (_i32, [_pdesc, _i32, _pi64]),
         "bcnf_fold_slab_bytes": (_i32, [_pdesc, _i32, _i64, _pi64]),
-        "bcnf_pack_params_fold": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
+        "bcnf_pack_params_fold": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
         "bcnf_fold_nll_forward": (_i32, [_pdesc, _vp, _vp, _i32, _vp, _vp, _i32, _i64, _vp, _vp, _i32, _vp, _vp,
                                          _i32, _vp, _vp, _vp]),
         "bcnf_fold_backward_tail": (_i32, [_pdesc, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _i64, _i32, _vp, _vp,

@@ -384,20 +384,26 @@ class CondRealNVP_v2(ConditionalInvertibleLayer):
             return z, condition
         return z
 
-    def nll_loss(self, y: torch.Tensor, *conditions: torch.Tensor, defer_reduction: bool = False) -> torch.Tensor:
+    def nll_loss(self, y: torch.Tensor, *conditions: torch.Tensor, defer_reduction: bool = False,
+                 gather=None) -> torch.Tensor:
         """The Trainer's training loss in one fused pass (trainer.py:260-266 with hybrid_weight = 0):
         returns vals = [loss, nll, mse] where loss = nll = inn_nll_loss(z, log_det_J) and mse = 0.
         `vals` is differentiable (backprop loss via vals[0] or with cotangent [1, 0, 0]); the feature
         network runs through autograd as usual, the coupling stack and the loss through the fused
         kernels with no dz / dldj tensors in between. defer_reduction=True (a backward certainly follows)
-        moves the loss reduction into the backward launch; vals is then valid only after backward."""
+        moves the loss reduction into the backward launch; vals is then valid only after backward.
+        `gather` (TrainStep, folded path only): the batch gather that fills y and the condition, run inside the
+        pack launch."""
         self._check_supported()
         if y.dim() == 1:
             y = y.unsqueeze(0)
         fold = self._foldable_linear(y, conditions)
         if fold is not None:
             x, lin = fold
-            return stack_nll_fold(self._fused, y, x, lin.weight, lin.bias, self.training, defer=defer_reduction)
+            return stack_nll_fold(self._fused, y, x, lin.weight, lin.bias, self.training, defer=defer_reduction,
+                                  gather=gather)
+        if gather is not None:
+            raise ValueError("bcnf_amd: a deferred batch gather needs the folded feature path")
         condition = self._features(conditions)
         return stack_nll(self._fused, y, condition, self.training, defer=defer_reduction)
 

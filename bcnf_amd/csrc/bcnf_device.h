@@ -29,6 +29,62 @@ inline int launched() {
 }
 }  // namespace bcnf_rt
 
+// dst0[r] = src0[idx[r]] (cols0 floats), dst1[r] = src1[idx[r]] (cols1 floats), one launch for both;
+// workgroup w copies rows [w * rpw, (w + 1) * rpw) (32-bit index math: n * (cols0 + cols1) < 2^31), each
+// thread BCNF_GU elements per round with every index and data load issued before the stores. With
+// `cursor` != NULL the rows are idx[cursor[0] * n + r] (the cursor is advanced by a later launch).
+constexpr int BCNF_GU = 8;
+__device__ __forceinline__ void gather2_rows(const int64_t* __restrict__ idx, int n, int rpw,
+                                             const float* __restrict__ s0, int c0, float* __restrict__ d0,
+                                             const float* __restrict__ s1, int c1, float* __restrict__ d1,
+                                             const long long* __restrict__ cursor, int bx) {
+  if (cursor) idx += cursor[0] * n;
+  const int r0 = bx * rpw, r1 = r0 + rpw < n ? r0 + rpw : n;
+  const int cw = c0 + c1, total = (r1 - r0) * cw;
+  for (int e0 = 0; e0 < total; e0 += BCNF_GU * BCNF_WG) {
+    int r[BCNF_GU], col[BCNF_GU];
+    long long src[BCNF_GU];
+    float v[BCNF_GU];
+#pragma unroll
+    for (int u = 0; u < BCNF_GU; ++u) {
+      int e = e0 + u * BCNF_WG + threadIdx.x;
+      e = e < total ? e : total - 1;
+      const int rr = e / cw;
+      r[u] = r0 + rr;
+      col[u] = e - rr * cw;
+      src[u] = idx[r[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < BCNF_GU; ++u)
+      v[u] = col[u] < c0 ? s0[src[u] * c0 + col[u]] : s1[src[u] * c1 + (col[u] - c0)];
+#pragma unroll
+    for (int u = 0; u < BCNF_GU; ++u) {
+      if (e0 + u * BCNF_WG + (int)threadIdx.x >= total) continue;
+      if (col[u] < c0)
+        d0[r[u] * c0 + col[u]] = v[u];
+      else
+        d1[r[u] * c1 + (col[u] - c0)] = v[u];
+    }
+  }
+}
+
+// Kernel-argument form of a two-tensor gather (k_gather2, or extra workgroups of another launch).
+struct BcnfGatherArgs {
+  const int64_t* idx;
+  const long long* cursor;
+  const float* s0;
+  float* d0;
+  const float* s1;
+  float* d1;
+  int n, rpw, c0, c1, nwg;     // nwg = 0: no gather
+};
+
+// Rows per workgroup and workgroup count of a gather of n rows (at most 512 workgroups).
+inline void gather2_plan(long long n, int* rpw, int* nwg) {
+  const int w = n < 512 ? (int)n : 512;
+  *rpw = w > 0 ? (int)((n + w - 1) / w) : 1;
+  *nwg = w > 0 ? (int)((n + *rpw - 1) / *rpw) : 0;
+}
 
 // Host-computed layout of one stack (passed by value to every kernel).
 struct BcnfLayout {

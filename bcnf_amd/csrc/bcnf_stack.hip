@@ -368,19 +368,26 @@ __device__ __forceinline__ void fold_body(const BcnfLayout& L, const float* __re
   *reinterpret_cast<floatx4*>(fold + (long long)xc * L.NKp + kj) = acc;
 }
 
-// NKp / 4 fold workgroups first (they start before the record workgroups), then k_pack's grid. The fold reads
-// the canonical parameters, not k_pack's output.
+// NKp / 4 fold workgroups first (they start before the record workgroups), then the optional batch gather's
+// workgroups (the step's batch feed: independent of the pack), then k_pack's grid. The fold reads the canonical
+// parameters, not k_pack's output.
 __global__ __launch_bounds__(BCNF_WG) void k_pack_fold(BcnfLayout L, const float* __restrict__ P,
                                                        const float* __restrict__ Q, float* __restrict__ out,
                                                        const float* __restrict__ wf, const float* __restrict__ bf,
-                                                       int X, float* __restrict__ fold) {
+                                                       int X, float* __restrict__ fold, BcnfGatherArgs ga) {
   __shared__ __attribute__((aligned(16))) float smem[4 * 16 * NC16_MAX];
-  const int n_fold = L.NKp / 16 * FOLD_SPLIT, bx = blockIdx.x;
+  const int n_fold = L.NKp / 16 * FOLD_SPLIT;
+  int bx = blockIdx.x;
   if (bx < n_fold) {
     fold_body(L, P, wf, bf, X, fold, bx, smem);
     return;
   }
-  pack_body(L, P, Q, out, bx - n_fold, smem);
+  bx -= n_fold;
+  if (bx < ga.nwg) {
+    gather2_rows(ga.idx, ga.n, ga.rpw, ga.s0, ga.c0, ga.d0, ga.s1, ga.c1, ga.d1, ga.cursor, bx);
+    return;
+  }
+  pack_body(L, P, Q, out, bx - ga.nwg, smem);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1964,13 +1971,24 @@ int bcnf_fold_slab_bytes(const BcnfStackDesc* desc, int32_t in_features, int64_t
 
 int bcnf_pack_params_fold(const BcnfStackDesc* desc, const float* params, const float* qmats,
                           const float* feat_weight, const float* feat_bias, int32_t in_features, void* packed,
-                          float* fold, void* stream) {
+                          float* fold, const BcnfGather2* gather, void* stream) {
   BcnfLayout L;
   int rc = fold_setup(desc, in_features, &L);
   if (rc) return rc;
   if (!params || !packed || !fold || !feat_weight || (L.nb > 1 && !qmats)) return BCNF_ERR_ARG;
-  hipLaunchKernelGGL(k_pack_fold, dim3(L.NKp / 16 * FOLD_SPLIT + PACK_WG + 1), dim3(BCNF_WG), 0, (hipStream_t)stream, L, params,
-                     qmats, (float*)packed, feat_weight, feat_bias, (int)in_features, fold);
+  BcnfGatherArgs ga = {};
+  if (gather) {
+    const BcnfGather2& g = *gather;
+    if (g.n < 1 || g.cols0 < 1 || g.cols1 < 1 || !g.idx || !g.src0 || !g.dst0 || !g.src1 || !g.dst1)
+      return BCNF_ERR_ARG;
+    if (g.n * (int64_t)(g.cols0 + g.cols1) >= (1LL << 31)) return BCNF_ERR_UNSUPPORTED;
+    ga = BcnfGatherArgs{g.idx, (const long long*)g.cursor, g.src0, g.dst0, g.src1, g.dst1, (int)g.n, 0, g.cols0,
+                        g.cols1, 0};
+    gather2_plan(g.n, &ga.rpw, &ga.nwg);
+  }
+  const unsigned grid = (unsigned)(L.NKp / 16 * FOLD_SPLIT + ga.nwg + PACK_WG + 1);
+  hipLaunchKernelGGL(k_pack_fold, dim3(grid), dim3(BCNF_WG), 0, (hipStream_t)stream, L, params, qmats, (float*)packed,
+                     feat_weight, feat_bias, (int)in_features, fold, ga);
   return check_launch();
 }
 

@@ -301,43 +301,11 @@ __global__ __launch_bounds__(BCNF_WG) void k_wt_reduce(const float* __restrict__
 
 using bcnf_rt::launched;
 
-// dst0[r] = src0[idx[r]] (cols0 floats), dst1[r] = src1[idx[r]] (cols1 floats), one launch for both;
-// workgroup w copies rows [w * rpw, (w + 1) * rpw) (32-bit index math: n * (cols0 + cols1) < 2^31), each
-// thread GU elements per round with every index and data load issued before the stores. With
-// `cursor` != NULL the rows are idx[cursor[0] * n + r] (the cursor is advanced by a later launch).
-constexpr int GU = 8;
 __global__ __launch_bounds__(BCNF_WG) void k_gather2(const int64_t* __restrict__ idx, int n, int rpw,
                                                      const float* __restrict__ s0, int c0, float* __restrict__ d0,
                                                      const float* __restrict__ s1, int c1, float* __restrict__ d1,
                                                      const long long* __restrict__ cursor) {
-  if (cursor) idx += cursor[0] * n;
-  const int r0 = blockIdx.x * rpw, r1 = r0 + rpw < n ? r0 + rpw : n;
-  const int cw = c0 + c1, total = (r1 - r0) * cw;
-  for (int e0 = 0; e0 < total; e0 += GU * BCNF_WG) {
-    int r[GU], col[GU];
-    long long src[GU];
-    float v[GU];
-#pragma unroll
-    for (int u = 0; u < GU; ++u) {
-      int e = e0 + u * BCNF_WG + threadIdx.x;
-      e = e < total ? e : total - 1;
-      const int rr = e / cw;
-      r[u] = r0 + rr;
-      col[u] = e - rr * cw;
-      src[u] = idx[r[u]];
-    }
-#pragma unroll
-    for (int u = 0; u < GU; ++u)
-      v[u] = col[u] < c0 ? s0[src[u] * c0 + col[u]] : s1[src[u] * c1 + (col[u] - c0)];
-#pragma unroll
-    for (int u = 0; u < GU; ++u) {
-      if (e0 + u * BCNF_WG + (int)threadIdx.x >= total) continue;
-      if (col[u] < c0)
-        d0[r[u] * c0 + col[u]] = v[u];
-      else
-        d1[r[u] * c1 + (col[u] - c0)] = v[u];
-    }
-  }
+  gather2_rows(idx, n, rpw, s0, c0, d0, s1, c1, d1, cursor, blockIdx.x);
 }
 
 int make_tlist(int n, float* const* p, float* const* g, float* const* m, float* const* v, const int64_t* numel,
@@ -441,9 +409,9 @@ namespace {
 int gather_launch(const int64_t* idx, int64_t n, const float* src0, int32_t cols0, float* dst0, const float* src1,
                   int32_t cols1, float* dst1, const int64_t* cursor, void* stream) {
   if (n * (int64_t)(cols0 + cols1) >= (1LL << 31)) return BCNF_ERR_UNSUPPORTED;
-  const int nwg = n < 512 ? (int)n : 512;
-  const int rpw = (int)((n + nwg - 1) / nwg);
-  hipLaunchKernelGGL(k_gather2, dim3((unsigned)((n + rpw - 1) / rpw)), dim3(BCNF_WG), 0, (hipStream_t)stream, idx,
+  int rpw, nwg;
+  gather2_plan(n, &rpw, &nwg);
+  hipLaunchKernelGGL(k_gather2, dim3((unsigned)nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, idx,
                      (int)n, rpw, src0, cols0, dst0, src1, cols1, dst1, (const long long*)cursor);
   return launched();
 }

@@ -334,9 +334,10 @@ class FusedStack:
         out = ctypes.c_int64(0)
         return N.lib().bcnf_fold_bytes(self._pdesc, ctypes.c_int32(int(in_features)), ctypes.byref(out)) == N.OK
 
-    def launch_fold_nll_forward(self, y, x, wf, bf, training: bool, finalize: bool = True):
+    def launch_fold_nll_forward(self, y, x, wf, bf, training: bool, finalize: bool = True, gather=None):
         """launch_nll_forward with h = x Wf^T + bf never formed: the pack launch also folds the Linear into
-        the projection weights (Wc = W1h Wf, bc = b1 + W1h bf) and the projection runs on x."""
+        the projection weights (Wc = W1h Wf, bc = b1 + W1h bf) and the projection runs on x. gather (an
+        N.BcnfGather2 that fills y and x): the batch gather runs inside the pack launch."""
         self._check_device(y, x, wf, bf)
         B, X = x.shape
         if y.dim() != 2 or y.shape != (B, self.cfg.size):
@@ -350,7 +351,9 @@ class FusedStack:
         fold = torch.empty(N.query_i64(L.bcnf_fold_bytes, self._pdesc, ctypes.c_int32(X)) // 4, dtype=torch.float32,
                            device=dev)
         N.check(L.bcnf_pack_params_fold(self._pdesc, N.ptr(self.flat), N.ptr(self.qflat), N.ptr(wf), N.ptr(bf),
-                                        ctypes.c_int32(X), N.ptr(pk), N.ptr(fold), stream), "bcnf_pack_params_fold")
+                                        ctypes.c_int32(X), N.ptr(pk), N.ptr(fold),
+                                        None if gather is None else ctypes.byref(gather), stream),
+                "bcnf_pack_params_fold")
         z = torch.empty_like(y)
         ldj = torch.empty(B, dtype=torch.float32, device=dev)
         vals = torch.empty(3, dtype=torch.float32, device=dev)
@@ -448,7 +451,7 @@ class FusedStack:
         fold = torch.empty(N.query_i64(L.bcnf_fold_bytes, self._pdesc, ctypes.c_int32(X)) // 4, dtype=torch.float32,
                            device=dev)
         N.check(L.bcnf_pack_params_fold(self._pdesc, N.ptr(self.flat), N.ptr(self.qflat), N.ptr(wf), N.ptr(bf),
-                                        ctypes.c_int32(X), N.ptr(pk), N.ptr(fold), stream), "pack_fold")
+                                        ctypes.c_int32(X), N.ptr(pk), N.ptr(fold), None, stream), "pack_fold")
         sb = N.query_i64(L.bcnf_fold_slab_bytes, self._pdesc, ctypes.c_int32(X), ctypes.c_int64(B))
         slab = torch.empty(max(sb // 4, 1), dtype=torch.float32, device=dev)
         dparams = torch.empty_like(self.flat)
@@ -457,7 +460,7 @@ class FusedStack:
         rng = self.rng_state() if (training and self.cfg.dropout > 0.0) else None
         calls = {
             "pack": lambda: L.bcnf_pack_params_fold(self._pdesc, N.ptr(self.flat), N.ptr(self.qflat), N.ptr(wf),
-                                                    N.ptr(bf), ctypes.c_int32(X), N.ptr(pk), N.ptr(fold), stream),
+                                                    N.ptr(bf), ctypes.c_int32(X), N.ptr(pk), N.ptr(fold), None, stream),
             "forward": lambda: L.bcnf_fold_nll_forward(self._pdesc, N.ptr(pk), N.ptr(fold), ctypes.c_int32(X),
                                                        N.ptr(y), N.ptr(x), ldx, ctypes.c_int64(B), N.ptr(z),
                                                        N.ptr(ldj), ctypes.c_int32(int(training)), N.ptr(rng),
@@ -565,8 +568,8 @@ class _FoldNLL(torch.autograd.Function):
     (y, x, Wf, bf, flat_param); gradients for Wf, bf and flat_param (not for y or x)."""
 
     @staticmethod
-    def forward(ctx, y, x, wf, bf, flat_param, stack: FusedStack, training: bool, defer: bool):
-        z, _, vals, saved = stack.launch_fold_nll_forward(y, x, wf, bf, training, finalize=not defer)
+    def forward(ctx, y, x, wf, bf, flat_param, stack: FusedStack, training: bool, defer: bool, gather):
+        z, _, vals, saved = stack.launch_fold_nll_forward(y, x, wf, bf, training, finalize=not defer, gather=gather)
         ctx.stack = stack
         ctx.training = training
         ctx.saved = saved
@@ -582,11 +585,14 @@ class _FoldNLL(torch.autograd.Function):
                                                                ctx.saved, want_feat=need[2] or need[3],
                                                                finalize_into=vals if ctx.defer else None)
         return (None, None, dwf if need[2] else None, dbf if need[3] else None, dparams if need[4] else None,
-                None, None, None)
+                None, None, None, None)
 
 
-def stack_nll_fold(stack: FusedStack, y, x, wf, bf, training: bool, defer: bool = False):
-    """stack_nll(stack, y, x Wf^T + bf) without forming the features (see launch_fold_nll_forward)."""
+def stack_nll_fold(stack: FusedStack, y, x, wf, bf, training: bool, defer: bool = False, gather=None):
+    """stack_nll(stack, y, x Wf^T + bf) without forming the features (see launch_fold_nll_forward). gather: the
+    batch gather that fills y and x, run inside the pack launch (TrainStep); y and x are then its outputs."""
+    if gather is not None and not (y.is_contiguous() and x.stride(1) == 1):
+        raise ValueError("bcnf_amd: a deferred gather needs its own (contiguous) output buffers")
     y = y.contiguous()
     if x.stride(1) != 1 or x.stride(0) < x.shape[1]:
         x = x.contiguous()              # rows may be padded (ldx = stride(0) > X: TrainStep's zero-padded pool)
@@ -595,8 +601,8 @@ def stack_nll_fold(stack: FusedStack, y, x, wf, bf, training: bool, defer: bool 
     fp = stack.flat_param
     feat_grad = wf.requires_grad or (bf is not None and bf.requires_grad)
     if torch.is_grad_enabled() and (params_grad or feat_grad):
-        return _FoldNLL.apply(y, x, wf, bf, fp if params_grad else fp.detach(), stack, training, defer)
-    return stack.launch_fold_nll_forward(y, x, wf, bf, training)[2]
+        return _FoldNLL.apply(y, x, wf, bf, fp if params_grad else fp.detach(), stack, training, defer, gather)
+    return stack.launch_fold_nll_forward(y, x, wf, bf, training, gather=gather)[2]
 
 
 class _StackInverse(torch.autograd.Function):

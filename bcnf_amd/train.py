@@ -76,10 +76,11 @@ class TrainStep:
             self._hist = torch.zeros((1, 3), dtype=torch.float32, pin_memory=True)
 
     # ------------------------------------------------------------------ step pieces
-    def _forward_backward(self, y, traj):
+    def _forward_backward(self, y, traj, gather=None):
         self.opt.zero_grad(set_to_none=True)
         if self.fused_loss:
-            vals = self.model.nll_loss(y, traj, defer_reduction=True)   # reduced in the backward launch
+            # reduced in the backward launch; a deferred gather runs inside the pack launch
+            vals = self.model.nll_loss(y, traj, defer_reduction=True, gather=gather)
             if self._cot is None or self._cot.device != vals.device:
                 self._cot = torch.tensor([1.0, 0.0, 0.0], device=vals.device)
             torch.autograd.backward(vals, self._cot)      # loss.backward()
@@ -144,15 +145,17 @@ class TrainStep:
                 dist.broadcast(p.data, src=src, group=self.pg)
 
     # ------------------------------------------------------------------ eager / graph
-    def eager_step(self, y, traj):
-        vals = self._forward_backward(y, traj)
+    def eager_step(self, y, traj, gather=None):
+        vals = self._forward_backward(y, traj, gather)
         self._allreduce()
         self._update(vals)
         return vals
 
-    def _gather(self):
+    def _gather(self, defer: bool = False):
         """Pool rows of the current batch, both tensors in one native launch: the static index buffer, or
-        (epoch mode) batch `cursor` of the device-resident epoch order, the cursor advancing on the device."""
+        (epoch mode) batch `cursor` of the device-resident epoch order, the cursor advancing on the device.
+        defer=True returns (y, traj, spec): when the step takes the folded path, spec is the gather (not yet
+        launched) for the pack launch to run (bcnf_pack_params_fold), else None and the gather has run."""
         from bcnf_amd import _native as N
         py, pt = self._pool
         n = self._epoch[3] if self._epoch is not None else self._static[2].shape[0]
@@ -160,6 +163,14 @@ class TrainStep:
         t = torch.empty((n,) + tuple(pt.shape[1:]), dtype=pt.dtype, device=pt.device)
         cy = py[0].numel()
         ct = pt[0].numel()
+        if defer and self.fused_loss and self.fuse_gather and \
+                self.model._foldable_linear(y, (self._unpad(t),)) is not None:
+            epoch = self._epoch is not None
+            spec = N.BcnfGather2(idx=(self._epoch[0] if epoch else self._static[2]).data_ptr(),
+                                 cursor=self._epoch[1].data_ptr() if epoch else None, n=n,
+                                 src0=py.data_ptr(), cols0=cy, dst0=y.data_ptr(),
+                                 src1=pt.data_ptr(), cols1=ct, dst1=t.data_ptr())
+            return y, self._unpad(t), spec
         st = N.stream_handle(py.device)
         if self._epoch is not None:
             order, cursor = self._epoch[0], self._epoch[1]
@@ -168,6 +179,8 @@ class TrainStep:
         else:
             N.check(N.lib().bcnf_gather_rows2(N.ptr(self._static[2]), n, N.ptr(py), cy, N.ptr(y), N.ptr(pt), ct,
                                               N.ptr(t), st), "bcnf_gather_rows2")
+        if defer:
+            return y, self._unpad(t), None
         return y, self._unpad(t)
 
     def _unpad(self, t):
@@ -217,8 +230,9 @@ class TrainStep:
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 if indexed:
-                    sy, st = self._gather()
-                self.eager_step(sy, st)
+                    self.eager_step(*self._gather(defer=True))
+                else:
+                    self.eager_step(sy, st)
             self._restore(snap)
         torch.cuda.current_stream().wait_stream(s)
         self.opt.zero_grad(set_to_none=True)
@@ -226,9 +240,10 @@ class TrainStep:
         # them after a stream sync, without a device-to-host copy node
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1):
+            spec = None
             if indexed:
-                sy, st = self._gather()
-            vals = self._forward_backward(sy, st)
+                sy, st, spec = self._gather(defer=True)
+            vals = self._forward_backward(sy, st, spec)
             if self.world == 1:
                 self._update(vals)
             else:
@@ -394,6 +409,8 @@ class TrainStep:
     # (measured, r01j), so run_epoch replays `epoch_unroll` device-driven steps (cursor, RNG offset, Adam step,
     # history row all advance on the device) per launch and the remainder one by one.
     epoch_unroll = 8
+    # The captured step runs the batch gather inside the folded path's pack launch (one launch fewer).
+    fuse_gather = True
 
     def _multi_graph(self):
         if self._multi is None or self._multi[1] != self.epoch_unroll:
@@ -401,8 +418,7 @@ class TrainStep:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 for _ in range(k):
-                    sy, st = self._gather()
-                    vals = self._forward_backward(sy, st)
+                    vals = self._forward_backward(*self._gather(defer=True))
                     self._update(vals)
             self._multi = (g, k, [p.grad for p in self.params])
             self._bind(self._single_grads)

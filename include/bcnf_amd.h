@@ -130,9 +130,22 @@ int bcnf_backward_tail(const BcnfStackDesc* desc, const void* packed, const void
  * padded pool, bcnf_amd/train.py); the padding columns are never used. */
 int bcnf_fold_bytes(const BcnfStackDesc* desc, int32_t in_features, int64_t* bytes);
 int bcnf_fold_slab_bytes(const BcnfStackDesc* desc, int32_t in_features, int64_t batch, int64_t* bytes);
+/* A batch gather to run inside bcnf_pack_params_fold's launch (the pack does not read the batch, so the two are
+ * independent): the arguments of bcnf_gather_rows2 (cursor = NULL) or bcnf_gather_batch (idx = the epoch order). */
+typedef struct BcnfGather2 {
+  const int64_t* idx;
+  const int64_t* cursor;
+  int64_t n;
+  const float* src0;
+  int32_t cols0;
+  float* dst0;
+  const float* src1;
+  int32_t cols1;
+  float* dst1;
+} BcnfGather2;
 int bcnf_pack_params_fold(const BcnfStackDesc* desc, const float* params, const float* qmats,
                           const float* feat_weight, const float* feat_bias, int32_t in_features, void* packed,
-                          float* fold, void* stream);
+                          float* fold, const BcnfGather2* gather /* nullable */, void* stream);
 int bcnf_fold_nll_forward(const BcnfStackDesc* desc, const void* packed, const float* fold, int32_t in_features,
                           const float* y, const float* x, int32_t ldx, int64_t batch, float* z, float* ldj,
                           int32_t training,

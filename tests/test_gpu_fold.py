@@ -175,3 +175,32 @@ def test_trainstep_pads_fold_pool(g1):
     st2 = TrainStep(m, lr=2e-4, capture=False)
     st2.set_pool(torch.randn(64, 19).to(DEV), torch.randn(64, 30, 3).to(DEV))
     assert st2._cond_shape is None and st2._pool[1].shape == (64, 30, 3)
+
+
+@pytest.mark.parametrize("epoch", [False, True])
+def test_gather_inside_pack_launch_is_exact(g1, epoch):
+    """The captured step's batch gather run inside the pack launch (BcnfGather2) == the separate gather launch:
+    logged values, parameters and gradients bit for bit (index buffer and epoch-cursor forms)."""
+    from bcnf_amd.train import TrainStep
+    gen = torch.Generator().manual_seed(31)
+    py = torch.randn(600, 19, generator=gen).to(DEV)
+    pt = torch.randn(600, 30, 3, generator=gen).to(DEV)
+    order = torch.randperm(600, generator=gen)[:3 * 200].to(DEV)
+    out = []
+    for fuse in (False, True):
+        m = _model(FC_SMALL_CFG, golden_sd(g1), train=True)
+        m.fused.set_seed(3)
+        st = TrainStep(m, lr=2e-4)
+        st.fuse_gather = fuse
+        st.epoch_unroll = 2
+        st.set_pool(py, pt)
+        if epoch:
+            st.set_epoch(order, 200)
+            vals = st.run_epoch()
+        else:
+            vals = [st.step_indexed(order[i * 200:(i + 1) * 200]) for i in range(3)]
+        out.append((vals, [p.detach().clone() for p in st.params], [p.grad.clone() for p in st.params]))
+    (v0, p0, g0), (v1, p1, g1_) = out
+    assert v0 == v1
+    for a, b in zip(p0 + g0, p1 + g1_):
+        assert torch.equal(a, b)

@@ -52,7 +52,7 @@ def main():
     calls = {
         "pack": lambda: L.bcnf_pack_params(st._pdesc, N.ptr(st.flat), N.ptr(st.qflat), N.ptr(pk_h), stream),
         "pack+fold": lambda: L.bcnf_pack_params_fold(st._pdesc, N.ptr(st.flat), N.ptr(st.qflat), N.ptr(wf), N.ptr(bf),
-                                                     ctypes.c_int32(X), N.ptr(pk), N.ptr(fold), stream),
+                                                     ctypes.c_int32(X), N.ptr(pk), N.ptr(fold), None, stream),
         "tail": lambda: L.bcnf_backward_tail(st._pdesc, N.ptr(pk_h), N.ptr(slab_h), N.ptr(h), N.ptr(ws_h),
                                              ctypes.c_int64(B), ctypes.c_int32(1), N.ptr(dh), N.ptr(dp), stream),
         "fold tail": lambda: L.bcnf_fold_backward_tail(st._pdesc, N.ptr(pk), N.ptr(slab), N.ptr(x), ctypes.c_int32(X),
