@@ -229,14 +229,15 @@ __device__ float rec_b(const BcnfLayout& L, const float* P, const float* Q, int 
   return 0.f;
 }
 
-// Grid: PACK_WG record workgroups (grid-stride over every packed float) + 1 workgroup that computes
-// the ActNorm log|det| constant  sum_k sum_i log|scale_k,i|  (cnf.py:350) in a fixed order.
-constexpr int PACK_WG = 512;
+// Grid: 1 workgroup that computes the ActNorm log|det| constant  sum_k sum_i log|scale_k,i|  (cnf.py:350) in a
+// fixed order, then npw record workgroups (grid-stride over every packed float; pack_wgs gives every thread about
+// one element, so the launch is one load round trip, not a chain of them).
+constexpr int PACK_WG_MAX = 4096;
 
 __device__ __forceinline__ void pack_body(const BcnfLayout& L, const float* __restrict__ P,
-                                          const float* __restrict__ Q, float* __restrict__ out, int bx,
+                                          const float* __restrict__ Q, float* __restrict__ out, int bx, int npw,
                                           float* __restrict__ part) {
-  if (bx == PACK_WG) {
+  if (bx == 0) {
     float acc = 0.f;
     if (L.act_norm) {
       const int n = (L.nb - 1) * L.D;
@@ -259,7 +260,7 @@ __device__ __forceinline__ void pack_body(const BcnfLayout& L, const float* __re
   const int n_pb = L.nb * 16 * L.RB;
   const int n_w = L.Cp * L.NKp;                       // each of W1hC, W1hR
   const int total = 2 * n_pf + n_pb + 2 * n_w + L.NKp;
-  for (int i = bx * BCNF_WG + threadIdx.x; i < total; i += PACK_WG * BCNF_WG) {
+  for (int i = (bx - 1) * BCNF_WG + threadIdx.x; i < total; i += npw * BCNF_WG) {
     float v;
     long long o;
     if (i < n_pf) {                                   // PF
@@ -296,9 +297,16 @@ __device__ __forceinline__ void pack_body(const BcnfLayout& L, const float* __re
 }
 
 __global__ __launch_bounds__(BCNF_WG) void k_pack(BcnfLayout L, const float* __restrict__ P,
-                                                  const float* __restrict__ Q, float* __restrict__ out) {
+                                                  const float* __restrict__ Q, float* __restrict__ out, int npw) {
   __shared__ float part[BCNF_WG];
-  pack_body(L, P, Q, out, blockIdx.x, part);
+  pack_body(L, P, Q, out, blockIdx.x, npw, part);
+}
+
+// Record workgroups of a pack launch (the log-det workgroup not included).
+int pack_wgs(const BcnfLayout& L) {
+  const long long total = 2LL * L.nb * 16 * L.RF + (long long)L.nb * 16 * L.RB + 2LL * L.Cp * L.NKp + L.NKp;
+  const long long w = (total + BCNF_WG - 1) / BCNF_WG;
+  return (int)(w < PACK_WG_MAX ? (w > 0 ? w : 1) : PACK_WG_MAX);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -374,7 +382,7 @@ __device__ __forceinline__ void fold_body(const BcnfLayout& L, const float* __re
 __global__ __launch_bounds__(BCNF_WG) void k_pack_fold(BcnfLayout L, const float* __restrict__ P,
                                                        const float* __restrict__ Q, float* __restrict__ out,
                                                        const float* __restrict__ wf, const float* __restrict__ bf,
-                                                       int X, float* __restrict__ fold, BcnfGatherArgs ga) {
+                                                       int X, float* __restrict__ fold, BcnfGatherArgs ga, int npw) {
   __shared__ __attribute__((aligned(16))) float smem[4 * 16 * NC16_MAX];
   const int n_fold = L.NKp / 16 * FOLD_SPLIT;
   int bx = blockIdx.x;
@@ -387,7 +395,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_pack_fold(BcnfLayout L, const float
     gather2_rows(ga.idx, ga.n, ga.rpw, ga.s0, ga.c0, ga.d0, ga.s1, ga.c1, ga.d1, ga.cursor, bx);
     return;
   }
-  pack_body(L, P, Q, out, bx - ga.nwg, smem);
+  pack_body(L, P, Q, out, bx - ga.nwg, npw, smem);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -718,12 +726,12 @@ __global__ __launch_bounds__(BCNF_WG) void k_gx_reduce(long long total, const fl
   if (i >= total) return;
   float acc = 0.f;
   int s = 0;
-  for (; s + 8 <= splits; s += 8) {
-    float v[8];
+  for (; s + 16 <= splits; s += 16) {               // 16 loads in flight per lane (32 splits at B = 4096)
+    float v[16];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) v[t] = work[(long long)(s + t) * total + i];
+    for (int t = 0; t < 16; ++t) v[t] = work[(long long)(s + t) * total + i];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) acc += v[t];
+    for (int t = 0; t < 16; ++t) acc += v[t];
   }
   for (; s < splits; ++s) acc += work[(long long)s * total + i];
   gx[i] = acc;
@@ -1855,7 +1863,8 @@ int bcnf_pack_params(const BcnfStackDesc* desc, const float* params, const float
   if (!layout_supported(L, desc)) return BCNF_ERR_UNSUPPORTED;
   if (!params || !packed || (L.nb > 1 && !qmats)) return BCNF_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_pack, dim3(PACK_WG + 1), dim3(BCNF_WG), 0, st, L, params, qmats, (float*)packed);
+  const int npw = pack_wgs(L);
+  hipLaunchKernelGGL(k_pack, dim3(npw + 1), dim3(BCNF_WG), 0, st, L, params, qmats, (float*)packed, npw);
   return check_launch();
 }
 
@@ -1986,9 +1995,10 @@ int bcnf_pack_params_fold(const BcnfStackDesc* desc, const float* params, const 
                         g.cols1, 0};
     gather2_plan(g.n, &ga.rpw, &ga.nwg);
   }
-  const unsigned grid = (unsigned)(L.NKp / 16 * FOLD_SPLIT + ga.nwg + PACK_WG + 1);
+  const int npw = pack_wgs(L);
+  const unsigned grid = (unsigned)(L.NKp / 16 * FOLD_SPLIT + ga.nwg + npw + 1);
   hipLaunchKernelGGL(k_pack_fold, dim3(grid), dim3(BCNF_WG), 0, (hipStream_t)stream, L, params, qmats, (float*)packed,
-                     feat_weight, feat_bias, (int)in_features, fold, ga);
+                     feat_weight, feat_bias, (int)in_features, fold, ga, npw);
   return check_launch();
 }
 

@@ -58,36 +58,46 @@ __global__ __launch_bounds__(BCNF_WG) void k_adam(TList T, const float* __restri
                                                   const int32_t* __restrict__ guard) {
   __shared__ float red[BCNF_WG];
   __shared__ float sc[2];
+  // every operand load is issued first: none depends on the guard, the step count or the bias corrections,
+  // so their round trip overlaps the scalar loads and thread 0's double pow
+  const long long total = T.start[T.n];
+  float g[EPT], p[EPT], m[EPT], v[EPT];
+  int t[EPT];
+  long long o[EPT];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    long long i = (long long)blockIdx.x * CHUNK + e * BCNF_WG + threadIdx.x;
+    i = i < total ? i : total - 1;
+    t[e] = find_tensor(T, i);
+    o[e] = i - T.start[t[e]];
+    g[e] = T.g[t[e]][o[e]];
+    p[e] = T.p[t[e]][o[e]];
+    m[e] = T.m[t[e]][o[e]];
+    v[e] = T.v[t[e]][o[e]];
+  }
   if (guard && guard[BCNF_GUARD_HALTED]) return;   // a halted step (see nll_finalize) leaves all state
   const float st = step[0] + 1.0f;
-  if (threadIdx.x == 0) {                          // double pow once per workgroup, not per thread
-    sc[0] = (float)(lr / (1.0 - pow(b1d, (double)st)));
-    sc[1] = (float)sqrt(1.0 - pow(b2d, (double)st));
-  }
+  // the two double pows once per workgroup, on two waves side by side
+  if (threadIdx.x == 0) sc[0] = (float)(lr / (1.0 - pow(b1d, (double)st)));
+  if (threadIdx.x == 64) sc[1] = (float)sqrt(1.0 - pow(b2d, (double)st));
   __syncthreads();
   const float step_size = sc[0], bc2s = sc[1];
   const float omb1 = (float)(1.0 - b1d), omb2 = (float)(1.0 - b2d);
   const float b2 = (float)b2d, eps = (float)epsd, wd = (float)wdd;
-  const long long total = T.start[T.n];
   float ss = 0.f;
 #pragma unroll
   for (int e = 0; e < EPT; ++e) {
     const long long i = (long long)blockIdx.x * CHUNK + e * BCNF_WG + threadIdx.x;
     if (i < total) {
-      const int t = find_tensor(T, i);
-      const long long o = i - T.start[t];
-      float g = T.g[t][o];
-      float p = T.p[t][o];
-      ss = fmaf(g, g, ss);
-      if (wd != 0.f) g = fmaf(wd, p, g);
-      float m = T.m[t][o];
-      m = m + omb1 * (g - m);                       // lerp, |weight| < 0.5 branch
-      const float v = T.v[t][o] * b2 + omb2 * (g * g);
-      const float denom = sqrtf(v) / bc2s + eps;
-      p = p + (-step_size) * (m / denom);
-      T.m[t][o] = m;
-      T.v[t][o] = v;
-      T.p[t][o] = p;
+      float gg = g[e];
+      ss = fmaf(gg, gg, ss);
+      if (wd != 0.f) gg = fmaf(wd, p[e], gg);
+      const float mm = m[e] + omb1 * (gg - m[e]);   // lerp, |weight| < 0.5 branch
+      const float vv = v[e] * b2 + omb2 * (gg * gg);
+      const float denom = sqrtf(vv) / bc2s + eps;
+      T.m[t[e]][o[e]] = mm;
+      T.v[t[e]][o[e]] = vv;
+      T.p[t[e]][o[e]] = p[e] + (-step_size) * (mm / denom);
     }
   }
   const float s = wg_sum(ss, red);
@@ -132,19 +142,28 @@ __global__ __launch_bounds__(BCNF_WG) void k_clip(TList T, const float* __restri
                                                   long long n_batches, const float* __restrict__ log_values,
                                                   float* log_history, const int32_t* __restrict__ guard) {
   __shared__ float red[BCNF_WG];
+  // the gradient loads go out first, beside the partials' (the scaling needs the total norm, not the loads)
+  const long long total = T.start[T.n];
+  float g[EPT];
+  int t[EPT];
+  long long o[EPT];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    long long i = (long long)blockIdx.x * CHUNK + e * BCNF_WG + threadIdx.x;
+    i = i < total ? i : total - 1;
+    t[e] = find_tensor(T, i);
+    o[e] = i - T.start[t[e]];
+    g[e] = T.g[t[e]][o[e]];
+  }
   if (guard && guard[BCNF_GUARD_HALTED]) return;
   float acc = 0.f;
   for (int i = threadIdx.x; i < nparts; i += BCNF_WG) acc += part[i];
   const float tot = sqrtf(wg_sum(acc, red));
   const float coef = fminf(max_norm / (tot + 1e-6f), 1.0f);
-  const long long total = T.start[T.n];
 #pragma unroll
   for (int e = 0; e < EPT; ++e) {
     const long long i = (long long)blockIdx.x * CHUNK + e * BCNF_WG + threadIdx.x;
-    if (i < total) {
-      const int t = find_tensor(T, i);
-      T.g[t][i - T.start[t]] *= coef;
-    }
+    if (i < total) T.g[t[e]][o[e]] = g[e] * coef;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (norm_out) norm_out[0] = tot;
