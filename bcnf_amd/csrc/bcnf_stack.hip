@@ -615,60 +615,83 @@ __global__ __launch_bounds__(BCNF_WG) void k_dh(BcnfLayout L, const float* __res
 
 // dW1h split-K partials: 64 kj (4 blocks, one per wave) x all columns over one split of KC rows.
 // grid = (ceil(nb/4), splits); work[s][k][16][Cp]
-template <bool VEC>
+template <bool VEC, int BPW = 4>
 __device__ __forceinline__ void dw1h_body(const BcnfLayout& L, const float* __restrict__ d1, const float* __restrict__ h,
                                           long long B, int rows_per_split, float* __restrict__ work, int bx, int by,
                                           float* __restrict__ smem, int ones = -1) {
   const int hs = bstride16(L.Cp);
-  float* As = smem;                    // [64][KCP] (kj, b)
-  float* Bs = smem + 64 * KCP;         // [KC][hs]  (b, c)
+  // BPW blocks per workgroup: 4 (one per wave, every column tile) or 2 (two waves per block, half the column
+  // tiles each: twice the workgroups, LDS for two resident per CU)
+  float* As = smem;                    // [16 BPW][KCP] (kj, b)
+  float* Bs = smem + 16 * BPW * KCP;   // [KC][hs]  (b, c)
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lq = l >> 4;
-  const int k0 = bx * 4, s = by;
+  const int k0 = bx * BPW, s = by;
   const long long m0 = (long long)s * rows_per_split;
   long long m1 = m0 + rows_per_split;
   if (m1 > B) m1 = B;
   const int NC16 = L.Cp >> 4;
   {
-    const int row = tid >> 1, j8 = (tid & 1) * 8;     // A: 4 blocks x [KC rows][16], transposed into [kj][b]
+    // every global load of the tile goes out before the first LDS store (one round trip, not three): A = the 4
+    // blocks' D1 rows [KC][16] (transposed into [kj][b]), B = the split's h rows [KC][Cp] in 64-row halves (a
+    // second K-chunk of columns only when Cp > KC)
+    const int row = tid >> 1, j8 = (tid & 1) * 8;
     const long long b = m0 + row;
     const bool ok = b < m1;
     const long long bb = ok ? b : m1 - 1;
+    floatx4 va[2 * BPW];
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
+    for (int kk = 0; kk < BPW; ++kk) {
       const int k = k0 + kk < L.nb ? k0 + kk : L.nb - 1;
       const floatx4* src = reinterpret_cast<const floatx4*>(d1 + ((long long)k * B + bb) * 16 + j8);
+      va[2 * kk] = src[0];
+      va[2 * kk + 1] = src[1];
+    }
+    floatx4 rv[2][8];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) load_rows64<VEC>(h, m1, L.C, L.ldh, m0 + 64 * half, 0, rv[half], ones);
+#pragma unroll
+    for (int kk = 0; kk < BPW; ++kk) {
       const float m = (ok && k0 + kk < L.nb) ? 1.f : 0.f;
-      const floatx4 v0 = src[0] * m, v1 = src[1] * m;
+      const floatx4 v0 = va[2 * kk] * m, v1 = va[2 * kk + 1] * m;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         As[(kk * 16 + j8 + q) * KCP + row] = v0[q];
         As[(kk * 16 + j8 + 4 + q) * KCP + row] = v1[q];
       }
     }
-    // B: the split's h rows [KC][Cp] (zero-padded), in 64-row halves
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
-      for (int c0 = 0; c0 < L.Cp; c0 += KC) {
-        floatx4 rv[8];
-        load_rows64<VEC>(h, m1, L.C, L.ldh, m0 + 64 * half, c0, rv, ones);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int i4 = tid + 256 * e, r = 64 * half + (i4 >> 5), col = (i4 & 31) * 4;
+        if (col < L.Cp) *reinterpret_cast<floatx4*>(Bs + r * hs + col) = rv[half][e];
+      }
+    }
+    for (int c0 = KC; c0 < L.Cp; c0 += KC) {           // Cp > 128 only
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        load_rows64<VEC>(h, m1, L.C, L.ldh, m0 + 64 * half, c0, rv[half], ones);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const int i4 = tid + 256 * e, row = 64 * half + (i4 >> 5), col = c0 + (i4 & 31) * 4;
-          if (col < L.Cp) *reinterpret_cast<floatx4*>(Bs + row * hs + col) = rv[e];
+          const int i4 = tid + 256 * e, r = 64 * half + (i4 >> 5), col = c0 + (i4 & 31) * 4;
+          if (col < L.Cp) *reinterpret_cast<floatx4*>(Bs + r * hs + col) = rv[half][e];
         }
       }
     }
   }
   __syncthreads();
-  const int k = k0 + wave;
+  const int kw = BPW == 4 ? wave : wave >> 1;
+  const int k = k0 + kw;
+  const int nh = BPW == 4 ? NC16 : (NC16 + 1) >> 1;
+  const int n_lo = BPW == 4 ? 0 : (wave & 1) * nh, n_hi = min(NC16, n_lo + nh);
   float* o = work + (((long long)s * L.nb + (k < L.nb ? k : 0)) * 16) * L.Cp;
-  for (int n = 0; n < NC16; ++n) {
+  for (int n = n_lo; n < n_hi; ++n) {
     floatx4 acc = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     for (int t0 = 0; t0 < KC / 4; t0 += 8) {            // LDS reads of 8 steps, then 8 MFMAs (2 chains)
       float a[8], bv[8];
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
-        a[t] = As[(16 * wave + lr) * KCP + 4 * (t0 + t) + lq];
+        a[t] = As[(16 * kw + lr) * KCP + 4 * (t0 + t) + lq];
         bv[t] = Bs[(4 * (t0 + t) + lq) * hs + 16 * n + lr];
       }
 #pragma unroll
@@ -695,7 +718,18 @@ __global__ __launch_bounds__(BCNF_WG) void k_dw1h(BcnfLayout L, const float* __r
 
 size_t hp_lds_bytes() { return sizeof(float) * (size_t)(64 * KCP + KC * BNS); }
 size_t dh_lds_bytes() { return sizeof(float) * (size_t)(64 * KCP + KC * 16); }
-size_t dw1h_lds_bytes(const BcnfLayout& L) { return sizeof(float) * (size_t)(64 * KCP + KC * bstride16(L.Cp)); }
+size_t dw1h_lds_bytes(const BcnfLayout& L, int bpw = 4) {
+  return sizeof(float) * (size_t)(16 * bpw * KCP + KC * bstride16(L.Cp));
+}
+
+// Folded path, first launch of the backward tail: the split-K D1^T [x | 1] alone, two blocks per workgroup.
+template <bool VEC>
+__global__ __launch_bounds__(BCNF_WG) void k_fold_splitk(BcnfLayout F, const float* __restrict__ d1,
+                                                         const float* __restrict__ x, long long B, int rows_per_split,
+                                                         float* __restrict__ work, int gx_dw, int ones) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  dw1h_body<VEC, 2>(F, d1, x, B, rows_per_split, work, blockIdx.x % gx_dw, blockIdx.x / gx_dw, smem, ones);
+}
 
 __global__ __launch_bounds__(BCNF_WG) void k_dw1h_reduce(BcnfLayout L, const float* __restrict__ work, int splits,
                                                          float* __restrict__ dparams) {
@@ -720,9 +754,8 @@ __global__ __launch_bounds__(BCNF_WG) void k_dw1h_reduce(BcnfLayout L, const flo
 }
 
 // Folded path: Gx[kj][xc] = sum of the split-K partials work[s][kj][xc] (fixed order), dense [nb*16][Xp].
-__global__ __launch_bounds__(BCNF_WG) void k_gx_reduce(long long total, const float* __restrict__ work, int splits,
-                                                       float* __restrict__ gx) {
-  const long long i = (long long)blockIdx.x * BCNF_WG + threadIdx.x;
+__device__ __forceinline__ void gx_reduce_body(long long total, const float* __restrict__ work, int splits,
+                                               float* __restrict__ gx, long long i) {
   if (i >= total) return;
   float acc = 0.f;
   int s = 0;
@@ -1586,6 +1619,22 @@ __global__ __launch_bounds__(BCNF_WG) void k_bwd_tail(BcnfLayout L, BcnfLayout L
   dw1h_body<VEC>(Lw, d1, h, B, rows_per_split, work, i % G.gx_dw, i / G.gx_dw, smem, G.ones);
 }
 
+// Folded path, second launch of the backward tail: the Gx reduce (latency-bound, 6 MB) placed first, then the
+// slab reduce (HBM-bound, 75 MB at B = 4096), so the former hides under the latter; the split-K that produces
+// the Gx partials ran alone in the launch before (the two roles in one launch did not overlap: 28 us vs 13 + 10).
+__global__ __launch_bounds__(BCNF_WG) void k_red_gx(BcnfLayout L, long long total, const float* __restrict__ work,
+                                                    int splits, float* __restrict__ gx, int n_gx,
+                                                    const float* __restrict__ slab, long long stride, int nwg,
+                                                    float* __restrict__ dparams) {
+  __shared__ __attribute__((aligned(16))) float smem[RED_G * RED_O4 * 4];
+  const int bx = blockIdx.x;
+  if (bx < n_gx) {
+    gx_reduce_body(total, work, splits, gx, (long long)bx * BCNF_WG + threadIdx.x);
+    return;
+  }
+  reduce_body(L, slab, stride, nwg, dparams, bx - n_gx, smem);
+}
+
 // ------------------------------------------------------------------------------------------------
 // Launch helpers
 // ------------------------------------------------------------------------------------------------
@@ -2033,27 +2082,24 @@ int bcnf_fold_backward_tail(const BcnfStackDesc* desc, const void* packed, const
   float* gx = work + w1h_work_floats(F, batch);
   const int rps = w1h_rows_per_split(batch);
   const long long splits = w1h_splits(batch);
-  TailGrid G;
-  G.gx_dh = 1;
-  G.n_dh = 0;
-  G.n_red = (int)((S / 4 + RED_O4 - 1) / RED_O4);
-  G.gx_dw = (L.nb + 3) / 4;
-  G.ones = in_features;
-  const dim3 grid((unsigned)(G.n_red + (long long)G.gx_dw * splits));
-  size_t lds = dw1h_lds_bytes(F);
+  const int n_red = (int)((S / 4 + RED_O4 - 1) / RED_O4);
+  const int gx_dw = (L.nb + 1) / 2;
+  const dim3 grid((unsigned)((long long)gx_dw * splits));
+  size_t lds = dw1h_lds_bytes(F, 2);
   if (vec_rows(F, x)) {
-    if ((rc = launch_lds(k_bwd_tail<true>, lds))) return rc;
-    hipLaunchKernelGGL(k_bwd_tail<true>, grid, dim3(BCNF_WG), lds, st, L, F, G, (const float*)packed, d1, x,
-                       (long long)batch, (float*)nullptr, (const float*)slab, S, nwg, dparams, rps, work);
+    if ((rc = launch_lds(k_fold_splitk<true>, lds))) return rc;
+    hipLaunchKernelGGL(k_fold_splitk<true>, grid, dim3(BCNF_WG), lds, st, F, d1, x, (long long)batch, rps, work, gx_dw,
+                       (int)in_features);
   } else {
-    if ((rc = launch_lds(k_bwd_tail<false>, lds))) return rc;
-    hipLaunchKernelGGL(k_bwd_tail<false>, grid, dim3(BCNF_WG), lds, st, L, F, G, (const float*)packed, d1, x,
-                       (long long)batch, (float*)nullptr, (const float*)slab, S, nwg, dparams, rps, work);
+    if ((rc = launch_lds(k_fold_splitk<false>, lds))) return rc;
+    hipLaunchKernelGGL(k_fold_splitk<false>, grid, dim3(BCNF_WG), lds, st, F, d1, x, (long long)batch, rps, work, gx_dw,
+                       (int)in_features);
   }
   if ((rc = check_launch())) return rc;
   const long long total = (long long)L.nb * 16 * F.Cp;
-  hipLaunchKernelGGL(k_gx_reduce, dim3((unsigned)((total + BCNF_WG - 1) / BCNF_WG)), dim3(BCNF_WG), 0, st, total,
-                     (const float*)work, (int)splits, gx);
+  const int n_gx = (int)((total + BCNF_WG - 1) / BCNF_WG);
+  hipLaunchKernelGGL(k_red_gx, dim3((unsigned)(n_gx + n_red)), dim3(BCNF_WG), 0, st, L, total, (const float*)work,
+                     (int)splits, gx, n_gx, (const float*)slab, S, nwg, dparams);
   if ((rc = check_launch())) return rc;
   const int n_fin = (L.nb + (F.Cp >> 4)) * (L.Cp >> 4);
   hipLaunchKernelGGL(k_fold_finish, dim3((unsigned)n_fin), dim3(BCNF_WG), 0, st, L, (const float*)packed,
