@@ -26,7 +26,8 @@ EXPORTS = (
     "bcnf_stack_supported", "bcnf_param_count", "bcnf_packed_bytes", "bcnf_workspace_bytes",
     "bcnf_slab_bytes", "bcnf_pack_params", "bcnf_stack_forward", "bcnf_stack_backward",
     "bcnf_stack_inverse", "bcnf_grad_reduce", "bcnf_status_string", "bcnf_last_hip_error",
-    "bcnf_nll_forward", "bcnf_nll_backward", "bcnf_grad_partials", "bcnf_adam_step", "bcnf_grad_sumsq",
+    "bcnf_nll_forward", "bcnf_nll_backward", "bcnf_grad_partials", "bcnf_adam_step", "bcnf_adam_step_bookkeep",
+    "bcnf_grad_sumsq",
     "bcnf_clip_grad_norm", "bcnf_linear_forward", "bcnf_linear_work_bytes", "bcnf_linear_backward",
     "bcnf_inverse_scratch_bytes", "bcnf_stack_dh", "bcnf_backward_tail", "bcnf_gather_rows2",
     "bcnf_gather_batch", "bcnf_advance_counters", "bcnf_fold_bytes", "bcnf_fold_slab_bytes",
@@ -123,6 +124,9 @@ def _bind(lib):
         "bcnf_grad_partials": (_i64, [_i64]),
         "bcnf_adam_step": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double,
                                   ctypes.c_double, ctypes.c_double, ctypes.c_double, _vp, _i32, _vp, _vp]),
+        "bcnf_adam_step_bookkeep": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double,
+                                           ctypes.c_double, ctypes.c_double, ctypes.c_double, _vp, _i64, _vp, _vp,
+                                           _vp, _vp, _vp]),
         "bcnf_grad_sumsq": (_i32, [_i32, _vp, _vp, _vp, _vp]),
         "bcnf_clip_grad_norm": (_i32, [_i32, _vp, _vp, _vp, ctypes.c_float, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                        _vp]),

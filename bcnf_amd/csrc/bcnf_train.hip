@@ -53,9 +53,37 @@ __device__ __forceinline__ float wg_sum(float v, float* red) {
 //   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
 // Hyper-parameters arrive as doubles (Python floats) and every scalar is derived in double, then
 // rounded once, as torch does (1 - beta2 in fp32 from 0.999f would be off by 1e-5 relative).
+// End-of-step bookkeeping carried by the Adam launch (bcnf_adam_step_bookkeep): done by its last workgroup.
+struct AdamBook {
+  float* step;                  // step count to advance (the kernel's own `step` operand)
+  long long* cursor;            // epoch cursor (nullable) and its modulo
+  long long n_batches;
+  const float* log_values;      // logged values -> log_history[3 * cursor] (nullable)
+  float* log_history;
+  int* done;                    // workgroups finished; 0 between launches (the last one resets it); NULL: off
+};
+
+__device__ __forceinline__ void store_log(const float* log_values, float* log_history, const long long* cursor) {
+  if (!log_values || !log_history) return;   // host memory: system-scope stores, read after a sync
+  float* dst = log_history + 3 * (cursor ? cursor[0] : 0LL);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) __hip_atomic_store(dst + i, log_values[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __threadfence_system();
+}
+
+// End-of-step bookkeeping by one thread of a LATER launch (every reader of these counters is done):
+// the Adam step count (torch keeps it as a float tensor) and an epoch cursor.
+__device__ __forceinline__ void advance_counters(float* step, long long* cursor, long long n_batches) {
+  if (step) step[0] += 1.0f;
+  if (cursor) {
+    const long long c = cursor[0] + 1;
+    cursor[0] = c < n_batches ? c : 0;
+  }
+}
+
 __global__ __launch_bounds__(BCNF_WG) void k_adam(TList T, const float* __restrict__ step, double lr, double b1d,
                                                   double b2d, double epsd, double wdd, float* __restrict__ part,
-                                                  const int32_t* __restrict__ guard) {
+                                                  const int32_t* __restrict__ guard, AdamBook bk) {
   __shared__ float red[BCNF_WG];
   __shared__ float sc[2];
   // every operand load is issued first: none depends on the guard, the step count or the bias corrections,
@@ -76,6 +104,9 @@ __global__ __launch_bounds__(BCNF_WG) void k_adam(TList T, const float* __restri
     v[e] = T.v[t[e]][o[e]];
   }
   if (guard && guard[BCNF_GUARD_HALTED]) return;   // a halted step (see nll_finalize) leaves all state
+  // bookkeeping: the logged values go out from workgroup 0 at the start (it reads the cursor before its own
+  // arrival below, hence before the last workgroup advances it), off the launch's critical path
+  if (bk.done && blockIdx.x == 0 && threadIdx.x == 0) store_log(bk.log_values, bk.log_history, bk.cursor);
   const float st = step[0] + 1.0f;
   // the two double pows once per workgroup, on two waves side by side
   if (threadIdx.x == 0) sc[0] = (float)(lr / (1.0 - pow(b1d, (double)st)));
@@ -102,15 +133,15 @@ __global__ __launch_bounds__(BCNF_WG) void k_adam(TList T, const float* __restri
   }
   const float s = wg_sum(ss, red);
   if (threadIdx.x == 0 && part) part[blockIdx.x] = s;
-}
-
-// End-of-step bookkeeping by one thread of a LATER launch (every reader of these counters is done):
-// the Adam step count (torch keeps it as a float tensor) and an epoch cursor.
-__device__ __forceinline__ void advance_counters(float* step, long long* cursor, long long n_batches) {
-  if (step) step[0] += 1.0f;
-  if (cursor) {
-    const long long c = cursor[0] + 1;
-    cursor[0] = c < n_batches ? c : 0;
+  if (bk.done && threadIdx.x == 0) {
+    // every thread of this workgroup has consumed its step[0] read (wg_sum synchronised), so the last workgroup
+    // to arrive advances the counters after every read of them. Nothing this launch wrote is read by the last
+    // workgroup, so a relaxed counter suffices (no release fence: on gfx950 that is an L2 write-back per
+    // workgroup); the bookkeeping's own stores reach the next launch through the kernel boundary.
+    if (__hip_atomic_fetch_add(bk.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+      advance_counters(bk.step, bk.cursor, bk.n_batches);
+      __hip_atomic_store(bk.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -167,13 +198,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_clip(TList T, const float* __restri
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (norm_out) norm_out[0] = tot;
-    if (log_values && log_history) {   // the step's logged values -> history slot of this batch (host memory:
-      float* dst = log_history + 3 * (cursor ? cursor[0] : 0LL);   // system-scope stores, read after a sync)
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-        __hip_atomic_store(dst + i, log_values[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __threadfence_system();
-    }
+    store_log(log_values, log_history, cursor);   // the step's logged values -> history slot of this batch
     advance_counters(step, cursor, n_batches);
   }
 }
@@ -384,9 +409,30 @@ int bcnf_adam_step(int32_t n_tensors, float* const* params, float* const* grads,
   const long long total = T.start[T.n];
   const unsigned nwg = (unsigned)n_partials(total);
   hipLaunchKernelGGL(k_adam, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, step, lr, beta1, beta2, eps,
-                     weight_decay, grad_partials, guard);
+                     weight_decay, grad_partials, guard, AdamBook{});
   if ((rc = launched()) || !advance_step) return rc;
   hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, (hipStream_t)stream, step, (long long*)nullptr, 0LL, guard);
+  return launched();
+}
+
+int bcnf_adam_step_bookkeep(int32_t n_tensors, float* const* params, float* const* grads, float* const* exp_avg,
+                            float* const* exp_avg_sq, const int64_t* numel, float* step, double lr, double beta1,
+                            double beta2, double eps, double weight_decay, int64_t* advance_cursor,
+                            int64_t cursor_modulo, const float* log_values, float* log_history, int32_t* done_counter,
+                            const int32_t* guard, void* stream) {
+  TList T;
+  int rc = make_tlist(n_tensors, params, grads, exp_avg, exp_avg_sq, numel, &T);
+  if (rc) return rc;
+  if (!params || !exp_avg || !exp_avg_sq || !step || !done_counter) return BCNF_ERR_ARG;
+  if (advance_cursor && cursor_modulo < 1) return BCNF_ERR_ARG;
+  for (int i = 0; i < n_tensors; ++i)
+    if (!T.p[i] || !T.m[i] || !T.v[i]) return BCNF_ERR_ARG;
+  const long long total = T.start[T.n];
+  const unsigned nwg = (unsigned)n_partials(total);
+  const AdamBook bk{step, (long long*)advance_cursor, (long long)cursor_modulo, log_values, log_history,
+                    (int*)done_counter};
+  hipLaunchKernelGGL(k_adam, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, step, lr, beta1, beta2, eps,
+                     weight_decay, (float*)nullptr, guard, bk);
   return launched();
 }
 

@@ -43,10 +43,15 @@ class FusedAdam(torch.optim.Optimizer):
         return st
 
     @torch.no_grad()
-    def step(self, closure=None, defer_step_count: bool = False, guard=None):
+    def step(self, closure=None, defer_step_count: bool = False, guard=None, bookkeep=None):
         """One Adam update. defer_step_count=True leaves the device step count to be advanced by the
         following clip_grad_norm_after_step (one launch less per training step). `guard` (device int32[4],
-        include/bcnf_amd.h) turns the update into a no-op on a halted step."""
+        include/bcnf_amd.h) turns the update into a no-op on a halted step. `bookkeep` = (cursor, log, counter)
+        (clip_grad_norm_after_step's cursor / log, plus a zeroed device int32): the launch's last workgroup
+        advances the step count and does that bookkeeping itself, for a step whose clip-after-step is
+        unobservable (bcnf_adam_step_bookkeep); no clip may follow."""
+        if bookkeep is not None:
+            return self._step_bookkeep(guard, *bookkeep)
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -86,6 +91,40 @@ class FusedAdam(torch.optim.Optimizer):
         self._partials = all_grads
         self._partials_for = [p for chunk, _, _, _ in all_grads for p in chunk]
         return loss
+
+    def can_bookkeep(self) -> bool:
+        """Whether step(bookkeep=...) applies: one parameter group updated in one launch."""
+        return len(self.param_groups) == 1 and 0 < len(self.param_groups[0]["params"]) <= N.MAX_TENSORS
+
+    def _step_bookkeep(self, guard, cursor, log, counter):
+        params = [p for g in self.param_groups for p in g["params"] if p.grad is not None]
+        if len(self.param_groups) != 1 or not params or len(params) > N.MAX_TENSORS:
+            raise NotImplementedError("bcnf_amd FusedAdam: bookkeeping needs one group in one launch")
+        group = self.param_groups[0]
+        for p in params:
+            if not p.is_cuda or p.dtype != torch.float32 or not p.is_contiguous() or not p.grad.is_contiguous():
+                raise RuntimeError("bcnf_amd FusedAdam: parameters and grads must be contiguous fp32 GPU tensors")
+        states = [self._state(p) for p in params]
+        step = states[0]["step"]
+        for st in states[1:]:
+            if st["step"] is not step:
+                st["step"] = step
+        b1, b2 = group["betas"]
+        cur, mod = cursor if cursor is not None else (None, 0)
+        L = N.lib()
+        rc = L.bcnf_adam_step_bookkeep(len(params), N.ptr_array(params), N.ptr_array([p.grad for p in params]),
+                                       N.ptr_array([s["exp_avg"] for s in states]),
+                                       N.ptr_array([s["exp_avg_sq"] for s in states]),
+                                       N.i64_array([p.numel() for p in params]), N.ptr(step),
+                                       ctypes.c_double(group["lr"]), ctypes.c_double(b1), ctypes.c_double(b2),
+                                       ctypes.c_double(group["eps"]), ctypes.c_double(group["weight_decay"]),
+                                       N.ptr(cur), ctypes.c_int64(mod), N.ptr(log[0] if log else None),
+                                       N.ptr(log[1] if log else None), N.ptr(counter), N.ptr(guard),
+                                       N.stream_handle(params[0].device))
+        N.check(rc, "bcnf_adam_step_bookkeep")
+        self._partials = None            # no clip may follow this step
+        self._partials_for = None
+        return None
 
     @torch.no_grad()
     def clip_grad_norm_after_step(self, max_norm: float = 1.0, cursor=None, log=None, guard=None):

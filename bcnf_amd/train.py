@@ -63,6 +63,7 @@ class TrainStep:
         self._multi = None      # (graph, steps, grads): run_epoch's multi-step graph (world 1)
         self._single_grads = None
         self._multi_bound = False
+        self._book = None       # Adam's finished-workgroup counter (bcnf_adam_step_bookkeep)
         self._cond_shape = None  # (per-sample condition shape, its size) when the pool rows are padded
         self._epoch = None      # (order, cursor, n_batches, batch) for the device-cursor batch walk
         self._bucket = None     # data parallel: every gradient in one buffer, one all-reduce per step
@@ -127,13 +128,21 @@ class TrainStep:
         self._scale_bucket()
         self._bind_grads()
 
-    def _update(self, vals=None):
+    def _update(self, vals=None, clip: bool = True):
         """Adam, then clip_grad_norm_ after the step (trainer.py:270-272); the clip launch also advances the
         Adam step count and, in epoch mode, the batch cursor, and stores the logged values into the pinned
         history (end-of-step bookkeeping, no extra launch)."""
-        self.opt.step(defer_step_count=True, guard=self._guard)
         cursor = (self._epoch[1], self._epoch[2]) if self._epoch is not None else None
         log = (vals, self._hist) if (vals is not None and self._hist is not None) else None
+        if not clip:
+            # a step inside a multi-step graph that the next step's backward follows: its clip-after-step
+            # would only scale gradients that are overwritten before anyone can read them (the reference
+            # discards the norm), so Adam's last workgroup does the step's bookkeeping and no clip runs
+            if self._book is None:
+                self._book = torch.zeros(1, dtype=torch.int32, device=self.params[0].device)
+            self.opt.step(guard=self._guard, bookkeep=(cursor, log, self._book))
+            return
+        self.opt.step(defer_step_count=True, guard=self._guard)
         self.opt.clip_grad_norm_after_step(self.max_norm, cursor=cursor, log=log, guard=self._guard)
 
     def broadcast_parameters(self, src: int = 0):
@@ -411,15 +420,17 @@ class TrainStep:
     epoch_unroll = 8
     # The captured step runs the batch gather inside the folded path's pack launch (one launch fewer).
     fuse_gather = True
+    # Inside a multi-step graph only the last step's clip-after-step is observable (see _update).
+    skip_hidden_clips = True
 
     def _multi_graph(self):
         if self._multi is None or self._multi[1] != self.epoch_unroll:
             k = self.epoch_unroll
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                for _ in range(k):
+                for i in range(k):
                     vals = self._forward_backward(*self._gather(defer=True))
-                    self._update(vals)
+                    self._update(vals, clip=(i == k - 1) or not (self.skip_hidden_clips and self.opt.can_bookkeep()))
             self._multi = (g, k, [p.grad for p in self.params])
             self._bind(self._single_grads)
             self._multi_bound = False

@@ -207,6 +207,18 @@ int bcnf_adam_step(int32_t n_tensors, float* const* params, float* const* grads,
                    double beta2, double eps, double weight_decay, float* grad_partials, int32_t advance_step,
                    const int32_t* guard, void* stream);
 
+/* bcnf_adam_step (step count advanced in the same launch) whose LAST workgroup to finish also does the end-of-step
+ * bookkeeping of bcnf_clip_grad_norm: epoch cursor advance and logged values -> log_history[3 * cursor]. It
+ * replaces Adam + clip for a training step whose clip-after-step (trainer.py:272) cannot be observed -- one that
+ * is followed, inside the same captured graph, by the next step's backward, which overwrites every gradient the
+ * clip would scale (the reference discards the returned norm). done_counter: device int32, 0 between launches
+ * (the last workgroup resets it). No squared-gradient partials are written. */
+int bcnf_adam_step_bookkeep(int32_t n_tensors, float* const* params, float* const* grads, float* const* exp_avg,
+                            float* const* exp_avg_sq, const int64_t* numel, float* step, double lr, double beta1,
+                            double beta2, double eps, double weight_decay, int64_t* advance_cursor,
+                            int64_t cursor_modulo, const float* log_values, float* log_history, int32_t* done_counter,
+                            const int32_t* guard, void* stream);
+
 /* Per-workgroup sums of squared gradients (when no bcnf_adam_step produced them). */
 int bcnf_grad_sumsq(int32_t n_tensors, float* const* grads, const int64_t* numel, float* grad_partials, void* stream);
 
