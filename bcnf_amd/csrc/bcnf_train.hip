@@ -2,7 +2,7 @@
 //
 //   k_adam     multi-tensor Adam over the flat parameter buffers (torch.optim.Adam semantics,
 //              trainer.py:136 / :270), fused with the per-workgroup sum of squared gradients that
-//              clip_grad_norm_ needs (trainer.py:272) and with the device-side step counter bump
+//              clip_grad_norm_ needs (trainer.py:275) and with the device-side step counter bump
 //   k_sumsq    per-workgroup sum of squared gradients (standalone clip)
 //   k_clip     total norm from the partials (fixed order) + in-place gradient scaling
 //   k_gemm     small fp32 MFMA GEMM C = A * op(B) (+ bias) for the feature network's nn.Linear

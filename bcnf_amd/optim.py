@@ -2,7 +2,7 @@
 
 The Trainer builds `torch.optim.Adam(model.parameters(), lr=...)` (src/bcnf/train/trainer.py:136) and,
 after every `optimizer.step()`, calls `torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)`
-(trainer.py:270-272). With the coupling stack held in one flat buffer (CondRealNVP_v2.flat_parameters())
+(trainer.py:273-275). With the coupling stack held in one flat buffer (CondRealNVP_v2.flat_parameters())
 torch's multi-tensor kernels see a handful of large tensors and parallelise poorly (one workgroup per
 64 K-element chunk); `FusedAdam` runs the whole update as ONE launch over the concatenated index space
 and emits the per-workgroup sums of squared gradients in the same pass, so the clip that follows is a

@@ -129,7 +129,7 @@ class TrainStep:
         self._bind_grads()
 
     def _update(self, vals=None, clip: bool = True):
-        """Adam, then clip_grad_norm_ after the step (trainer.py:270-272); the clip launch also advances the
+        """Adam, then clip_grad_norm_ after the step (trainer.py:273-275); the clip launch also advances the
         Adam step count and, in epoch mode, the batch cursor, and stores the logged values into the pinned
         history (end-of-step bookkeeping, no extra launch)."""
         cursor = (self._epoch[1], self._epoch[2]) if self._epoch is not None else None

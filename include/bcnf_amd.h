@@ -27,7 +27,7 @@
  *   bcnf_nll_backward    <- loss.backward() of that loss through the stack (trainer.py:268)
  *   bcnf_adam_step       <- optimizer.step() of torch.optim.Adam built by the Trainer (trainer.py:136,270)
  *   bcnf_clip_grad_norm  <- torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)
- *                           (trainer.py:272, after the step)
+ *                           (trainer.py:275, after the step)
  *   bcnf_linear_forward / bcnf_linear_backward
  *                        <- nn.Linear of FullyConnectedFeatureNetwork (feature_network.py:114-145)
  *   bcnf_wide_*          <- the same stack interfaces for the wide-MLP shapes (FC_large / LSTM_large)
@@ -209,7 +209,7 @@ int bcnf_adam_step(int32_t n_tensors, float* const* params, float* const* grads,
 
 /* bcnf_adam_step (step count advanced in the same launch) whose LAST workgroup to finish also does the end-of-step
  * bookkeeping of bcnf_clip_grad_norm: epoch cursor advance and logged values -> log_history[3 * cursor]. It
- * replaces Adam + clip for a training step whose clip-after-step (trainer.py:272) cannot be observed -- one that
+ * replaces Adam + clip for a training step whose clip-after-step (trainer.py:275) cannot be observed -- one that
  * is followed, inside the same captured graph, by the next step's backward, which overwrites every gradient the
  * clip would scale (the reference discards the returned norm). done_counter: device int32, 0 between launches
  * (the last workgroup resets it). No squared-gradient partials are written. */
