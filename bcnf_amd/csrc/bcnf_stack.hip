@@ -508,6 +508,9 @@ __global__ __launch_bounds__(BCNF_WG) void k_hp(BcnfLayout L, const float* __res
 #pragma unroll
   for (int u = 0; u < 4; ++u) acc[u] = floatx4{0.f, 0.f, 0.f, 0.f};
   load(0);
+  float b1v[4];                                        // the epilogue's biases, fetched with the first chunk
+#pragma unroll
+  for (int u = 0; u < 4; ++u) b1v[u] = pk[L.b1c_off + n0 + 16 * u + lr];
   for (int c0 = 0; c0 < Cp; c0 += KC) {
     store();
     __syncthreads();
@@ -532,11 +535,10 @@ __global__ __launch_bounds__(BCNF_WG) void k_hp(BcnfLayout L, const float* __res
   for (int u = 0; u < 4; ++u) {
     const int kj = n0 + 16 * u + lr, k = kj >> 4;
     if (k < L.nb) {
-      const float b1 = pk[L.b1c_off + kj];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const long long r = b0 + 16 * wave + 4 * lq + i;
-        if (r < R) hp[((long long)k * R + r) * 16 + lr] = acc[u][i] + b1;
+        if (r < R) hp[((long long)k * R + r) * 16 + lr] = acc[u][i] + b1v[u];
       }
     }
   }
@@ -825,13 +827,25 @@ __global__ __launch_bounds__(BCNF_WG) void k_fold_finish(BcnfLayout L, const flo
   if ((int)blockIdx.x < L.nb * nct) {
     const int k = blockIdx.x / nct, c0 = (blockIdx.x % nct) * 16;
     const float* g = gx + (long long)k * 16 * Xp;     // [16][Xp], contiguous
-    for (int i = tid; i < 16 * Xp; i += BCNF_WG) {
-      const int j = i / Xp, xc = i - j * Xp;
-      As[xc * 16 + j] = g[i];
-      const int cc = j, c = c0 + cc;                  // the same (row, xc) walk over Wf1[c0 + cc][xc]
+    float va[16], vb[16];                             // every load issued before the first LDS store
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {                    // 16 Xp <= 16 * 256: at most 16 elements per thread
+      const int i = tid + BCNF_WG * e;
+      const int j = i / Xp, xc = i - j * Xp, c = c0 + j;   // (row, xc) of Gx_k and of Wf1[c0 + row]
+      const bool in = i < 16 * Xp;
+      va[e] = in ? g[i] : 0.f;
       float v = 0.f;
-      if (c < L.C) v = xc < X ? wf[(long long)c * X + xc] : ((xc == X && bf) ? bf[c] : 0.f);
-      Bs[xc * 16 + cc] = v;
+      if (in && c < L.C) v = xc < X ? wf[(long long)c * X + xc] : ((xc == X && bf) ? bf[c] : 0.f);
+      vb[e] = v;
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int i = tid + BCNF_WG * e;
+      if (i < 16 * Xp) {
+        const int j = i / Xp, xc = i - j * Xp;
+        As[xc * 16 + j] = va[e];
+        Bs[xc * 16 + j] = vb[e];
+      }
     }
     __syncthreads();
     tile16_accum(As, Bs, Xp, acc);
