@@ -255,6 +255,9 @@ def main():
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
                          "avg_us": round(us, 2), "flop_per_launch": flop,
+                         # both fractions -- the PMC HBM bytes of the same launch over its duration
+                         "hbm_achieved_GBps": round(traffic / (us * 1e3), 1) if traffic else None,
+                         "hbm_frac": round(traffic / (us * 1e3) / PEAK_HBM_GBS, 4) if traffic else None,
                          "note": "fp32 VALU (DPP rotations) + fp32 MFMA; peak is the fp32 vector = MFMA-f32 rate"},
             "kernels_us": {k: round(v, 2) for k, v in kern.items()},
         }
