@@ -39,7 +39,7 @@ def _model(cfg):
     return CondRealNVP_v2.from_config(cfg).cuda().train()
 
 
-def _worker(rank, world, port, cfg, q):
+def _worker(rank, world, port, cfg, q, mode="step"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -51,8 +51,13 @@ def _worker(rank, world, port, cfg, q):
         step.broadcast_parameters()
         y, t = _data()
         n = y.shape[0] // world
-        for _ in range(2):
-            step.step(y[rank * n:(rank + 1) * n].cuda(), t[rank * n:(rank + 1) * n].cuda())
+        if mode == "epoch":     # bench.py's N > 1 path: device pool, epoch order, run_epoch (gather in the graph)
+            step.set_pool(y[rank * n:(rank + 1) * n].cuda(), t[rank * n:(rank + 1) * n].cuda())
+            step.set_epoch(torch.arange(n, device="cuda").repeat(2), n)
+            step.run_epoch()
+        else:
+            for _ in range(2):
+                step.step(y[rank * n:(rank + 1) * n].cuda(), t[rank * n:(rank + 1) * n].cuda())
         q.put((rank, [p.detach().cpu().numpy() for p in m.parameters()]))
     except Exception:
         q.put((rank, traceback.format_exc()))
@@ -60,12 +65,13 @@ def _worker(rank, world, port, cfg, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("mode", ["step", "epoch"])
 @pytest.mark.parametrize("cfg", [CFG, WIDE], ids=["small_family", "wide_family"])
-def test_two_rank_step_equals_union_batch_step(cfg):
+def test_two_rank_step_equals_union_batch_step(cfg, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, cfg, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, cfg, q, mode)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=180) for _ in procs)
