@@ -52,6 +52,27 @@ class BcnfStackDesc(ctypes.Structure):
     ]
 
 
+class BcnfFoldAdam(ctypes.Structure):
+    """include/bcnf_amd.h BcnfFoldAdam: Adam fused into bcnf_fold_backward_tail."""
+    _fields_ = [
+        ("params", ctypes.c_void_p * 3),
+        ("exp_avg", ctypes.c_void_p * 3),
+        ("exp_avg_sq", ctypes.c_void_p * 3),
+        ("step", ctypes.c_void_p),
+        ("lr", ctypes.c_double),
+        ("beta1", ctypes.c_double),
+        ("beta2", ctypes.c_double),
+        ("eps", ctypes.c_double),
+        ("weight_decay", ctypes.c_double),
+        ("advance_cursor", ctypes.c_void_p),
+        ("cursor_modulo", ctypes.c_int64),
+        ("log_values", ctypes.c_void_p),
+        ("log_history", ctypes.c_void_p),
+        ("done_counter", ctypes.c_void_p),
+        ("guard", ctypes.c_void_p),
+    ]
+
+
 class BcnfGather2(ctypes.Structure):
     """include/bcnf_amd.h BcnfGather2: a batch gather run inside bcnf_pack_params_fold's launch."""
     _fields_ = [
@@ -120,7 +141,7 @@ def _bind(lib):
         "bcnf_fold_nll_forward": (_i32, [_pdesc, _vp, _vp, _i32, _vp, _vp, _i32, _i64, _vp, _vp, _i32, _vp, _vp,
                                          _i32, _vp, _vp, _vp]),
         "bcnf_fold_backward_tail": (_i32, [_pdesc, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _i64, _i32, _vp, _vp,
-                                           _vp, _vp]),
+                                           _vp, _vp, _vp]),
         "bcnf_grad_partials": (_i64, [_i64]),
         "bcnf_adam_step": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double,
                                   ctypes.c_double, ctypes.c_double, ctypes.c_double, _vp, _i32, _vp, _vp]),

@@ -86,6 +86,65 @@ inline void gather2_plan(long long n, int* rpw, int* nwg) {
   *nwg = w > 0 ? (int)((n + *rpw - 1) / *rpw) : 0;
 }
 
+// torch.optim.Adam (amsgrad=False, maximize=False) per element -- the one definition every Adam kernel uses, so the
+// standalone update (k_adam) and the ones fused into the backward tail round identically:
+//   g += wd p;  m = lerp(m, g, 1 - b1);  v = b2 v + (1 - b2) g g;  p -= (lr / bc1) m / (sqrt(v) / sqrt(bc2) + eps)
+struct AdamScalars {
+  float step_size, bc2s, omb1, omb2, b2, eps, wd;
+};
+
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamScalars& a) {
+  if (a.wd != 0.f) g = fmaf(a.wd, p, g);
+  m = m + a.omb1 * (g - m);                          // lerp, |weight| < 0.5 branch
+  v = v * a.b2 + a.omb2 * (g * g);
+  const float denom = sqrtf(v) / a.bc2s + a.eps;
+  p = p + (-a.step_size) * (m / denom);
+}
+
+// Hyper-parameters arrive as doubles (Python floats); every scalar is derived in double and rounded once, as
+// torch does. `sc` is 2 floats of LDS; the two pows run on two waves; ends with a __syncthreads.
+__device__ __forceinline__ AdamScalars adam_scalars(float step_next, double lr, double b1d, double b2d, double epsd,
+                                                    double wdd, float* sc) {
+  if (threadIdx.x == 0) sc[0] = (float)(lr / (1.0 - pow(b1d, (double)step_next)));
+  if (threadIdx.x == 64) sc[1] = (float)sqrt(1.0 - pow(b2d, (double)step_next));
+  __syncthreads();
+  return AdamScalars{sc[0], sc[1], (float)(1.0 - b1d), (float)(1.0 - b2d), (float)b2d, (float)epsd, (float)wdd};
+}
+
+__device__ __forceinline__ void store_log(const float* log_values, float* log_history, const long long* cursor) {
+  if (!log_values || !log_history) return;   // host memory: system-scope stores, read after a sync
+  float* dst = log_history + 3 * (cursor ? cursor[0] : 0LL);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) __hip_atomic_store(dst + i, log_values[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __threadfence_system();
+}
+
+// End-of-step bookkeeping by one thread of a LATER launch (every reader of these counters is done):
+// the Adam step count (torch keeps it as a float tensor) and an epoch cursor.
+__device__ __forceinline__ void advance_counters(float* step, long long* cursor, long long n_batches) {
+  if (step) step[0] += 1.0f;
+  if (cursor) {
+    const long long c = cursor[0] + 1;
+    cursor[0] = c < n_batches ? c : 0;
+  }
+}
+
+// Kernel-side form of BcnfFoldAdam (include/bcnf_amd.h): Adam applied inside the folded backward tail.
+struct FoldAdamArgs {
+  float* p[3];                  // 0: the coupling stack's flat parameters, 1: feature W, 2: feature b (nullable)
+  float* m[3];
+  float* v[3];
+  float* step;
+  double lr, b1, b2, eps, wd;
+  long long* cursor;
+  long long n_batches;
+  const float* log_values;
+  float* log_history;
+  int* done;
+  const int* guard;
+  int on;
+};
+
 // Host-computed layout of one stack (passed by value to every kernel).
 struct BcnfLayout {
   int D, Da, Db, C, Cp, NH, nb, act_norm;

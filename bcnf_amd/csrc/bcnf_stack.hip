@@ -780,6 +780,8 @@ __device__ __forceinline__ void gx_reduce_body(long long total, const float* __r
 // Tile product: thread (ks = lane & 15, rb = lane >> 4, cb = wave) accumulates the 4 x 4 block rows 4rb.., cols
 // 4cb.. over k = ks + 16 i (conflict-free ds_read_b128: 16 consecutive rows x 4 float4 per wave), then the 16
 // k-slices are summed in a fixed order through LDS.
+__device__ __forceinline__ int c0_of_finish(int bx, int nct) { return (bx % nct) * 16; }
+
 constexpr int FIN_KC = 256;                           // K chunk (role a: Xp <= 256 fits one)
 constexpr int FIN_SMEM = 2 * FIN_KC * 16;             // As + Bs; the 16 x 256 reduction aliases them
 
@@ -816,14 +818,65 @@ __global__ __launch_bounds__(BCNF_WG) void k_fold_finish(BcnfLayout L, const flo
                                                          const float* __restrict__ gx, const float* __restrict__ wf,
                                                          const float* __restrict__ bf, int X,
                                                          float* __restrict__ dparams, float* __restrict__ dwf,
-                                                         float* __restrict__ dbf) {
+                                                         float* __restrict__ dbf, FoldAdamArgs A) {
   __shared__ __attribute__((aligned(16))) float smem[FIN_SMEM];
+  __shared__ float sc[2];
   float* As = smem;
   float* Bs = smem + FIN_KC * 16;
   const int Xp = fold_xp(X), tid = threadIdx.x, nct = L.Cp >> 4;
   floatx4 acc[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // fused Adam (FoldAdamArgs): this thread's output is one parameter whose gradient it computes; its parameter and
+  // moments are fetched now, the update follows the tile product. The launch's last workgroup does the step's
+  // bookkeeping (bcnf_adam_step_bookkeep semantics), workgroup 0 stores the logged values.
+  const bool adam = A.on && !(A.guard && A.guard[BCNF_GUARD_HALTED]);
+  AdamScalars as{};
+  if (adam) {
+    if (blockIdx.x == 0 && tid == 0) store_log(A.log_values, A.log_history, A.cursor);
+    as = adam_scalars(A.step[0] + 1.0f, A.lr, A.b1, A.b2, A.eps, A.wd, sc);
+  }
+  int slot = -1;                                       // which parameter tensor / element this thread updates
+  long long idx = 0;
+  float ap = 0.f, am = 0.f, av = 0.f;
+  if ((int)blockIdx.x < L.nb * nct) {
+    const int j = tid >> 4, c = c0_of_finish(blockIdx.x, nct) + (tid & 15), k = blockIdx.x / nct;
+    if (j < L.H[1] && c < L.C) {
+      slot = 0;
+      idx = coupling_base(L, k) + L.lin_w[1] + j * L.lin_in[1] + L.Da + c;
+    }
+  } else {
+    const int tile = blockIdx.x - L.nb * nct, c = (tile % nct) * 16 + (tid >> 4), x = (tile / nct) * 16 + (tid & 15);
+    if (c < L.C) {
+      if (x < X) {
+        slot = 1;
+        idx = (long long)c * X + x;
+      } else if (x == X && dbf) {
+        slot = 2;
+        idx = c;
+      }
+    }
+  }
+  if (adam && slot >= 0 && A.p[slot]) {
+    ap = A.p[slot][idx];
+    am = A.m[slot][idx];
+    av = A.v[slot][idx];
+  }
+  auto finish_elem = [&](float gval) {
+    if (!adam || slot < 0 || !A.p[slot]) return;
+    adam_elem(ap, gval, am, av, as);
+    A.p[slot][idx] = ap;
+    A.m[slot][idx] = am;
+    A.v[slot][idx] = av;
+  };
+  auto arrive = [&]() {
+    if (!adam || tid != 0) return;
+    // every thread of this workgroup read the step count before this point (adam_scalars synchronised)
+    if (__hip_atomic_fetch_add(A.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+      advance_counters(A.step, A.cursor, A.n_batches);
+      __hip_atomic_store(A.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
   if ((int)blockIdx.x < L.nb * nct) {
     const int k = blockIdx.x / nct, c0 = (blockIdx.x % nct) * 16;
     const float* g = gx + (long long)k * 16 * Xp;     // [16][Xp], contiguous
@@ -852,6 +905,9 @@ __global__ __launch_bounds__(BCNF_WG) void k_fold_finish(BcnfLayout L, const flo
     const float v = tile16_reduce(smem, acc);
     const int j = tid >> 4, c = c0 + (tid & 15);
     if (j < L.H[1] && c < L.C) dparams[coupling_base(L, k) + L.lin_w[1] + j * L.lin_in[1] + L.Da + c] = v;
+    finish_elem(v);
+    __syncthreads();
+    arrive();
     return;
   }
   const int tile = blockIdx.x - L.nb * nct, c0 = (tile % nct) * 16, x0 = (tile / nct) * 16;
@@ -885,6 +941,9 @@ __global__ __launch_bounds__(BCNF_WG) void k_fold_finish(BcnfLayout L, const flo
       dbf[c] = v;
     }
   }
+  finish_elem(v);
+  __syncthreads();
+  arrive();
 }
 
 // Compile-time mirror of the forward / backward record layouts of make_layout (checked on the host).
@@ -1569,13 +1628,29 @@ __device__ __forceinline__ long long compact_to_canonical(const BcnfLayout& L, i
 // flight: 32 lanes x 16 B x 16 loads per group keeps ~35 MB in flight over the ~580-workgroup grid at B=4096.
 constexpr int RED_G = 8, RED_O4 = 32, RED_T = 16;
 
+// With `A` (folded training step inside a multi-step graph, FoldAdamArgs): the reduced gradient of each output also
+// takes its Adam update here; the parameters / moments are fetched before the slab stream, the scalars are `as`.
 __device__ __forceinline__ void reduce_body(const BcnfLayout& L, const float* __restrict__ slab, long long stride,
-                                            int nwg, float* __restrict__ out, int bx, float* __restrict__ smem) {
+                                            int nwg, float* __restrict__ out, int bx, float* __restrict__ smem,
+                                            const FoldAdamArgs* A = nullptr, const AdamScalars* as = nullptr) {
   floatx4 (*part)[RED_O4] = reinterpret_cast<floatx4 (*)[RED_O4]>(smem);   // [RED_G][RED_O4]
   const int g = threadIdx.x / RED_O4, o4 = threadIdx.x % RED_O4;
   const long long i = ((long long)bx * RED_O4 + o4) * 4;
   const bool live = i < stride;
   const long long ic = live ? i : 0;
+  const int m = (int)(ic / L.blk_pad), o = (int)(ic - (long long)m * L.blk_pad);
+  const int size_m = L.cblk - ((m < L.nb - 1) ? 0 : L.an_size);
+  long long ci[4];
+  float ap[4], am[4], av[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    ci[e] = compact_to_canonical(L, m, o + e < size_m ? o + e : 0);
+    if (A && g == 0) {
+      ap[e] = A->p[0][ci[e]];
+      am[e] = A->m[0][ci[e]];
+      av[e] = A->v[0][ci[e]];
+    }
+  }
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
   int w = g;
   for (; w + RED_G * (RED_T - 1) < nwg; w += RED_G * RED_T) {
@@ -1593,11 +1668,17 @@ __device__ __forceinline__ void reduce_body(const BcnfLayout& L, const float* __
   floatx4 tot = part[0][o4];
 #pragma unroll
   for (int q = 1; q < RED_G; ++q) tot += part[q][o4];
-  const int m = (int)(i / L.blk_pad), o = (int)(i - (long long)m * L.blk_pad);
-  const int size_m = L.cblk - ((m < L.nb - 1) ? 0 : L.an_size);
 #pragma unroll
-  for (int e = 0; e < 4; ++e)
-    if (o + e < size_m) out[compact_to_canonical(L, m, o + e)] = tot[e];
+  for (int e = 0; e < 4; ++e) {
+    if (o + e >= size_m) continue;
+    out[ci[e]] = tot[e];
+    if (A) {
+      adam_elem(ap[e], tot[e], am[e], av[e], *as);
+      A->p[0][ci[e]] = ap[e];
+      A->m[0][ci[e]] = am[e];
+      A->v[0][ci[e]] = av[e];
+    }
+  }
 }
 
 // The backward's tail in ONE launch: dL/dh tiles, the slab reduction and the W1 condition-part split-K
@@ -1639,11 +1720,17 @@ __global__ __launch_bounds__(BCNF_WG) void k_bwd_tail(BcnfLayout L, BcnfLayout L
 __global__ __launch_bounds__(BCNF_WG) void k_red_gx(BcnfLayout L, long long total, const float* __restrict__ work,
                                                     int splits, float* __restrict__ gx, int n_gx,
                                                     const float* __restrict__ slab, long long stride, int nwg,
-                                                    float* __restrict__ dparams) {
+                                                    float* __restrict__ dparams, FoldAdamArgs A) {
   __shared__ __attribute__((aligned(16))) float smem[RED_G * RED_O4 * 4];
+  __shared__ float sc[2];
   const int bx = blockIdx.x;
   if (bx < n_gx) {
     gx_reduce_body(total, work, splits, gx, (long long)bx * BCNF_WG + threadIdx.x);
+    return;
+  }
+  if (A.on && !(A.guard && A.guard[BCNF_GUARD_HALTED])) {      // (a halted step updates nothing)
+    const AdamScalars as = adam_scalars(A.step[0] + 1.0f, A.lr, A.b1, A.b2, A.eps, A.wd, sc);
+    reduce_body(L, slab, stride, nwg, dparams, bx - n_gx, smem, &A, &as);
     return;
   }
   reduce_body(L, slab, stride, nwg, dparams, bx - n_gx, smem);
@@ -2080,12 +2167,39 @@ int bcnf_fold_nll_forward(const BcnfStackDesc* desc, const void* packed, const f
 int bcnf_fold_backward_tail(const BcnfStackDesc* desc, const void* packed, const void* slab, const float* x,
                             int32_t ldx, int32_t in_features, const float* feat_weight, const float* feat_bias,
                             const void* workspace, int64_t batch, int32_t training, float* dparams,
-                            float* dfeat_weight, float* dfeat_bias, void* stream) {
+                            float* dfeat_weight, float* dfeat_bias, const BcnfFoldAdam* adam, void* stream) {
   BcnfLayout L;
   int rc = fold_setup(desc, in_features, &L);
   if (rc) return rc;
   if (!packed || !slab || !x || !feat_weight || !workspace || !dparams || batch < 1 || ldx < in_features)
     return BCNF_ERR_ARG;
+  FoldAdamArgs A = {};
+  if (adam) {
+    const BcnfFoldAdam& a = *adam;
+    if (!a.params[0] || !a.exp_avg[0] || !a.exp_avg_sq[0] || !a.params[1] || !a.exp_avg[1] || !a.exp_avg_sq[1] ||
+        !a.step || !a.done_counter || (feat_bias && (!a.params[2] || !a.exp_avg[2] || !a.exp_avg_sq[2])) ||
+        (a.advance_cursor && a.cursor_modulo < 1))
+      return BCNF_ERR_ARG;
+    for (int t = 0; t < 3; ++t) {
+      A.p[t] = a.params[t];
+      A.m[t] = a.exp_avg[t];
+      A.v[t] = a.exp_avg_sq[t];
+    }
+    if (!feat_bias) A.p[2] = A.m[2] = A.v[2] = nullptr;
+    A.step = a.step;
+    A.lr = a.lr;
+    A.b1 = a.beta1;
+    A.b2 = a.beta2;
+    A.eps = a.eps;
+    A.wd = a.weight_decay;
+    A.cursor = (long long*)a.advance_cursor;
+    A.n_batches = (long long)a.cursor_modulo;
+    A.log_values = a.log_values;
+    A.log_history = a.log_history;
+    A.done = (int*)a.done_counter;
+    A.guard = (const int*)a.guard;
+    A.on = 1;
+  }
   const BcnfLayout F = fold_layout(L, in_features, ldx);
   hipStream_t st = (hipStream_t)stream;
   const long long S = slab_stride_of(L);
@@ -2113,11 +2227,11 @@ int bcnf_fold_backward_tail(const BcnfStackDesc* desc, const void* packed, const
   const long long total = (long long)L.nb * 16 * F.Cp;
   const int n_gx = (int)((total + BCNF_WG - 1) / BCNF_WG);
   hipLaunchKernelGGL(k_red_gx, dim3((unsigned)(n_gx + n_red)), dim3(BCNF_WG), 0, st, L, total, (const float*)work,
-                     (int)splits, gx, n_gx, (const float*)slab, S, nwg, dparams);
+                     (int)splits, gx, n_gx, (const float*)slab, S, nwg, dparams, A);
   if ((rc = check_launch())) return rc;
   const int n_fin = (L.nb + (F.Cp >> 4)) * (L.Cp >> 4);
   hipLaunchKernelGGL(k_fold_finish, dim3((unsigned)n_fin), dim3(BCNF_WG), 0, st, L, (const float*)packed,
-                     (const float*)gx, feat_weight, feat_bias, (int)in_features, dparams, dfeat_weight, dfeat_bias);
+                     (const float*)gx, feat_weight, feat_bias, (int)in_features, dparams, dfeat_weight, dfeat_bias, A);
   return check_launch();
 }
 

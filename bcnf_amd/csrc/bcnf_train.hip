@@ -63,24 +63,6 @@ struct AdamBook {
   int* done;                    // workgroups finished; 0 between launches (the last one resets it); NULL: off
 };
 
-__device__ __forceinline__ void store_log(const float* log_values, float* log_history, const long long* cursor) {
-  if (!log_values || !log_history) return;   // host memory: system-scope stores, read after a sync
-  float* dst = log_history + 3 * (cursor ? cursor[0] : 0LL);
-#pragma unroll
-  for (int i = 0; i < 3; ++i) __hip_atomic_store(dst + i, log_values[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __threadfence_system();
-}
-
-// End-of-step bookkeeping by one thread of a LATER launch (every reader of these counters is done):
-// the Adam step count (torch keeps it as a float tensor) and an epoch cursor.
-__device__ __forceinline__ void advance_counters(float* step, long long* cursor, long long n_batches) {
-  if (step) step[0] += 1.0f;
-  if (cursor) {
-    const long long c = cursor[0] + 1;
-    cursor[0] = c < n_batches ? c : 0;
-  }
-}
-
 __global__ __launch_bounds__(BCNF_WG) void k_adam(TList T, const float* __restrict__ step, double lr, double b1d,
                                                   double b2d, double epsd, double wdd, float* __restrict__ part,
                                                   const int32_t* __restrict__ guard, AdamBook bk) {
@@ -107,28 +89,17 @@ __global__ __launch_bounds__(BCNF_WG) void k_adam(TList T, const float* __restri
   // bookkeeping: the logged values go out from workgroup 0 at the start (it reads the cursor before its own
   // arrival below, hence before the last workgroup advances it), off the launch's critical path
   if (bk.done && blockIdx.x == 0 && threadIdx.x == 0) store_log(bk.log_values, bk.log_history, bk.cursor);
-  const float st = step[0] + 1.0f;
-  // the two double pows once per workgroup, on two waves side by side
-  if (threadIdx.x == 0) sc[0] = (float)(lr / (1.0 - pow(b1d, (double)st)));
-  if (threadIdx.x == 64) sc[1] = (float)sqrt(1.0 - pow(b2d, (double)st));
-  __syncthreads();
-  const float step_size = sc[0], bc2s = sc[1];
-  const float omb1 = (float)(1.0 - b1d), omb2 = (float)(1.0 - b2d);
-  const float b2 = (float)b2d, eps = (float)epsd, wd = (float)wdd;
+  const AdamScalars as = adam_scalars(step[0] + 1.0f, lr, b1d, b2d, epsd, wdd, sc);
   float ss = 0.f;
 #pragma unroll
   for (int e = 0; e < EPT; ++e) {
     const long long i = (long long)blockIdx.x * CHUNK + e * BCNF_WG + threadIdx.x;
     if (i < total) {
-      float gg = g[e];
-      ss = fmaf(gg, gg, ss);
-      if (wd != 0.f) gg = fmaf(wd, p[e], gg);
-      const float mm = m[e] + omb1 * (gg - m[e]);   // lerp, |weight| < 0.5 branch
-      const float vv = v[e] * b2 + omb2 * (gg * gg);
-      const float denom = sqrtf(vv) / bc2s + eps;
-      T.m[t[e]][o[e]] = mm;
-      T.v[t[e]][o[e]] = vv;
-      T.p[t[e]][o[e]] = p[e] + (-step_size) * (mm / denom);
+      ss = fmaf(g[e], g[e], ss);
+      adam_elem(p[e], g[e], m[e], v[e], as);
+      T.m[t[e]][o[e]] = m[e];
+      T.v[t[e]][o[e]] = v[e];
+      T.p[t[e]][o[e]] = p[e];
     }
   }
   const float s = wg_sum(ss, red);

@@ -367,9 +367,13 @@ class FusedStack:
         N.check(rc, "bcnf_fold_nll_forward")
         return z, ldj, vals, (ws, pk)
 
+    # A BcnfFoldAdam for the next folded backward (TrainStep, multi-step graphs): consumed by that launch.
+    pending_adam = None
+
     def launch_fold_nll_backward(self, x, z, dvals, wf, bf, training: bool, saved, want_feat: bool,
-                                 finalize_into=None):
-        """Fused NLL backward of the folded pass: (dparams, dWf, dbf); no dL/dh, no dL/dx."""
+                                 finalize_into=None, adam=None):
+        """Fused NLL backward of the folded pass: (dparams, dWf, dbf); no dL/dh, no dL/dx. adam (an
+        N.BcnfFoldAdam): the optimizer update of every parameter runs inside the backward tail."""
         ws, pk = saved
         B, X = x.shape
         L = N.lib()
@@ -389,7 +393,9 @@ class FusedStack:
         N.check(L.bcnf_fold_backward_tail(self._pdesc, N.ptr(pk), N.ptr(slab), N.ptr(x), ctypes.c_int32(x.stride(0)),
                                           ctypes.c_int32(X), N.ptr(wf),
                                           N.ptr(bf), N.ptr(ws), ctypes.c_int64(B), ctypes.c_int32(int(training)),
-                                          N.ptr(dparams), N.ptr(dwf), N.ptr(dbf), stream), "bcnf_fold_backward_tail")
+                                          N.ptr(dparams), N.ptr(dwf), N.ptr(dbf),
+                                          None if adam is None else ctypes.byref(adam), stream),
+                "bcnf_fold_backward_tail")
         return dparams, dwf, dbf
 
     @torch.no_grad()
@@ -471,7 +477,7 @@ class FusedStack:
             "tail": lambda: L.bcnf_fold_backward_tail(self._pdesc, N.ptr(pk), N.ptr(slab), N.ptr(x), ldx,
                                                       ctypes.c_int32(X), N.ptr(wf), N.ptr(bf), N.ptr(ws),
                                                       ctypes.c_int64(B), ctypes.c_int32(int(training)),
-                                                      N.ptr(dparams), N.ptr(dwf), N.ptr(dbf), stream),
+                                                      N.ptr(dparams), N.ptr(dwf), N.ptr(dbf), None, stream),
         }
         return self._event_times(calls, iters)
 
@@ -581,9 +587,11 @@ class _FoldNLL(torch.autograd.Function):
     def backward(ctx, dvals):
         x, wf, bf, z, vals = ctx.saved_tensors
         need = ctx.needs_input_grad
+        adam, ctx.stack.pending_adam = ctx.stack.pending_adam, None
         dparams, dwf, dbf = ctx.stack.launch_fold_nll_backward(x, z, dvals.contiguous(), wf, bf, ctx.training,
-                                                               ctx.saved, want_feat=need[2] or need[3],
-                                                               finalize_into=vals if ctx.defer else None)
+                                                               ctx.saved, want_feat=need[2] or need[3] or
+                                                               adam is not None,
+                                                               finalize_into=vals if ctx.defer else None, adam=adam)
         return (None, None, dwf if need[2] else None, dbf if need[3] else None, dparams if need[4] else None,
                 None, None, None, None)
 

@@ -126,6 +126,45 @@ class FusedAdam(torch.optim.Optimizer):
         self._partials_for = None
         return None
 
+    def fold_adam_spec(self, slots, cursor=None, log=None, counter=None, guard=None):
+        """An N.BcnfFoldAdam for the folded backward tail (include/bcnf_amd.h): the update of exactly `slots` =
+        (coupling flat parameter, feature weight, feature bias or None) -- all of this optimizer's parameters, one
+        group -- fused where their gradients are produced, with step()'s bookkeep semantics. None if that does
+        not describe this optimizer."""
+        if len(self.param_groups) != 1:
+            return None
+        group = self.param_groups[0]
+        live = [p for p in slots if p is not None]
+        if {id(p) for p in live} != {id(p) for p in group["params"]} or len(live) != len(group["params"]):
+            return None
+        states = [self._state(p) for p in live]
+        step = states[0]["step"]
+        for st in states[1:]:
+            if st["step"] is not step:
+                st["step"] = step
+        spec = N.BcnfFoldAdam()
+        it = iter(states)
+        for t, p in enumerate(slots):
+            if p is None:
+                continue
+            st = next(it)
+            spec.params[t] = p.data_ptr()
+            spec.exp_avg[t] = st["exp_avg"].data_ptr()
+            spec.exp_avg_sq[t] = st["exp_avg_sq"].data_ptr()
+        b1, b2 = group["betas"]
+        spec.step = step.data_ptr()
+        spec.lr, spec.beta1, spec.beta2 = float(group["lr"]), float(b1), float(b2)
+        spec.eps, spec.weight_decay = float(group["eps"]), float(group["weight_decay"])
+        if cursor is not None:
+            spec.advance_cursor, spec.cursor_modulo = cursor[0].data_ptr(), int(cursor[1])
+        if log is not None:
+            spec.log_values, spec.log_history = log[0].data_ptr(), log[1].data_ptr()
+        spec.done_counter = counter.data_ptr()
+        spec.guard = None if guard is None else guard.data_ptr()
+        self._partials = None            # no clip may follow this step
+        self._partials_for = None
+        return spec
+
     @torch.no_grad()
     def clip_grad_norm_after_step(self, max_norm: float = 1.0, cursor=None, log=None, guard=None):
         """clip_grad_norm_(params, max_norm) for exactly the gradients the last step() consumed (unchanged

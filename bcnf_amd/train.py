@@ -77,14 +77,19 @@ class TrainStep:
             self._hist = torch.zeros((1, 3), dtype=torch.float32, pin_memory=True)
 
     # ------------------------------------------------------------------ step pieces
-    def _forward_backward(self, y, traj, gather=None):
+    def _forward_backward(self, y, traj, gather=None, adam=None):
         self.opt.zero_grad(set_to_none=True)
         if self.fused_loss:
             # reduced in the backward launch; a deferred gather runs inside the pack launch
             vals = self.model.nll_loss(y, traj, defer_reduction=True, gather=gather)
             if self._cot is None or self._cot.device != vals.device:
                 self._cot = torch.tensor([1.0, 0.0, 0.0], device=vals.device)
+            if adam is not None:                          # the optimizer step, inside the folded backward tail
+                self.model.fused.pending_adam = adam(vals)
             torch.autograd.backward(vals, self._cot)      # loss.backward()
+            if adam is not None and self.model.fused.pending_adam is not None:
+                self.model.fused.pending_adam = None
+                raise RuntimeError("bcnf_amd TrainStep: the folded backward did not take the fused Adam update")
             return vals.detach()
         z, h = self.model(y, traj, log_det_J=True, return_features=True)
         nll = inn_nll_loss(z, self.model.log_det_J)
@@ -428,13 +433,47 @@ class TrainStep:
             k = self.epoch_unroll
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
+                slots = self._fold_adam_slots()
                 for i in range(k):
-                    vals = self._forward_backward(*self._gather(defer=True))
-                    self._update(vals, clip=(i == k - 1) or not (self.skip_hidden_clips and self.opt.can_bookkeep()))
+                    hidden = i < k - 1 and self.skip_hidden_clips
+                    sy, st, spec = self._gather(defer=True)
+                    if hidden and slots is not None and self.model._foldable_linear(sy, (st,)) is not None:
+                        # Adam of this step runs inside its folded backward tail (bcnf_fold_backward_tail)
+                        self._forward_backward(sy, st, spec, adam=lambda v: self._fold_adam(slots, v))
+                        continue
+                    vals = self._forward_backward(sy, st, spec)
+                    self._update(vals, clip=not (hidden and self.opt.can_bookkeep()))
             self._multi = (g, k, [p.grad for p in self.params])
             self._bind(self._single_grads)
             self._multi_bound = False
         return self._multi
+
+    # Hidden steps of a folded model update their parameters inside the backward tail (no Adam launch).
+    fuse_adam = True
+
+    def _fold_adam_slots(self):
+        """(coupling flat parameter, feature weight, feature bias) when the fused-Adam tail applies: the model
+        folds its feature Linear and those are exactly this optimizer's parameters; else None."""
+        if not self.fuse_adam or self.world != 1 or not self.fused_loss:
+            return None
+        lin = self.model._fold_linear() if hasattr(self.model, "_fold_linear") else None
+        if lin is None:
+            return None
+        slots = (self.model.fused.flat_param, lin.weight, lin.bias)
+        live = [p for p in slots if p is not None]
+        if [id(p) for p in sorted(live, key=id)] != [id(p) for p in sorted(self.params, key=id)]:
+            return None
+        return slots
+
+    def _fold_adam(self, slots, vals):
+        if self._book is None:
+            self._book = torch.zeros(1, dtype=torch.int32, device=self.params[0].device)
+        cursor = (self._epoch[1], self._epoch[2]) if self._epoch is not None else None
+        log = (vals, self._hist) if self._hist is not None else None
+        spec = self.opt.fold_adam_spec(slots, cursor=cursor, log=log, counter=self._book, guard=self._guard)
+        if spec is None:
+            raise RuntimeError("bcnf_amd TrainStep: the optimizer does not match the fused-Adam slots")
+        return spec
 
     def _bind(self, grads):
         """.grad = the gradient buffers of the graph that ran last (each captured graph owns its own)."""

@@ -151,10 +151,30 @@ int bcnf_fold_nll_forward(const BcnfStackDesc* desc, const void* packed, const f
                           int32_t training,
                           uint64_t* rng_state, void* workspace, int32_t finalize, float* loss_out, int32_t* guard,
                           void* stream);
+/* Adam fused into bcnf_fold_backward_tail (nullable argument): every gradient the tail produces -- the flat coupling
+ * parameters (slot 0), the feature Linear's weight (1) and bias (2, NULL without bias) -- also takes its
+ * torch.optim.Adam update where it is produced, with the end-of-step bookkeeping of bcnf_adam_step_bookkeep
+ * (step count, epoch cursor, logged values; done_counter: device int32, 0 between launches). For a training step
+ * whose clip-after-step cannot be observed (trainer.py:273-275; see bcnf_adam_step_bookkeep): it replaces that
+ * step's Adam launch. The gradients are still written. */
+typedef struct BcnfFoldAdam {
+  float* params[3];
+  float* exp_avg[3];
+  float* exp_avg_sq[3];
+  float* step;
+  double lr, beta1, beta2, eps, weight_decay;
+  int64_t* advance_cursor;
+  int64_t cursor_modulo;
+  const float* log_values;
+  float* log_history;
+  int32_t* done_counter;
+  const int32_t* guard;
+} BcnfFoldAdam;
 int bcnf_fold_backward_tail(const BcnfStackDesc* desc, const void* packed, const void* slab, const float* x,
                             int32_t ldx, int32_t in_features, const float* feat_weight, const float* feat_bias,
                             const void* workspace, int64_t batch, int32_t training, float* dparams,
-                            float* dfeat_weight, float* dfeat_bias, void* stream);
+                            float* dfeat_weight, float* dfeat_bias, const BcnfFoldAdam* adam /* nullable */,
+                            void* stream);
 
 /* Deterministic (fixed-order) reduction of a backward's gradient scratch into dparams, including the
  * W1 condition columns (split-K GEMM of D1 with h). Replaces autograd's implicit batch reduction. */

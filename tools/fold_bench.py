@@ -58,11 +58,11 @@ def main():
         "fold tail": lambda: L.bcnf_fold_backward_tail(st._pdesc, N.ptr(pk), N.ptr(slab), N.ptr(x), ctypes.c_int32(X),
                                                        ctypes.c_int32(X),
                                                        N.ptr(wf), N.ptr(bf), N.ptr(ws), ctypes.c_int64(B),
-                                                       ctypes.c_int32(1), N.ptr(dp), N.ptr(dwf), N.ptr(dbf), stream),
+                                                       ctypes.c_int32(1), N.ptr(dp), N.ptr(dwf), N.ptr(dbf), None, stream),
         "fold tail pad": lambda: L.bcnf_fold_backward_tail(st._pdesc, N.ptr(pk), N.ptr(slab), N.ptr(xp),
                                                            ctypes.c_int32(xp.stride(0)), ctypes.c_int32(X), N.ptr(wf),
                                                            N.ptr(bf), N.ptr(ws), ctypes.c_int64(B), ctypes.c_int32(1),
-                                                           N.ptr(dp), N.ptr(dwf), N.ptr(dbf), stream),
+                                                           N.ptr(dp), N.ptr(dwf), N.ptr(dbf), None, stream),
     }
     for name, fn in calls.items():
         N.check(fn(), name)
