@@ -64,6 +64,7 @@ class TrainStep:
         self._single_grads = None
         self._multi_bound = False
         self._book = None       # Adam's finished-workgroup counter (bcnf_adam_step_bookkeep)
+        self._g2_hidden = None  # data parallel: update segment without the (unobservable) clip
         self._cond_shape = None  # (per-sample condition shape, its size) when the pool rows are padded
         self._epoch = None      # (order, cursor, n_batches, batch) for the device-cursor batch walk
         self._bucket = None     # data parallel: every gradient in one buffer, one all-reduce per step
@@ -269,6 +270,15 @@ class TrainStep:
             with torch.cuda.graph(g2):
                 self._scale_bucket()
                 self._update(vals)
+            # the update segment of a step whose clip-after-step is unobservable (every run_epoch step but the
+            # last: the next step's backward overwrites the gradients): Adam with the bookkeeping, no clip launch
+            if self.skip_hidden_clips and self.opt.can_bookkeep():
+                if self._book is None:
+                    self._book = torch.zeros(1, dtype=torch.int32, device=self.params[0].device)
+                self._g2_hidden = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self._g2_hidden):
+                    self._scale_bucket()
+                    self._update(vals, clip=False)
         self._graphs = (g1, g2, vals)
         self._single_grads = [p.grad for p in self.params]   # what .grad shows after a g1 replay
 
@@ -406,7 +416,7 @@ class TrainStep:
             self._bind(grads)
             self._multi_bound = True
         while i < n:
-            self._replay()
+            self._replay(hidden=i < n - 1)
             i += 1
         torch.cuda.current_stream().synchronize()
         vals = [tuple(r) for r in self._hist[start:start + n].tolist()]
@@ -482,7 +492,7 @@ class TrainStep:
         for p, gr in zip(self.params, grads):
             p.grad = gr
 
-    def _replay(self):
+    def _replay(self, hidden: bool = False):
         if self._multi_bound:
             self._bind(self._single_grads)
             self._multi_bound = False
@@ -490,7 +500,7 @@ class TrainStep:
         g1.replay()
         if g2 is not None:
             self._reduce_bucket()           # the one collective of the step, between the two graph segments
-            g2.replay()
+            (self._g2_hidden if hidden and self._g2_hidden is not None else g2).replay()
         return vals
 
 
