@@ -369,6 +369,9 @@ class FusedStack:
 
     # A BcnfFoldAdam for the next folded backward (TrainStep, multi-step graphs): consumed by that launch.
     pending_adam = None
+    # (bucket, (flat offset, feature W offset, feature b offset)): TrainStep's data-parallel gradient bucket, which
+    # the folded backward writes its gradients into.
+    grad_bucket = None
 
     def launch_fold_nll_backward(self, x, z, dvals, wf, bf, training: bool, saved, want_feat: bool,
                                  finalize_into=None, adam=None):
@@ -381,9 +384,18 @@ class FusedStack:
         stream = N.stream_handle(dev)
         sb = N.query_i64(L.bcnf_fold_slab_bytes, self._pdesc, ctypes.c_int32(X), ctypes.c_int64(B))
         slab = torch.empty(max(sb // 4, 1), dtype=torch.float32, device=dev)
-        dparams = torch.empty_like(self.flat)
-        dwf = torch.empty_like(wf) if want_feat else None
-        dbf = torch.empty_like(bf) if (want_feat and bf is not None) else None
+        gb = self.grad_bucket
+        if gb is not None and want_feat:
+            # data parallel (TrainStep): the gradients land in the all-reduce bucket itself, as fresh views that
+            # autograd adopts as .grad, so no bucket copy follows the backward
+            bucket, offs = gb
+            dparams = bucket.narrow(0, offs[0], self.flat.numel()).view_as(self.flat)
+            dwf = bucket.narrow(0, offs[1], wf.numel()).view_as(wf)
+            dbf = bucket.narrow(0, offs[2], bf.numel()).view_as(bf) if bf is not None else None
+        else:
+            dparams = torch.empty_like(self.flat)
+            dwf = torch.empty_like(wf) if want_feat else None
+            dbf = torch.empty_like(bf) if (want_feat and bf is not None) else None
         rng = self.rng_state() if (finalize_into is not None and training and self.cfg.dropout > 0.0) else None
         rc = L.bcnf_nll_backward(self._pdesc, N.ptr(pk), N.ptr(x), N.ptr(z), N.ptr(dvals), ctypes.c_int64(B),
                                  ctypes.c_int32(int(training)), N.ptr(ws), None, None, None, N.ptr(slab),

@@ -68,6 +68,7 @@ class TrainStep:
         self._cond_shape = None  # (per-sample condition shape, its size) when the pool rows are padded
         self._epoch = None      # (order, cursor, n_batches, batch) for the device-cursor batch walk
         self._bucket = None     # data parallel: every gradient in one buffer, one all-reduce per step
+        self._packed_inplace = False   # the last bucket pack found the gradients already in place
         self._host_cursor = 0   # host mirror of the epoch cursor (the history row of the next step)
         dev = self.params[0].device
         self._guard = None
@@ -108,7 +109,33 @@ class TrainStep:
         if self._bucket is None:
             n = sum(g.numel() for g in grads)
             self._bucket = torch.empty(n, dtype=torch.float32, device=grads[0].device)
-        torch.cat([g.reshape(-1) for g in grads], out=self._bucket)
+        base, off, inplace = self._bucket.data_ptr(), 0, True
+        for g in grads:                     # the folded backward wrote straight into the bucket (_setup_bucket)
+            inplace = inplace and g.is_contiguous() and g.data_ptr() == base + 4 * off
+            off += g.numel()
+        self._packed_inplace = inplace
+        if not inplace:
+            torch.cat([g.reshape(-1) for g in grads], out=self._bucket)
+
+    def _setup_bucket(self):
+        """Data parallel: allocate the gradient bucket up front and, when the model folds its feature Linear, let
+        the folded backward write its gradients into it (FusedStack.grad_bucket): no copy before the all-reduce."""
+        if self.world == 1 or self._bucket is not None:
+            return
+        dev = self.params[0].device
+        self._bucket = torch.empty(sum(p.numel() for p in self.params), dtype=torch.float32, device=dev)
+        lin = self.model._fold_linear() if hasattr(self.model, "_fold_linear") else None
+        if lin is None or not self.fused_loss:
+            return
+        offs, off = {}, 0
+        for p in self.params:
+            offs[id(p)] = off
+            off += p.numel()
+        fp = self.model.fused.flat_param
+        if len(self.params) != (3 if lin.bias is not None else 2) or id(fp) not in offs or id(lin.weight) not in offs:
+            return
+        self.model.fused.grad_bucket = (self._bucket, (offs[id(fp)], offs[id(lin.weight)],
+                                                       offs[id(lin.bias)] if lin.bias is not None else 0))
 
     def _bind_grads(self):
         """Every .grad becomes a view of the (reduced) bucket: Adam and the clip read it in place."""
@@ -161,6 +188,7 @@ class TrainStep:
 
     # ------------------------------------------------------------------ eager / graph
     def eager_step(self, y, traj, gather=None):
+        self._setup_bucket()
         vals = self._forward_backward(y, traj, gather)
         self._allreduce()
         self._update(vals)
@@ -236,6 +264,7 @@ class TrainStep:
     def _build_graphs(self, y, traj, idx=None, warmup: int = 2):
         """Warm up (allocations, kernel attributes) on a side stream, undo the warm-up's updates, then
         capture: the first step() applies exactly one update, like every later one."""
+        self._setup_bucket()
         self._static = (y.clone(), traj.clone(), None if idx is None else idx.clone())
         sy, st, _ = self._static
         indexed = idx is not None

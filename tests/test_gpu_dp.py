@@ -58,7 +58,7 @@ def _worker(rank, world, port, cfg, q, mode="step"):
         else:
             for _ in range(2):
                 step.step(y[rank * n:(rank + 1) * n].cuda(), t[rank * n:(rank + 1) * n].cuda())
-        q.put((rank, [p.detach().cpu().numpy() for p in m.parameters()]))
+        q.put((rank, ([p.detach().cpu().numpy() for p in m.parameters()], step._packed_inplace)))
     except Exception:
         q.put((rank, traceback.format_exc()))
     finally:
@@ -79,6 +79,9 @@ def test_two_rank_step_equals_union_batch_step(cfg, mode):
         p.join(timeout=60)
     for r in (0, 1):
         assert not isinstance(res[r], str), res[r]
+        res[r], inplace = res[r]
+        # the folded backward (small family) writes its gradients into the all-reduce bucket: no copy
+        assert inplace == (cfg is CFG)
     from bcnf_amd.train import TrainStep
     m = _model(cfg)
     step = TrainStep(m, lr=1e-3, capture=True)
