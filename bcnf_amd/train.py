@@ -16,14 +16,20 @@
 
 MI355X specifics:
 * hybrid_weight == 0 (every shipped config): forward + loss are ONE fused launch (`model.nll_loss`,
-  bcnf_nll_forward) and loss.backward() is the fused NLL backward + deterministic slab reduce; the
-  feature network's nn.Linear runs on the library's MFMA GEMMs. No elementwise loss kernels.
+  bcnf_nll_forward) and loss.backward() is the fused NLL backward + deterministic slab reduce. A feature
+  network that is one nn.Linear (trajectory_FC_small) is folded into the condition projection (no h, no
+  dL/dh); other feature networks run on the library's MFMA GEMMs / PyTorch-ROCm.
 * the coupling-stack parameters are ONE flat leaf (model.flat_parameters()); Adam is ONE launch over
   all parameters (bcnf_amd.optim.FusedAdam) that also emits the squared-gradient partials, so the
   clip after the step is one more launch.
 * the whole step is captured once into a HIP graph and replayed (world > 1: the RCCL all-reduce runs
   between two captured segments). `step_indexed` also captures the batch gather from a
-  device-resident pool, so a replay needs only the index copy.
+  device-resident pool (inside the folded path's pack launch), so a replay needs only the index copy.
+* `run_epoch` replays 8 device-driven steps per graph. Only the last step of such a graph clips: the
+  clip after the step (trainer.py:275) scales gradients the next step's backward overwrites and its norm
+  is discarded, so every other step ("hidden") runs Adam with the bookkeeping instead -- on the folded
+  path inside the backward tail itself (BcnfFoldAdam), with no Adam launch. run_epoch equals the per-step
+  loop bit for bit (tests/test_gpu_train.py).
 * the three logged values are stored by the clip launch straight into pinned host memory (a history
   row per batch of the epoch), so no copy node and, with `run_epoch`, no host sync per step: the epoch's
   steps are replayed back to back and the Trainer's per-batch divergence check (trainer.py:168) runs
