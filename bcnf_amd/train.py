@@ -71,6 +71,7 @@ class TrainStep:
         self._multi_bound = False
         self._book = None       # Adam's finished-workgroup counter (bcnf_adam_step_bookkeep)
         self._g2_hidden = None  # data parallel: update segment without the (unobservable) clip
+        self._g21 = None        # data parallel: hidden update + the next step's forward/backward, one graph
         self._cond_shape = None  # (per-sample condition shape, its size) when the pool rows are padded
         self._epoch = None      # (order, cursor, n_batches, batch) for the device-cursor batch walk
         self._bucket = None     # data parallel: every gradient in one buffer, one all-reduce per step
@@ -314,6 +315,19 @@ class TrainStep:
                 with torch.cuda.graph(self._g2_hidden):
                     self._scale_bucket()
                     self._update(vals, clip=False)
+                if indexed:
+                    # step i's hidden update and step i+1's gather / forward / backward / bucket in ONE graph: one
+                    # inter-graph idle per step instead of two (run_epoch); step i+1's logged values are copied
+                    # into g1's buffer, which every update segment logs from
+                    self._g21 = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(self._g21):
+                        self._scale_bucket()
+                        self._update(vals, clip=False)
+                        sy2, st2, spec2 = self._gather(defer=True)
+                        vals2 = self._forward_backward(sy2, st2, spec2)
+                        self._pack_grads()
+                        vals.copy_(vals2)
+                    self._bind_grads()
         self._graphs = (g1, g2, vals)
         self._single_grads = [p.grad for p in self.params]   # what .grad shows after a g1 replay
 
@@ -450,6 +464,15 @@ class TrainStep:
                 i += k
             self._bind(grads)
             self._multi_bound = True
+        if self.world > 1 and self._g21 is not None and n >= 2:
+            g1, g2, _ = self._graphs          # g1, then (all-reduce, g21) per later step, then the last update
+            g1.replay()
+            for _ in range(n - 1):
+                self._reduce_bucket()
+                self._g21.replay()
+            self._reduce_bucket()
+            g2.replay()
+            i = n
         while i < n:
             self._replay(hidden=i < n - 1)
             i += 1

@@ -22,6 +22,9 @@ WIDE = {"global": CFG["global"], "feature_networks": CFG["feature_networks"],
                              "dropout": 0.0, "act_norm": True}}}
 
 
+STEPS = 3      # run_epoch at world 2: g1, then (all-reduce, merged update + next step) twice, then the last update
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -53,10 +56,16 @@ def _worker(rank, world, port, cfg, q, mode="step"):
         n = y.shape[0] // world
         if mode == "epoch":     # bench.py's N > 1 path: device pool, epoch order, run_epoch (gather in the graph)
             step.set_pool(y[rank * n:(rank + 1) * n].cuda(), t[rank * n:(rank + 1) * n].cuda())
-            step.set_epoch(torch.arange(n, device="cuda").repeat(2), n)
-            step.run_epoch()
+            step.set_epoch(torch.arange(n, device="cuda").repeat(STEPS), n)
+            logged = step.run_epoch()
+            # the logged (loss, nll, mse) of every step == those of the same steps through step()
+            m2 = _model(cfg)
+            s2 = TrainStep(m2, lr=1e-3, capture=True)
+            s2.broadcast_parameters()
+            ref = [s2.step(y[rank * n:(rank + 1) * n].cuda(), t[rank * n:(rank + 1) * n].cuda()) for _ in range(STEPS)]
+            assert logged == ref, (logged, ref)
         else:
-            for _ in range(2):
+            for _ in range(STEPS):
                 step.step(y[rank * n:(rank + 1) * n].cuda(), t[rank * n:(rank + 1) * n].cuda())
         q.put((rank, ([p.detach().cpu().numpy() for p in m.parameters()], step._packed_inplace)))
     except Exception:
@@ -86,7 +95,7 @@ def test_two_rank_step_equals_union_batch_step(cfg, mode):
     m = _model(cfg)
     step = TrainStep(m, lr=1e-3, capture=True)
     y, t = _data()
-    for _ in range(2):
+    for _ in range(STEPS):
         step.step(y.cuda(), t.cuda())
     ref = [p.detach().cpu() for p in m.parameters()]
     for a, b, c in zip(res[0], res[1], ref):
