@@ -1760,15 +1760,6 @@ size_t lds_floor_bytes() {
   return v;
 }
 
-// Experiment knob (env BCNF_TAIL_ROLES, bit mask, default all): 1 dh, 2 slab reduce, 4 W1h split-K, 8 its reduce.
-// Timing only (tools/tail_bench.py); results are incomplete with any bit cleared. Read once.
-int tail_roles() {
-  static int v = [] {
-    const char* e = getenv("BCNF_TAIL_ROLES");
-    return e ? atoi(e) : 15;
-  }();
-  return v;
-}
 
 template <typename K>
 int launch_lds(K kernel, size_t& lds) {
@@ -2073,11 +2064,7 @@ int bcnf_backward_tail(const BcnfStackDesc* desc, const void* packed, const void
   const long long n_dw = (long long)G.gx_dw * splits;
   size_t lds = dw1h_lds_bytes(L);
   if (dh_lds_bytes() > lds) lds = dh_lds_bytes();
-  const int roles = tail_roles();
-  if (!(roles & 1)) G.n_dh = 0;
-  if (!(roles & 2)) G.n_red = 0;
-  const long long n_dw_run = (roles & 4) ? n_dw : 0;
-  const dim3 grid((unsigned)(G.n_dh + G.n_red + n_dw_run));
+  const dim3 grid((unsigned)(G.n_dh + G.n_red + n_dw));
   if (vec_rows(L, h)) {
     if ((rc = launch_lds(k_bwd_tail<true>, lds))) return rc;
     hipLaunchKernelGGL(k_bwd_tail<true>, grid, dim3(BCNF_WG), lds, st, L, L, G, (const float*)packed, d1, h,
@@ -2088,7 +2075,6 @@ int bcnf_backward_tail(const BcnfStackDesc* desc, const void* packed, const void
                        (long long)batch, dh, (const float*)slab, S, nwg, dparams, rps, work);
   }
   if ((rc = check_launch())) return rc;
-  if (!(roles & 8)) return BCNF_OK;
   const long long outs = (long long)L.nb * 16 * L.Cp;
   hipLaunchKernelGGL(k_dw1h_reduce, dim3((unsigned)((outs + BCNF_WG - 1) / BCNF_WG)), dim3(BCNF_WG), 0, st, L,
                      (const float*)work, (int)splits, dparams);
