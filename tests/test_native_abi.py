@@ -156,3 +156,49 @@ def test_two_way_parameter_layout_matches_module_tree():
     assert m.fused.flat.numel() == m.fused.counts()[0] == 3 * (mlp_a + mlp_b) + 2 * 38
     w_b = m.layers[1].nn_b.nn[0].weight
     assert w_b.data_ptr() == m.fused.flat.data_ptr() + (38 + mlp_a) * 4
+
+
+def _c_layout(struct, fields):
+    """sizeof / offsetof of a struct of include/bcnf_amd.h as the C compiler lays it out (gcc, host)."""
+    import subprocess
+    import tempfile
+    body = "\n".join(f'  printf("%zu\\n", offsetof({struct}, {f}));' for f in fields)
+    src = (f'#include <stddef.h>\n#include <stdio.h>\n#include "bcnf_amd.h"\nint main(void) {{\n'
+           f'  printf("%zu\\n", sizeof({struct}));\n{body}\n  return 0;\n}}\n')
+    with tempfile.TemporaryDirectory() as d:
+        c, exe = os.path.join(d, "l.c"), os.path.join(d, "l")
+        open(c, "w").write(src)
+        subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), c, "-o", exe])
+        out = [int(v) for v in subprocess.check_output([exe]).split()]
+    return out[0], out[1:]
+
+
+@pytest.mark.parametrize("name", ["BcnfStackDesc", "BcnfGather2", "BcnfFoldAdam"])
+def test_ctypes_structs_match_the_c_abi(name):
+    """The ctypes mirrors in bcnf_amd/_native.py have the size and field offsets of the header's structs."""
+    from bcnf_amd import _native as N
+    cls = getattr(N, name)
+    fields = [f[0] for f in cls._fields_]
+    size, offs = _c_layout(name, fields)
+    assert ctypes.sizeof(cls) == size
+    assert [getattr(cls, f).offset for f in fields] == offs
+
+
+def test_fold_adam_spec_host_logic():
+    """FusedAdam.fold_adam_spec: pointers of each slot's parameter / moments, the shared step, hyper-parameters;
+    None unless the slots are exactly the optimizer's parameters."""
+    from bcnf_amd.optim import FusedAdam
+    flat, w, b = (torch.nn.Parameter(torch.zeros(n)) for n in (10, 6, 3))
+    opt = FusedAdam([flat, w, b], lr=2e-4)
+    counter = torch.zeros(1, dtype=torch.int32)
+    spec = opt.fold_adam_spec((flat, w, b), counter=counter)
+    for t, p in enumerate((flat, w, b)):
+        st = opt.state[p]
+        assert spec.params[t] == p.data_ptr()
+        assert spec.exp_avg[t] == st["exp_avg"].data_ptr() and spec.exp_avg_sq[t] == st["exp_avg_sq"].data_ptr()
+        assert st["step"] is opt.state[flat]["step"]
+    assert spec.step == opt.state[flat]["step"].data_ptr() and spec.done_counter == counter.data_ptr()
+    assert (spec.lr, spec.beta1, spec.beta2, spec.eps) == (2e-4, 0.9, 0.999, 1e-8)
+    assert opt.fold_adam_spec((flat, w, None), counter=counter) is None       # b would not be updated
+    other = torch.nn.Parameter(torch.zeros(2))
+    assert opt.fold_adam_spec((flat, w, other), counter=counter) is None
