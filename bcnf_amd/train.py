@@ -550,6 +550,15 @@ class TrainStep:
         for p, gr in zip(self.params, grads):
             p.grad = gr
 
+    def prepare_epoch(self, n_steps: int):
+        """Capture, without running anything, every graph a later run_epoch(n_steps) replays (the step graphs and,
+        at world 1, the multi-step graph), so no capture lands inside a timed region."""
+        if self._epoch is None or not self.capture or not self.fused_loss:
+            return
+        self._ensure_epoch_graphs()
+        if self.world == 1 and self.epoch_unroll > 1 and n_steps >= self.epoch_unroll:
+            self._multi_graph()
+
     def _replay(self, hidden: bool = False):
         if self._multi_bound:
             self._bind(self._single_grads)

@@ -213,6 +213,8 @@ def main():
             return vals[-1] if vals else None
 
     run_range(0, args.warmup)
+    if not (args.indexed or args.per_step_sync):
+        step.prepare_epoch(args.steps)      # graph captures (host work) stay out of the timed region at any --warmup
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -319,6 +321,7 @@ def main_wide(args):
     batches = [data.next_indices() for _ in range(args.warmup + args.steps)]
     step.set_epoch(torch.cat(batches), args.batch)
     step.run_epoch(args.warmup)
+    step.prepare_epoch(args.steps)          # no graph capture inside the timed region
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
