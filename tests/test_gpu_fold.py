@@ -204,3 +204,29 @@ def test_gather_inside_pack_launch_is_exact(g1, epoch):
     assert v0 == v1
     for a, b in zip(p0 + g0, p1 + g1_):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("train", [False, True])
+def test_fold_without_feature_bias(g1, train):
+    """A feature Linear without bias (bf = NULL through the fold kernels) == the unfolded path."""
+    gen = torch.Generator().manual_seed(17)
+    B = 257
+    y = torch.randn(B, 19, generator=gen).to(DEV)
+    traj = torch.randn(B, 30, 3, generator=gen).to(DEV)
+    m = _model(FC_SMALL_CFG, golden_sd(g1), train=train)
+    m.feature_network_stack.feature_networks[1].nn[0].bias = None
+    out = []
+    for fold in (True, False):
+        m.fold_features = fold
+        m.zero_grad(set_to_none=True)
+        m.fused.flat_param.grad = None
+        m.fused.set_seed(8)
+        vals = m.nll_loss(y, traj)
+        torch.autograd.backward(vals, torch.tensor([1.0, 0.0, 0.0], device=DEV))
+        lin = m.feature_network_stack.feature_networks[1].nn[0]
+        out.append((vals.detach().clone(), m.fused.flat_param.grad.clone(), lin.weight.grad.clone()))
+    (v1, g1_, w1), (v0, g0, w0) = out
+    assert abs(v1[0].item() - v0[0].item()) <= 2e-6 * abs(v0[0].item()) + 1e-6
+    for a, b, what in ((g1_, g0, "stack"), (w1, w0, "feature W")):
+        ok, err = close(a.cpu(), b.cpu(), rtol=1e-4, floor=1e-5)
+        assert ok, (what, err)
