@@ -35,6 +35,7 @@ EXPORTS = (
     "bcnf_wide_supported", "bcnf_wide_param_count", "bcnf_wide_packed_bytes", "bcnf_wide_workspace_bytes", "bcnf_wide_inverse_scratch_bytes",
     "bcnf_wide_pack", "bcnf_wide_forward", "bcnf_wide_nll_finalize", "bcnf_wide_backward", "bcnf_wide_inverse",
     "bcnf_wide_gemm_test", "bcnf_wide_force_tiling", "bcnf_wide_debug_phases", "bcnf_rank_count",
+    "bcnf_guard_check_global",
 )
 MAX_TENSORS = 48
 
@@ -128,6 +129,7 @@ def _bind(lib):
         "bcnf_gather_rows2": (_i32, [_vp, _i64, _vp, _i32, _vp, _vp, _i32, _vp, _vp]),
         "bcnf_gather_batch": (_i32, [_vp, _vp, _i64, _vp, _i32, _vp, _vp, _i32, _vp, _vp]),
         "bcnf_advance_counters": (_i32, [_vp, _vp, _i64, _vp]),
+        "bcnf_guard_check_global": (_i32, [_vp, _vp, _vp]),
         "bcnf_stack_forward": (_i32, [_pdesc, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _vp]),
         "bcnf_stack_backward": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
         "bcnf_stack_inverse": (_i32, [_pdesc, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i32, _vp, _vp, _vp]),

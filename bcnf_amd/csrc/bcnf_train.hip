@@ -475,6 +475,18 @@ int bcnf_advance_counters(float* step, int64_t* cursor, int64_t n_batches, void*
   return launched();
 }
 
+__global__ void k_guard_global(const float* __restrict__ vals, int32_t* guard) {
+  if (threadIdx.x != 0 || guard[BCNF_GUARD_HALTED] || !guard[BCNF_GUARD_CHECK_GLOBAL]) return;
+  const float loss = vals[0];
+  if (loss > 1e5f || isnan(loss)) guard[BCNF_GUARD_DIVERGED] = 1;
+}
+
+int bcnf_guard_check_global(const float* global_values, int32_t* guard, void* stream) {
+  if (!global_values || !guard) return BCNF_ERR_ARG;
+  hipLaunchKernelGGL(k_guard_global, dim3(1), dim3(64), 0, (hipStream_t)stream, global_values, guard);
+  return launched();
+}
+
 int bcnf_linear_forward(const float* x, const float* weight, const float* bias, int64_t rows, int32_t in_features,
                         int32_t out_features, float* y, void* stream) {
   if (rows < 0 || in_features < 1 || out_features < 1) return BCNF_ERR_ARG;

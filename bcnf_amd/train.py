@@ -46,7 +46,7 @@ from bcnf_amd.errors import TrainingDivergedError
 from bcnf_amd.optim import FusedAdam, clip_grad_norm_
 from bcnf_amd.utils import inn_nll_loss
 
-GUARD_CHECK, GUARD_DIVERGED, GUARD_HALTED, GUARD_WORDS = 0, 1, 2, 4    # include/bcnf_amd.h
+GUARD_CHECK, GUARD_DIVERGED, GUARD_HALTED, GUARD_CHECK_GLOBAL, GUARD_WORDS = 0, 1, 2, 3, 4    # include/bcnf_amd.h
 
 
 class TrainStep:
@@ -68,13 +68,15 @@ class TrainStep:
         self._pool = None
         self._multi = None      # (graph, steps, grads): run_epoch's multi-step graph (world 1)
         self._single_grads = None
-        self._multi_bound = False
+        self._rebind = False    # .grad currently points at buffers other than the single-step graph's
         self._book = None       # Adam's finished-workgroup counter (bcnf_adam_step_bookkeep)
         self._g2_hidden = None  # data parallel: update segment without the (unobservable) clip
         self._g21 = None        # data parallel: hidden update + the next step's forward/backward, one graph
         self._cond_shape = None  # (per-sample condition shape, its size) when the pool rows are padded
         self._epoch = None      # (order, cursor, n_batches, batch) for the device-cursor batch walk
         self._bucket = None     # data parallel: every gradient in one buffer, one all-reduce per step
+        self._n_grad = 0        # gradient floats in the bucket; the 3 logged values follow (reduced with them)
+        self._gvals = None      # data parallel: the all-reduced (loss, nll, mse) -- a view of the bucket tail
         self._packed_inplace = False   # the last bucket pack found the gradients already in place
         self._host_cursor = 0   # host mirror of the epoch cursor (the history row of the next step)
         dev = self.params[0].device
@@ -114,23 +116,28 @@ class TrainStep:
         if any(g is None for g in grads):
             raise RuntimeError("bcnf_amd TrainStep: a parameter received no gradient")
         if self._bucket is None:
-            n = sum(g.numel() for g in grads)
-            self._bucket = torch.empty(n, dtype=torch.float32, device=grads[0].device)
+            self._alloc_bucket(grads[0].device)
         base, off, inplace = self._bucket.data_ptr(), 0, True
         for g in grads:                     # the folded backward wrote straight into the bucket (_setup_bucket)
             inplace = inplace and g.is_contiguous() and g.data_ptr() == base + 4 * off
             off += g.numel()
         self._packed_inplace = inplace
         if not inplace:
-            torch.cat([g.reshape(-1) for g in grads], out=self._bucket)
+            torch.cat([g.reshape(-1) for g in grads], out=self._bucket[:self._n_grad])
+
+    def _alloc_bucket(self, dev):
+        """The gradient bucket + a 4-float tail holding the step's logged (loss, nll, mse): the one all-reduce of the
+        step also averages them, so every rank logs -- and judges divergence on -- the global loss."""
+        self._n_grad = sum(p.numel() for p in self.params)
+        self._bucket = torch.zeros(self._n_grad + 4, dtype=torch.float32, device=dev)
+        self._gvals = self._bucket[self._n_grad:self._n_grad + 3]
 
     def _setup_bucket(self):
         """Data parallel: allocate the gradient bucket up front and, when the model folds its feature Linear, let
         the folded backward write its gradients into it (FusedStack.grad_bucket): no copy before the all-reduce."""
         if self.world == 1 or self._bucket is not None:
             return
-        dev = self.params[0].device
-        self._bucket = torch.empty(sum(p.numel() for p in self.params), dtype=torch.float32, device=dev)
+        self._alloc_bucket(self.params[0].device)
         lin = self.model._fold_linear() if hasattr(self.model, "_fold_linear") else None
         if lin is None or not self.fused_loss:
             return
@@ -160,18 +167,33 @@ class TrainStep:
     def _scale_bucket(self):
         self._bucket.mul_(1.0 / self.world)
 
-    def _allreduce(self):
+    def _allreduce(self, vals=None):
+        """Eager data-parallel exchange; returns the all-reduced logged values (or `vals` at world 1)."""
         if self.world == 1:
-            return
+            return vals
         self._pack_grads()
+        if vals is not None:
+            self._gvals.copy_(vals)
         self._reduce_bucket()
         self._scale_bucket()
         self._bind_grads()
+        return self._gvals if vals is not None else None
+
+    def _check_global(self):
+        """Data parallel: the divergence guard judged on the all-reduced loss (bcnf_guard_check_global)."""
+        if self.world == 1 or self._guard is None:
+            return
+        from bcnf_amd import _native as N
+        N.check(N.lib().bcnf_guard_check_global(N.ptr(self._gvals), N.ptr(self._guard),
+                                                N.stream_handle(self._gvals.device)), "bcnf_guard_check_global")
 
     def _update(self, vals=None, clip: bool = True):
         """Adam, then clip_grad_norm_ after the step (trainer.py:273-275); the clip launch also advances the
         Adam step count and, in epoch mode, the batch cursor, and stores the logged values into the pinned
         history (end-of-step bookkeeping, no extra launch)."""
+        if self.world > 1 and vals is not None:
+            vals = self._gvals              # every rank logs the global values and halts on the same step
+            self._check_global()
         cursor = (self._epoch[1], self._epoch[2]) if self._epoch is not None else None
         log = (vals, self._hist) if (vals is not None and self._hist is not None) else None
         if not clip:
@@ -197,8 +219,9 @@ class TrainStep:
     def eager_step(self, y, traj, gather=None):
         self._setup_bucket()
         vals = self._forward_backward(y, traj, gather)
-        self._allreduce()
+        vals = self._allreduce(vals)
         self._update(vals)
+        self._rebind = self._graphs is not None     # .grad now holds this step's buffers, not a graph's
         return vals
 
     def _gather(self, defer: bool = False):
@@ -299,6 +322,7 @@ class TrainStep:
                 self._update(vals)
             else:
                 self._pack_grads()          # the bucket copy is part of the captured step
+                self._gvals.copy_(vals)     # the logged values travel with the gradients
         g2 = None
         if self.world > 1:
             self._bind_grads()              # the update reads the reduced bucket
@@ -326,6 +350,7 @@ class TrainStep:
                         sy2, st2, spec2 = self._gather(defer=True)
                         vals2 = self._forward_backward(sy2, st2, spec2)
                         self._pack_grads()
+                        self._gvals.copy_(vals2)
                         vals.copy_(vals2)
                     self._bind_grads()
         self._graphs = (g1, g2, vals)
@@ -350,6 +375,10 @@ class TrainStep:
         if self._graphs is None:
             self._build_graphs(y, traj)
         sy, st, _ = self._static
+        if sy is None or y.shape != sy.shape or traj.shape != st.shape:
+            # a batch of another size (the DataLoader's last, drop_last=False): the captured graph holds buffers of
+            # the first batch's size, so this one runs eagerly on the same kernels and optimizer state
+            return self.eager_step(y, traj)
         sy.copy_(y, non_blocking=True)
         st.copy_(traj, non_blocking=True)
         return self._replay()
@@ -379,14 +408,27 @@ class TrainStep:
         if self._pool is None:
             raise RuntimeError("step_indexed() needs set_pool()")
         idx = idx.to(dtype=torch.int64).contiguous()
+        self._check_indices(idx)
         if not self.capture:
             self._static = (None, None, idx)
             return tuple(self.eager_step(*self._gather()).tolist())
         if self._graphs is None:
             self._build_graphs(*self._pool_rows(idx), idx=idx)
+        if self._static[2] is None or idx.shape != self._static[2].shape:
+            return tuple(self.eager_step(*self._pool_rows(idx)).tolist())     # another batch size: eager
         self._static[2].copy_(idx, non_blocking=True)
         self._replay()
         return self._host_values()
+
+    def _check_indices(self, idx):
+        """Pool indices in range (the reference's DataLoader raises IndexError; the device gather would read out of
+        bounds). One host round trip, before anything is launched."""
+        if idx.numel() == 0:
+            return
+        lo, hi = torch.aminmax(idx)
+        n = self._pool[0].shape[0]
+        if int(lo) < 0 or int(hi) >= n:
+            raise IndexError(f"bcnf_amd TrainStep: batch index out of range [0, {n}) (got {int(lo)}..{int(hi)})")
 
     # ------------------------------------------------------------------ device-resident epoch order
     def set_epoch(self, order, batch: int):
@@ -398,7 +440,11 @@ class TrainStep:
         order = order.to(dtype=torch.int64).contiguous()
         nb = order.numel() // batch
         if nb < 1 or order.numel() != nb * batch:
-            raise ValueError("set_epoch: order must hold a whole number of batches")
+            # whole batches only: a ragged last batch (drop_last=False) goes through step_indexed, which runs a
+            # batch of another size eagerly
+            raise ValueError(f"set_epoch: order must hold a whole number of batches ({order.numel()} indices, "
+                             f"batch {batch}); pass the remainder to step_indexed()")
+        self._check_indices(order)
         if self._epoch is None:
             if self._graphs is not None:
                 raise RuntimeError("set_epoch() must precede the first step of a non-epoch TrainStep")
@@ -447,15 +493,17 @@ class TrainStep:
         if n == 0:
             return []
         if not self.capture or not self.fused_loss:    # per-step host check (the device guard sits in
-            out = [self.step_epoch() for _ in range(n)]   # the fused loss finalize)
-            for i, v in enumerate(out):
+            out = []                                     # the fused loss finalize), right after each update
+            for i in range(n):                           # as trainer.py:166-168 does
+                v = self.step_epoch()
+                out.append(v)
                 if check_divergence and (v[0] > 1e5 or math.isnan(v[0])):
                     raise TrainingDivergedError(f"Loss exploded to {v[0]} at batch {start + i}")
             return out
         self._ensure_epoch_graphs()
         self._guard.zero_()
-        if check_divergence:
-            self._guard[GUARD_CHECK] = 1
+        if check_divergence:        # data parallel: judged on the all-reduced loss, the same on every rank
+            self._guard[GUARD_CHECK if self.world == 1 else GUARD_CHECK_GLOBAL] = 1
         i = 0
         if self.world == 1 and self.epoch_unroll > 1 and n >= self.epoch_unroll:
             g, k, grads = self._multi_graph()
@@ -463,7 +511,7 @@ class TrainStep:
                 g.replay()
                 i += k
             self._bind(grads)
-            self._multi_bound = True
+            self._rebind = True
         if self.world > 1 and self._g21 is not None and n >= 2:
             g1, g2, _ = self._graphs          # g1, then (all-reduce, g21) per later step, then the last update
             g1.replay()
@@ -513,7 +561,7 @@ class TrainStep:
                     self._update(vals, clip=not (hidden and self.opt.can_bookkeep()))
             self._multi = (g, k, [p.grad for p in self.params])
             self._bind(self._single_grads)
-            self._multi_bound = False
+            self._rebind = False
         return self._multi
 
     # Hidden steps of a folded model update their parameters inside the backward tail (no Adam launch).
@@ -560,9 +608,9 @@ class TrainStep:
             self._multi_graph()
 
     def _replay(self, hidden: bool = False):
-        if self._multi_bound:
+        if self._rebind:
             self._bind(self._single_grads)
-            self._multi_bound = False
+            self._rebind = False
         g1, g2, vals = self._graphs
         g1.replay()
         if g2 is not None:

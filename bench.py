@@ -7,14 +7,18 @@ weight-gradient GEMM], (N>1: RCCL all-reduce of the gradients), Adam step (one f
 after the step, one host sync for the three logged losses. The step is one HIP-graph replay.
 Synthetic ballistic trajectories (bcnf_amd/data.py), device-resident, pre-shuffled; dropout active.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]    (N>1: launched by torch.distributed.run)
-Prints ONE JSON line on rank 0.
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+N>1: either launched by torch.distributed.run (RANK / WORLD_SIZE in the environment), or run directly, in which
+case this process -- before it touches the GPU -- starts `torch.distributed.run --nproc-per-node N` on itself as a
+child process and exits with the child's status. Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
 import math
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -90,18 +94,86 @@ def parse():
     ap.add_argument("--indexed", action="store_true", help="per-step index copy instead of the device epoch cursor")
     ap.add_argument("--per-step-sync", action="store_true",
                     help="one host sync + logged-value read per step (the Trainer loop shape) instead of run_epoch")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary figures (Trainer loop shape, unchanged-Trainer DataLoader)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="only bring up the N-rank process group (gloo without a GPU) and report the ranks seen")
     return ap.parse_args()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`python bench.py --gpus N` (N > 1) outside torch.distributed.run: run N fresh worker processes through
+    torch.distributed.run as a CHILD of this process (which has not touched the GPU: nothing before this point
+    initialises HIP) and exit with its status. Returns when this process is itself a rank (or N == 1)."""
+    if "WORLD_SIZE" in os.environ or args.gpus <= 1:
+        return
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd, env=env))
+
+
+def host_cores():
+    """CPU cores this process may use: the scheduler affinity set, capped by a cgroup CPU quota (the GPU box's
+    16-CPU share of a larger machine) -- what torch.set_num_threads can actually occupy."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit():
+        n = min(n, int(omp))
+    return max(1, n)
 
 
 def init_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.launch_check and not torch.cuda.is_available():
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
     return world, rank, local
+
+
+def ranks_seen(world, device):
+    """Number of ranks that took part in the timed run (an all-reduce of ones), reported in the JSON line."""
+    if world == 1:
+        return 1
+    t = torch.ones(1, device=device)
+    dist.all_reduce(t)
+    return int(t.item())
+
+
+def launch_check(args):
+    world, rank, _ = init_dist(args)
+    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0"))) if torch.cuda.is_available() else "cpu"
+    seen = ranks_seen(world, dev)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_seen": seen,
+                          "backend": dist.get_backend() if world > 1 else None}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def log_prob_error(model, device):
@@ -128,7 +200,7 @@ def cpu_baseline(args):
     cores: same FC_small step at the same batch, bounded sample."""
     from oracle import cnf_oracle as O
     from bcnf_amd.data import simulate
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_cores()
     torch.set_num_threads(threads)
     torch.manual_seed(2024_03_25)
     from bcnf_amd import CondRealNVP_v2
@@ -172,6 +244,9 @@ def kernel_timing(model, data, args):
 
 def main():
     args = parse()
+    launch_ranks(args)
+    if args.launch_check:
+        return launch_check(args)
     if args.batch is None:
         args.batch = WORKLOADS[args.workload][1]
     if args.workload == "sample":
@@ -230,6 +305,7 @@ def main():
         dt = float(tt.item())
     ms_per_step = dt / args.steps * 1e3
     value = world * args.batch * args.steps / dt
+    seen = ranks_seen(world, device)
 
     kern = kernel_timing(model, data, args) if rank == 0 else {}
     if rank == 0:
@@ -246,7 +322,7 @@ def main():
         lp_abs, lp_rel = log_prob_error(model, device)
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "ranks_seen": seen,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic ballistic trajectories (bcnf_amd/data.py RK4 restatement of physics.py), device-resident",
             "config": {"workload": "trajectory_FC_small NLL training step (configs[1])", "batch_per_gpu": B,
@@ -263,7 +339,9 @@ def main():
                          "note": "fp32 VALU (DPP rotations) + fp32 MFMA; peak is the fp32 vector = MFMA-f32 rate"},
             "kernels_us": {k: round(v, 2) for k, v in kern.items()},
         }
-        if not args.no_cpu_baseline:
+        if not args.no_secondary and world == 1 and not (args.indexed or args.per_step_sync):
+            line["secondary"] = secondary_figures(step, args, device)
+        if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -271,10 +349,77 @@ def main():
         dist.destroy_process_group()
 
 
+def secondary_figures(step, args, device, n_loop=50, n_trainer=12):
+    """SURVEY §8d's two side figures, measured after the headline run (not part of `value`):
+    * trainer_loop_shape: the same captured step replayed one batch at a time with a host sync and a read of the
+      three logged values after every step -- the shape of Trainer.train's loop (trainer.py:164-173, the three
+      .item() of trainer.py:277) -- instead of run_epoch's one sync per epoch;
+    * unchanged_trainer: Trainer._train_batch (trainer.py:244-277) restated statement for statement over a host
+      TensorDataset + DataLoader(batch_size=B, shuffle=True, num_workers=0, pin_memory=False) -- the settings of
+      configs/runs/old/trajectory_FC_small.yaml:66-69 -- with torch.optim.Adam(lr=2e-4) and clip_grad_norm_ on a
+      fresh bcnf_amd model: what a user gets by swapping the import and changing nothing else."""
+    from bcnf_amd import CondRealNVP_v2, inn_nll_loss
+    B = args.batch
+    out = {}
+    for _ in range(5):
+        step.step_epoch()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n_loop):
+        step.step_epoch()
+    dt = time.perf_counter() - t0
+    out["trainer_loop_shape"] = {"value": round(B * n_loop / dt, 1), "unit": "samples/s",
+                                 "ms_per_step": round(dt / n_loop * 1e3, 4), "steps": n_loop,
+                                 "what": "captured step + host sync + 3 logged values read per step"}
+    from torch.utils.data import DataLoader, TensorDataset
+    from bcnf_amd.data import simulate
+    y, traj = simulate(B * 4, seed=11)
+    y = torch.from_numpy(y)
+    traj = torch.from_numpy(traj)
+    y = (y - y.mean(0)) / (y.std(0) + 1e-6)
+    traj = (traj - traj.mean((0, 1))) / (traj.std((0, 1)) + 1e-6)
+    loader = DataLoader(TensorDataset(y, traj), batch_size=B, shuffle=True, num_workers=0, pin_memory=False)
+    torch.manual_seed(2024_03_25)
+    model = CondRealNVP_v2.from_config(FC_SMALL).to(device)
+    model.train()
+    optimizer = torch.optim.Adam(model.parameters(), lr=2e-4)
+    times = []
+
+    def train_batch(yb, *conditions):           # trainer.py:244-277, hybrid_weight = 0
+        optimizer.zero_grad()
+        z, h = model.forward(yb.to(model.device), *[c.to(model.device) for c in conditions], log_det_J=True,
+                             return_features=True)
+        mse_loss = torch.tensor(0.0)
+        nll_loss = inn_nll_loss(z, model.log_det_J)
+        loss = (nll_loss + mse_loss * 0.0) / (1 + 0.0)
+        loss.backward()
+        optimizer.step()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)
+        return loss.item(), nll_loss.item(), mse_loss.item()
+
+    done = 0
+    while done < 3 + n_trainer:
+        t_prev = time.perf_counter()
+        for data in loader:                      # the DataLoader's fetch + collate is inside the timing
+            yb, *conds = data
+            train_batch(yb, *conds)
+            now = time.perf_counter()
+            times.append(now - t_prev)
+            t_prev = now
+            done += 1
+            if done >= 3 + n_trainer:
+                break
+    med = statistics.median(times[3:])
+    out["unchanged_trainer"] = {"value": round(B / med, 1), "unit": "samples/s", "ms_per_step": round(med * 1e3, 3),
+                                "steps": n_trainer,
+                                "what": "Trainer._train_batch restated + host DataLoader (num_workers=0), torch Adam"}
+    return out
+
+
 def cpu_baseline_wide(args, cfg, batch=256, steps=4):
     """CPU oracle training step of the wide workload (FC_large shapes) on this host, bounded: B=256, a few steps."""
     from oracle import cnf_oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_cores()
     torch.set_num_threads(threads)
     torch.manual_seed(2024_03_25)
     from bcnf_amd import CondRealNVP_v2
@@ -336,6 +481,7 @@ def main_wide(args):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     value = world * args.batch * args.steps / dt
+    seen = ranks_seen(world, device)
     kern = kernel_timing(model, data, args) if rank == 0 else {}
     if rank == 0:
         B = args.batch
@@ -346,8 +492,8 @@ def main_wide(args):
         line = {
             "metric": f"NLL-training samples/sec, {WIDE_NAMES[args.workload]}",
             "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "ranks_seen": seen,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic ballistic trajectories (bcnf_amd/data.py), device-resident",
             "config": {"workload": f"trajectory_{args.workload} NLL training step", "batch_per_gpu": B,
                        "global_batch": B * world, "parallelism": f"dp{world}", "hip_graph": not args.no_graph,
@@ -361,7 +507,7 @@ def main_wide(args):
                          "traffic": None, "flop_per_step": flop_step},
             "kernels_us": {k: round(v, 2) for k, v in kern.items()},
         }
-        if not args.no_cpu_baseline and args.workload == "fc_large":
+        if not args.no_cpu_baseline and world == 1 and args.workload == "fc_large":
             line["cpu_baseline"] = cpu_baseline_wide(args, cfg)
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -418,13 +564,15 @@ def main_sample(args, n_draws=500):
             torch.cuda.synchronize()
             inv_us = e0.elapsed_time(e1) * 1e3 / 5
     value = n_draws * args.batch * args.steps / dt
+    seen = ranks_seen(world, device)
     if rank == 0:
         flop = FWD_FLOP_PER_SAMPLE * rows
         achieved = flop / (inv_us * 1e-6) / 1e12
         line = {
             "metric": "posterior draws/sec (inverse sampling, 500 draws x 1024 conditions), trajectory_FC_small",
             "value": round(value, 1), "unit": "draws/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
+            "ms_per_step": round(dt / args.steps * 1e3, 4), "ranks_seen": seen, "higher_is_better": True,
+            "scaling": "strong",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic ballistic trajectories as conditions, device z",
             "config": {"workload": "CondRealNVP_v2.sample-equivalent draw (configs[4])", "conditions": args.batch,
                        "draws_per_condition": n_draws, "parallelism": f"condition shards x{world}",
@@ -433,7 +581,7 @@ def main_sample(args, n_draws=500):
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
                          "traffic": None, "avg_us": round(inv_us, 2), "flop_per_launch": flop},
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline_sample()
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -444,7 +592,7 @@ def main_sample(args, n_draws=500):
 def cpu_baseline_sample(n_draws=500, n_cond=1024):
     """The oracle's sample(outer=True, batch_size=100) (CPU restatement of cnf.py:510-588) on the host, bounded."""
     from oracle import cnf_oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_cores()
     torch.set_num_threads(threads)
     torch.manual_seed(2024_03_25)
     from bcnf_amd import CondRealNVP_v2

@@ -263,7 +263,16 @@ int bcnf_clip_grad_norm(int32_t n_tensors, float* const* grads, const int64_t* n
 #define BCNF_GUARD_CHECK 0
 #define BCNF_GUARD_DIVERGED 1
 #define BCNF_GUARD_HALTED 2
+#define BCNF_GUARD_CHECK_GLOBAL 3
 #define BCNF_GUARD_WORDS 4
+
+/* Data parallel form of the divergence check (trainer.py:168 on the loss every rank logs): the host leaves
+ * [BCNF_GUARD_CHECK] at 0, so no rank's loss finalize judges its local shard, and sets
+ * [BCNF_GUARD_CHECK_GLOBAL]; after the gradient all-reduce this one-thread launch raises [BCNF_GUARD_DIVERGED]
+ * when the all-reduced loss global_values[0] > 1e5 or NaN (unless the step is already halted). Every rank sees
+ * the same value, so every rank halts on the same step; the next step's loss finalize turns DIVERGED into
+ * HALTED exactly as in the single-process case. */
+int bcnf_guard_check_global(const float* global_values, int32_t* guard, void* stream);
 
 /* The same bookkeeping as a one-thread launch. */
 int bcnf_advance_counters(float* step, int64_t* cursor, int64_t n_batches, void* stream);

@@ -51,3 +51,47 @@ def close(a, b, rtol=1e-5, floor=1e-5):
 @pytest.fixture(scope="session")
 def g1():
     return load_golden("g1_fc_small.npz")
+
+
+# configs/runs/old/trajectory_LSTM_large.yaml / trajectory_FC_large.yaml as from_config sees them (identical to
+# tests/golden/make_golden.py's LSTM_LARGE / FC_LARGE)
+LSTM_LARGE_CFG = {
+    "global": FC_SMALL_CFG["global"],
+    "model": {"kwargs": {"size": 19, "nested_sizes": [526] * 5, "n_conditions": 1360, "n_blocks": 26,
+                         "dropout": 0.407, "act_norm": True, "layer": "Linear", "activation": "GELU",
+                         "random_state": 2024_03_25}},
+    "feature_networks": [
+        {"type": "ConcatenateCondition", "kwargs": {"input_size": None, "output_size": 3}},
+        {"type": "LSTM", "kwargs": {"input_size": 3, "hidden_size": 140, "output_size": 1360, "num_layers": 2,
+                                    "dropout": 0.111, "bidirectional": True, "pooling": "mean"}},
+    ],
+}
+FC_LARGE_CFG = {
+    "global": FC_SMALL_CFG["global"],
+    "model": {"kwargs": {"size": 19, "nested_sizes": [526] * 5, "n_conditions": 1360, "n_blocks": 26,
+                         "dropout": 0.407, "act_norm": True}},
+    "feature_networks": [
+        {"type": "ConcatenateCondition", "kwargs": {"input_size": None, "output_size": 90}},
+        {"type": "FullyConnected", "kwargs": {"sizes": [90] + [310] * 7 + [1360], "dropout": 0.111}},
+    ],
+}
+
+
+def large_proxy_sd(model, seed):
+    """tests/golden/make_golden.py:large_proxy_state -- numpy PCG64 weights in state_dict order (the orthonormal
+    matrices are kept), so full-depth fixtures need no 195 MB weight file."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    sd = {}
+    for k, v in model.state_dict().items():
+        if k.endswith("orthonormal_matrix"):
+            sd[k] = v.detach().cpu().numpy()
+            continue
+        shape = tuple(v.shape)
+        if k.endswith(".scale"):
+            a = rng.uniform(0.7, 1.3, size=shape)
+        elif len(shape) == 2:
+            a = rng.uniform(-1.0, 1.0, size=shape) / np.sqrt(shape[1])
+        else:
+            a = rng.uniform(-0.05, 0.05, size=shape)
+        sd[k] = a.astype(np.float32)
+    return sd

@@ -17,6 +17,14 @@ Fixtures:
   g8_q.npz           OrthonormalTransformation(19, random_state=2024_03_25) Q bytes
   g9_ballistic.npz   64 physical trajectories from the reference ODE simulator + forward on them
   g_init.npz         state_dict of CondRealNVP_v2.from_config(FC_small) right after torch.manual_seed
+  g10_lstm_large.npz trajectory_LSTM_large at FULL depth (nb=26, random_state=2024_03_25, biLSTM 3->140 x2 +
+                     Linear 280->1360) with numpy-PCG64 weights (large_proxy_state, LSTM included): the
+                     reference-faithful pool over the batch axis at B=30 (the only batch it runs at,
+                     feature_network.py:174) -> h, z, ldj, inverse; the documented pool_dim=1 fix at B=48 (the
+                     reference's own LSTM + Linear modules, mean over the time axis) -> h, z, ldj; Q of one block
+                     + whether all 25 Q are bit-identical (random_state reseeds, cnf.py:319-320)
+  g11_fc_large.npz   trajectory_FC_large at FULL depth (nb=26, FC[90,310x7,1360]) with PCG64 weights, eval, B=48:
+                     h, z, ldj, inverse(z), every Q
 """
 import os
 import sys
@@ -250,8 +258,90 @@ def make_g9(cnf, utils, physics):
                         inv=inv.numpy())
 
 
+LSTM_LARGE = {
+    "global": FC_SMALL["global"],
+    "model": {"kwargs": {"size": 19, "nested_sizes": [526] * 5, "n_conditions": 1360, "n_blocks": 26,
+                         "dropout": 0.407, "act_norm": True, "layer": "Linear", "activation": "GELU",
+                         "random_state": 2024_03_25}},
+    "feature_networks": [
+        {"type": "ConcatenateCondition", "kwargs": {"input_size": None, "output_size": 3}},
+        {"type": "LSTM", "kwargs": {"input_size": 3, "hidden_size": 140, "output_size": 1360, "num_layers": 2,
+                                    "dropout": 0.111, "bidirectional": True, "pooling": "mean"}},
+    ],
+}
+FC_LARGE = {
+    "global": FC_SMALL["global"],
+    "model": {"kwargs": {"size": 19, "nested_sizes": [526] * 5, "n_conditions": 1360, "n_blocks": 26,
+                         "dropout": 0.407, "act_norm": True}},
+    "feature_networks": [
+        {"type": "ConcatenateCondition", "kwargs": {"input_size": None, "output_size": 90}},
+        {"type": "FullyConnected", "kwargs": {"sizes": [90] + [310] * 7 + [1360], "dropout": 0.111}},
+    ],
+}
+
+
+def _load_proxy(m, seed):
+    sd = large_proxy_state(m, seed)
+    m.load_state_dict({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in sd.items()})
+    m.eval()
+
+
+def make_g10(cnf):
+    """configs/runs/old/trajectory_LSTM_large.yaml at full depth."""
+    torch.manual_seed(SEED + 12)
+    m = cnf.CondRealNVP_v2.from_config(LSTM_LARGE)
+    _load_proxy(m, SEED + 13)
+    qs = [v for k, v in m.state_dict().items() if k.endswith("orthonormal_matrix")]
+    same_q = all(torch.equal(q, qs[0]) for q in qs)
+    rng = np.random.Generator(np.random.PCG64(SEED + 14))
+    y = rng.standard_normal((30, 19)).astype(np.float32)
+    traj = rng.standard_normal((30, 30, 3)).astype(np.float32)
+    with torch.no_grad():
+        z, h = m.forward(torch.from_numpy(y), torch.from_numpy(traj), log_det_J=True, return_features=True)
+        ldj = m.log_det_J.clone()
+        inv = m.inverse(z, torch.from_numpy(traj))
+    # the pool_dim=1 fix (bcnf_amd LSTMFeatureNetwork(pool_dim=1)): the reference's own LSTM and Linear modules,
+    # pooled over the time axis instead of the batch axis, at a batch != 30
+    fn = m.feature_network_stack.feature_networks[1]
+
+    def pooled_over_time(x):
+        out, _ = fn.lstm.forward(x)
+        return fn.linear.forward(out).mean(dim=1)
+    fn.forward = pooled_over_time
+    y1 = rng.standard_normal((48, 19)).astype(np.float32)
+    traj1 = rng.standard_normal((48, 30, 3)).astype(np.float32)
+    with torch.no_grad():
+        z1, h1 = m.forward(torch.from_numpy(y1), torch.from_numpy(traj1), log_det_J=True, return_features=True)
+        ldj1 = m.log_det_J.clone()
+    np.savez_compressed(os.path.join(OUT, "g10_lstm_large.npz"), y=y, traj=traj, h=h.numpy(), z=z.numpy(),
+                        ldj=ldj.numpy(), inv=inv.numpy(), q=qs[0].numpy(), n_q=np.int32(len(qs)),
+                        q_all_identical=np.bool_(same_q), y1=y1, traj1=traj1, h1=h1.numpy(), z1=z1.numpy(),
+                        ldj1=ldj1.numpy())
+
+
+def make_g11(cnf):
+    """configs/runs/old/trajectory_FC_large.yaml at full depth."""
+    torch.manual_seed(SEED + 15)
+    m = cnf.CondRealNVP_v2.from_config(FC_LARGE)
+    _load_proxy(m, SEED + 16)
+    rng = np.random.Generator(np.random.PCG64(SEED + 17))
+    y = rng.standard_normal((48, 19)).astype(np.float32)
+    traj = rng.standard_normal((48, 30, 3)).astype(np.float32)
+    with torch.no_grad():
+        z, h = m.forward(torch.from_numpy(y), torch.from_numpy(traj), log_det_J=True, return_features=True)
+        ldj = m.log_det_J.clone()
+        inv = m.inverse(z, torch.from_numpy(traj))
+    q = {("q/" + k): v.numpy() for k, v in m.state_dict().items() if k.endswith("orthonormal_matrix")}
+    np.savez_compressed(os.path.join(OUT, "g11_fc_large.npz"), y=y, traj=traj, h=h.numpy(), z=z.numpy(),
+                        ldj=ldj.numpy(), inv=inv.numpy(), **q)
+
+
 def main():
     cnf, utils, physics = _import_reference()
+    if len(sys.argv) > 1:                      # e.g. `make_golden.py g10 g11`: only those fixtures
+        for name in sys.argv[1:]:
+            {"g10": lambda: make_g10(cnf), "g11": lambda: make_g11(cnf)}[name]()
+        return
     torch.set_num_threads(8)
     make_g1(cnf, utils)
     make_g3(cnf)
@@ -259,6 +349,8 @@ def main():
     make_g7(cnf)
     make_g8(cnf)
     make_g9(cnf, utils, physics)
+    make_g10(cnf)
+    make_g11(cnf)
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

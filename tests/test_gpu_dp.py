@@ -54,6 +54,20 @@ def _worker(rank, world, port, cfg, q, mode="step"):
         step.broadcast_parameters()
         y, t = _data()
         n = y.shape[0] // world
+        if mode == "diverge":   # only rank 1's shard of batch 1 blows up; the global loss decides, on both ranks
+            yl, tl = y[rank * n:(rank + 1) * n].clone(), t[rank * n:(rank + 1) * n]
+            step.set_pool(torch.cat([yl, yl * (1e4 if rank == 1 else 1.0)]).cuda(), torch.cat([tl, tl]).cuda())
+            order = torch.cat([torch.arange(n), torch.arange(n) + n, torch.arange(n), torch.arange(n)])
+            step.set_epoch(order.cuda(), n)
+            from bcnf_amd.train import TrainingDivergedError
+            try:
+                step.run_epoch(check_divergence=True)
+                raised = None
+            except TrainingDivergedError as e:
+                raised = str(e)
+            q.put((rank, ([p.detach().cpu().numpy() for p in m.parameters()],
+                          (raised, step._host_cursor, int(step._epoch[1].item())))))
+            return
         if mode == "epoch":     # bench.py's N > 1 path: device pool, epoch order, run_epoch (gather in the graph)
             step.set_pool(y[rank * n:(rank + 1) * n].cuda(), t[rank * n:(rank + 1) * n].cuda())
             step.set_epoch(torch.arange(n, device="cuda").repeat(STEPS), n)
@@ -102,3 +116,25 @@ def test_two_rank_step_equals_union_batch_step(cfg, mode):
         a, b = torch.from_numpy(a), torch.from_numpy(b)
         assert torch.equal(a, b)                                  # replicas stay identical
         assert torch.allclose(a, c, rtol=1e-4, atol=1e-6), float((a - c).abs().max())
+
+
+def test_two_rank_divergence_halts_every_rank_on_the_same_step():
+    """One rank's shard diverges (local NLL ~1e8, the other's is normal): the divergence guard judges the
+    all-reduced loss, so BOTH ranks raise at the same batch, with the same cursor and identical parameters (no rank
+    left blocked in a later all-reduce)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, CFG, q, "diverge")) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        assert not isinstance(res[r], str), res[r]
+    (p0, st0), (p1, st1) = res[0], res[1]
+    assert st0 == st1, (st0, st1)
+    assert st0[0] is not None and "at batch 1" in st0[0] and st0[1] == 2 and st0[2] == 2
+    for a, b in zip(p0, p1):
+        assert (a == b).all()

@@ -263,10 +263,10 @@ def test_run_epoch_divergence_halts_like_the_trainer(g1):
     py, pt = _epoch_pool(gen, blow_up=bad)
     order = order.to(DEV)
     res = []
-    for mode in ("per_step", "epoch"):
+    for mode in ("per_step", "epoch", "eager_epoch"):
         m = fresh_model(g1, train=True)
         m.fused.set_seed(9)
-        st = TrainStep(m, lr=2e-4)
+        st = TrainStep(m, lr=2e-4, capture=mode != "eager_epoch")
         st.epoch_unroll = 2                                   # the halt lands inside a multi-step graph
         st.set_pool(py, pt)
         st.set_epoch(order, 128)
@@ -274,13 +274,50 @@ def test_run_epoch_divergence_halts_like_the_trainer(g1):
             vals = [st.step_epoch() for _ in range(3)]
             assert vals[2][0] > 1e5 and all(v[0] < 1e5 for v in vals[:2])
         else:
+            # eager_epoch: the per-step host check raises right after batch 2's update, before batch 3 runs
             with pytest.raises(TrainingDivergedError, match="at batch 2"):
                 st.run_epoch(check_divergence=True)
+            assert st._host_cursor == 3
         state = [v.clone() for s in st.opt.state.values() for v in s.values()]
         res.append(([p.detach().clone() for p in m.parameters()], state, m.fused.rng_state().clone(),
                     st._epoch[1].item()))
-    (p0, s0, r0, c0), (p1, s1, r1, c1) = res
-    assert c0 == c1 == 3 and torch.equal(r0, r1)
-    for a, b in zip(p0 + s0, p1 + s1):
+    (p0, s0, r0, c0) = res[0]
+    for (p1, s1, r1, c1) in res[1:]:
+        assert c0 == c1 == 3 and torch.equal(r0, r1)
+        for a, b in zip(p0 + s0, p1 + s1):
+            assert torch.equal(a, b)
+        assert float(s1[0]) == 3.0                           # Adam step count: three updates applied
+
+
+def test_captured_step_with_ragged_batches_equals_eager(g1):
+    """The DataLoader's last batch is smaller (drop_last=False, trainer_data_handler.py:146): a captured TrainStep
+    given batches of 128, 128, 1, 127, 128 samples runs the odd sizes eagerly and matches an eager TrainStep bit for
+    bit (logged values and parameters); the 1-sample batch is not broadcast into the captured buffers."""
+    from bcnf_amd.train import TrainStep
+    gen = torch.Generator().manual_seed(31)
+    sizes = [128, 128, 1, 127, 128]
+    batches = [(torch.randn(n, 19, generator=gen).to(DEV), torch.randn(n, 30, 3, generator=gen).to(DEV))
+               for n in sizes]
+    res = []
+    for capture in (False, True):
+        m = fresh_model(g1, train=True)
+        m.fused.set_seed(41)
+        st = TrainStep(m, lr=2e-4, capture=capture)
+        vals = [st.step(y, tr) for y, tr in batches]
+        res.append((vals, [p.detach().clone() for p in m.parameters()], [p.grad.clone() for p in st.params]))
+    (v0, p0, g0), (v1, p1, g1_) = res
+    assert v0 == v1
+    for a, b in zip(p0 + g0, p1 + g1_):
         assert torch.equal(a, b)
-    assert float(s1[0]) == 3.0                               # Adam step count: three updates applied
+
+
+def test_step_indexed_rejects_out_of_range_indices(g1):
+    from bcnf_amd.train import TrainStep
+    m = fresh_model(g1, train=True)
+    st = TrainStep(m, lr=2e-4)
+    gen = torch.Generator().manual_seed(3)
+    st.set_pool(torch.randn(64, 19, generator=gen).to(DEV), torch.randn(64, 30, 3, generator=gen).to(DEV))
+    with pytest.raises(IndexError):
+        st.step_indexed(torch.tensor([0, 5, 64], device=DEV))
+    with pytest.raises(IndexError):
+        st.set_epoch(torch.tensor([0, -1], device=DEV), 2)
