@@ -33,6 +33,15 @@ def _build(cfg, init_seed, weight_seed, pool_dim=None):
     torch.manual_seed(init_seed)
     m = CondRealNVP_v2.from_config(cfg)
     sd = large_proxy_sd(m, weight_seed)
+    if "random_state" in cfg["model"]["kwargs"]:
+        # every block's Q is the reference's one reseeded Q (g10); pin it to the reference's bytes rather than this
+        # host's LAPACK rounding of the same QR
+        q = load_golden("g10_lstm_large.npz")["q"]
+        for k in sd:
+            if k.endswith("orthonormal_matrix"):
+                ok, err = close(sd[k], q, rtol=0.0, floor=1e-6)
+                assert ok, (k, err)
+                sd[k] = np.ascontiguousarray(q)
     m.load_state_dict({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in sd.items()})
     assert type(m.fused).__name__ == "WideStack"
     return m, sd
@@ -98,9 +107,11 @@ def test_lstm_large_pool_dim1_gradients_vs_fp64():
     O.inn_nll_loss(zo, lo).backward()
     m.to(DEV).eval()
     m.zero_grad(set_to_none=True)
-    z, h = m.forward(y0.to(DEV), t0.to(DEV), log_det_J=True, return_features=True)
-    h.retain_grad()
-    inn_nll_loss(z, m.log_det_J).backward()
+    # MIOpen's RNN backward refuses eval mode; torch's own LSTM kernels (same math) take it
+    with torch.backends.cudnn.flags(enabled=False):
+        z, h = m.forward(y0.to(DEV), t0.to(DEV), log_det_J=True, return_features=True)
+        h.retain_grad()
+        inn_nll_loss(z, m.log_det_J).backward()
     ok, err = close(h.grad.cpu(), h64.grad, rtol=1e-4, floor=1e-4)
     assert ok, ("dL/dh", err)
     named_ref = dict(fref.named_parameters())
@@ -119,9 +130,14 @@ def test_lstm_large_pool_dim1_gradients_vs_fp64():
 def fc_large():
     d = load_golden("g11_fc_large.npz")
     m, sd = _build(FC_LARGE_CFG, SEED + 15, SEED + 16)
+    # The seeded construction reproduces every Q up to the host LAPACK's QR rounding (bit-exact on the host that
+    # generated g11; a few ulps on other CPUs), so the flow runs on the reference's own Q matrices.
     for k in sd:
         if k.endswith("orthonormal_matrix"):
-            assert np.array_equal(sd[k], d["q/" + k]), k     # the seeded construction reproduces every Q
+            ok, err = close(sd[k], d["q/" + k], rtol=0.0, floor=1e-6)
+            assert ok, (k, err)
+            sd[k] = np.ascontiguousarray(d["q/" + k])
+    m.load_state_dict({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in sd.items()})
     return m.to(DEV).eval(), sd, d
 
 
