@@ -153,7 +153,8 @@ struct BcnfLayout {
   int an_size;          // 2*D if act_norm else 0
   int blk_stride;       // canonical floats per (ActNorm + coupling) block
   int cblk;             // slab floats per block: blk_stride without the W1 condition columns (H1 x C)
-  int blk_pad;          // cblk rounded up to 4: per-block stride of the gradient slab
+  int blk_pad;          // cblk rounded up to 4
+  int sblk;             // floats per block of a workgroup's gradient slab (slab_blk_floats: MFMA tiles + column sums)
   int n_trainable;
   float p, keep_scale;
   uint32_t thresh16;    // drop if u16 < thresh16

@@ -21,8 +21,9 @@
 #include <mutex>
 
 // Experiment switches for A/B timing only (tools/exp_variants.sh builds separate libraries; results of a
-// nonzero BCNF_EXP are NOT valid): 1 = records read by row 0 only, 2 = no slab stores, 4 = no MFMA
-// gradient phase, 8 = no dropout RNG in the forward.
+// nonzero BCNF_EXP are NOT valid): 1 = records read by row 0 only, 8 = no dropout RNG in the forward, 2048 =
+// GELU -> x/2 in the forward, 4096 = no orthonormal mix in the forward, 8192 = no activation-record stores in
+// the forward.
 #ifndef BCNF_EXP
 #define BCNF_EXP 0
 #endif
@@ -38,6 +39,8 @@ constexpr int NC16_MAX = 16;           // C <= 256: register-resident column til
 constexpr int TILE = BCNF_ROWS * BCNF_TSTRIDE;   // 272 floats
 constexpr int STAGE_REC = 4;   // 16 * RF (RB) floats  <= 4 float4 per thread (RF, RB <= 256)
 constexpr int RING = STAGE_REC * BCNF_WG * 4;    // floats per record-ring slot: a Stage stores all of it
+// floats per block of a backward workgroup's gradient slab: NH + 2 MFMA tiles + NH + 6 column sums (BwdJobs)
+__host__ __device__ constexpr int slab_blk_floats(int NH) { return (NH + 2) * 256 + (NH + 6) * 16; }
 
 // ------------------------------------------------------------------------------------------------
 // Host-side layout
@@ -83,6 +86,7 @@ int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
   L->n_trainable = (L->nb - 1) * L->blk_stride + off;
   L->cblk = L->blk_stride - L->H[1] * L->C;
   L->blk_pad = (L->cblk + 3) & ~3;
+  L->sblk = slab_blk_floats(L->NH);
   L->p = d->dropout;
   L->keep_scale = (d->dropout > 0.f) ? (1.0f / (1.0f - d->dropout)) : 1.0f;
   double t = (double)d->dropout * 65536.0;
@@ -119,14 +123,10 @@ int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
 size_t fwd_lds_bytes(const BcnfLayout& L) {   // forward / inverse record ring (2 blocks)
   return sizeof(float) * (size_t)(2 * RING);
 }
-size_t bwd_lds_bytes(const BcnfLayout& L) {   // backward record ring, gradient tiles (2), job table, gradient block
+size_t bwd_lds_bytes(const BcnfLayout& L) {   // backward record ring, gradient tiles (2)
   const int NT = 2 * L.NH + NT_EXTRA;
-  return sizeof(float) * (size_t)(2 * RING + 2 * NT * TILE + 8 * (2 * (BCNF_MAX_HIDDEN + 2) + 4) +
-                                  L.blk_pad + 64);
+  return sizeof(float) * (size_t)(2 * RING + 2 * NT * TILE);
 }
-// float4 stores per thread that copy one block's gradient partials from LDS to the slab (fixed count)
-constexpr int COPY4_MAX = 8;
-int copy4_of(const BcnfLayout& L) { return (L.blk_pad / 4 + BCNF_WG - 1) / BCNF_WG <= 4 ? 4 : 8; }
 constexpr size_t LDS_MAX = 160 * 1024;
 
 bool layout_supported(const BcnfLayout& L, const BcnfStackDesc* d) {
@@ -139,7 +139,6 @@ bool layout_supported(const BcnfLayout& L, const BcnfStackDesc* d) {
   if (sizeof(float) * (size_t)(64 * 132 + 128 * (L.Cp + 32)) > LDS_MAX) return false;   // k_dw1h staging
   if (16 * L.RF > 4 * 4 * BCNF_WG || 16 * L.RB > 4 * 4 * BCNF_WG) return false;
   if (fwd_lds_bytes(L) > LDS_MAX || bwd_lds_bytes(L) > LDS_MAX) return false;
-  if (L.blk_pad / 4 > COPY4_MAX * BCNF_WG) return false;
   return true;
 }
 
@@ -1009,7 +1008,10 @@ __device__ __forceinline__ void mlp_forward(const BcnfLayout& L, const float* __
     const float bias = (l == 1) ? hp : w[16];            // hp = h W1h^T + b1 (k_hp)
     const float pre = rot16(a, w, bias);
     const float m = drop ? (((bits >> (l - 1)) & 1u) ? L.keep_scale : 0.f) : 1.f;
-    if (KEEP) {
+    if (BCNF_EXP & 2048) {
+      a = pre * 0.5f * m;
+      if (KEEP) { act[l - 1] = a; gd[l - 1] = 0.5f * m; }
+    } else if (KEEP) {
       float g, dg;
       gelu_fg(pre, g, dg);
       a = g * m;
@@ -1095,7 +1097,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
     const float S = tanh_bf(Sp);                      // cnf.py:107
     const float zb = fmaf(exp_fast(S), xb, T);        // cnf.py:179
     ldj += S;                                          // cnf.py:190
-    if (SAVE) {                                        // 16-B stores, a lane's record contiguous
+    if (SAVE && !(BCNF_EXP & 8192)) {                  // 16-B stores, a lane's record contiguous
       ar[AR::S] = S;
       ar[AR::YA] = ya;
       ar[AR::YB] = yb;
@@ -1107,6 +1109,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
       for (int i = 0; i < AR::AR / 4; ++i)
         dst[i * BCNF_WG] = floatx4{ar[4 * i], ar[4 * i + 1], ar[4 * i + 2], ar[4 * i + 3]};
     }
+    if (BCNF_EXP & 4096) { ya = xa; yb = zb; } else
     mix(rr + RecF<NH>::Q, xa, zb, ya, yb);             // y @ Q (cnf.py:335); identity after the last block
     sr.store(rec + (cur ^ 1) * RING);          // past the end these refill a buffer nobody reads
     __syncthreads();
@@ -1139,13 +1142,14 @@ __global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* 
 // enabled raises `diverged` (trainer.py:168 raises after that step's update); the NEXT step's finalize
 // then raises `halted`, which turns that step's RNG advance, Adam update, clip and counter advances into
 // no-ops -- so an epoch replayed without host syncs stops with the state the reference raises in.
+template <int NTH = BCNF_WG>
 __device__ void nll_finalize(const float* __restrict__ part, int nparts, long long B, float* __restrict__ loss_out,
                              uint64_t* rng_w, int32_t* guard, float* __restrict__ red) {
   float acc = 0.f;
-  for (int i = threadIdx.x; i < nparts; i += BCNF_WG) acc += part[i];
+  for (int i = threadIdx.x; i < nparts; i += NTH) acc += part[i];
   red[threadIdx.x] = acc;
   __syncthreads();
-  for (int w = BCNF_WG / 2; w > 0; w >>= 1) {
+  for (int w = NTH / 2; w > 0; w >>= 1) {
     if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }
@@ -1252,64 +1256,22 @@ struct BwdTiles {   // tile indices inside one tile buffer
   __device__ __forceinline__ int count() const { return 2 * NH + NT_EXTRA; }
 };
 
-// Gradient jobs of one block, built once per workgroup into LDS:
-//   W jobs   (NH + 2): dW of every Linear (the last one as its t and s row halves): 4 fp32 MFMAs over the
-//            workgroup's 16 samples, out[j][i] = sum_s delta[s][j] * act[s][i] ([16][17] LDS tiles);
-//            for Linear 1 only the y-part columns (the condition part is the k_dw1h GEMM)
-//   sum jobs (NH + 2 + 4): bias and ActNorm gradients = column sums of a tile over the 16 samples (VALU +
-//            two cross-row permlane swaps; no MFMA against a ones tile)
-// Output offsets are in the slab's compact block layout: canonical order without Linear 1's condition
-// columns, i.e. [ActNorm][W1y: H1 x Da][b1][Linear 2 ...] (k_reduce maps it back).
-struct GradDesc {
-  int a_tile;   // float offset of the delta tile in the tile buffer
-  int b_tile;   // W jobs: offset of the activation tile
-  int out;      // compact block-relative output offset of element (0, 0), coupling offset excluded
-  int rs;       // output row stride
-  int nrows;    // valid rows (W) / valid elements (sum jobs)
-  int ncols;    // valid columns
-  int flags;    // 1: coupling-relative (add the ActNorm size for blocks that have one), 2: ActNorm job
-  int pad;
-};
-constexpr int GD_COUPLING = 1, GD_ACTNORM = 2;
-constexpr int MAX_JOBS = 2 * (BCNF_MAX_HIDDEN + 2) + 4;
-
+// Gradient jobs of one block (compile-time for a given NH; the slab layout they write is decoded by
+// slab_to_canonical):
+//   W jobs   c = 0 .. NH+1: dW of Linear c+1 (c = NH, NH+1: the last Linear's t and s row halves) as one
+//            16 x 16 fp32-MFMA tile over the workgroup's 16 samples, out[i][j] = sum_s delta[s][i] act[s][j]
+//            (Linear 1: only its y-part columns; the condition part is the split-K GEMM of the tail)
+//   sum jobs c = 0 .. NH+5: column sums over the 16 samples (VALU + two cross-row permlane swaps): the biases of
+//            Linear 1 .. NH, the last Linear's t and s halves, then ActNorm scale_a, bias_a, scale_b, bias_b
 template <int NH>
-__device__ void build_jobs(const BcnfLayout& L, GradDesc* gd) {
-  const BwdTiles TI{NH};
-  constexpr int NW = NH + 2, NS = NH + 6;
-  const int shift = L.H[1] * L.C;                       // canonical -> compact, past Linear 1's weight
-  for (int c = threadIdx.x; c < NW + NS; c += BCNF_WG) {
-    GradDesc d;
-    d.pad = 0;
-    d.flags = GD_COUPLING;
-    d.b_tile = 0;
-    d.rs = 1;
-    d.ncols = 16;
-    if (c < NW) {                                         // dW of Linear l (t rows, s rows for l = NH + 1)
-      const int l = (c < NH) ? c + 1 : NH + 1;
-      d.a_tile = TILE * ((c < NH) ? TI.D(l) : (c == NH ? TI.DT() : TI.DS()));
-      d.b_tile = TILE * ((c < NH) ? TI.A(l - 1) : TI.A(NH));
-      const int row0 = (c == NH + 1) ? L.Db : 0;
-      d.rs = (l == 1) ? L.Da : L.lin_in[l];
-      d.out = ((l == 1) ? 0 : L.lin_w[l] - shift) + row0 * d.rs;
-      d.nrows = (c < NH) ? L.H[l] : L.Db;
-      d.ncols = (l == 1) ? L.Da : L.H[l - 1];
-    } else if (c < NW + NH + 2) {                         // bias of Linear l (t half, s half)
-      const int cc = c - NW;
-      const int l = (cc < NH) ? cc + 1 : NH + 1;
-      d.a_tile = TILE * ((cc < NH) ? TI.D(l) : (cc == NH ? TI.DT() : TI.DS()));
-      d.out = L.lin_b[l] - shift + ((cc == NH + 1) ? L.Db : 0);
-      d.nrows = (cc < NH) ? L.H[l] : L.Db;
-    } else {                                              // ActNorm scale_a, bias_a, scale_b, bias_b
-      const int a = c - (NW + NH + 2);
-      d.a_tile = TILE * ((a == 0) ? TI.PA() : (a == 1 ? TI.GA() : (a == 2 ? TI.PB() : TI.GB())));
-      d.flags = GD_ACTNORM;
-      d.out = ((a & 1) ? L.D : 0) + ((a < 2) ? 0 : L.Da);
-      d.nrows = (a < 2) ? L.Da : L.Db;
-    }
-    gd[c] = d;
-  }
-}
+struct BwdJobs {
+  static constexpr int NW = NH + 2, NS = NH + 6;
+  static constexpr int SUM_OFF = NW * 256;                 // slab block: [NW][64 lanes][4] then [NS][16]
+  static constexpr int BLK = NW * 256 + NS * 16;
+  __device__ static constexpr int wa(int c) { return c < NH ? c : (c == NH ? NH : NH + 1); }      // delta tile
+  __device__ static constexpr int wb(int c) { return c < NH ? NH + 2 + c : 2 * NH + 2; }          // act tile
+  __device__ static constexpr int sa(int c) { return c < NH + 2 ? c : 2 * NH + 3 + (c - NH - 2); }
+};
 
 // Sum of v over the 4 rows (16-lane groups) of the wave, returned in every lane (gfx950 permlane swaps:
 // the two results of each swap are the row pairs, so adding them is the pairwise sum whatever the order).
@@ -1320,307 +1282,254 @@ __device__ __forceinline__ float sum_rows4(float v) {
   return __uint_as_float(p2[0]) + __uint_as_float(p2[1]);
 }
 
-// MFMA phase of one block: every parameter gradient of block m (except W1's condition part) into the
-// LDS gradient block `gbuf`. Masked-off lanes store into a private dummy slot (gbuf[blk_pad + lane]) so
-// no store needs an exec-mask branch.
-// c ? a : b through an all-ones / zero mask the optimizer cannot see through: per-lane
-// select-then-store sequences stay straight-line VALU code (a plain select whose operands are only
-// needed on one side is otherwise turned into exec-mask branches around the stores).
-__device__ __forceinline__ int lane_select(bool c, int a, int b) {
-  int m = c ? -1 : 0;
-  asm("" : "+v"(m));
-  return b + ((a - b) & m);
+// Helper-wave work for block m: every parameter gradient of the block except W1's condition part, from the
+// [16 samples][16] LDS tiles the compute waves wrote, straight to slab block m (no LDS gradient block):
+//   W job c: lane l holds D[4(l>>4) + r][l & 15], r = 0..3, stored as ONE float4 at [c][l] (1 KB per wave, coalesced)
+//   sum job c: 16 floats at SUM_OFF + 16 c (lanes 0..15)
+template <int NH>
+__device__ __forceinline__ void bwd_grad_jobs(const float* __restrict__ T, float* __restrict__ out, int hw) {
+  using J = BwdJobs<NH>;
+  const int l64 = threadIdx.x & 63, q = l64 >> 4, r = l64 & 15;
+  constexpr int UW = (J::NW + 3) / 4, US = (J::NS + 3) / 4;
+  float a[UW][4], bv[UW][4], v[US][4];
+#pragma unroll
+  for (int u = 0; u < UW; ++u) {                           // all operand reads first
+    const int c = hw + 4 * u < J::NW ? hw + 4 * u : J::NW - 1;
+    const float* ta = T + J::wa(c) * TILE + q * BCNF_TSTRIDE + r;
+    const float* tb = T + J::wb(c) * TILE + q * BCNF_TSTRIDE + r;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      a[u][t] = ta[4 * t * BCNF_TSTRIDE];
+      bv[u][t] = tb[4 * t * BCNF_TSTRIDE];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < US; ++u) {
+    const int c = hw + 4 * u < J::NS ? hw + 4 * u : J::NS - 1;
+    const float* ts = T + J::sa(c) * TILE + q * BCNF_TSTRIDE + r;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[u][t] = ts[4 * t * BCNF_TSTRIDE];
+  }
+  floatx4 acc[UW];
+#pragma unroll
+  for (int u = 0; u < UW; ++u) acc[u] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 4; ++t)                              // independent chains interleaved
+#pragma unroll
+    for (int u = 0; u < UW; ++u) acc[u] = mfma4(a[u][t], bv[u][t], acc[u]);
+#pragma unroll
+  for (int u = 0; u < US; ++u) {
+    const float tot = sum_rows4((v[u][0] + v[u][1]) + (v[u][2] + v[u][3]));
+    if (hw + 4 * u < J::NS && q == 0) out[J::SUM_OFF + 16 * (hw + 4 * u) + r] = tot;
+  }
+#pragma unroll
+  for (int u = 0; u < UW; ++u)
+    if (hw + 4 * u < J::NW) reinterpret_cast<floatx4*>(out + 256 * (hw + 4 * u))[l64] = acc[u];
 }
+
+// Copy of n floats global -> registers -> LDS by the 256 helper threads (t = 0..255): the record of the block
+// after next is staged while the compute waves work on this one.
+template <int N>
+struct HStage {
+  floatx4 r[N];
+  __device__ __forceinline__ void load(const float* __restrict__ g, int n, int t) {
+    const floatx4* g4 = reinterpret_cast<const floatx4*>(g);
+    const int n4 = n >> 2;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int idx = t + i * BCNF_WG;
+      r[i] = g4[idx < n4 ? idx : 0];
+    }
+  }
+  __device__ __forceinline__ void store(float* __restrict__ s, int t) const {
+    floatx4* s4 = reinterpret_cast<floatx4*>(s);
+#pragma unroll
+    for (int i = 0; i < N; ++i) s4[t + i * BCNF_WG] = r[i];
+  }
+};
+
+// Whole-stack backward, one launch, 512 threads = two roles per SIMD (waves w and w + 4 share a SIMD):
+//  * compute waves 0..3 (4 samples each, row layout): back-propagate block k from its saved activation record
+//    (VALU, DPP rotations) and write the [16 samples][16] tiles of block k (deltas, activations, ActNorm terms);
+//  * helper waves 4..7: in the same interval, the MFMA / column-sum gradient jobs of block k+1 from the tiles
+//    written in the previous interval, stored straight to the slab, and the staging of block k-1's backward
+//    record into the LDS ring.
+// One barrier per block. The helpers' loads, MFMAs and stores fill the issue slots the compute waves' dependent
+// chains leave idle instead of sitting on their critical path.
+constexpr int BWD_WG = 2 * BCNF_WG;
 
 template <int NH>
-__device__ __forceinline__ void bwd_mfma_phase(const BcnfLayout& L,
-                                               const float* __restrict__ T, const GradDesc* __restrict__ gd,
-                                               float* __restrict__ gbuf, int m) {
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int l64 = threadIdx.x & 63, q = l64 >> 4, r = l64 & 15;
-  constexpr int NW = NH + 2, NS = NH + 6;
-  constexpr int UW = (NW + 3) / 4, US = (NS + 3) / 4;
-  const bool has_an = L.act_norm && m < L.nb - 1;
-  const int cpl = has_an ? L.an_size : 0;
-  const int dummy = L.blk_pad + l64;     // per-lane dummy slot of the masked stores
-  // ---- weight gradients (MFMA), all operand reads first, independent chains interleaved
-  {
-    GradDesc d[UW];
-    float a[UW][4], bv[UW][4];
-    floatx4 acc[UW];
-#pragma unroll
-    for (int u = 0; u < UW; ++u) {
-      const int c = wave + 4 * u;
-      d[u] = gd[c < NW ? c : NW - 1];
-    }
-#pragma unroll
-    for (int u = 0; u < UW; ++u) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        a[u][t] = T[d[u].a_tile + (4 * t + q) * BCNF_TSTRIDE + r];
-        bv[u][t] = T[d[u].b_tile + (4 * t + q) * BCNF_TSTRIDE + r];
-      }
-      acc[u] = floatx4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int u = 0; u < UW; ++u) acc[u] = mfma4(a[u][t], bv[u][t], acc[u]);
-#pragma unroll
-    for (int u = 0; u < UW; ++u) {                        // no branches: surplus jobs store to dummies
-      const int base = d[u].out + cpl + __mul24(4 * q, d[u].rs) + r;
-      const bool colok = (r < d[u].ncols) & (wave + 4 * u < NW);   // & : no short-circuit branches
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool ok = colok & (4 * q + i < d[u].nrows) & !(BCNF_EXP & 2);
-        gbuf[lane_select(ok, base + i * d[u].rs, dummy)] = acc[u][i];
-      }
-    }
-  }
-  // ---- bias / ActNorm gradients: column sums over the 16 samples (VALU)
-  {
-    GradDesc e[US];
-    float v[US][4];
-#pragma unroll
-    for (int u = 0; u < US; ++u) {
-      const int c = wave + 4 * u;
-      e[u] = gd[NW + (c < NS ? c : NS - 1)];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) v[u][t] = T[e[u].a_tile + (4 * t + q) * BCNF_TSTRIDE + r];
-    }
-#pragma unroll
-    for (int u = 0; u < US; ++u) {
-      const float tot = sum_rows4((v[u][0] + v[u][1]) + (v[u][2] + v[u][3]));
-      const bool live = (!(e[u].flags & GD_ACTNORM) | has_an) & (wave + 4 * u < NS);
-      const bool ok = live & (q == 0) & (r < e[u].nrows) & !(BCNF_EXP & 2);
-      gbuf[lane_select(ok, e[u].out + ((e[u].flags & GD_COUPLING) ? cpl : 0) + r, dummy)] = tot;
-    }
-  }
-}
-
-// LDS gradient block (bwd_mfma_phase output) -> slab block m: CP4 unconditional float4 stores per thread
-// (indices clamped; duplicates rewrite the same value), fully coalesced.
-__device__ float g_exp_sink;
-// BCNF_EXP & 128: per-phase cycle counts of the backward loop (wave 0 of workgroup 0)
-__device__ unsigned long long g_phase[16];
-#define PH(i)                                                                          \
-  if (BCNF_EXP & 128) {                                                                \
-    const unsigned long long _t = __builtin_amdgcn_s_memtime();                        \
-    if (blockIdx.x == 0 && threadIdx.x == 0) ph_acc[i] += _t - ph_t;                   \
-    ph_t = _t;                                                                         \
-  }
-template <int CP4>
-__device__ __forceinline__ void copy_out(const BcnfLayout& L, const float* __restrict__ gbuf,
-                                         float* __restrict__ slab, int m, float& sink) {
-  const int n4 = L.blk_pad >> 2;
-  const floatx4* g4 = reinterpret_cast<const floatx4*>(gbuf);
-  floatx4* s4 = reinterpret_cast<floatx4*>(slab + ((BCNF_EXP & 16) ? 0LL : (long long)m * L.blk_pad));
-  floatx4 v[CP4];
-#pragma unroll
-  for (int u = 0; u < CP4; ++u) {
-    const int i = (int)threadIdx.x + u * BCNF_WG;
-    v[u] = g4[i < n4 ? i : n4 - 1];
-  }
-#pragma unroll
-  for (int u = 0; u < CP4; ++u) {
-    const int i = (int)threadIdx.x + u * BCNF_WG;
-    if (BCNF_EXP & 64)
-      sink += v[u].x + v[u].y + v[u].z + v[u].w;
-    else if (!(BCNF_EXP & 2))
-      s4[i < n4 ? i : n4 - 1] = v[u];
-  }
-}
-
-template <int NH, int CP4>
-__global__ __launch_bounds__(BCNF_WG) void k_backward(BcnfLayout L, const float* __restrict__ pk,
-                                                      const float* __restrict__ dz, const float* __restrict__ dldj,
-                                                      const float* __restrict__ dloss, int nll, long long B,
-                                                      const float* __restrict__ arec,
-                                                      float* __restrict__ dy, float* __restrict__ d1,
-                                                      float* __restrict__ slab_all, long long slab_stride,
-                                                      const float* __restrict__ nll_part, float* __restrict__ loss_out,
-                                                      uint64_t* rng_w, int32_t* guard) {
+__global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* __restrict__ pk,
+                                                     const float* __restrict__ dz, const float* __restrict__ dldj,
+                                                     const float* __restrict__ dloss, int nll, long long B,
+                                                     const float* __restrict__ arec,
+                                                     float* __restrict__ dy, float* __restrict__ d1,
+                                                     float* __restrict__ slab_all, long long slab_stride,
+                                                     const float* __restrict__ nll_part, float* __restrict__ loss_out,
+                                                     uint64_t* rng_w, int32_t* guard) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const BwdTiles TI{NH};
   using AR = ActRec<NH>;
   using RBk = RecB<NH>;
+  using J = BwdJobs<NH>;
   const int RBL = 16 * L.RB;
   const int NT = TI.count();
   float* recB = smem;                   // [2][16*RB]
   float* tiles = recB + 2 * RING;       // [2][NT][272]
-  GradDesc* cd = reinterpret_cast<GradDesc*>(tiles + 2 * NT * TILE);   // [MAX_JOBS]
-  float* gbuf = tiles + 2 * NT * TILE + MAX_JOBS * 8;                  // [blk_pad + 64] block gradient + dummies
-  float exp_sink = 0.f;
-  unsigned long long ph_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long ph_t = (BCNF_EXP & 128) ? __builtin_amdgcn_s_memtime() : 0ULL;
-  const int tid = threadIdx.x, j = tid & 15, s = tid >> 4;
-  build_jobs<NH>(L, cd);
-  const long long b = (long long)blockIdx.x * 16 + s;
-  const bool valid = b < B;
-  const long long bc = valid ? b : B - 1;
-  const int D = L.D, Da = L.Da, Db = L.Db, nb = L.nb;
-  float* slab = slab_all + ((BCNF_EXP & 32) ? 0LL : (long long)blockIdx.x * slab_stride);
+  const int nb = L.nb;
   const float* pbk = pk + L.pb_off;
-  // activation records [k][workgroup][AR/4][256 threads] float4 (k_forward)
-  const floatx4* arl = reinterpret_cast<const floatx4*>(arec) + (long long)blockIdx.x * (AR::AR / 4) * BCNF_WG + tid;
-  const long long ars = (long long)gridDim.x * (AR::AR / 4) * BCNF_WG;
-  float* d1l = d1 + bc * 16 + j;                    // D1[k][b][j]  = d1l[k * B * 16]
-  float* d1_dummy = d1 + (long long)nb * B * 16 + j; // rows past the batch (workspace slack)
-  const long long hps = B * 16;
+  float* slab = slab_all + (long long)blockIdx.x * slab_stride;
+  const bool helper = threadIdx.x >= BCNF_WG;
+  const int ht = (int)threadIdx.x - BCNF_WG;                   // helper thread 0..255
 
-  float gya = 0.f, gyb = 0.f, dl = 0.f;
-  if (valid) {                                      // padded rows carry zero gradient
-    if (nll) {    // d/dz, d/dldj of mean_b(0.5 |z_b|^2 - ldj_b); dz holds z here
-      const float sc = (dloss ? dloss[0] + dloss[1] : 1.f) / (float)B;   // d loss/d nll = d nll/d nll = 1
-      gya = (j < Da) ? dz[b * D + j] * sc : 0.f;
-      gyb = (j < Db) ? dz[b * D + Da + j] * sc : 0.f;
-      dl = -sc;
-    } else {
-      if (dz) {
-        gya = (j < Da) ? dz[b * D + j] : 0.f;
-        gyb = (j < Db) ? dz[b * D + Da + j] : 0.f;
-      }
-      if (dldj) dl = dldj[b];
+  {   // record of the last block
+    HStage<STAGE_REC> sr;
+    const int t = helper ? ht : (int)threadIdx.x;
+    if (!helper) {
+      sr.load(pbk + (long long)(nb - 1) * RBL, RBL, t);
+      sr.store(recB + ((nb - 1) & 1) * RING, t);
     }
-  }
-  // activation record of the block about to be processed (saved by the forward; one block ahead)
-  floatx4 ar_n[AR::AR / 4];
-#pragma unroll
-  for (int i = 0; i < AR::AR / 4; ++i) ar_n[i] = arl[(long long)(nb - 1) * ars + i * BCNF_WG];
-  {
-    const int kl = nb - 1;
-    Stage<STAGE_REC> sr;
-    sr.load(pbk + (long long)kl * RBL, RBL);
-    sr.store(recB + (kl & 1) * RING);
   }
   __syncthreads();
 
-  for (int k = nb - 1; k >= 0; --k) {
-    const int cur = k & 1;
-    const int k1 = k >= 1 ? k - 1 : 0;               // clamped: no branches
-    float ar[AR::AR];
-#pragma unroll
-    for (int i = 0; i < AR::AR / 4; ++i) {
-      ar[4 * i] = ar_n[i][0];
-      ar[4 * i + 1] = ar_n[i][1];
-      ar[4 * i + 2] = ar_n[i][2];
-      ar[4 * i + 3] = ar_n[i][3];
-    }
-    // (0) gradient block k+2 (MFMA phase of the previous iteration) LDS -> slab, before any load of
-    // this iteration is issued; then the MFMA phase below may overwrite the LDS block
-    if (k + 2 < nb) {
-      copy_out<CP4>(L, gbuf, slab, k + 2, exp_sink);
+  if (helper) {
+    const int hw = __builtin_amdgcn_readfirstlane(ht >> 6);
+    for (int k = nb - 1; k >= 0; --k) {
+      HStage<STAGE_REC> sB;
+      if (k >= 1) sB.load(pbk + (long long)(k - 1) * RBL, RBL, ht);
+      if (k + 1 < nb) bwd_grad_jobs<NH>(tiles + ((k + 1) & 1) * NT * TILE, slab + (long long)(k + 1) * J::BLK, hw);
+      if (k >= 1) sB.store(recB + ((k - 1) & 1) * RING, ht);
       __syncthreads();
     }
-    PH(0)
-    // (a) prefetch: next backward record and the next block's activation record
-    Stage<STAGE_REC> sB;
-    sB.load(pbk + (long long)k1 * RBL, RBL);
-#pragma unroll
-    for (int i = 0; i < AR::AR / 4; ++i)
-      ar_n[i] = (BCNF_EXP & 512) ? ar_n[i] : arl[(long long)k1 * ars + i * BCNF_WG];
-    __builtin_amdgcn_sched_barrier(0);                // the prefetch is issued HERE, not sunk to its use
-    PH(1)
-    // (b) MFMA phase: parameter gradients of block k+1 (in the first iteration, of no block: its LDS
-    // output is never copied out). Unconditional, so (b) and (c) form one basic block and the MFMA
-    // chains can overlap the VALU back-propagation.
-    if (!(BCNF_EXP & 4))
-      bwd_mfma_phase<NH>(L, tiles + ((k + 1) & 1) * NT * TILE, cd, gbuf, k + 1);
-    PH(2)
-    PH(3)
-    // (c) VALU phase: back-propagate through block k from its saved activations (no recompute)
-    float* Tt = tiles + cur * NT * TILE;
-    const int tix = s * BCNF_TSTRIDE + j;
-    float rb[RBk::USED];
-    ld_rec_exp<0, RBk::USED>(rb, recB + cur * RING + j * L.RB);
-    const float ya = ar[AR::YA], yb = ar[AR::YB], S = ar[AR::S];
-    const float* act = ar + AR::ACT;
-    const float* gd = ar + AR::GD;
-    const float an_sa = rb[RBk::AN], an_ba = rb[RBk::AN + 1], an_sb = rb[RBk::AN + 2], an_bb = rb[RBk::AN + 3];
-    const float xa = fmaf(an_sa, ya, an_ba);
-    const float xb = fmaf(an_sb, yb, an_bb);
-    PH(4)
-    PH(5)
-    const float e = exp_fast(S);
-    float gza, gzb;
-    mix(rb + RBk::QT, gya, gyb, gza, gzb);            // g @ Q^T (identity for the last block)
-    const float dT = gzb;                              // z_b = exp(s) y_b + t
-    const float dS = (j < Db) ? fmaf(gzb * e, xb, dl) : 0.f;
-    const float dSp = dS * (1.f - S * S);
-    const float dxb = gzb * e;
-    Tt[TI.DT() * TILE + tix] = dT;
-    Tt[TI.DS() * TILE + tix] = dSp;
-    Tt[TI.A(NH) * TILE + tix] = act[NH - 1];
-    float da = 0.f, da2 = 0.f;
-    rot16x2(dT, rb + RBk::TT, da, dSp, rb + RBk::ST, da2);
-    da += da2;
-#pragma unroll
-    for (int l = NH; l >= 2; --l) {
-      const float dpre = da * gd[l - 1];
-      Tt[TI.D(l) * TILE + tix] = dpre;
-      Tt[TI.A(l - 1) * TILE + tix] = act[l - 2];
-      da = rot16(dpre, rb + RBk::HID + 16 * (l - 2), 0.f);
+    bwd_grad_jobs<NH>(tiles, slab, hw);                        // block 0 (tiles written in the last interval)
+  } else {
+    const int tid = threadIdx.x, j = tid & 15, s = tid >> 4;
+    const long long b = (long long)blockIdx.x * 16 + s;
+    const bool valid = b < B;
+    const long long bc = valid ? b : B - 1;
+    const int D = L.D, Da = L.Da, Db = L.Db;
+    // activation records [k][workgroup][AR/4][256 threads] float4 (k_forward)
+    const floatx4* arl = reinterpret_cast<const floatx4*>(arec) + (long long)blockIdx.x * (AR::AR / 4) * BCNF_WG + tid;
+    const long long ars = (long long)gridDim.x * (AR::AR / 4) * BCNF_WG;
+    float* d1l = d1 + bc * 16 + j;                    // D1[k][b][j]  = d1l[k * B * 16]
+    float* d1_dummy = d1 + (long long)nb * B * 16 + j; // rows past the batch (workspace slack)
+    const long long hps = B * 16;
+
+    float gya = 0.f, gyb = 0.f, dl = 0.f;
+    if (valid) {                                      // padded rows carry zero gradient
+      if (nll) {    // d/dz, d/dldj of mean_b(0.5 |z_b|^2 - ldj_b); dz holds z here
+        const float sc = (dloss ? dloss[0] + dloss[1] : 1.f) / (float)B;   // d loss/d nll = d nll/d nll = 1
+        gya = (j < Da) ? dz[b * D + j] * sc : 0.f;
+        gyb = (j < Db) ? dz[b * D + Da + j] * sc : 0.f;
+        dl = -sc;
+      } else {
+        if (dz) {
+          gya = (j < Da) ? dz[b * D + j] : 0.f;
+          gyb = (j < Db) ? dz[b * D + Da + j] : 0.f;
+        }
+        if (dldj) dl = dldj[b];
+      }
     }
-    const float dpre1 = da * gd[0];
-    Tt[TI.D(1) * TILE + tix] = dpre1;
-    Tt[TI.A(0) * TILE + tix] = xa;
-    if (!(BCNF_EXP & 1024)) *(valid ? d1l + k * hps : d1_dummy) = dpre1;   // dL/d pre-activation of Linear 1 (k_dh, k_dw1h)
-    const float dxa = rot16(dpre1, rb + RBk::W1T, gza);
-    {   // ActNorm tiles (consumed only for blocks that have an ActNorm)
-      const float inv_a = (j < Da) ? __builtin_amdgcn_rcpf(an_sa) : 0.f;
-      const float inv_b = (j < Db) ? __builtin_amdgcn_rcpf(an_sb) : 0.f;
-      Tt[TI.PA() * TILE + tix] = fmaf(dxa, ya, dl * inv_a);
-      Tt[TI.GA() * TILE + tix] = dxa;
-      Tt[TI.PB() * TILE + tix] = fmaf(dxb, yb, dl * inv_b);
-      Tt[TI.GB() * TILE + tix] = dxb;
+    floatx4 ar_n[AR::AR / 4];
+#pragma unroll
+    for (int i = 0; i < AR::AR / 4; ++i) ar_n[i] = arl[(long long)(nb - 1) * ars + i * BCNF_WG];
+
+    for (int k = nb - 1; k >= 0; --k) {
+      const int cur = k & 1;
+      const int k1 = k >= 1 ? k - 1 : 0;               // clamped: no branches
+      float ar[AR::AR];
+#pragma unroll
+      for (int i = 0; i < AR::AR / 4; ++i) {
+        ar[4 * i] = ar_n[i][0];
+        ar[4 * i + 1] = ar_n[i][1];
+        ar[4 * i + 2] = ar_n[i][2];
+        ar[4 * i + 3] = ar_n[i][3];
+      }
+#pragma unroll
+      for (int i = 0; i < AR::AR / 4; ++i) ar_n[i] = arl[(long long)k1 * ars + i * BCNF_WG];
+      __builtin_amdgcn_sched_barrier(0);                // the prefetch is issued HERE, not sunk to its use
+      float* Tt = tiles + cur * NT * TILE;
+      const int tix = s * BCNF_TSTRIDE + j;
+      float rb[RBk::USED];
+      ld_rec<0, RBk::USED>(rb, recB + cur * RING + j * L.RB);
+      const float ya = ar[AR::YA], yb = ar[AR::YB], S = ar[AR::S];
+      const float* act = ar + AR::ACT;
+      const float* gd = ar + AR::GD;
+      const float an_sa = rb[RBk::AN], an_ba = rb[RBk::AN + 1], an_sb = rb[RBk::AN + 2], an_bb = rb[RBk::AN + 3];
+      const float xa = fmaf(an_sa, ya, an_ba);
+      const float xb = fmaf(an_sb, yb, an_bb);
+      const float e = exp_fast(S);
+      float gza, gzb;
+      mix(rb + RBk::QT, gya, gyb, gza, gzb);            // g @ Q^T (identity for the last block)
+      const float dT = gzb;                              // z_b = exp(s) y_b + t
+      const float dS = (j < Db) ? fmaf(gzb * e, xb, dl) : 0.f;
+      const float dSp = dS * (1.f - S * S);
+      const float dxb = gzb * e;
+      Tt[TI.DT() * TILE + tix] = dT;
+      Tt[TI.DS() * TILE + tix] = dSp;
+      Tt[TI.A(NH) * TILE + tix] = act[NH - 1];
+      float da = 0.f, da2 = 0.f;
+      rot16x2(dT, rb + RBk::TT, da, dSp, rb + RBk::ST, da2);
+      da += da2;
+#pragma unroll
+      for (int l = NH; l >= 2; --l) {
+        const float dpre = da * gd[l - 1];
+        Tt[TI.D(l) * TILE + tix] = dpre;
+        Tt[TI.A(l - 1) * TILE + tix] = act[l - 2];
+        da = rot16(dpre, rb + RBk::HID + 16 * (l - 2), 0.f);
+      }
+      const float dpre1 = da * gd[0];
+      Tt[TI.D(1) * TILE + tix] = dpre1;
+      Tt[TI.A(0) * TILE + tix] = xa;
+      *(valid ? d1l + k * hps : d1_dummy) = dpre1;      // dL/d pre-activation of Linear 1 (split-K, dh)
+      const float dxa = rot16(dpre1, rb + RBk::W1T, gza);
+      {   // ActNorm tiles (consumed only for blocks that have an ActNorm)
+        const float inv_a = (j < Da) ? __builtin_amdgcn_rcpf(an_sa) : 0.f;
+        const float inv_b = (j < Db) ? __builtin_amdgcn_rcpf(an_sb) : 0.f;
+        Tt[TI.PA() * TILE + tix] = fmaf(dxa, ya, dl * inv_a);
+        Tt[TI.GA() * TILE + tix] = dxa;
+        Tt[TI.PB() * TILE + tix] = fmaf(dxb, yb, dl * inv_b);
+        Tt[TI.GB() * TILE + tix] = dxb;
+      }
+      gya = an_sa * dxa;
+      gyb = an_sb * dxb;
+      __syncthreads();
     }
-    gya = an_sa * dxa;
-    gyb = an_sb * dxb;
-    PH(6)
-    // (d) commit the prefetched record (past the end it refills a buffer nobody reads)
-    sB.store(recB + (cur ^ 1) * RING);
-    PH(7)
-    __syncthreads();
-    PH(8)
+    __syncthreads();                                   // pairs with the helpers' block-0 jobs
+    if (dy && valid) {
+      if (j < Da) dy[b * D + j] = gya;
+      if (j < Db) dy[b * D + Da + j] = gyb;
+    }
   }
-  if ((BCNF_EXP & 128) && blockIdx.x == 0 && threadIdx.x == 0)
-    for (int i = 0; i < 10; ++i) g_phase[i] = ph_acc[i];
-  if (nb >= 2) {                                   // block 1 (MFMA phase of the last iteration)
-    copy_out<CP4>(L, gbuf, slab, 1, exp_sink);
-    __syncthreads();
-  }
-  bwd_mfma_phase<NH>(L, tiles, cd, gbuf, 0);
-  __syncthreads();
-  copy_out<CP4>(L, gbuf, slab, 0, exp_sink);
-  if ((BCNF_EXP & 64) && exp_sink == 1234.5f) g_exp_sink = exp_sink;
-  if (dy && valid) {
-    if (j < Da) dy[b * D + j] = gya;
-    if (j < Db) dy[b * D + Da + j] = gyb;
-  }
+  if (helper) __syncthreads();
   if (loss_out && blockIdx.x == 0) {                 // deferred NLL reduction of the forward
     __syncthreads();
-    nll_finalize(nll_part, (int)gridDim.x, B, loss_out, rng_w, guard, gbuf);
+    nll_finalize<BWD_WG>(nll_part, (int)gridDim.x, B, loss_out, rng_w, guard, tiles);
   }
 }
 
-// Deterministic sum of the per-workgroup gradient slabs (fixed order over workgroups). Slab block m holds
-// block m's parameters in the compact layout [ActNorm][W1y: H1 x Da][b1][Linear 2 ...] at [m * blk_pad, ...);
-// this maps them back to canonical positions (W1's condition columns come from k_dw1h_reduce).
-__device__ __forceinline__ long long compact_to_canonical(const BcnfLayout& L, int m, int o) {
-  const int an = (m < L.nb - 1) ? L.an_size : 0;
-  long long rel;
-  if (o < an) {
-    rel = o;
-  } else {
-    const int c = o - an, w1y = L.H[1] * L.Da;
-    if (c < w1y) {
-      const int j = c / L.Da, i = c - j * L.Da;
-      rel = an + j * L.lin_in[1] + i;
-    } else {
-      rel = an + c + L.H[1] * L.C;
-    }
+// Deterministic sum of the per-workgroup gradient slabs (fixed order over workgroups). Slab block m (slab_blk_floats
+// floats at m * L.sblk) is what the backward's helper waves wrote (BwdJobs): NH + 2 MFMA tiles in lane order, then
+// NH + 6 column sums; this maps each element back to its canonical position, or -1 for tile padding (rows / columns
+// past a Linear's shape, ActNorm sums of the last block). W1's condition columns come from the split-K GEMM.
+__device__ __forceinline__ long long slab_to_canonical(const BcnfLayout& L, int m, int o) {
+  const int NH = L.NH, NW = NH + 2;
+  const int cb = m * L.blk_stride + ((m < L.nb - 1) ? L.an_size : 0);      // coupling base
+  if (o < NW * 256) {
+    const int c = o >> 8, e = o & 255, lane = e >> 2;
+    const int row = 4 * (lane >> 4) + (e & 3), col = lane & 15;
+    const int l = c < NH ? c + 1 : NH + 1;
+    const int nrows = c < NH ? L.H[l] : L.Db, ncols = (l == 1) ? L.Da : L.H[l - 1];
+    if (row >= nrows || col >= ncols) return -1;
+    const int row0 = (c == NH + 1) ? L.Db : 0;
+    return (long long)cb + L.lin_w[l] + (row0 + row) * L.lin_in[l] + col;
   }
-  return (long long)m * L.blk_stride + rel;
+  const int o2 = o - NW * 256, c = o2 >> 4, r = o2 & 15;
+  if (c < NH) return r < L.H[c + 1] ? (long long)cb + L.lin_b[c + 1] + r : -1;
+  if (c < NH + 2) return r < L.Db ? (long long)cb + L.lin_b[NH + 1] + ((c == NH + 1) ? L.Db : 0) + r : -1;
+  const int a = c - NH - 2;
+  if (a >= 4 || !L.act_norm || m >= L.nb - 1 || r >= ((a < 2) ? L.Da : L.Db)) return -1;
+  return (long long)m * L.blk_stride + ((a & 1) ? L.D : 0) + ((a < 2) ? 0 : L.Da) + r;
 }
 
 // RED_O4 output float4 per workgroup x RED_G slab groups (group g sums workgroups g, g+RED_G, ...; RED_T loads
@@ -1638,17 +1547,17 @@ __device__ __forceinline__ void reduce_body(const BcnfLayout& L, const float* __
   const long long i = ((long long)bx * RED_O4 + o4) * 4;
   const bool live = i < stride;
   const long long ic = live ? i : 0;
-  const int m = (int)(ic / L.blk_pad), o = (int)(ic - (long long)m * L.blk_pad);
-  const int size_m = L.cblk - ((m < L.nb - 1) ? 0 : L.an_size);
+  const int m = (int)(ic / L.sblk), o = (int)(ic - (long long)m * L.sblk);
   long long ci[4];
   float ap[4], am[4], av[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    ci[e] = compact_to_canonical(L, m, o + e < size_m ? o + e : 0);
+    ci[e] = slab_to_canonical(L, m, o + e);
     if (A && g == 0) {
-      ap[e] = A->p[0][ci[e]];
-      am[e] = A->m[0][ci[e]];
-      av[e] = A->v[0][ci[e]];
+      const long long c = ci[e] >= 0 ? ci[e] : 0;
+      ap[e] = A->p[0][c];
+      am[e] = A->m[0][c];
+      av[e] = A->v[0][c];
     }
   }
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -1670,7 +1579,7 @@ __device__ __forceinline__ void reduce_body(const BcnfLayout& L, const float* __
   for (int q = 1; q < RED_G; ++q) tot += part[q][o4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    if (o + e >= size_m) continue;
+    if (ci[e] < 0) continue;
     out[ci[e]] = tot[e];
     if (A) {
       adam_elem(ap[e], tot[e], am[e], av[e], *as);
@@ -1864,18 +1773,14 @@ int bwd_dispatch(const BcnfLayout& L, const float* pk, const float* dz, const fl
   if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
   const dim3 grid((unsigned)((B + 15) / 16));
   size_t lds = bwd_lds_bytes(L);
-  int rc;
-#define BCNF_BWD(CP)                                                                                      \
-  rc = launch_lds(k_backward<NH, CP>, lds);                                                               \
-  if (rc) return rc;                                                                                      \
-  hipLaunchKernelGGL((k_backward<NH, CP>), grid, dim3(BCNF_WG), lds, st, L, pk, dz, dldj, dloss, nll, B, arec, \
-                     dy, d1, slab, stride, part, loss_out, rng_w, guard);
-  if (copy4_of(L) == 4) { BCNF_BWD(4) } else { BCNF_BWD(8) }
-#undef BCNF_BWD
+  const int rc = launch_lds(k_backward<NH>, lds);
+  if (rc) return rc;
+  hipLaunchKernelGGL((k_backward<NH>), grid, dim3(BWD_WG), lds, st, L, pk, dz, dldj, dloss, nll, B, arec, dy, d1,
+                     slab, stride, part, loss_out, rng_w, guard);
   return check_launch();
 }
 
-long long slab_stride_of(const BcnfLayout& L) { return (long long)L.nb * L.blk_pad; }
+long long slab_stride_of(const BcnfLayout& L) { return (long long)L.nb * L.sblk; }
 
 // split-K geometry of the W1 condition-part gradient
 int w1h_rows_per_split(long long) { return KC; }   // one LDS chunk of rows per split
@@ -2279,11 +2184,6 @@ const char* bcnf_status_string(int status) {
 
 int bcnf_last_hip_error(void) { return bcnf_rt::last_hip; }
 
-#if BCNF_EXP & 128
-int bcnf_debug_phases(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(g_phase)) == hipSuccess ? 0 : 3;
-}
-#endif
 
 }  // extern "C"
 

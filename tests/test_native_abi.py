@@ -49,7 +49,7 @@ def test_layout_queries_match_module_tree():
     sb = N.query_i64(N.lib().bcnf_slab_bytes, ctypes.byref(d), ctypes.c_int64(4096))
     # per workgroup: nb blocks of the compact block (3430 - 16*80 condition columns = 2150, padded to 4),
     # plus 32 split-K partials (128 rows each) of the condition columns [nb][16][80]
-    assert sb == 256 * 32 * 2152 * 4 + 32 * 32 * 16 * 80 * 4
+    assert sb == 256 * 32 * (9 * 256 + 13 * 16) * 4 + 32 * 32 * 16 * 80 * 4   # MFMA tiles + column sums per block
 
 
 def test_unsupported_shapes_are_rejected():
