@@ -123,6 +123,9 @@ int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
 size_t fwd_lds_bytes(const BcnfLayout& L) {   // forward / inverse record ring (2 blocks)
   return sizeof(float) * (size_t)(2 * RING);
 }
+size_t fwd2_lds_bytes(const BcnfLayout& L) {  // forward: record ring + projection partials + dropout bits (2 slots)
+  return sizeof(float) * (size_t)(2 * RING + 2 * 4 * 256 + 2 * 256);
+}
 size_t bwd_lds_bytes(const BcnfLayout& L) {   // backward record ring, gradient tiles (2)
   const int NT = 2 * L.NH + NT_EXTRA;
   return sizeof(float) * (size_t)(2 * RING + 2 * NT * TILE);
@@ -415,9 +418,19 @@ struct Stage {
     }
   }
   // all N float4 per thread, no bounds branch: the destination is a RING-sized slot
-  __device__ __forceinline__ void store(float* __restrict__ s) const {
+  __device__ __forceinline__ void store(float* __restrict__ s) const { store_t(s, (int)threadIdx.x); }
+  // the same for thread t of a 256-thread role inside a larger workgroup
+  __device__ __forceinline__ void load_t(const float* __restrict__ g, int n, int t) {
+    const floatx4* g4 = reinterpret_cast<const floatx4*>(g);
+    const int n4 = n >> 2;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int idx = t + i * BCNF_WG;
+      r[i] = g4[idx < n4 ? idx : 0];
+    }
+  }
+  __device__ __forceinline__ void store_t(float* __restrict__ s, int t) const {
     floatx4* s4 = reinterpret_cast<floatx4*>(s);
-    const int t = (int)threadIdx.x;
 #pragma unroll
     for (int i = 0; i < N; ++i) s4[t + i * BCNF_WG] = r[i];
   }
@@ -1038,98 +1051,146 @@ __device__ __forceinline__ void mix(const float* __restrict__ rq, float a, float
 // ------------------------------------------------------------------------------------------------
 // Forward
 // ------------------------------------------------------------------------------------------------
+// Condition projection operands of the forward (the y-independent part of Linear 1, cnf.py:98-107 with the
+// condition columns): HP[b][16k + j] = sum_c h[b][c] W1hC[c][16k + j] + b1c[16k + j]; on the folded path h = x and
+// W1hC / b1c are the folded Wc / bc (fold_layout).
+struct ProjArgs {
+  const float* h;
+  const float* w1c;      // [Cp][NKp], rows >= C zero
+  const float* b1c;      // [NKp]
+  long long ldh;
+  int C, Cp, NKp;
+};
+constexpr int FWD_WG = 2 * BCNF_WG;
+constexpr int HP_SMAX = 16;            // K-steps of 4 per helper wave: Cp / 16 <= 16 (Cp <= 256)
+constexpr int FWD_HP = 2 * 4 * 256;    // LDS: [2 slots][4 helper waves][16 samples][16] partial HP tiles
+constexpr int FWD_BITS = 2 * 256;      // LDS: [2 slots][256] dropout keep-bits (u32)
+
+// Whole-stack forward, one launch, 512 threads = two roles per SIMD (waves w and w + 4 share a SIMD):
+//  * compute waves 0..3 (4 samples each, row layout): ActNorm -> nested MLP (GELU, dropout) -> affine coupling ->
+//    log-det -> orthonormal mix of block k, reading its record, condition projection and dropout bits from LDS;
+//  * helper waves 4..7, in the same interval, prepare block k+1: stage its forward record into the LDS ring,
+//    compute its condition projection for the workgroup's 16 samples on fp32 MFMA (one K-quarter per helper
+//    wave; the compute lanes add the four partials in a fixed order), and draw its dropout bits (Philox).
+// The projection therefore needs no separate GEMM launch and no HBM round trip, and the compute waves' loop
+// issues no global loads (the record stores of SAVE are its only VMEM traffic).
 template <int NH, bool DROP, bool SAVE>
-__global__ __launch_bounds__(BCNF_WG) void k_forward(BcnfLayout L, const float* __restrict__ pk,
-                                                     const float* __restrict__ y, const float* __restrict__ hp,
-                                                     long long B, float* __restrict__ z, float* __restrict__ ldj_out,
-                                                     float* __restrict__ logp, const uint64_t* rng,
-                                                     float* __restrict__ arec, float* __restrict__ nll_part) {
+__global__ __launch_bounds__(FWD_WG) void k_forward(BcnfLayout L, const float* __restrict__ pk,
+                                                    const float* __restrict__ y, ProjArgs P,
+                                                    long long B, float* __restrict__ z, float* __restrict__ ldj_out,
+                                                    float* __restrict__ logp, const uint64_t* rng,
+                                                    float* __restrict__ arec, float* __restrict__ nll_part) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int RFL = 16 * L.RF;
-  float* rec = smem;                    // [2][16*RF]
-  const int tid = threadIdx.x, j = tid & 15, s = tid >> 4;
-  const long long b = (long long)blockIdx.x * 16 + s;
-  const long long bc = b < B ? b : B - 1;           // rows past the batch replay the last sample
-  const int D = L.D, Da = L.Da, Db = L.Db, nb = L.nb;
+  float* rec = smem;                          // [2][16*RF]
+  float* hpb = rec + 2 * RING;                // [2][4][16][16]
+  uint32_t* bitb = reinterpret_cast<uint32_t*>(hpb + FWD_HP);   // [2][256]
+  const int nb = L.nb;
   const float* pf = pk + L.pf_off;
-  const float* hpl = hp + bc * 16 + j;              // HP[k][bc][j] = hpl[k * B * 16]
-  const long long hps = B * 16;
-
-  // every global input the loop reads is loaded before the prologue barrier, so the loop's only
-  // outstanding VMEM ops are its own (unconditional) prefetches
-  float ya = (j < Da) ? y[bc * D + j] : 0.f;
-  float yb = (j < Db) ? y[bc * D + Da + j] : 0.f;
-  float hp_n = hpl[0];
+  const bool helper = threadIdx.x >= BCNF_WG;
+  const int t8 = (int)threadIdx.x & (BCNF_WG - 1);              // thread index within the role
+  const int j = t8 & 15, s = t8 >> 4;                           // (sample, lane) of a compute / Philox thread
+  const long long b = (long long)blockIdx.x * 16 + s;
+  const long long bc = b < B ? b : B - 1;                       // rows past the batch replay the last sample
   uint64_t seed = 0, off = 0;
   if (DROP) { seed = rng[0]; off = rng[1]; }
-  const float ldc = pk[L.ldc_off];
-  {
-    Stage<STAGE_REC> sr;
-    sr.load(pf, RFL);
-    sr.store(rec);
-  }
-  __syncthreads();
 
-  float ldj = 0.f;
-  using AR = ActRec<NH>;
-
-  for (int k = 0; k < nb; ++k) {
-    const int cur = k & 1;
-    const int k1 = k + 1 < nb ? k + 1 : nb - 1;      // clamped: no branches
-    Stage<STAGE_REC> sr;
-    sr.load(pf + (long long)k1 * RFL, RFL);
-    const float hpk = hp_n;
-    hp_n = hpl[k1 * hps];
-    __builtin_amdgcn_sched_barrier(0);                // the prefetch is issued HERE, not sunk to its use
-
-    float rr[RecF<NH>::USED];
-    ld_rec_exp<0, RecF<NH>::USED>(rr, rec + cur * RING + j * L.RF);
-    const float xa = fmaf(rr[0], ya, rr[1]);          // ActNorm (cnf.py:349)
-    const float xb = fmaf(rr[2], yb, rr[3]);
-    uint32_t bits = 0xffu;
-    if (DROP && !(BCNF_EXP & 8)) bits = dropout_bits(L, seed, off, bc, k, j, 0u);
-    float T, Sp;
-    float ar[AR::AR];                                   // activation record of this block (SAVE)
-    if (SAVE)
-      mlp_forward<NH, true>(L, rr, xa, hpk, bits, DROP, T, Sp, ar + AR::ACT, ar + AR::GD);
-    else
-      mlp_forward<NH, false>(L, rr, xa, hpk, bits, DROP, T, Sp, nullptr, nullptr);
-    const float S = tanh_bf(Sp);                      // cnf.py:107
-    const float zb = fmaf(exp_fast(S), xb, T);        // cnf.py:179
-    ldj += S;                                          // cnf.py:190
-    if (SAVE && !(BCNF_EXP & 8192)) {                  // 16-B stores, a lane's record contiguous
-      ar[AR::S] = S;
-      ar[AR::YA] = ya;
-      ar[AR::YB] = yb;
+  if (helper) {
+    const int hw = __builtin_amdgcn_readfirstlane(t8 >> 6);
+    const int l64 = t8 & 63, lr = l64 & 15, lq = l64 >> 4;
+    const int S = P.Cp >> 4;                                     // K-steps per helper wave
+    const long long row = (long long)blockIdx.x * 16 + lr;
+    const float* hrow = P.h + (row < B ? row : B - 1) * P.ldh;
+    float xa[HP_SMAX];                                           // A operand: this wave's K-quarter of h / x
 #pragma unroll
-      for (int i = AR::YB + 1; i < AR::AR; ++i) ar[i] = 0.f;
-      // record [k][workgroup][AR/4][256 threads] float4: every store coalesced across the wave
-      floatx4* dst = reinterpret_cast<floatx4*>(arec) + ((long long)k * gridDim.x + blockIdx.x) * (AR::AR / 4) * BCNF_WG + tid;
-#pragma unroll
-      for (int i = 0; i < AR::AR / 4; ++i)
-        dst[i * BCNF_WG] = floatx4{ar[4 * i], ar[4 * i + 1], ar[4 * i + 2], ar[4 * i + 3]};
+    for (int t = 0; t < HP_SMAX; ++t) {
+      const int kk = 4 * (hw * S + t) + lq;
+      xa[t] = (t < S && kk < P.C) ? hrow[kk < P.C ? kk : 0] : 0.f;
     }
-    if (BCNF_EXP & 4096) { ya = xa; yb = zb; } else
-    mix(rr + RecF<NH>::Q, xa, zb, ya, yb);             // y @ Q (cnf.py:335); identity after the last block
-    sr.store(rec + (cur ^ 1) * RING);          // past the end these refill a buffer nobody reads
+    const float* wcol = P.w1c + (long long)(4 * hw * S + lq) * P.NKp + lr;   // + 4 t NKp + 16 k
+    // block k's projection partial, dropout bits and record -> slot k & 1
+    auto prepare = [&](int k) {
+      Stage<STAGE_REC> sr;
+      sr.load_t(pf + (long long)k * RFL, RFL, t8);
+      float wb[HP_SMAX];
+#pragma unroll
+      for (int t = 0; t < HP_SMAX; ++t) wb[t] = (t < S) ? wcol[(long long)4 * t * P.NKp + 16 * k] : 0.f;
+      uint32_t bits = 0xffu;
+      if (DROP) bits = dropout_bits(L, seed, off, bc, k, j, 0u);
+      const float bias = (hw == 0) ? P.b1c[16 * k + lr] : 0.f;
+      floatx4 acc = {bias, bias, bias, bias};
+#pragma unroll
+      for (int t = 0; t < HP_SMAX; ++t)
+        if (t < S) acc = mfma4(xa[t], wb[t], acc);
+      float* hd = hpb + (k & 1) * 1024 + hw * 256 + 64 * lq + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hd[16 * r] = acc[r];
+      bitb[(k & 1) * 256 + t8] = bits;
+      sr.store_t(rec + (k & 1) * RING, t8);
+    };
+    prepare(0);
     __syncthreads();
-  }
-  const float ltot = row_sum16(ldj) + ldc;
-  if (j < Da) z[bc * D + j] = ya;
-  if (j < Db) z[bc * D + Da + j] = yb;
-  if (j == 0 && ldj_out) ldj_out[bc] = ltot;
-  if (logp) {
+    for (int k = 0; k < nb; ++k) {
+      if (k + 1 < nb) prepare(k + 1);
+      __syncthreads();
+    }
+  } else {
+    const int tid = t8;
+    const int D = L.D, Da = L.Da, Db = L.Db;
+    float ya = (j < Da) ? y[bc * D + j] : 0.f;
+    float yb = (j < Db) ? y[bc * D + Da + j] : 0.f;
+    const float ldc = pk[L.ldc_off];
+    __syncthreads();
+    float ldj = 0.f;
+    using AR = ActRec<NH>;
+    for (int k = 0; k < nb; ++k) {
+      const int cur = k & 1;
+      float rr[RecF<NH>::USED];
+      ld_rec_exp<0, RecF<NH>::USED>(rr, rec + cur * RING + j * L.RF);
+      const float* hq = hpb + cur * 1024 + tid;
+      const float hpk = ((hq[0] + hq[256]) + hq[512]) + hq[768];
+      uint32_t bits = bitb[cur * 256 + tid];
+      if (BCNF_EXP & 8) bits = 0xffu;
+      const float xa = fmaf(rr[0], ya, rr[1]);          // ActNorm (cnf.py:349)
+      const float xb = fmaf(rr[2], yb, rr[3]);
+      float T, Sp;
+      float ar[AR::AR];                                   // activation record of this block (SAVE)
+      if (SAVE)
+        mlp_forward<NH, true>(L, rr, xa, hpk, bits, DROP, T, Sp, ar + AR::ACT, ar + AR::GD);
+      else
+        mlp_forward<NH, false>(L, rr, xa, hpk, bits, DROP, T, Sp, nullptr, nullptr);
+      const float Sv = tanh_bf(Sp);                      // cnf.py:107
+      const float zb = fmaf(exp_fast(Sv), xb, T);        // cnf.py:179
+      ldj += Sv;                                         // cnf.py:190
+      if (SAVE && !(BCNF_EXP & 8192)) {                  // 16-B stores, a lane's record contiguous
+        ar[AR::S] = Sv;
+        ar[AR::YA] = ya;
+        ar[AR::YB] = yb;
+#pragma unroll
+        for (int i = AR::YB + 1; i < AR::AR; ++i) ar[i] = 0.f;
+        // record [k][workgroup][AR/4][256 threads] float4: every store coalesced across the wave
+        floatx4* dst = reinterpret_cast<floatx4*>(arec) + ((long long)k * gridDim.x + blockIdx.x) * (AR::AR / 4) * BCNF_WG + tid;
+#pragma unroll
+        for (int i = 0; i < AR::AR / 4; ++i)
+          dst[i * BCNF_WG] = floatx4{ar[4 * i], ar[4 * i + 1], ar[4 * i + 2], ar[4 * i + 3]};
+      }
+      if (BCNF_EXP & 4096) { ya = xa; yb = zb; } else
+      mix(rr + RecF<NH>::Q, xa, zb, ya, yb);             // y @ Q (cnf.py:335); identity after the last block
+      __syncthreads();
+    }
+    const float ltot = row_sum16(ldj) + ldc;
+    if (j < Da) z[bc * D + j] = ya;
+    if (j < Db) z[bc * D + Da + j] = yb;
+    if (j == 0 && ldj_out) ldj_out[bc] = ltot;
     const float q2 = row_sum16(ya * ya + yb * yb);
-    if (j == 0) logp[bc] = -(0.5f * q2 - ltot) - 0.5f * (float)D * 1.8378770664093454836f;
+    if (logp && j == 0) logp[bc] = -(0.5f * q2 - ltot) - 0.5f * (float)D * 1.8378770664093454836f;
+    if (nll_part && j == 0) rec[s] = (b < B) ? 0.5f * q2 - ltot : 0.f;   // rec: free after the last barrier
   }
   if (nll_part) {   // per-workgroup partial of inn_nll_loss (utils.py:40-46); reduced by nll_finalize
-    const float q2 = row_sum16(ya * ya + yb * yb);
-    float* red = rec;                                  // free after the loop's last barrier
-    if (j == 0) red[s] = (b < B) ? 0.5f * q2 - ltot : 0.f;
     __syncthreads();
-    if (tid == 0) {
+    if (threadIdx.x == 0) {
       float acc = 0.f;
-      for (int i = 0; i < 16; ++i) acc += red[i];
+      for (int i = 0; i < 16; ++i) acc += rec[i];
       nll_part[blockIdx.x] = acc;
     }
   }
@@ -1327,27 +1388,6 @@ __device__ __forceinline__ void bwd_grad_jobs(const float* __restrict__ T, float
     if (hw + 4 * u < J::NW) reinterpret_cast<floatx4*>(out + 256 * (hw + 4 * u))[l64] = acc[u];
 }
 
-// Copy of n floats global -> registers -> LDS by the 256 helper threads (t = 0..255): the record of the block
-// after next is staged while the compute waves work on this one.
-template <int N>
-struct HStage {
-  floatx4 r[N];
-  __device__ __forceinline__ void load(const float* __restrict__ g, int n, int t) {
-    const floatx4* g4 = reinterpret_cast<const floatx4*>(g);
-    const int n4 = n >> 2;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const int idx = t + i * BCNF_WG;
-      r[i] = g4[idx < n4 ? idx : 0];
-    }
-  }
-  __device__ __forceinline__ void store(float* __restrict__ s, int t) const {
-    floatx4* s4 = reinterpret_cast<floatx4*>(s);
-#pragma unroll
-    for (int i = 0; i < N; ++i) s4[t + i * BCNF_WG] = r[i];
-  }
-};
-
 // Whole-stack backward, one launch, 512 threads = two roles per SIMD (waves w and w + 4 share a SIMD):
 //  * compute waves 0..3 (4 samples each, row layout): back-propagate block k from its saved activation record
 //    (VALU, DPP rotations) and write the [16 samples][16] tiles of block k (deltas, activations, ActNorm terms);
@@ -1383,11 +1423,10 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
   const int ht = (int)threadIdx.x - BCNF_WG;                   // helper thread 0..255
 
   {   // record of the last block
-    HStage<STAGE_REC> sr;
-    const int t = helper ? ht : (int)threadIdx.x;
+    Stage<STAGE_REC> sr;
     if (!helper) {
-      sr.load(pbk + (long long)(nb - 1) * RBL, RBL, t);
-      sr.store(recB + ((nb - 1) & 1) * RING, t);
+      sr.load_t(pbk + (long long)(nb - 1) * RBL, RBL, (int)threadIdx.x);
+      sr.store_t(recB + ((nb - 1) & 1) * RING, (int)threadIdx.x);
     }
   }
   __syncthreads();
@@ -1395,10 +1434,10 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
   if (helper) {
     const int hw = __builtin_amdgcn_readfirstlane(ht >> 6);
     for (int k = nb - 1; k >= 0; --k) {
-      HStage<STAGE_REC> sB;
-      if (k >= 1) sB.load(pbk + (long long)(k - 1) * RBL, RBL, ht);
+      Stage<STAGE_REC> sB;
+      if (k >= 1) sB.load_t(pbk + (long long)(k - 1) * RBL, RBL, ht);
       if (k + 1 < nb) bwd_grad_jobs<NH>(tiles + ((k + 1) & 1) * NT * TILE, slab + (long long)(k + 1) * J::BLK, hw);
-      if (k >= 1) sB.store(recB + ((k - 1) & 1) * RING, ht);
+      if (k >= 1) sB.store_t(recB + ((k - 1) & 1) * RING, ht);
       __syncthreads();
     }
     bwd_grad_jobs<NH>(tiles, slab, hw);                        // block 0 (tiles written in the last interval)
@@ -1725,18 +1764,19 @@ int launch_hp(const BcnfLayout& L, const float* pk, const float* h, long long R,
 }
 
 template <int NH>
-int fwd_dispatch(const BcnfLayout& L, const float* pk, const float* y, const float* hp, long long B, float* z,
+int fwd_dispatch(const BcnfLayout& L, const float* pk, const float* y, const ProjArgs& P, long long B, float* z,
                  float* ldj, float* logp, bool drop, const uint64_t* rng, float* arec, const NllOut& no,
                  hipStream_t st) {
   if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
+  if (P.Cp % 16 != 0 || P.Cp / 16 > HP_SMAX || P.C > P.Cp) return BCNF_ERR_UNSUPPORTED;
   const dim3 grid((unsigned)((B + 15) / 16));
-  size_t lds = fwd_lds_bytes(L);
+  size_t lds = fwd2_lds_bytes(L);
   const bool save = arec != nullptr;
   int rc;
 #define BCNF_FWD(DR, SV)                                                                                    \
   rc = launch_lds(k_forward<NH, DR, SV>, lds);                                                              \
   if (rc) return rc;                                                                                        \
-  hipLaunchKernelGGL((k_forward<NH, DR, SV>), grid, dim3(BCNF_WG), lds, st, L, pk, y, hp, B, z, ldj, logp,  \
+  hipLaunchKernelGGL((k_forward<NH, DR, SV>), grid, dim3(FWD_WG), lds, st, L, pk, y, P, B, z, ldj, logp,     \
                      rng, arec, no.part);
   if (drop) {
     if (save) { BCNF_FWD(true, true) } else { BCNF_FWD(true, false) }
@@ -1816,19 +1856,17 @@ int forward_impl(const BcnfStackDesc* desc, const void* packed, const float* y, 
   if (drop && !rng_state) return BCNF_ERR_ARG;
   float* ws = (float*)workspace;
   float* arec = (save || nll) ? ws : nullptr;
-  float* hp = ws + ws_hp_off(L, batch, drop);
   NllOut no;
   if (nll) no.part = ws + ws_part_off(L, batch, drop);
   const float* pk = (const float*)packed;
   hipStream_t st = (hipStream_t)stream;
-  // h, or x with the folded feature Linear (fold_layout: Wc / bc instead of W1h^T / b1)
-  if (fold) {
-    if ((rc = launch_hp(fold_layout(L, X, ldx), fold, h, batch, hp, st))) return rc;
-  } else if ((rc = launch_hp(L, pk, h, batch, hp, st))) {
-    return rc;
-  }
+  // the condition projection runs inside k_forward: h, or x with the folded feature Linear (fold_layout: Wc / bc
+  // instead of W1h^T / b1)
+  const BcnfLayout Lp = fold ? fold_layout(L, X, ldx) : L;
+  const float* pbase = fold ? fold : pk;
+  const ProjArgs P{h, pbase + Lp.w1c_off, pbase + Lp.b1c_off, (long long)Lp.ldh, Lp.C, Lp.Cp, Lp.NKp};
   switch (L.NH) {
-#define BCNF_CASE(N) case N: rc = fwd_dispatch<N>(L, pk, y, hp, batch, z, ldj, log_prob, drop, rng_state, arec, no, st); break;
+#define BCNF_CASE(N) case N: rc = fwd_dispatch<N>(L, pk, y, P, batch, z, ldj, log_prob, drop, rng_state, arec, no, st); break;
     BCNF_CASE(1) BCNF_CASE(2) BCNF_CASE(3) BCNF_CASE(4) BCNF_CASE(5) BCNF_CASE(6) BCNF_CASE(7) BCNF_CASE(8)
 #undef BCNF_CASE
     default: return BCNF_ERR_UNSUPPORTED;
