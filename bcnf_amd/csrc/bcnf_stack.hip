@@ -34,11 +34,18 @@ thread_local int last_hip = 0;
 
 namespace {
 
-constexpr int NT_EXTRA = 7;
 constexpr int NC16_MAX = 16;           // C <= 256: register-resident column tiles of k_hp / k_dh / k_dw1h            // tiles: D_1..D_NH, D_T, D_S, A_0..A_NH, PA, GA, PB, GB
-constexpr int TILE = BCNF_ROWS * BCNF_TSTRIDE;   // 272 floats
+// Backward LDS tile of [16 samples s][16 columns r]: element (s, r) at r * TPITCH + 4 (s & 3) + (s >> 2), so the MFMA
+// operand of lane (q, r) for the four K-steps t (sample 4 t + q) is ONE 16-B read at r * TPITCH + 4 q (pitch 24:
+// conflict-free ds_read_b128).
+constexpr int TPITCH = 24;
+constexpr int TILE = 16 * TPITCH;                // 384 floats
+__host__ __device__ constexpr int tile_ix(int s, int r) { return r * TPITCH + 4 * (s & 3) + (s >> 2); }
 constexpr int STAGE_REC = 4;   // 16 * RF (RB) floats  <= 4 float4 per thread (RF, RB <= 256)
 constexpr int RING = STAGE_REC * BCNF_WG * 4;    // floats per record-ring slot: a Stage stores all of it
+// floats per lane of a block's activation record (ActRec); the AR1 single floats follow all the float4 parts
+__host__ __device__ constexpr int act_rec_floats(int NH) { return 2 * NH + 3; }
+__host__ __device__ constexpr long long ar1_off(int nb, long long nwg, int ar4) { return (long long)nb * nwg * ar4 * 4 * 256; }
 // floats per block of a backward workgroup's gradient slab: NH + 2 MFMA tiles + NH + 6 column sums (BwdJobs)
 __host__ __device__ constexpr int slab_blk_floats(int NH) { return (NH + 2) * 256 + (NH + 6) * 16; }
 
@@ -123,12 +130,11 @@ int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
 size_t fwd_lds_bytes(const BcnfLayout& L) {   // forward / inverse record ring (2 blocks)
   return sizeof(float) * (size_t)(2 * RING);
 }
-size_t fwd2_lds_bytes(const BcnfLayout& L) {  // forward: record ring + projection partials + dropout bits (2 slots)
+size_t fwd2_lds_bytes(const BcnfLayout& L) {  // forward: record ring, projection partials, dropout bits (2 slots)
   return sizeof(float) * (size_t)(2 * RING + 2 * 4 * 256 + 2 * 256);
 }
-size_t bwd_lds_bytes(const BcnfLayout& L) {   // backward record ring, gradient tiles (2)
-  const int NT = 2 * L.NH + NT_EXTRA;
-  return sizeof(float) * (size_t)(2 * RING + 2 * NT * TILE);
+size_t bwd_lds_bytes(const BcnfLayout& L) {   // backward record ring, delta tiles (2), activation tiles (3), derivative slots (2)
+  return sizeof(float) * (size_t)(2 * RING + 2 * (L.NH + 6) * TILE + 3 * (L.NH + 1) * TILE + 2 * 3 * 4 * 256);
 }
 constexpr size_t LDS_MAX = 160 * 1024;
 
@@ -969,14 +975,14 @@ struct RecB {
   static constexpr int W1T = 0, HID = 16, TT = 16 + 16 * (NH - 1), ST = TT + 16, QT = ST + 16, AN = QT + 64;
   static constexpr int USED = AN + 4;
 };
-// Activation record a training forward saves per (block, sample, lane) for the backward, so the backward
-// never recomputes the MLP: masked activations, masked GELU derivatives, tanh(s), and the block input.
+// Activation record a training forward saves per (block, sample, lane) for the backward, so the backward never
+// recomputes the MLP: masked activations, masked GELU derivatives, tanh(s) and the block input, 2 NH + 3 floats
+// stored as AR4 float4 [k][workgroup][AR4][256 threads] plus AR1 floats [k][workgroup][AR1][256] (no padding).
 template <int NH>
 struct ActRec {
   static constexpr int ACT = 0, GD = NH, S = 2 * NH, YA = 2 * NH + 1, YB = 2 * NH + 2;
-  static constexpr int AR = (2 * NH + 3 + 3) & ~3;   // floats per lane (float4 aligned)
+  static constexpr int AR = 2 * NH + 3, AR4 = AR / 4, AR1 = AR - 4 * AR4;
 };
-__host__ __device__ constexpr int act_rec_floats(int NH) { return (2 * NH + 3 + 3) & ~3; }
 
 // Burst-load floats [lo, hi) of this lane's LDS record into registers (compile-time indices, so the
 // array lives in VGPRs): one LDS wait per block instead of one per layer.
@@ -1007,12 +1013,10 @@ __device__ __forceinline__ void ld_rec_exp(float* __restrict__ rr, const float* 
 
 // Nested MLP forward on the row layout (cnf.py:98-107) from a register-resident forward record.
 // Input x (layer-1 y-part operand) and hp (its condition part + bias, from k_hp); returns t and s'
-// (pre-tanh). KEEP: also the (masked) activations
-// and masked GELU derivatives for the backward.
+// (pre-tanh). KEEP: also the masked activations and masked GELU derivatives for the backward's record.
 template <int NH, bool KEEP>
 __device__ __forceinline__ void mlp_forward(const BcnfLayout& L, const float* __restrict__ rr, float x, float hp,
-                                            uint32_t bits, bool drop, float& T, float& Sp,
-                                            float* act, float* gd) {
+                                            uint32_t bits, bool drop, float& T, float& Sp, float* act, float* gd) {
   using F = RecF<NH>;
   float a = x;
 #pragma unroll
@@ -1085,6 +1089,7 @@ __global__ __launch_bounds__(FWD_WG) void k_forward(BcnfLayout L, const float* _
   float* rec = smem;                          // [2][16*RF]
   float* hpb = rec + 2 * RING;                // [2][4][16][16]
   uint32_t* bitb = reinterpret_cast<uint32_t*>(hpb + FWD_HP);   // [2][256]
+  using AR = ActRec<NH>;
   const int nb = L.nb;
   const float* pf = pk + L.pf_off;
   const bool helper = threadIdx.x >= BCNF_WG;
@@ -1142,7 +1147,6 @@ __global__ __launch_bounds__(FWD_WG) void k_forward(BcnfLayout L, const float* _
     const float ldc = pk[L.ldc_off];
     __syncthreads();
     float ldj = 0.f;
-    using AR = ActRec<NH>;
     for (int k = 0; k < nb; ++k) {
       const int cur = k & 1;
       float rr[RecF<NH>::USED];
@@ -1155,24 +1159,21 @@ __global__ __launch_bounds__(FWD_WG) void k_forward(BcnfLayout L, const float* _
       const float xb = fmaf(rr[2], yb, rr[3]);
       float T, Sp;
       float ar[AR::AR];                                   // activation record of this block (SAVE)
-      if (SAVE)
-        mlp_forward<NH, true>(L, rr, xa, hpk, bits, DROP, T, Sp, ar + AR::ACT, ar + AR::GD);
-      else
-        mlp_forward<NH, false>(L, rr, xa, hpk, bits, DROP, T, Sp, nullptr, nullptr);
+      mlp_forward<NH, SAVE>(L, rr, xa, hpk, bits, DROP, T, Sp, ar + AR::ACT, ar + AR::GD);
       const float Sv = tanh_bf(Sp);                      // cnf.py:107
       const float zb = fmaf(exp_fast(Sv), xb, T);        // cnf.py:179
       ldj += Sv;                                         // cnf.py:190
-      if (SAVE && !(BCNF_EXP & 8192)) {                  // 16-B stores, a lane's record contiguous
+      if (SAVE && !(BCNF_EXP & 8192)) {                  // coalesced across the wave
         ar[AR::S] = Sv;
         ar[AR::YA] = ya;
         ar[AR::YB] = yb;
+        const long long rb0 = (long long)k * gridDim.x + blockIdx.x;
+        floatx4* d4 = reinterpret_cast<floatx4*>(arec) + rb0 * AR::AR4 * BCNF_WG + tid;
 #pragma unroll
-        for (int i = AR::YB + 1; i < AR::AR; ++i) ar[i] = 0.f;
-        // record [k][workgroup][AR/4][256 threads] float4: every store coalesced across the wave
-        floatx4* dst = reinterpret_cast<floatx4*>(arec) + ((long long)k * gridDim.x + blockIdx.x) * (AR::AR / 4) * BCNF_WG + tid;
+        for (int i = 0; i < AR::AR4; ++i) d4[i * BCNF_WG] = floatx4{ar[4 * i], ar[4 * i + 1], ar[4 * i + 2], ar[4 * i + 3]};
+        float* d1p = arec + ar1_off(nb, gridDim.x, AR::AR4) + rb0 * AR::AR1 * BCNF_WG + tid;
 #pragma unroll
-        for (int i = 0; i < AR::AR / 4; ++i)
-          dst[i * BCNF_WG] = floatx4{ar[4 * i], ar[4 * i + 1], ar[4 * i + 2], ar[4 * i + 3]};
+        for (int i = 0; i < AR::AR1; ++i) d1p[i * BCNF_WG] = ar[4 * AR::AR4 + i];
       }
       if (BCNF_EXP & 4096) { ya = xa; yb = zb; } else
       mix(rr + RecF<NH>::Q, xa, zb, ya, yb);             // y @ Q (cnf.py:335); identity after the last block
@@ -1304,34 +1305,18 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse(BcnfLayout L, const float* 
 // ------------------------------------------------------------------------------------------------
 // Backward
 // ------------------------------------------------------------------------------------------------
-struct BwdTiles {   // tile indices inside one tile buffer
-  int NH;
-  __device__ __forceinline__ int D(int l) const { return l - 1; }          // l = 1..NH
-  __device__ __forceinline__ int DT() const { return NH; }
-  __device__ __forceinline__ int DS() const { return NH + 1; }
-  __device__ __forceinline__ int A(int l) const { return NH + 2 + l; }     // l = 0..NH
-  __device__ __forceinline__ int PA() const { return 2 * NH + 3; }
-  __device__ __forceinline__ int GA() const { return 2 * NH + 4; }
-  __device__ __forceinline__ int PB() const { return 2 * NH + 5; }
-  __device__ __forceinline__ int GB() const { return 2 * NH + 6; }
-  __device__ __forceinline__ int count() const { return 2 * NH + NT_EXTRA; }
-};
-
-// Gradient jobs of one block (compile-time for a given NH; the slab layout they write is decoded by
-// slab_to_canonical):
-//   W jobs   c = 0 .. NH+1: dW of Linear c+1 (c = NH, NH+1: the last Linear's t and s row halves) as one
-//            16 x 16 fp32-MFMA tile over the workgroup's 16 samples, out[i][j] = sum_s delta[s][i] act[s][j]
-//            (Linear 1: only its y-part columns; the condition part is the split-K GEMM of the tail)
-//   sum jobs c = 0 .. NH+5: column sums over the 16 samples (VALU + two cross-row permlane swaps): the biases of
-//            Linear 1 .. NH, the last Linear's t and s halves, then ActNorm scale_a, bias_a, scale_b, bias_b
+// Backward LDS tiles ([16 samples][17] each): the compute waves' delta tiles of a block, [D_1 .. D_NH, D_T, D_S, PA,
+// GA, PB, GB] (2 slots), and the helper waves' activation tiles A_0 .. A_NH (A_0 = ActNorm output of the y-part,
+// A_l = masked GELU output of hidden layer l; 3 slots, since they are built one block ahead of the compute waves).
 template <int NH>
 struct BwdJobs {
+  static constexpr int ND = NH + 6, NA = NH + 1;
   static constexpr int NW = NH + 2, NS = NH + 6;
   static constexpr int SUM_OFF = NW * 256;                 // slab block: [NW][64 lanes][4] then [NS][16]
   static constexpr int BLK = NW * 256 + NS * 16;
-  __device__ static constexpr int wa(int c) { return c < NH ? c : (c == NH ? NH : NH + 1); }      // delta tile
-  __device__ static constexpr int wb(int c) { return c < NH ? NH + 2 + c : 2 * NH + 2; }          // act tile
-  __device__ static constexpr int sa(int c) { return c < NH + 2 ? c : 2 * NH + 3 + (c - NH - 2); }
+  // W job c = dW of Linear c + 1 (c = NH, NH + 1: the last Linear's t / s row halves): delta tile c x act tile wb(c)
+  __device__ static constexpr int wb(int c) { return c < NH ? c : NH; }
+  // sum job c = column sum of delta tile c (biases of Linear 1 .. NH, t / s halves, then ActNorm PA, GA, PB, GB)
 };
 
 // Sum of v over the 4 rows (16-lane groups) of the wave, returned in every lane (gfx950 permlane swaps:
@@ -1343,33 +1328,31 @@ __device__ __forceinline__ float sum_rows4(float v) {
   return __uint_as_float(p2[0]) + __uint_as_float(p2[1]);
 }
 
-// Helper-wave work for block m: every parameter gradient of the block except W1's condition part, from the
-// [16 samples][16] LDS tiles the compute waves wrote, straight to slab block m (no LDS gradient block):
-//   W job c: lane l holds D[4(l>>4) + r][l & 15], r = 0..3, stored as ONE float4 at [c][l] (1 KB per wave, coalesced)
-//   sum job c: 16 floats at SUM_OFF + 16 c (lanes 0..15)
+// Helper-wave gradient jobs of block m, from its delta tiles Td and activation tiles Ta, straight to slab block m
+// (no LDS gradient block):
+//   W job c: 16 x 16 fp32-MFMA tile over the workgroup's 16 samples, out[i][j] = sum_s delta[s][i] act[s][j]; lane l
+//            holds D[4(l>>4) + r][l & 15], r = 0..3, stored as ONE float4 at [c][l] (1 KB per wave, coalesced)
+//            (Linear 1: only its y-part columns; the condition part is the split-K GEMM of the tail)
+//   sum job c: 16 column sums at SUM_OFF + 16 c (lanes 0..15)
+// The slab layout is decoded by slab_to_canonical.
 template <int NH>
-__device__ __forceinline__ void bwd_grad_jobs(const float* __restrict__ T, float* __restrict__ out, int hw) {
+__device__ __forceinline__ void bwd_grad_jobs(const float* __restrict__ Td, const float* __restrict__ Ta,
+                                              float* __restrict__ out, int hw) {
   using J = BwdJobs<NH>;
   const int l64 = threadIdx.x & 63, q = l64 >> 4, r = l64 & 15;
   constexpr int UW = (J::NW + 3) / 4, US = (J::NS + 3) / 4;
-  float a[UW][4], bv[UW][4], v[US][4];
+  floatx4 a[UW], bv[UW], v[US];                            // lane (q, r): samples 4 t + q of column r, t = 0..3
+  const int o = r * TPITCH + 4 * q;
 #pragma unroll
   for (int u = 0; u < UW; ++u) {                           // all operand reads first
     const int c = hw + 4 * u < J::NW ? hw + 4 * u : J::NW - 1;
-    const float* ta = T + J::wa(c) * TILE + q * BCNF_TSTRIDE + r;
-    const float* tb = T + J::wb(c) * TILE + q * BCNF_TSTRIDE + r;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      a[u][t] = ta[4 * t * BCNF_TSTRIDE];
-      bv[u][t] = tb[4 * t * BCNF_TSTRIDE];
-    }
+    a[u] = *reinterpret_cast<const floatx4*>(Td + c * TILE + o);
+    bv[u] = *reinterpret_cast<const floatx4*>(Ta + J::wb(c) * TILE + o);
   }
 #pragma unroll
   for (int u = 0; u < US; ++u) {
     const int c = hw + 4 * u < J::NS ? hw + 4 * u : J::NS - 1;
-    const float* ts = T + J::sa(c) * TILE + q * BCNF_TSTRIDE + r;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) v[u][t] = ts[4 * t * BCNF_TSTRIDE];
+    v[u] = *reinterpret_cast<const floatx4*>(Td + c * TILE + o);
   }
   floatx4 acc[UW];
 #pragma unroll
@@ -1388,15 +1371,17 @@ __device__ __forceinline__ void bwd_grad_jobs(const float* __restrict__ T, float
     if (hw + 4 * u < J::NW) reinterpret_cast<floatx4*>(out + 256 * (hw + 4 * u))[l64] = acc[u];
 }
 
+__device__ unsigned long long g_phase[16];
 // Whole-stack backward, one launch, 512 threads = two roles per SIMD (waves w and w + 4 share a SIMD):
-//  * compute waves 0..3 (4 samples each, row layout): back-propagate block k from its saved activation record
-//    (VALU, DPP rotations) and write the [16 samples][16] tiles of block k (deltas, activations, ActNorm terms);
-//  * helper waves 4..7: in the same interval, the MFMA / column-sum gradient jobs of block k+1 from the tiles
-//    written in the previous interval, stored straight to the slab, and the staging of block k-1's backward
-//    record into the LDS ring.
-// One barrier per block. The helpers' loads, MFMAs and stores fill the issue slots the compute waves' dependent
-// chains leave idle instead of sitting on their critical path.
+//  * compute waves 0..3 (4 samples each, row layout): back-propagate block k (VALU, DPP rotations) from its
+//    backward record and its masked GELU derivatives (LDS), writing block k's delta tiles;
+//  * helper waves 4..7, in the same interval: the MFMA / column-sum gradient jobs of block k+1 (tiles of the
+//    previous interval) straight to the slab, and block k-1's inputs -- its activation record (loaded one interval
+//    earlier) split into activation tiles and the compute waves' derivative slot, its backward record staged into
+//    the LDS ring.
+// One barrier per block; the compute waves issue no global loads.
 constexpr int BWD_WG = 2 * BCNF_WG;
+constexpr int BWD_G4 = 3;                // float4 per thread of the derivative slot: gd[NH], S, ya, yb (NH <= 9)
 
 template <int NH>
 __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* __restrict__ pk,
@@ -1407,49 +1392,122 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
                                                      float* __restrict__ slab_all, long long slab_stride,
                                                      const float* __restrict__ nll_part, float* __restrict__ loss_out,
                                                      uint64_t* rng_w, int32_t* guard) {
+  static_assert(NH + 3 <= 4 * BWD_G4, "derivative slot");
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const BwdTiles TI{NH};
   using AR = ActRec<NH>;
   using RBk = RecB<NH>;
   using J = BwdJobs<NH>;
   const int RBL = 16 * L.RB;
-  const int NT = TI.count();
-  float* recB = smem;                   // [2][16*RB]
-  float* tiles = recB + 2 * RING;       // [2][NT][272]
+  float* recB = smem;                                   // [2][16*RB]
+  float* dT = recB + 2 * RING;                          // [2][ND][TILE]
+  float* aT = dT + 2 * J::ND * TILE;                    // [3][NA][TILE]
+  floatx4* gsl = reinterpret_cast<floatx4*>(aT + 3 * J::NA * TILE);   // [2][BWD_G4][256]
   const int nb = L.nb;
   const float* pbk = pk + L.pb_off;
-  float* slab = slab_all + (long long)blockIdx.x * slab_stride;
   const bool helper = threadIdx.x >= BCNF_WG;
-  const int ht = (int)threadIdx.x - BCNF_WG;                   // helper thread 0..255
-
-  {   // record of the last block
-    Stage<STAGE_REC> sr;
-    if (!helper) {
-      sr.load_t(pbk + (long long)(nb - 1) * RBL, RBL, (int)threadIdx.x);
-      sr.store_t(recB + ((nb - 1) & 1) * RING, (int)threadIdx.x);
-    }
+  const int t8 = (int)threadIdx.x & (BCNF_WG - 1);
+  const int j = t8 & 15, s = t8 >> 4;
+  const int tix = tile_ix(s, j);
+  // BCNF_EXP & 256: per-phase cycles of workgroup 0's wave 0 (compute) and wave 4 (helper) -> g_phase
+  unsigned long long ph_t = (BCNF_EXP & 256) ? __builtin_amdgcn_s_memtime() : 0ULL, ph_acc[4] = {0, 0, 0, 0};
+#define PHS(i)                                                                                   \
+  if (BCNF_EXP & 256) {                                                                          \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();                                  \
+    ph_acc[i] += _t - ph_t;                                                                      \
+    ph_t = _t;                                                                                   \
   }
-  __syncthreads();
 
   if (helper) {
-    const int hw = __builtin_amdgcn_readfirstlane(ht >> 6);
-    for (int k = nb - 1; k >= 0; --k) {
-      Stage<STAGE_REC> sB;
-      if (k >= 1) sB.load_t(pbk + (long long)(k - 1) * RBL, RBL, ht);
-      if (k + 1 < nb) bwd_grad_jobs<NH>(tiles + ((k + 1) & 1) * NT * TILE, slab + (long long)(k + 1) * J::BLK, hw);
-      if (k >= 1) sB.store_t(recB + ((k - 1) & 1) * RING, ht);
+    const int hw = __builtin_amdgcn_readfirstlane(t8 >> 6);
+    float* slab = slab_all + (long long)blockIdx.x * slab_stride;
+    // activation records [k][workgroup][AR/4][256 threads] float4 (k_forward)
+    const floatx4* arl = reinterpret_cast<const floatx4*>(arec) + (long long)blockIdx.x * AR::AR4 * BCNF_WG + t8;
+    const long long ars = (long long)gridDim.x * AR::AR4 * BCNF_WG;
+    struct Prep {
+      Stage<STAGE_REC> sr;
+      floatx4 rec[AR::AR4];
+      float rec1[AR::AR1 > 0 ? AR::AR1 : 1];
+      float sa, ba;
+    };
+    const float* ar1l = arec + ar1_off(nb, gridDim.x, AR::AR4) + (long long)blockIdx.x * AR::AR1 * BCNF_WG + t8;
+    const long long ar1s = (long long)gridDim.x * AR::AR1 * BCNF_WG;
+    auto prep_load = [&](Prep& P, int k) {                  // block k's inputs: HBM / L2 -> registers
+      P.sr.load_t(pbk + (long long)k * RBL, RBL, t8);
+#pragma unroll
+      for (int i = 0; i < AR::AR4; ++i) P.rec[i] = arl[(long long)k * ars + i * BCNF_WG];
+#pragma unroll
+      for (int i = 0; i < AR::AR1; ++i) P.rec1[i] = ar1l[(long long)k * ar1s + i * BCNF_WG];
+      const float* an = pbk + (long long)k * RBL + j * L.RB + RBk::AN;
+      P.sa = an[0];
+      P.ba = an[1];
+    };
+    auto prep_store = [&](Prep& P, int k) {                 // registers -> LDS slots of block k
+      // every loaded register stays live until here: a register the compiler reallocated while its load is in
+      // flight would cost a wait for that load
+#pragma unroll
+      for (int i = 0; i < AR::AR4; ++i) asm volatile("" : "+v"(P.rec[i]));
+#pragma unroll
+      for (int i = 0; i < AR::AR1; ++i) asm volatile("" : "+v"(P.rec1[i]));
+      asm volatile("" : "+v"(P.sa), "+v"(P.ba));
+      float ar[4 * AR::AR4 + AR::AR1];
+#pragma unroll
+      for (int i = 0; i < AR::AR4; ++i) {
+        ar[4 * i] = P.rec[i][0];
+        ar[4 * i + 1] = P.rec[i][1];
+        ar[4 * i + 2] = P.rec[i][2];
+        ar[4 * i + 3] = P.rec[i][3];
+      }
+#pragma unroll
+      for (int i = 0; i < AR::AR1; ++i) ar[4 * AR::AR4 + i] = P.rec1[i];
+      float* ta = aT + (k % 3) * J::NA * TILE + tix;
+#pragma unroll
+      for (int l = 1; l <= NH; ++l) ta[l * TILE] = ar[AR::ACT + l - 1];
+      ta[0] = fmaf(P.sa, ar[AR::YA], P.ba);                // A_0: ActNorm output of the y-part (cnf.py:349)
+      float gs[4 * BWD_G4];
+#pragma unroll
+      for (int l = 0; l < NH; ++l) gs[l] = ar[AR::GD + l];
+      gs[NH] = ar[AR::S];
+      gs[NH + 1] = ar[AR::YA];
+      gs[NH + 2] = ar[AR::YB];
+#pragma unroll
+      for (int i = NH + 3; i < 4 * BWD_G4; ++i) gs[i] = 0.f;
+      floatx4* gd = gsl + (k & 1) * BWD_G4 * BCNF_WG + t8;
+#pragma unroll
+      for (int i = 0; i < BWD_G4; ++i) gd[i * BCNF_WG] = floatx4{gs[4 * i], gs[4 * i + 1], gs[4 * i + 2], gs[4 * i + 3]};
+      P.sr.store_t(recB + (k & 1) * RING, t8);
+    };
+    // two-deep pipeline: block k-1 is rebuilt from registers loaded one interval earlier, while block k-2's
+    // loads are in flight (an HBM round trip under load is longer than one interval)
+    // (the two register sets alternate by hand-unrolling: a copy of in-flight loads would wait for them)
+    Prep Pa, Pb;
+    prep_load(Pa, nb - 1);
+    prep_load(Pb, nb >= 2 ? nb - 2 : 0);
+    prep_store(Pa, nb - 1);
+    __syncthreads();
+    auto step = [&](int k, Prep& Pc, Prep& Pnext) {  // interval k: Pc holds block k-1's loads
+      PHS(0)
+      prep_load(Pnext, k >= 2 ? k - 2 : 0);             // unconditional (clamped): no branch around loads in flight
+      PHS(1)
+      if (k + 1 < nb && !(BCNF_EXP & 32))
+        bwd_grad_jobs<NH>(dT + ((k + 1) & 1) * J::ND * TILE, aT + ((k + 1) % 3) * J::NA * TILE,
+                          slab + (long long)(k + 1) * J::BLK, hw);
+      PHS(2)
+      if (k >= 1) prep_store(Pc, k - 1);
+      PHS(3)
       __syncthreads();
+    };
+    for (int k = nb - 1; k >= 0; k -= 2) {
+      step(k, Pb, Pa);
+      if (k == 0) break;
+      step(k - 1, Pa, Pb);
     }
-    bwd_grad_jobs<NH>(tiles, slab, hw);                        // block 0 (tiles written in the last interval)
+    bwd_grad_jobs<NH>(dT, aT, slab, hw);                     // block 0 (tiles of the last interval)
   } else {
-    const int tid = threadIdx.x, j = tid & 15, s = tid >> 4;
+    const int tid = t8;
     const long long b = (long long)blockIdx.x * 16 + s;
     const bool valid = b < B;
     const long long bc = valid ? b : B - 1;
     const int D = L.D, Da = L.Da, Db = L.Db;
-    // activation records [k][workgroup][AR/4][256 threads] float4 (k_forward)
-    const floatx4* arl = reinterpret_cast<const floatx4*>(arec) + (long long)blockIdx.x * (AR::AR / 4) * BCNF_WG + tid;
-    const long long ars = (long long)gridDim.x * (AR::AR / 4) * BCNF_WG;
     float* d1l = d1 + bc * 16 + j;                    // D1[k][b][j]  = d1l[k * B * 16]
     float* d1_dummy = d1 + (long long)nb * B * 16 + j; // rows past the batch (workspace slack)
     const long long hps = B * 16;
@@ -1469,81 +1527,76 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
         if (dldj) dl = dldj[b];
       }
     }
-    floatx4 ar_n[AR::AR / 4];
-#pragma unroll
-    for (int i = 0; i < AR::AR / 4; ++i) ar_n[i] = arl[(long long)(nb - 1) * ars + i * BCNF_WG];
-
+    __syncthreads();
+    PHS(0)
     for (int k = nb - 1; k >= 0; --k) {
       const int cur = k & 1;
-      const int k1 = k >= 1 ? k - 1 : 0;               // clamped: no branches
-      float ar[AR::AR];
+      float gs[4 * BWD_G4];
+      {
+        const floatx4* gd4 = gsl + cur * BWD_G4 * BCNF_WG + tid;
 #pragma unroll
-      for (int i = 0; i < AR::AR / 4; ++i) {
-        ar[4 * i] = ar_n[i][0];
-        ar[4 * i + 1] = ar_n[i][1];
-        ar[4 * i + 2] = ar_n[i][2];
-        ar[4 * i + 3] = ar_n[i][3];
+        for (int i = 0; i < BWD_G4; ++i) {
+          const floatx4 v = gd4[i * BCNF_WG];
+          gs[4 * i] = v[0];
+          gs[4 * i + 1] = v[1];
+          gs[4 * i + 2] = v[2];
+          gs[4 * i + 3] = v[3];
+        }
       }
-#pragma unroll
-      for (int i = 0; i < AR::AR / 4; ++i) ar_n[i] = arl[(long long)k1 * ars + i * BCNF_WG];
-      __builtin_amdgcn_sched_barrier(0);                // the prefetch is issued HERE, not sunk to its use
-      float* Tt = tiles + cur * NT * TILE;
-      const int tix = s * BCNF_TSTRIDE + j;
+      float* Tt = dT + cur * J::ND * TILE + tix;
       float rb[RBk::USED];
       ld_rec<0, RBk::USED>(rb, recB + cur * RING + j * L.RB);
-      const float ya = ar[AR::YA], yb = ar[AR::YB], S = ar[AR::S];
-      const float* act = ar + AR::ACT;
-      const float* gd = ar + AR::GD;
-      const float an_sa = rb[RBk::AN], an_ba = rb[RBk::AN + 1], an_sb = rb[RBk::AN + 2], an_bb = rb[RBk::AN + 3];
-      const float xa = fmaf(an_sa, ya, an_ba);
+      const float* gd = gs;
+      const float S = gs[NH], ya = gs[NH + 1], yb = gs[NH + 2];
+      const float an_sa = rb[RBk::AN], an_sb = rb[RBk::AN + 2], an_bb = rb[RBk::AN + 3];
       const float xb = fmaf(an_sb, yb, an_bb);
       const float e = exp_fast(S);
       float gza, gzb;
       mix(rb + RBk::QT, gya, gyb, gza, gzb);            // g @ Q^T (identity for the last block)
-      const float dT = gzb;                              // z_b = exp(s) y_b + t
+      const float dT_ = gzb;                             // z_b = exp(s) y_b + t
       const float dS = (j < Db) ? fmaf(gzb * e, xb, dl) : 0.f;
       const float dSp = dS * (1.f - S * S);
       const float dxb = gzb * e;
-      Tt[TI.DT() * TILE + tix] = dT;
-      Tt[TI.DS() * TILE + tix] = dSp;
-      Tt[TI.A(NH) * TILE + tix] = act[NH - 1];
+      Tt[NH * TILE] = dT_;
+      Tt[(NH + 1) * TILE] = dSp;
       float da = 0.f, da2 = 0.f;
-      rot16x2(dT, rb + RBk::TT, da, dSp, rb + RBk::ST, da2);
+      rot16x2(dT_, rb + RBk::TT, da, dSp, rb + RBk::ST, da2);
       da += da2;
 #pragma unroll
       for (int l = NH; l >= 2; --l) {
         const float dpre = da * gd[l - 1];
-        Tt[TI.D(l) * TILE + tix] = dpre;
-        Tt[TI.A(l - 1) * TILE + tix] = act[l - 2];
+        Tt[(l - 1) * TILE] = dpre;
         da = rot16(dpre, rb + RBk::HID + 16 * (l - 2), 0.f);
       }
       const float dpre1 = da * gd[0];
-      Tt[TI.D(1) * TILE + tix] = dpre1;
-      Tt[TI.A(0) * TILE + tix] = xa;
+      Tt[0] = dpre1;
       *(valid ? d1l + k * hps : d1_dummy) = dpre1;      // dL/d pre-activation of Linear 1 (split-K, dh)
       const float dxa = rot16(dpre1, rb + RBk::W1T, gza);
       {   // ActNorm tiles (consumed only for blocks that have an ActNorm)
         const float inv_a = (j < Da) ? __builtin_amdgcn_rcpf(an_sa) : 0.f;
         const float inv_b = (j < Db) ? __builtin_amdgcn_rcpf(an_sb) : 0.f;
-        Tt[TI.PA() * TILE + tix] = fmaf(dxa, ya, dl * inv_a);
-        Tt[TI.GA() * TILE + tix] = dxa;
-        Tt[TI.PB() * TILE + tix] = fmaf(dxb, yb, dl * inv_b);
-        Tt[TI.GB() * TILE + tix] = dxb;
+        Tt[(NH + 2) * TILE] = fmaf(dxa, ya, dl * inv_a);
+        Tt[(NH + 3) * TILE] = dxa;
+        Tt[(NH + 4) * TILE] = fmaf(dxb, yb, dl * inv_b);
+        Tt[(NH + 5) * TILE] = dxb;
       }
       gya = an_sa * dxa;
       gyb = an_sb * dxb;
+      PHS(1)
       __syncthreads();
+      PHS(2)
     }
-    __syncthreads();                                   // pairs with the helpers' block-0 jobs
     if (dy && valid) {
       if (j < Da) dy[b * D + j] = gya;
       if (j < Db) dy[b * D + Da + j] = gyb;
     }
   }
-  if (helper) __syncthreads();
+  if ((BCNF_EXP & 256) && blockIdx.x == 0 && (threadIdx.x == 0 || threadIdx.x == BCNF_WG))
+    for (int i = 0; i < 4; ++i) g_phase[(helper ? 4 : 0) + i] = ph_acc[i];
+#undef PHS
   if (loss_out && blockIdx.x == 0) {                 // deferred NLL reduction of the forward
-    __syncthreads();
-    nll_finalize<BWD_WG>(nll_part, (int)gridDim.x, B, loss_out, rng_w, guard, tiles);
+    __syncthreads();                                  // (the helpers' last jobs have read the tiles)
+    nll_finalize<BWD_WG>(nll_part, (int)gridDim.x, B, loss_out, rng_w, guard, dT);
   }
 }
 
@@ -1815,8 +1868,8 @@ int bwd_dispatch(const BcnfLayout& L, const float* pk, const float* dz, const fl
   size_t lds = bwd_lds_bytes(L);
   const int rc = launch_lds(k_backward<NH>, lds);
   if (rc) return rc;
-  hipLaunchKernelGGL((k_backward<NH>), grid, dim3(BWD_WG), lds, st, L, pk, dz, dldj, dloss, nll, B, arec, dy, d1,
-                     slab, stride, part, loss_out, rng_w, guard);
+  hipLaunchKernelGGL((k_backward<NH>), grid, dim3(BWD_WG), lds, st, L, pk, dz, dldj, dloss, nll, B, arec, dy,
+                     d1, slab, stride, part, loss_out, rng_w, guard);
   return check_launch();
 }
 
@@ -2221,6 +2274,12 @@ const char* bcnf_status_string(int status) {
 }
 
 int bcnf_last_hip_error(void) { return bcnf_rt::last_hip; }
+
+#if BCNF_EXP & 256
+int bcnf_debug_phases(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(g_phase)) == hipSuccess ? 0 : 3;
+}
+#endif
 
 
 }  // extern "C"

@@ -195,6 +195,67 @@ def log_prob_error(model, device):
     return float(err.max()), float((err / ref.abs().clamp_min(1.0)).max())
 
 
+def _proxy_sd(model, seed):
+    """numpy-PCG64 weights in state_dict order, the orthonormal matrices kept (tests/golden/make_golden.py's
+    large_proxy_state, the recipe the g7 fixture was made with)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    sd = {}
+    for k, v in model.state_dict().items():
+        if k.endswith("orthonormal_matrix"):
+            sd[k] = v.detach().cpu().numpy()
+            continue
+        shape = tuple(v.shape)
+        if k.endswith(".scale"):
+            a = rng.uniform(0.7, 1.3, size=shape)
+        elif len(shape) == 2:
+            a = rng.uniform(-1.0, 1.0, size=shape) / np.sqrt(shape[1])
+        else:
+            a = rng.uniform(-0.05, 0.05, size=shape)
+        sd[k] = a.astype(np.float32)
+    return sd
+
+
+def _lp_err(lp, z_ref, ldj_ref):
+    ref = -(0.5 * (torch.from_numpy(z_ref).double() ** 2).sum(1) - torch.from_numpy(ldj_ref).double()) \
+        - 0.5 * z_ref.shape[1] * math.log(2 * math.pi)
+    err = (lp.double().cpu() - ref).abs()
+    return float(err.max()), float((err / ref.abs().clamp_min(1.0)).max())
+
+
+def log_prob_errors_more(device):
+    """log_prob max-abs / max-rel error on the reference's other fixtures -- G7 (FC_large-shaped proxy:
+    C = 1360, [526] x 5, 2 blocks, the wide kernel family) and G9 (physical ballistic trajectories from the
+    reference's ODE simulator on the seeded FC_small init)."""
+    from bcnf_amd import CondRealNVP_v2
+    out = {}
+    p9 = os.path.join(ROOT, "tests", "golden", "g9_ballistic.npz")
+    if os.path.exists(p9):
+        d = np.load(p9)
+        torch.manual_seed(2024_03_25)
+        m = CondRealNVP_v2.from_config(FC_SMALL).to(device).eval()
+        with torch.no_grad():
+            lp = m.log_prob(torch.from_numpy(d["y"]).to(device), torch.from_numpy(d["traj"]).to(device))
+        out["g9"] = _lp_err(lp, d["z"], d["ldj"])
+    p7 = os.path.join(ROOT, "tests", "golden", "g7_large_proxy.npz")
+    if os.path.exists(p7):
+        d = np.load(p7)
+        shape = dict(size=19, nested_sizes=[526] * 5, n_blocks=2, n_conditions=1360, dropout=0.407, act_norm=True)
+        cfg = {"global": {"parameter_selection": [f"p{i}" for i in range(19)]}, "model": {"kwargs": shape},
+               "feature_networks": [
+                   {"type": "ConcatenateCondition", "kwargs": {"input_size": None, "output_size": 90}},
+                   {"type": "FullyConnected", "kwargs": {"sizes": [90, 1360], "dropout": 0.0}}]}
+        torch.manual_seed(7)
+        m = CondRealNVP_v2.from_config(cfg)
+        sd = _proxy_sd(m, 2024_03_25)
+        sd["layers.2.orthonormal_matrix"] = d["q/layers.2.orthonormal_matrix"]
+        m.load_state_dict({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in sd.items()})
+        m.to(device).eval()
+        with torch.no_grad():
+            lp = m.log_prob(torch.from_numpy(d["y"]).to(device), torch.from_numpy(d["traj"]).to(device))
+        out["g7"] = _lp_err(lp, d["z"], d["ldj"])
+    return {f"{k}_{n}": v[i] for k, v in out.items() for i, n in enumerate(("max_abs", "max_rel"))}
+
+
 def cpu_baseline(args):
     """The CPU oracle (PyTorch-eager restatement of the reference, pinned to its outputs) timed on this host's
     cores: same FC_small step at the same batch, bounded sample."""
@@ -329,6 +390,7 @@ def main():
                        "global_batch": B * world, "parallelism": f"dp{world}", "hip_graph": not args.no_graph,
                        "n_blocks": 32, "nested_sizes": [16] * 7, "n_conditions": 80, "dropout": 0.383},
             "log_prob_max_abs_err": lp_abs, "log_prob_max_rel_err": lp_rel,
+            "log_prob_err_other_fixtures": log_prob_errors_more(device),
             "last_loss": losses[0] if losses else None,
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,

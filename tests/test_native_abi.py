@@ -45,7 +45,7 @@ def test_layout_queries_match_module_tree():
     ws = N.query_i64(N.lib().bcnf_workspace_bytes, ctypes.byref(d), ctypes.c_int64(4096), ctypes.c_int32(1))
     # activation records (7 masked activations, 7 masked GELU derivatives, tanh(s), y_a, y_b -> 20 floats
     # per lane and block), loss partials, condition projection HP, Linear-1 deltas D1 (+ a dummy row)
-    assert ws == 32 * 4096 * 16 * 20 * 4 + 256 * 4 + 2 * 32 * 4096 * 16 * 4 + 16 * 4   # + D1 dummy row
+    assert ws == 32 * 4096 * 16 * 17 * 4 + 256 * 4 + 2 * 32 * 4096 * 16 * 4 + 16 * 4   # 17-float records, + D1 dummy row
     sb = N.query_i64(N.lib().bcnf_slab_bytes, ctypes.byref(d), ctypes.c_int64(4096))
     # per workgroup: nb blocks of the compact block (3430 - 16*80 condition columns = 2150, padded to 4),
     # plus 32 split-K partials (128 rows each) of the condition columns [nb][16][80]

@@ -60,7 +60,7 @@ def main():
 
 
 def phases():
-    """Per-phase cycles of the backward loop (experiment build with BCNF_EXP & 128)."""
+    """Per-phase cycles of the backward loop, workgroup 0 (experiment build with BCNF_EXP & 256)."""
     import ctypes
     from bcnf_amd import _native as N
     L = N.lib()
@@ -68,11 +68,11 @@ def phases():
         return
     buf = (ctypes.c_ulonglong * 16)()
     L.bcnf_debug_phases(buf)
-    names = ["copy_out+bar", "prefetch issue", "mfma phase", "hp_quarter", "ld_rec+setup", "mlp recompute",
-             "backprop", "commit", "end barrier"]
-    tot = sum(buf[i] for i in range(9))
+    names = ["compute: prologue", "compute: chain", "compute: barrier wait", "-",
+             "helper: loop top/barrier", "helper: prep_load issue", "helper: grad jobs", "helper: prep_store"]
     for i, n in enumerate(names):
-        print(f"  {n:16s} {buf[i]:10d} cycles  {100.0 * buf[i] / max(tot, 1):5.1f}%")
+        if n != "-":
+            print(f"  {n:26s} {buf[i]:10d} cycles")
 
 
 if __name__ == "__main__":
