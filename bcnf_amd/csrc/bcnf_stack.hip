@@ -1055,6 +1055,8 @@ __device__ __forceinline__ void mix(const float* __restrict__ rq, float a, float
 // ------------------------------------------------------------------------------------------------
 // Forward
 // ------------------------------------------------------------------------------------------------
+__device__ unsigned long long g_phase[16];   // BCNF_EXP & 256 phase stamps (bcnf_debug_phases)
+
 // Condition projection operands of the forward (the y-independent part of Linear 1, cnf.py:98-107 with the
 // condition columns): HP[b][16k + j] = sum_c h[b][c] W1hC[c][16k + j] + b1c[16k + j]; on the folded path h = x and
 // W1hC / b1c are the folded Wc / bc (fold_layout).
@@ -1099,6 +1101,14 @@ __global__ __launch_bounds__(FWD_WG) void k_forward(BcnfLayout L, const float* _
   const long long bc = b < B ? b : B - 1;                       // rows past the batch replay the last sample
   uint64_t seed = 0, off = 0;
   if (DROP) { seed = rng[0]; off = rng[1]; }
+  // BCNF_EXP & 256: per-phase cycles of workgroup 0's wave 0 (compute) and wave 4 (helper) -> g_phase[8..]
+  unsigned long long ph_t = (BCNF_EXP & 256) ? __builtin_amdgcn_s_memtime() : 0ULL, ph_acc[3] = {0, 0, 0};
+#define PHF(i)                                                                                   \
+  if (BCNF_EXP & 256) {                                                                          \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();                                  \
+    ph_acc[i] += _t - ph_t;                                                                      \
+    ph_t = _t;                                                                                   \
+  }
 
   if (helper) {
     const int hw = __builtin_amdgcn_readfirstlane(t8 >> 6);
@@ -1135,9 +1145,12 @@ __global__ __launch_bounds__(FWD_WG) void k_forward(BcnfLayout L, const float* _
     };
     prepare(0);
     __syncthreads();
+    PHF(0)
     for (int k = 0; k < nb; ++k) {
       if (k + 1 < nb) prepare(k + 1);
+      PHF(1)
       __syncthreads();
+      PHF(2)
     }
   } else {
     const int tid = t8;
@@ -1177,7 +1190,9 @@ __global__ __launch_bounds__(FWD_WG) void k_forward(BcnfLayout L, const float* _
       }
       if (BCNF_EXP & 4096) { ya = xa; yb = zb; } else
       mix(rr + RecF<NH>::Q, xa, zb, ya, yb);             // y @ Q (cnf.py:335); identity after the last block
+      PHF(1)
       __syncthreads();
+      PHF(2)
     }
     const float ltot = row_sum16(ldj) + ldc;
     if (j < Da) z[bc * D + j] = ya;
@@ -1187,6 +1202,9 @@ __global__ __launch_bounds__(FWD_WG) void k_forward(BcnfLayout L, const float* _
     if (logp && j == 0) logp[bc] = -(0.5f * q2 - ltot) - 0.5f * (float)D * 1.8378770664093454836f;
     if (nll_part && j == 0) rec[s] = (b < B) ? 0.5f * q2 - ltot : 0.f;   // rec: free after the last barrier
   }
+  if ((BCNF_EXP & 256) && SAVE && blockIdx.x == 0 && (threadIdx.x == 0 || threadIdx.x == BCNF_WG))
+    for (int i = 0; i < 3; ++i) g_phase[8 + (helper ? 4 : 0) + i] = ph_acc[i];
+#undef PHF
   if (nll_part) {   // per-workgroup partial of inn_nll_loss (utils.py:40-46); reduced by nll_finalize
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1371,7 +1389,6 @@ __device__ __forceinline__ void bwd_grad_jobs(const float* __restrict__ Td, cons
     if (hw + 4 * u < J::NW) reinterpret_cast<floatx4*>(out + 256 * (hw + 4 * u))[l64] = acc[u];
 }
 
-__device__ unsigned long long g_phase[16];
 // Whole-stack backward, one launch, 512 threads = two roles per SIMD (waves w and w + 4 share a SIMD):
 //  * compute waves 0..3 (4 samples each, row layout): back-propagate block k (VALU, DPP rotations) from its
 //    backward record and its masked GELU derivatives (LDS), writing block k's delta tiles;

@@ -68,8 +68,10 @@ def phases():
         return
     buf = (ctypes.c_ulonglong * 16)()
     L.bcnf_debug_phases(buf)
-    names = ["compute: prologue", "compute: chain", "compute: barrier wait", "-",
-             "helper: loop top/barrier", "helper: prep_load issue", "helper: grad jobs", "helper: prep_store"]
+    names = ["bwd compute: prologue", "bwd compute: chain", "bwd compute: barrier wait", "-",
+             "bwd helper: loop top/barrier", "bwd helper: prep_load issue", "bwd helper: grad jobs",
+             "bwd helper: prep_store", "fwd compute: prologue", "fwd compute: chain", "fwd compute: barrier wait", "-",
+             "fwd helper: prologue", "fwd helper: prepare", "fwd helper: barrier wait", "-"]
     for i, n in enumerate(names):
         if n != "-":
             print(f"  {n:26s} {buf[i]:10d} cycles")
