@@ -176,6 +176,30 @@ def launch_check(args):
         dist.destroy_process_group()
 
 
+N_SIMD = 1024                  # 256 CUs x 4 SIMDs
+CLOCK_GHZ = 2.4
+
+
+def pmc_utilisation(kernel, avg_us):
+    """Matrix-pipe utilisation and occupancy of `kernel` from the committed rocprofv3 SQ counters of the same
+    build (profiles/pmc_insts.json, tools/profile_round.sh): mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x
+    launch cycles at 2.4 GHz), waves_per_simd = SQ_WAVES / SIMDs, and the per-launch instruction counts."""
+    path = os.path.join(ROOT, "profiles", "pmc_insts.json")
+    if not os.path.exists(path) or not (avg_us == avg_us):
+        return {}
+    with open(path) as f:
+        c = json.load(f).get(kernel)
+    if not c:
+        return {}
+    out = {"waves_per_simd": round(c.get("SQ_WAVES", 0.0) / N_SIMD, 3)}
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
+        out["mfma_busy_frac"] = round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / (N_SIMD * avg_us * 1e3 * CLOCK_GHZ), 4)
+    for k in ("SQ_INSTS_VALU", "SQ_INSTS_MFMA", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT"):
+        if k in c:
+            out[k.lower()] = c[k]
+    return out
+
+
 def log_prob_error(model, device):
     """log_prob max-abs-err vs the reference's own outputs (golden fixture produced by running psaegert/bcnf)."""
     path = os.path.join(ROOT, "tests", "golden", "g1_fc_small.npz")
@@ -380,6 +404,7 @@ def main():
         if os.path.exists(pmc):
             with open(pmc) as f:
                 traffic = json.load(f).get(dom)
+        util = pmc_utilisation(dom, us)
         lp_abs, lp_rel = log_prob_error(model, device)
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
@@ -398,6 +423,7 @@ def main():
                          # both fractions -- the PMC HBM bytes of the same launch over its duration
                          "hbm_achieved_GBps": round(traffic / (us * 1e3), 1) if traffic else None,
                          "hbm_frac": round(traffic / (us * 1e3) / PEAK_HBM_GBS, 4) if traffic else None,
+                         **util,
                          "note": "fp32 VALU (DPP rotations) + fp32 MFMA; peak is the fp32 vector = MFMA-f32 rate"},
             "kernels_us": {k: round(v, 2) for k, v in kern.items()},
         }

@@ -2,6 +2,9 @@
   profiles/<tag>_kernel_stats.csv   rocprofv3 --stats kernel summary (the bench command)
   profiles/<tag>_pmc_traffic.csv    per-kernel HBM bytes per launch from FETCH_SIZE / WRITE_SIZE
   profiles/pmc_traffic.json         {kernel: bytes_per_launch} read by bench.py (roofline.traffic)
+  profiles/<tag>_pmc_insts.csv      per-kernel SQ counters per launch (waves, MFMA busy cycles, VALU / MFMA / LDS
+                                    instructions, LDS bank conflicts)
+  profiles/pmc_insts.json           {kernel: {counter: per_launch}} read by bench.py (roofline.mfma_busy_frac, ...)
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch; on gfx950 FETCH_SIZE reports half the bytes of a wide
 coalesced stream (MI355X_MICROARCH.md §HBM), so traffic = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024."""
 import csv
@@ -24,7 +27,8 @@ if stats:
 
 
 def short(name):
-    for k in ("k_forward", "k_backward", "k_inverse", "k_reduce", "k_pack", "k_ldc"):
+    for k in ("k_forward", "k_backward", "k_inverse", "k_red_gx", "k_fold_splitk", "k_fold_finish", "k_pack_fold",
+              "k_bwd_tail", "k_adam", "k_clip", "k_pack", "k_hp"):
         if k in name:
             return k
     return None
@@ -38,6 +42,22 @@ def per_kernel(counter_glob, counter):
             if k and r["Counter_Name"] == counter:
                 out.setdefault(k, []).append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in out.items()}
+
+
+INSTS = ("SQ_WAVES", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU", "SQ_INSTS_MFMA",
+         "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT")
+insts = {}
+for c in INSTS:
+    for k, v in per_kernel("insts", c).items():
+        insts.setdefault(k, {})[c] = round(v, 1)
+if insts:
+    with open(os.path.join(dst, f"{tag}_pmc_insts.csv"), "w") as f:
+        f.write("kernel," + ",".join(INSTS) + "\n")
+        for k in sorted(insts):
+            f.write(k + "," + ",".join(str(insts[k].get(c, "")) for c in INSTS) + "\n")
+    with open(os.path.join(dst, "pmc_insts.json"), "w") as f:
+        json.dump(insts, f, indent=1)
+    print(json.dumps(insts, indent=1))
 
 
 fetch = per_kernel("fetch", "FETCH_SIZE")
