@@ -259,12 +259,13 @@ struct GemmArgs {
 __device__ __forceinline__ floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
 __device__ __forceinline__ void st4(float* p, floatx4 v) { *reinterpret_cast<floatx4*>(p) = v; }
 
-// Global -> register -> LDS staging of one BM x BK (A) and BK x BN (B) tile pair, shared by both MFMA tilings.
-template <int BM, int BN, int BK, bool AKC, bool BKC>
+// Global -> register -> LDS staging of one BM x BK (A) and BK x BN (B) tile pair by NT threads, shared by both MFMA
+// tilings.
+template <int BM, int BN, int BK, bool AKC, bool BKC, int NT = WWG>
 struct TileIO {
   static constexpr int ASZ = AKC ? BM * (BK + 4) : BK * (BM + 4);
   static constexpr int BSZ = BKC ? BN * (BK + 4) : BK * (BN + 4);
-  static constexpr int AV = (BM * BK / 4 + WWG - 1) / WWG, BV = (BN * BK / 4 + WWG - 1) / WWG;
+  static constexpr int AV = (BM * BK / 4 + NT - 1) / NT, BV = (BN * BK / 4 + NT - 1) / NT;
   floatx4 ra[AV], rb[BV];
 
   template <int ROWS, bool KC>
@@ -299,15 +300,15 @@ struct TileIO {
   }
   __device__ __forceinline__ void load(const GemmArgs& g, const float* A, const float* B, int m0, int n0, int k0) {
 #pragma unroll
-    for (int i = 0; i < AV; ++i) ra[i] = fetch<BM, AKC>(A, g.lda, threadIdx.x + WWG * i, m0, k0, g.M, g.K);
+    for (int i = 0; i < AV; ++i) ra[i] = fetch<BM, AKC>(A, g.lda, threadIdx.x + NT * i, m0, k0, g.M, g.K);
 #pragma unroll
-    for (int i = 0; i < BV; ++i) rb[i] = fetch<BN, BKC>(B, g.ldb, threadIdx.x + WWG * i, n0, k0, g.N, g.K);
+    for (int i = 0; i < BV; ++i) rb[i] = fetch<BN, BKC>(B, g.ldb, threadIdx.x + NT * i, n0, k0, g.N, g.K);
   }
   __device__ __forceinline__ void store(float* As, float* Bs) const {
 #pragma unroll
-    for (int i = 0; i < AV; ++i) put<BM, AKC>(As, threadIdx.x + WWG * i, ra[i]);
+    for (int i = 0; i < AV; ++i) put<BM, AKC>(As, threadIdx.x + NT * i, ra[i]);
 #pragma unroll
-    for (int i = 0; i < BV; ++i) put<BN, BKC>(Bs, threadIdx.x + WWG * i, rb[i]);
+    for (int i = 0; i < BV; ++i) put<BN, BKC>(Bs, threadIdx.x + NT * i, rb[i]);
   }
   // four consecutive-k operand values of row / column mn at k offset kb of the staged tile
   template <int ROWS, bool KC>
@@ -515,13 +516,15 @@ __global__ __launch_bounds__(WWG, 2) void k_wgemm(const GemmArgs g) {
     }
 }
 
-// Tiling B: v_mfma_f32_16x16x4_f32, 4 waves stacked along M, each (BM/4) x BN as 16x16 accumulators (>= 2
+// Tiling B: v_mfma_f32_16x16x4_f32, NW waves stacked along M, each (BM/NW) x BN as 16x16 accumulators (>= 2
 // independent chains cover the 40-cycle dependent latency). Inside a 16-k chunk lane group q = lane >> 4 consumes
-// k = 4q + s at MFMA step s. Finer N granularity than tiling A: e.g. BN = 48 tiles N = 528 exactly.
-template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI>
-__global__ __launch_bounds__(WWG, 2) void k_wgemm16(const GemmArgs g) {
-  using IO = TileIO<BM, BN, BK, AKC, BKC>;
-  constexpr int WM = BM / 4;
+// k = 4q + s at MFMA step s. Finer N granularity than tiling A: e.g. BN = 48 tiles N = 528 exactly. NW = 8: two
+// waves per SIMD in one workgroup, so a wave's barrier / LDS / staging stalls run under its partner's MFMAs (the
+// small-M GEMMs of the wide family leave most CUs with one workgroup).
+template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI, int NW = 4>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_wgemm16(const GemmArgs g) {
+  using IO = TileIO<BM, BN, BK, AKC, BKC, 64 * NW>;
+  constexpr int WM = BM / NW;
   constexpr int TI = WM / 16, TJ = BN / 16;
   __shared__ __attribute__((aligned(16))) float lds[2 * (IO::ASZ + IO::BSZ)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1252,10 +1255,10 @@ int launch_cfg(const GemmArgs& g, int groups, hipStream_t st) {
   return bcnf_rt::launched();
 }
 
-template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI>
+template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI, int NW = 4>
 int launch_cfg16(const GemmArgs& g, int groups, hipStream_t st) {
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, groups);
-  hipLaunchKernelGGL((k_wgemm16<BM, BN, BK, AKC, BKC, EPI>), grid, dim3(WWG), 0, st, g);
+  hipLaunchKernelGGL((k_wgemm16<BM, BN, BK, AKC, BKC, EPI, NW>), grid, dim3(64 * NW), 0, st, g);
   return bcnf_rt::launched();
 }
 
@@ -1266,7 +1269,8 @@ double tile_cost(const GemmArgs& g, int groups, int BM, int BN, double eff) {
   return (double)((wgs + N_CU - 1) / N_CU) * BM * BN / eff;
 }
 
-int g_force_tiling = -1;   // test hook: 0 = 128x128, 1 = 64x64, 2 = 128x48 (16x16 MFMA)
+int g_force_tiling = -1;   // test hook: 0 = 128x128, 1 = 64x64, 2 = 128x48 (16x16 MFMA), 3 = 128x48 on 8 waves,
+                           // 4 = 96x48 on 6 waves
 
 template <bool AKC, bool BKC, int EPI>
 int gemm(const GemmArgs& g, int groups, hipStream_t st) {
@@ -1281,9 +1285,16 @@ int gemm(const GemmArgs& g, int groups, hipStream_t st) {
     const double c1 = tile_cost(g, groups, 64, 64, e1);
     const double c2 = tile_cost(g, groups, 128, 48, e2);
     pick = (c0 <= c1 && c0 <= c2) ? 0 : (c2 <= c1 ? 2 : 1);
+    // two waves per SIMD inside the workgroup pay off once the 16x16 tiling's grid covers most CUs
+    // (tools/gemm_bench.py, M = 2048, N = K = 528: 128x48 on 4 waves 23.4-27.9 us, 96x48 on 6 waves 21.0-25.2,
+    // 128x48 on 8 waves 21.6-23.5; at M = 1024 the 4-wave tile stays fastest)
+    if (pick == 2 && (long long)((g.M + 127) / 128) * ((g.N + 47) / 48) * groups >= N_CU / 2)
+      pick = (AKC && !BKC) || !AKC ? 3 : 4;
   }
   if (pick == 0) return launch_cfg<128, 128, 16, AKC, BKC, EPI>(g, groups, st);
   if (pick == 2) return launch_cfg16<128, 48, 64, AKC, BKC, EPI>(g, groups, st);
+  if (pick == 3) return launch_cfg16<128, 48, 64, AKC, BKC, EPI, 8>(g, groups, st);
+  if (pick == 4) return launch_cfg16<96, 48, 64, AKC, BKC, EPI, 6>(g, groups, st);
   return launch_cfg<64, 64, 64, AKC, BKC, EPI>(g, groups, st);
 }
 
@@ -1791,7 +1802,7 @@ int bcnf_wide_debug_phases(unsigned long long* dbg) {
 // Tiling override for every wide GEMM launch (-1 = the cost model's choice; 0 = 128x128, 1 = 64x64, 2 = 128x48).
 int bcnf_wide_force_tiling(int32_t tiling) {
   const int prev = g_force_tiling;
-  g_force_tiling = (tiling >= 0 && tiling <= 2) ? tiling : -1;
+  g_force_tiling = (tiling >= 0 && tiling <= 4) ? tiling : -1;
   return prev;
 }
 

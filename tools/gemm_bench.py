@@ -24,8 +24,9 @@ def bench(fn, iters=50):
 def main():
     dev = torch.device("cuda")
     L = N.lib()
-    shapes = [(2048, 528, 528), (16384, 528, 528), (2048, 13728, 1360), (2048, 1360, 13728), (528, 528, 2048),
-              (4096, 4096, 4096)]
+    shapes = [(2048, 528, 528), (1024, 528, 528), (2048, 13728, 1360), (2048, 1360, 13728), (528, 528, 2048)]
+    if len(sys.argv) > 1:
+        shapes = shapes[:int(sys.argv[1])]
     for (M, Nn, K) in shapes:
         for layout in (0, 1, 2):
             if layout == 2:
@@ -36,7 +37,7 @@ def main():
             C = torch.empty(M, Nn, device=dev)
             st = N.stream_handle(dev)
             res = []
-            for t in (1, 2, 3):
+            for t in (1, 2, 3, 4, 5):
                 def f():
                     L.bcnf_wide_gemm_test(layout | (t << 4), M, Nn, K, N.ptr(A), A.shape[1], N.ptr(B), B.shape[1],
                                           N.ptr(C), Nn, st)
