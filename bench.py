@@ -137,7 +137,14 @@ def host_cores():
     return max(1, n)
 
 
+SHARED_DEVICES = False          # set by init_dist: more ranks than visible GPUs (a rehearsal, reported in the JSON)
+
+
 def init_dist(args):
+    """One process per GPU over RCCL (backend "nccl"). With fewer visible GPUs than ranks (a 1-GPU box rehearsing
+    --gpus 2) the ranks share devices round-robin and talk over gloo -- RCCL refuses two ranks on one device -- and
+    the JSON line says so ("shared_devices": true): such a number is not a scaling measurement."""
+    global SHARED_DEVICES
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -145,7 +152,13 @@ def init_dist(args):
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        ndev = torch.cuda.device_count()
         if args.launch_check and not torch.cuda.is_available():
+            dist.init_process_group("gloo")
+        elif ndev < world:
+            SHARED_DEVICES = True
+            local = local % max(ndev, 1)
+            torch.cuda.set_device(local)
             dist.init_process_group("gloo")
         else:
             torch.cuda.set_device(local)
@@ -409,6 +422,7 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "ranks_seen": seen,
+            **({"shared_devices": True} if SHARED_DEVICES else {}),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic ballistic trajectories (bcnf_amd/data.py RK4 restatement of physics.py), device-resident",
             "config": {"workload": "trajectory_FC_small NLL training step (configs[1])", "batch_per_gpu": B,
@@ -581,6 +595,7 @@ def main_wide(args):
             "metric": f"NLL-training samples/sec, {WIDE_NAMES[args.workload]}",
             "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "ranks_seen": seen,
+            **({"shared_devices": True} if SHARED_DEVICES else {}),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic ballistic trajectories (bcnf_amd/data.py), device-resident",
             "config": {"workload": f"trajectory_{args.workload} NLL training step", "batch_per_gpu": B,
@@ -660,6 +675,7 @@ def main_sample(args, n_draws=500):
             "metric": "posterior draws/sec (inverse sampling, 500 draws x 1024 conditions), trajectory_FC_small",
             "value": round(value, 1), "unit": "draws/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 4), "ranks_seen": seen, "higher_is_better": True,
+            **({"shared_devices": True} if SHARED_DEVICES else {}),
             "scaling": "strong",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic ballistic trajectories as conditions, device z",
             "config": {"workload": "CondRealNVP_v2.sample-equivalent draw (configs[4])", "conditions": args.batch,
