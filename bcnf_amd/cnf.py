@@ -26,9 +26,11 @@ import torch.nn as nn
 from bcnf_amd.factories import FeatureNetworkFactory, LayerFactory
 from bcnf_amd.feature_network import (ConcatenateCondition, FeatureNetwork, FeatureNetworkStack,
                                       FullyConnectedFeatureNetwork)
+from bcnf_amd.fft_stack import FFTWideStack
 from bcnf_amd.fused import FusedStack, StackConfig, stack_forward, stack_inverse, stack_nll, stack_nll_fold
+from bcnf_amd.layers import AnyGLU, LinearFFTEnriched
 from bcnf_amd.wide import make_stack
-from bcnf_amd.utils import ParameterIndexMapping, log_prob_from_latent
+from bcnf_amd.utils import ParameterIndexMapping, inn_nll_loss, log_prob_from_latent
 
 
 class InvertibleLayer(nn.Module):
@@ -100,7 +102,9 @@ class ConditionalNestedNeuralNetwork(nn.Module):
         return sum(p.numel() for p in self.parameters())
 
     def linears(self) -> list[nn.Linear]:
-        return [m for m in self.nn if isinstance(m, nn.Linear)]
+        """The Linear of every layer: nn.Linear itself, or a LinearFFTEnriched's inner `linear`."""
+        return [m.linear if isinstance(m, LinearFFTEnriched) else m for m in self.nn
+                if isinstance(m, (nn.Linear, LinearFFTEnriched))]
 
     def canonical_params(self) -> list[nn.Parameter]:
         out = []
@@ -108,12 +112,46 @@ class ConditionalNestedNeuralNetwork(nn.Module):
             out += [lin.weight, lin.bias]
         return out
 
+    def fft_widths(self) -> list[int | None]:
+        """Per canonical parameter: the input width n of a LinearFFTEnriched weight, else None."""
+        out = []
+        for m in self.nn:
+            if isinstance(m, LinearFFTEnriched):
+                out += [m.input_size, None]
+            elif isinstance(m, nn.Linear):
+                out += [None, None]
+        return out
+
+    def forward(self, y: torch.Tensor, h: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        """cnf.py:98-107, layer by layer (the "layerwise" path of AnyGLU stacks; the fused families never call it):
+        t, tanh(s) from nn(cat(y, h))."""
+        if self.n_conditions > 0:
+            y = torch.cat([y, h], dim=1)
+        t, s = self.nn(y).chunk(2, dim=1)
+        return t, torch.tanh(s)
+
+
+def _coupling_path(layer: str, activation: str, layer_kwargs, activation_kwargs) -> str:
+    """Which implementation runs a coupling stack: "fused" (Linear + GELU: the small or wide HIP kernel family),
+    "fft" (LinearFFTEnriched + GELU: the wide family on the folded weights, bcnf_amd/fft_stack.py) or "layerwise"
+    (AnyGLU: the reference's layer sequence on the GPU, its Linear layers on the library's MFMA GEMMs)."""
+    if activation != "GELU" or activation_kwargs:
+        raise NotImplementedError(f"bcnf_amd's coupling kernels implement activation='GELU' (exact erf); got "
+                                  f"activation={activation!r}")
+    if layer == "Linear" and not layer_kwargs:
+        return "fused"
+    if layer == "LinearFFTEnriched" and not layer_kwargs:
+        return "fft"
+    if layer == "AnyGLU":
+        return "layerwise"
+    raise NotImplementedError(f"bcnf_amd: no coupling path implements layer={layer!r} with {layer_kwargs!r}")
+
 
 def _check_fused_family(layer: str, activation: str, layer_kwargs, activation_kwargs, two_way: bool):
-    if layer != "Linear" or activation != "GELU" or layer_kwargs or activation_kwargs:
+    if _coupling_path(layer, activation, layer_kwargs, activation_kwargs) != "fused":
         raise NotImplementedError(
-            f"bcnf_amd's HIP coupling kernels implement layer='Linear' with activation='GELU' "
-            f"(exact erf); got layer={layer!r}, activation={activation!r}")
+            f"bcnf_amd: a standalone coupling layer runs on the fused Linear + GELU kernels; layer={layer!r} couplings "
+            f"run inside CondRealNVP_v2")
 
 
 class ConditionalAffineCouplingLayer(ConditionalInvertibleLayer):
@@ -179,6 +217,31 @@ class ConditionalAffineCouplingLayer(ConditionalInvertibleLayer):
     def inverse(self, z: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         stack, flat = self._standalone()
         return stack_inverse(stack, z, y, training=self.training, flat=flat.detach())
+
+    # the layerwise path (AnyGLU couplings): cnf.py:165-213 as written, on the GPU
+    def layerwise_forward(self, y: torch.Tensor, x: torch.Tensor):
+        y_a, y_b = y.chunk(2, dim=-1)
+        t_a, log_s_a = self.nn_a(y_a, x)
+        z_b = torch.exp(log_s_a) * y_b + t_a
+        ldj = log_s_a.sum(dim=-1)
+        if self.two_way:
+            t_b, log_s_b = self.nn_b(z_b, x)
+            z_a = torch.exp(log_s_b) * y_a + t_b
+            ldj = ldj + log_s_b.sum(dim=-1)
+        else:
+            z_a = y_a
+        return torch.cat([z_a, z_b], dim=-1), ldj
+
+    def layerwise_inverse(self, z: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        z_a, z_b = z.chunk(2, dim=-1)
+        t_a, log_s_a = self.nn_a(z_a, y)
+        y_b = (z_b - t_a) * torch.exp(-log_s_a)
+        if self.two_way:
+            t_b, log_s_b = self.nn_b(y_b, y)        # the reference's two_way inverse, as written (cnf.py:206-208)
+            y_a = (z_a - t_b) * torch.exp(-log_s_b)
+        else:
+            y_a = z_a
+        return torch.cat([y_a, y_b], dim=-1)
 
 
 class OrthonormalTransformation(ConditionalInvertibleLayer):
@@ -289,7 +352,19 @@ class CondRealNVP_v2(ConditionalInvertibleLayer):
         cfg = StackConfig(self.size, tuple(self.nested_sizes), self.n_blocks, self.n_conditions, self.dropout,
                           self.act_norm, self.two_way)
         trainable, frozen = self._canonical()
-        object.__setattr__(self, "_fused", make_stack(cfg, trainable, frozen))
+        self._path = _coupling_path(*self._fam)
+        if self._path == "layerwise":
+            object.__setattr__(self, "_fused", _LayerwiseStack(self))
+        elif self._path == "fft":
+            fft_n = []
+            for layer in self.layers:
+                if isinstance(layer, ActNorm):
+                    fft_n += [None, None]
+                elif isinstance(layer, ConditionalAffineCouplingLayer):
+                    fft_n += layer.nn_a.fft_widths() + (layer.nn_b.fft_widths() if layer.two_way else [])
+            object.__setattr__(self, "_fused", FFTWideStack(cfg, trainable, frozen, fft_n))
+        else:
+            object.__setattr__(self, "_fused", make_stack(cfg, trainable, frozen))
 
     def _apply(self, fn, recurse=True):
         out = super()._apply(fn, recurse)
@@ -314,11 +389,12 @@ class CondRealNVP_v2(ConditionalInvertibleLayer):
         return out
 
     def _check_supported(self):
-        _check_fused_family(*self._fam, self.two_way)
         if self.n_conditions <= 0:
             # cnf.py:479-485: with n_conditions == 0 no layer matches and the reference raises
             raise ValueError("Layer must be an instance of ConditionalInvertibleLayer or InvertibleLayer, but got "
                              f"{type(self.layers[0])}")
+        if self._path == "layerwise":
+            return
         if not self._fused.supported:
             raise NotImplementedError(
                 "bcnf_amd: this stack shape fits neither HIP kernel family: the register-resident small family "
@@ -377,7 +453,10 @@ class CondRealNVP_v2(ConditionalInvertibleLayer):
         condition = self._features(conditions, deterministic_features)
         if y.dim() == 1:
             y = y.unsqueeze(0)
-        z, ldj = stack_forward(self._fused, y, condition, self.training)
+        if self._path == "layerwise":
+            z, ldj = self._fused.forward(y, condition)
+        else:
+            z, ldj = stack_forward(self._fused, y, condition, self.training)
         if log_det_J:
             self.log_det_J = ldj
         if return_features:
@@ -397,6 +476,12 @@ class CondRealNVP_v2(ConditionalInvertibleLayer):
         self._check_supported()
         if y.dim() == 1:
             y = y.unsqueeze(0)
+        if self._path == "layerwise":
+            if gather is not None:
+                raise ValueError("bcnf_amd: a deferred batch gather needs the folded feature path")
+            z, ldj = self._fused.forward(y, self._features(conditions))
+            nll = inn_nll_loss(z, ldj)
+            return torch.stack([nll, nll, torch.zeros_like(nll)])
         fold = self._foldable_linear(y, conditions)
         if fold is not None:
             x, lin = fold
@@ -466,9 +551,13 @@ class CondRealNVP_v2(ConditionalInvertibleLayer):
     def inverse(self, z: torch.Tensor, *conditions: torch.Tensor) -> torch.Tensor:
         self._check_supported()
         condition = self.feature_network_stack(*conditions)
+        if self._path == "layerwise":
+            return self._fused.inverse(z, condition)
         return stack_inverse(self._fused, z, condition, training=self.training)
 
     def _inverse_indexed(self, z, h_unique, cond_index):
+        if self._path == "layerwise":
+            return self._fused.inverse(z, h_unique[cond_index])
         return stack_inverse(self._fused, z, h_unique, cond_index=cond_index, training=self.training)
 
     def sample(self, n_samples: int, *conditions: torch.Tensor, sigma: float = 1, outer: bool = False,
@@ -509,5 +598,58 @@ class CondRealNVP_v2(ConditionalInvertibleLayer):
                 return self._inverse_indexed(z, h, idx).view(n_samples, nc, self.size)
             z = (sigma * torch.randn(n_samples, self.size)).to(self.device)
             h = self.feature_network_stack(*conditions)
+            if self._path == "layerwise":
+                return self._fused.inverse(z, h).view(n_samples, self.size)
             return stack_inverse(self._fused, z, h, training=self.training).view(n_samples, self.size)
         raise ValueError(f"Conditions have invalid shape: {[c.shape for c in conditions]}")
+
+
+class _LayerwiseStack:
+    """The coupling stack of an AnyGLU model (reference layers.py:9-31, dev configs): the reference's layer sequence
+    (cnf.py:467-508) on the GPU, each AnyGLU's two Linear layers on the library's fp32 MFMA GEMMs (HIPLinear), the
+    elementwise work in PyTorch-ROCm, gradients by autograd. Not fused: no HIP kernel family implements GLU
+    couplings. CPU tensors raise, as on the fused paths."""
+
+    supported = True
+
+    def __init__(self, model: "CondRealNVP_v2"):
+        self._model = model
+
+    def _check(self, t: torch.Tensor):
+        if not t.is_cuda:
+            raise RuntimeError("bcnf_amd: the coupling stack runs on the GPU (MI355X); got a CPU tensor")
+
+    def forward(self, y: torch.Tensor, h: torch.Tensor):
+        self._check(y)
+        ldj = torch.zeros(y.shape[0], dtype=y.dtype, device=y.device)
+        for layer in self._model.layers:
+            if isinstance(layer, ActNorm):
+                y = layer(y)
+                ldj = ldj + torch.sum(torch.log(torch.abs(layer.scale)), dim=-1)
+            elif isinstance(layer, ConditionalAffineCouplingLayer):
+                y, l = layer.layerwise_forward(y, h)
+                ldj = ldj + l
+            else:
+                y = y @ layer.orthonormal_matrix
+        return y, ldj
+
+    def inverse(self, z: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
+        self._check(z)
+        for layer in reversed(self._model.layers):
+            if isinstance(layer, ActNorm):
+                z = layer.inverse(z)
+            elif isinstance(layer, ConditionalAffineCouplingLayer):
+                z = layer.layerwise_inverse(z, h)
+            else:
+                z = z @ layer.orthonormal_matrix.T
+        return z
+
+    def reuse_pack(self):
+        import contextlib
+        return contextlib.nullcontext(self)
+
+    def flatten(self):
+        pass
+
+    def sync_grad_state(self):
+        pass

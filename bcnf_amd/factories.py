@@ -37,11 +37,15 @@ class FeatureNetworkFactory:
 
 
 class LayerFactory:
-    """Resolves `layer` / `activation` strings (cnf.py:80-81). The fused HIP stack implements
-    Linear + GELU; anything else is rejected when the model is built (no silent fallback)."""
+    """Resolves `layer` / `activation` strings (cnf.py:80-81; factories.py:61-73): torch.nn first, then the
+    variant layers of bcnf_amd.layers (AnyGLU, LinearFFTEnriched, ...), as the reference falls back to bcnf.models.
+    Which kernel path a coupling stack takes is decided when the model is built (bcnf_amd/cnf.py)."""
 
     @staticmethod
     def get_layer(layer: str, *args: Any, **kwargs: Any) -> nn.Module:
         if hasattr(nn, layer):
             return getattr(nn, layer)(*args, **kwargs)
+        from bcnf_amd.layers import LAYERS
+        if layer in LAYERS:
+            return LAYERS[layer](*args, **kwargs)
         raise NotImplementedError(f"Layer {layer} not implemented")

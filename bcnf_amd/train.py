@@ -52,6 +52,10 @@ GUARD_CHECK, GUARD_DIVERGED, GUARD_HALTED, GUARD_CHECK_GLOBAL, GUARD_WORDS = 0, 
 class TrainStep:
     def __init__(self, model, lr: float = 2e-4, hybrid_weight: float = 0.0, capture: bool = True,
                  max_norm: float = 1.0, process_group=None):
+        if getattr(model, "_path", "fused") != "fused":
+            raise NotImplementedError(
+                f"bcnf_amd.TrainStep drives the fused Linear + GELU coupling kernels; a layer={model._fam[0]!r} model "
+                "trains through the reference's Trainer loop (torch.optim on model.parameters())")
         self.model = model
         self.params = model.flat_parameters()
         self.hybrid_weight = float(hybrid_weight)

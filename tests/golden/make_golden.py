@@ -25,6 +25,9 @@ Fixtures:
                      + whether all 25 Q are bit-identical (random_state reseeds, cnf.py:319-320)
   g11_fc_large.npz   trajectory_FC_large at FULL depth (nb=26, FC[90,310x7,1360]) with PCG64 weights, eval, B=48:
                      h, z, ldj, inverse(z), every Q
+  g12_fft_enriched.npz  layer="LinearFFTEnriched" coupling stack (dev config, test size): z, ldj, inverse, the
+                     state_dict and every parameter gradient of the eval NLL (reference autograd)
+  g13_anyglu.npz     layer="AnyGLU" (Sigmoid gate) two_way coupling stack (dev config, test size): the same
 """
 import os
 import sys
@@ -336,11 +339,59 @@ def make_g11(cnf):
                         ldj=ldj.numpy(), inv=inv.numpy(), **q)
 
 
+def _variant_fixture(cnf, utils, cfg, init_seed, weight_seed, data_seed, name):
+    """A variant-layer model (configs/runs/dev/*): PCG64 weights, eval mode, B = 48 with a ConcatenateCondition-only
+    feature stack: z, ldj, inverse(z) and the gradients of inn_nll_loss w.r.t. every parameter (reference autograd)."""
+    torch.manual_seed(init_seed)
+    m = cnf.CondRealNVP_v2.from_config(cfg)
+    _load_proxy(m, weight_seed)
+    C = cfg["model"]["kwargs"]["n_conditions"]
+    rng = np.random.Generator(np.random.PCG64(data_seed))
+    y = rng.standard_normal((48, 19)).astype(np.float32)
+    cond = rng.standard_normal((48, C)).astype(np.float32)
+    z = m.forward(torch.from_numpy(y), torch.from_numpy(cond), log_det_J=True)
+    ldj = m.log_det_J
+    loss = utils.inn_nll_loss(z, ldj)
+    loss.backward()
+    grads = {("grad/" + k): p.grad.numpy() for k, p in m.named_parameters() if p.grad is not None}
+    with torch.no_grad():
+        inv = m.inverse(z.detach(), torch.from_numpy(cond))
+    np.savez_compressed(os.path.join(OUT, name), y=y, cond=cond, z=z.detach().numpy(), ldj=ldj.detach().numpy(),
+                        inv=inv.numpy(), loss=np.float64(loss.item()),
+                        **sd_to_np({k: v for k, v in m.state_dict().items()}), **grads)
+
+
+# configs/runs/dev/trajectory_LSTM_FFT_large_small_cond.yaml's coupling (layer LinearFFTEnriched, one-way, random_state)
+# at a test size; the feature stack is a bare ConcatenateCondition
+FFT_DEV = {"global": FC_SMALL["global"],
+           "model": {"kwargs": {"size": 19, "nested_sizes": [40, 40, 40], "n_conditions": 12, "n_blocks": 3,
+                                "dropout": 0.407, "act_norm": True, "layer": "LinearFFTEnriched", "activation": "GELU",
+                                "random_state": SEED}},
+           "feature_networks": [{"type": "ConcatenateCondition", "kwargs": {"input_size": None, "output_size": 12}}]}
+# configs/runs/dev/trajectory_SFrExp_LSTM_SiGLU_GELU_2_large.yaml's coupling (AnyGLU with a Sigmoid gate, GELU,
+# two_way, random_state) at a test size
+GLU_DEV = {"global": FC_SMALL["global"],
+           "model": {"kwargs": {"size": 19, "nested_sizes": [24, 24, 24], "n_conditions": 12, "n_blocks": 3,
+                                "dropout": 0.407, "act_norm": True, "two_way": True, "layer": "AnyGLU",
+                                "layer_kwargs": {"activation": "Sigmoid"}, "activation": "GELU",
+                                "random_state": SEED}},
+           "feature_networks": [{"type": "ConcatenateCondition", "kwargs": {"input_size": None, "output_size": 12}}]}
+
+
+def make_g12(cnf, utils):
+    _variant_fixture(cnf, utils, FFT_DEV, SEED + 18, SEED + 19, SEED + 20, "g12_fft_enriched.npz")
+
+
+def make_g13(cnf, utils):
+    _variant_fixture(cnf, utils, GLU_DEV, SEED + 21, SEED + 22, SEED + 23, "g13_anyglu.npz")
+
+
 def main():
     cnf, utils, physics = _import_reference()
     if len(sys.argv) > 1:                      # e.g. `make_golden.py g10 g11`: only those fixtures
         for name in sys.argv[1:]:
-            {"g10": lambda: make_g10(cnf), "g11": lambda: make_g11(cnf)}[name]()
+            {"g10": lambda: make_g10(cnf), "g11": lambda: make_g11(cnf), "g12": lambda: make_g12(cnf, utils),
+             "g13": lambda: make_g13(cnf, utils)}[name]()
         return
     torch.set_num_threads(8)
     make_g1(cnf, utils)
@@ -351,6 +402,8 @@ def main():
     make_g9(cnf, utils, physics)
     make_g10(cnf)
     make_g11(cnf)
+    make_g12(cnf, utils)
+    make_g13(cnf, utils)
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))
