@@ -25,11 +25,11 @@ import torch.nn as nn
 
 from bcnf_amd.factories import FeatureNetworkFactory, LayerFactory
 from bcnf_amd.feature_network import (ConcatenateCondition, FeatureNetwork, FeatureNetworkStack,
-                                      FullyConnectedFeatureNetwork)
+                                      FullyConnectedFeatureNetwork, HIPLinear, LSTMFeatureNetwork)
 from bcnf_amd.fft_stack import FFTWideStack
 from bcnf_amd.fused import FusedStack, StackConfig, stack_forward, stack_inverse, stack_nll, stack_nll_fold
 from bcnf_amd.layers import AnyGLU, LinearFFTEnriched
-from bcnf_amd.wide import make_stack
+from bcnf_amd.wide import WideStack, make_stack, stack_nll_wide_fold
 from bcnf_amd.utils import ParameterIndexMapping, inn_nll_loss, log_prob_from_latent
 
 
@@ -487,6 +487,10 @@ class CondRealNVP_v2(ConditionalInvertibleLayer):
             x, lin = fold
             return stack_nll_fold(self._fused, y, x, lin.weight, lin.bias, self.training, defer=defer_reduction,
                                   gather=gather)
+        wfold = self._wide_fold(y, conditions)
+        if wfold is not None and gather is None:
+            x, lin = wfold
+            return stack_nll_wide_fold(self._fused, y, x, lin.weight, lin.bias, self.training, defer=defer_reduction)
         if gather is not None:
             raise ValueError("bcnf_amd: a deferred batch gather needs the folded feature path")
         condition = self._features(conditions)
@@ -527,6 +531,36 @@ class CondRealNVP_v2(ConditionalInvertibleLayer):
             return None
         x = c.reshape(c.shape[0], -1)       # a view for TrainStep's padded rows (stride(0) = padded width)
         if x.shape[1] != lin.in_features:
+            return None
+        return x, lin
+
+    # The wide family's training path: the feature network's LAST Linear (FC_large: 310 -> 1360; LSTM_large with
+    # pool_dim=1 and mean pooling: 280 -> 1360, mean over time commutes with it) folds into the condition projection
+    # (bcnf_amd/wide.py, bcnf_wide_fold_*): the layers before it run as usual and hand x to the stack.
+    def _wide_fold(self, y, conditions):
+        if not self.fold_features or type(self._fused) is not WideStack or len(conditions) != 1 or y.requires_grad:
+            return None
+        c = conditions[0]
+        if not c.is_cuda or c.dtype != torch.float32:
+            return None
+        fns = list(self.feature_network_stack.feature_networks)
+        if len(fns) != 2 or not isinstance(fns[0], ConcatenateCondition):
+            return None
+        fn = fns[1]
+        if isinstance(fn, FullyConnectedFeatureNetwork):
+            mods = list(fn.nn)
+            if not mods or type(mods[-1]) not in (nn.Linear, HIPLinear):
+                return None
+            x = c.reshape(c.shape[0], -1)
+            for mod in mods[:-1]:
+                x = mod(x)
+            lin = mods[-1]
+        elif isinstance(fn, LSTMFeatureNetwork) and fn.pooling == "mean" and fn.pool_dim == 1:
+            x = fn.lstm(c)[0].mean(dim=1)
+            lin = fn.linear
+        else:
+            return None
+        if lin.weight.dtype != torch.float32 or not lin.weight.is_cuda or x.shape[1] != lin.in_features:
             return None
         return x, lin
 

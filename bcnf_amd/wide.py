@@ -141,14 +141,103 @@ class WideStack(FusedStack):
             self._finalize(saved[0], h.shape[0], finalize_into, training)
         return self._backward(h, z, None, None, dvals, True, saved, want_dy, want_dh)
 
+    # ------------------------------------------------------------------ folded last feature Linear
+    # h = x Wf^T + bf enters the stack only through the condition projection: P = [x | 1] (W0h_all [Wf | bf])^T, and
+    # the backward forms Gx = dZ0^T [x | 1] instead of dL/dh (include/bcnf_amd.h, bcnf_wide_fold_*).
+    def fold_supported(self, in_features: int) -> bool:
+        return in_features >= 1
+
+    def _fold_operands(self, x, wf, bf, pk):
+        B, X = x.shape
+        xp = (X + 1 + 3) // 4 * 4
+        dev = x.device
+        x1 = torch.zeros((B, xp), dtype=torch.float32, device=dev)
+        x1[:, :X] = x
+        x1[:, X] = 1.0
+        wfb = torch.zeros((wf.shape[0], xp), dtype=torch.float32, device=dev)
+        wfb[:, :X] = wf
+        if bf is not None:
+            wfb[:, X] = bf
+        rows = N.query_i64(N.lib().bcnf_wide_proj_rows, self._pdesc)
+        wcb = torch.empty((rows, xp), dtype=torch.float32, device=dev)
+        N.check(N.lib().bcnf_wide_fold_prepare(self._pdesc, N.ptr(pk), N.ptr(wfb), ctypes.c_int32(xp), N.ptr(wcb),
+                                               N.stream_handle(dev)), "bcnf_wide_fold_prepare")
+        return x1, wfb, wcb, xp
+
+    def launch_fold_nll_forward(self, y, x, wf, bf, training: bool, finalize: bool = True):
+        cfg = self.cfg
+        if y.dim() != 2 or y.shape[1] != cfg.size:
+            raise ValueError(f"bcnf_amd forward: expected (N, {cfg.size}) input, got {tuple(y.shape)}")
+        if x.dim() != 2 or x.shape[0] != y.shape[0] or tuple(wf.shape) != (cfg.n_conditions, x.shape[1]):
+            raise ValueError(f"bcnf_amd forward: folded features need x (N, X) and Wf ({cfg.n_conditions}, X), got "
+                             f"{tuple(x.shape)} and {tuple(wf.shape)}")
+        self._check_device(y, x, wf, bf)
+        B = y.shape[0]
+        if B == 0:
+            raise ValueError("bcnf_amd: the NLL of an empty batch is undefined")
+        dev = y.device
+        z = torch.empty_like(y)
+        ldj = torch.empty(B, dtype=torch.float32, device=dev)
+        drop = training and self.cfg.dropout > 0.0
+        rng = self.rng_state() if drop else None
+        ws = self._workspace(B, True, dev)
+        pk = self.packed(fresh=True)
+        x1, wfb, wcb, xp = self._fold_operands(x, wf, bf, pk)
+        rc = self._timed("k_forward", lambda: N.lib().bcnf_wide_fold_forward(
+            self._pdesc, N.ptr(self.flat), N.ptr(pk), N.ptr(y), N.ptr(x1), ctypes.c_int32(xp), N.ptr(wcb),
+            ctypes.c_int64(B), N.ptr(z), N.ptr(ldj), ctypes.c_int32(int(training)), N.ptr(rng), N.ptr(ws),
+            N.stream_handle(dev)))
+        N.check(rc, "bcnf_wide_fold_forward")
+        vals = torch.empty(3, dtype=torch.float32, device=dev)
+        if finalize:
+            self._finalize(ws, B, vals, training)
+        return z, ldj, vals, (ws, pk, x1, wfb, wcb, xp, x.shape[1])
+
+    def launch_fold_nll_backward(self, z, dvals, training: bool, saved, want_x: bool, finalize_into=None):
+        ws, pk, x1, wfb, wcb, xp, X = saved
+        B = z.shape[0]
+        dev = z.device
+        if finalize_into is not None:
+            self._finalize(ws, B, finalize_into, training)
+        gx = torch.empty_like(wcb)
+        dparams = torch.empty_like(self.flat)
+        dwfb = torch.empty_like(wfb)
+        dx = torch.empty((B, xp), dtype=torch.float32, device=dev) if want_x else None
+        rc = self._timed("k_backward", lambda: N.lib().bcnf_wide_fold_backward(
+            self._pdesc, N.ptr(self.flat), N.ptr(pk), N.ptr(x1), ctypes.c_int32(xp), N.ptr(wfb), N.ptr(wcb), N.ptr(z),
+            N.ptr(dvals), ctypes.c_int64(B), N.ptr(ws), N.ptr(gx), N.ptr(dparams), N.ptr(dwfb), N.ptr(dx),
+            N.stream_handle(dev)))
+        N.check(rc, "bcnf_wide_fold_backward")
+        return dparams, dwfb[:, :X], dwfb[:, X], (dx[:, :X] if want_x else None)
+
     @torch.no_grad()
-    def time_kernels(self, y, h, training: bool = True, iters: int = 20):
+    def time_kernels(self, y, h, training: bool = True, iters: int = 20, fold=None):
         """Average device time (us) of the wide forward (save on) and backward launches, HIP events on the launch
-        stream around `iters` back-to-back calls."""
+        stream around `iters` back-to-back calls. fold = (x, Wf, bf): the folded training launches instead."""
         L = N.lib()
         dev = y.device
         stream = N.stream_handle(dev)
         B = y.shape[0]
+        if fold is not None:
+            z, _, vals, saved = self.launch_fold_nll_forward(y, *fold, training, finalize=False)
+            ws, pk, x1, wfb, wcb, xp, _ = saved
+            ldj = torch.empty(B, dtype=torch.float32, device=dev)
+            gx = torch.empty_like(wcb)
+            dparams = torch.empty_like(self.flat)
+            dwfb = torch.empty_like(wfb)
+            dx = torch.empty((B, xp), dtype=torch.float32, device=dev)
+            rng = self.rng_state() if (training and self.cfg.dropout > 0.0) else None
+            calls = {
+                "forward": lambda: L.bcnf_wide_fold_forward(
+                    self._pdesc, N.ptr(self.flat), N.ptr(pk), N.ptr(y), N.ptr(x1), ctypes.c_int32(xp), N.ptr(wcb),
+                    ctypes.c_int64(B), N.ptr(z), N.ptr(ldj), ctypes.c_int32(int(training)), N.ptr(rng), N.ptr(ws),
+                    stream),
+                "backward": lambda: L.bcnf_wide_fold_backward(
+                    self._pdesc, N.ptr(self.flat), N.ptr(pk), N.ptr(x1), ctypes.c_int32(xp), N.ptr(wfb), N.ptr(wcb),
+                    N.ptr(z), None, ctypes.c_int64(B), N.ptr(ws), N.ptr(gx), N.ptr(dparams), N.ptr(dwfb), N.ptr(dx),
+                    stream),
+            }
+            return self._time_calls(calls, iters)
         z, _, vals, (ws, pk) = self.launch_nll_forward(y, h, training, finalize=False)
         ldj = torch.empty(B, dtype=torch.float32, device=dev)
         dparams = torch.empty_like(self.flat)
@@ -163,6 +252,10 @@ class WideStack(FusedStack):
                                                      None, None, None, ctypes.c_int32(1), ctypes.c_int64(B),
                                                      N.ptr(ws), None, N.ptr(dh), N.ptr(dparams), stream),
         }
+        return self._time_calls(calls, iters)
+
+    @staticmethod
+    def _time_calls(calls, iters):
         out = {}
         for name, fn in calls.items():
             N.check(fn(), name)
@@ -199,6 +292,36 @@ class WideStack(FusedStack):
         return y
 
 
+class _WideFoldNLL(torch.autograd.Function):
+    """vals = [loss, nll, mse] of the wide stack with the feature network's last Linear folded into the condition
+    projection: inputs (y, x, Wf, bf, flat_param); gradients for x (the earlier feature layers), Wf, bf and flat_param."""
+
+    @staticmethod
+    def forward(ctx, y, x, wf, bf, flat_param, stack: WideStack, training: bool, defer: bool):
+        z, _, vals, saved = stack.launch_fold_nll_forward(y, x, wf, bf, training, finalize=not defer)
+        ctx.stack, ctx.training, ctx.saved, ctx.defer = stack, training, saved, defer
+        ctx.has_bias = bf is not None
+        ctx.save_for_backward(z, vals)
+        return vals
+
+    @staticmethod
+    def backward(ctx, dvals):
+        z, vals = ctx.saved_tensors
+        need_x = ctx.needs_input_grad[1]
+        dparams, dwf, dbf, dx = ctx.stack.launch_fold_nll_backward(
+            z, dvals.contiguous(), ctx.training, ctx.saved, want_x=need_x, finalize_into=vals if ctx.defer else None)
+        return (None, dx, dwf, (dbf if ctx.has_bias else None), (dparams if ctx.needs_input_grad[4] else None), None,
+                None, None)
+
+
+def stack_nll_wide_fold(stack: WideStack, y, x, wf, bf, training: bool, defer: bool = False):
+    y = y.contiguous()
+    x = x.contiguous()
+    stack.sync_grad_state()
+    fp = stack.flat_param if stack.trainable[0].requires_grad else stack.flat_param.detach()
+    return _WideFoldNLL.apply(y, x, wf, bf, fp, stack, training, defer)
+
+
 def make_stack(cfg, trainable, frozen, bind: bool = True) -> FusedStack:
     """The register-resident small family when the shape fits it (FC_small), else the wide-MLP family."""
     st = FusedStack(cfg, trainable, frozen, bind=False)
@@ -212,4 +335,4 @@ def make_stack(cfg, trainable, frozen, bind: bool = True) -> FusedStack:
     return st
 
 
-__all__ = ["WideStack", "make_stack"]
+__all__ = ["WideStack", "make_stack", "stack_nll_wide_fold"]

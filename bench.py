@@ -337,6 +337,13 @@ def kernel_timing(model, data, args):
         xp[:, :X] = traj.reshape(traj.shape[0], X)
         fold = (xp[:, :X], lin.weight.detach(), None if lin.bias is None else lin.bias.detach())
         return model.fused.time_kernels(y, h, training=True, iters=args.kernel_iters, fold=fold)
+    with torch.no_grad():
+        wfold = model._wide_fold(y, (traj,)) if hasattr(model, "_wide_fold") else None
+    if wfold is not None:               # the wide family's folded step (the last feature Linear in the projection)
+        with torch.no_grad():
+            x, lin = wfold
+            fold = (x.contiguous(), lin.weight.detach(), None if lin.bias is None else lin.bias.detach())
+            return model.fused.time_kernels(y, h, training=True, iters=args.kernel_iters, fold=fold)
     return model.fused.time_kernels(y, h, training=True, iters=args.kernel_iters)
 
 

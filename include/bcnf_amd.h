@@ -332,6 +332,26 @@ int bcnf_wide_nll_finalize(const BcnfStackDesc* desc, const void* workspace, int
 int bcnf_wide_backward(const BcnfStackDesc* desc, const float* params, const void* packed, const float* h,
                        const float* z, const float* dz, const float* dldj, const float* dloss, int32_t nll,
                        int64_t batch, void* workspace, float* dy, float* dh, float* dparams, void* stream);
+/* Folded last feature Linear of a wide stack (trajectory_FC_large: h = x Wf^T + bf, feature_network.py:114-145 with
+ * the stack's condition projection cnf.py:98-107): with x1 = [x | 1 | 0] (B x xp, xp = roundup(X + 1, 4), 16-B
+ * aligned rows), wfb = [Wf | bf | 0] (C x xp) and Wcb = W0h_all wfb (nv*HP x xp):
+ *   prepare:  Wcb = W0h_all wfb (after bcnf_wide_pack; wcb holds nv*HP*xp floats, nv*HP = bcnf_wide_param_count's
+ *             layout: blocks x sides x 16-padded hidden width)
+ *   forward:  P = x1 Wcb^T, then the unchanged stack (save is implied: a backward follows)
+ *   backward: through the NLL (dloss nullable = 1): Gx = dZ0^T x1 (gx_scratch, nv*HP*xp floats), dW0h = Gx wfb^T
+ *             into dparams, dwfb = W0h_all^T Gx (C x xp: [dWf | dbf]), dx = dZ0 Wcb (B x xp, columns < X).
+ * h and dL/dh are never formed. */
+int bcnf_wide_fold_prepare(const BcnfStackDesc* desc, const void* packed, const float* wfb, int32_t xp, float* wcb,
+                           void* stream);
+int bcnf_wide_fold_forward(const BcnfStackDesc* desc, const float* params, const void* packed, const float* y,
+                           const float* x1, int32_t xp, const float* wcb, int64_t batch, float* z, float* ldj,
+                           int32_t training, const uint64_t* rng_state, void* workspace, void* stream);
+int bcnf_wide_fold_backward(const BcnfStackDesc* desc, const float* params, const void* packed, const float* x1,
+                            int32_t xp, const float* wfb, const float* wcb, const float* z, const float* dloss,
+                            int64_t batch, void* workspace, float* gx_scratch, float* dparams, float* dwfb, float* dx,
+                            void* stream);
+/* Rows of the padded projection (nv*HP) of a wide stack. */
+int bcnf_wide_proj_rows(const BcnfStackDesc* desc, int64_t* rows);
 /* Inverse: as bcnf_stack_inverse (cond_index selects feature rows; scratch = bcnf_wide_inverse_scratch_bytes). */
 int bcnf_wide_inverse(const BcnfStackDesc* desc, const float* params, const void* packed, const float* z,
                       const float* h, int64_t h_rows, const int64_t* cond_index, int64_t n_rows, float* y,

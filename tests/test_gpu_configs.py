@@ -173,3 +173,83 @@ def test_fc_large_full_depth_gradients_vs_fp64(fc_large):
         assert ok, (name, err)
         n += 1
     assert n == sum(1 for k in sd if not k.endswith("orthonormal_matrix"))
+
+
+def _nll_and_grads(m, y, cond, fold):
+    m.fold_features = fold
+    try:
+        m.zero_grad(set_to_none=True)
+        with torch.backends.cudnn.flags(enabled=False):
+            vals = m.nll_loss(y, cond)
+            vals[0].backward()
+        with torch.no_grad():      # after the step: the probe runs the feature layers (and their dropout RNG)
+            assert (m._wide_fold(y, (cond,)) is not None) == fold
+    finally:
+        del m.fold_features
+    return vals.detach().cpu(), {n: p.grad.detach().cpu().clone() for n, p in m.named_parameters()
+                                 if p.grad is not None}
+
+
+def test_fc_large_folded_nll_gradients_vs_fp64(fc_large):
+    """The training path (nll_loss) with the feature MLP's last Linear (310 -> 1360) folded into the condition
+    projection (bcnf_wide_fold_*): loss and every gradient vs the fp64 oracle, and vs the unfolded launch."""
+    m, sd, d = fc_large
+    spec = O.StackSpec(size=19, nested_sizes=[526] * 5, n_blocks=26, n_conditions=1360, dropout=0.407,
+                       act_norm=True, feature_sizes=[90] + [310] * 7 + [1360], feature_dropout=0.111)
+    sdg = {k: torch.from_numpy(np.ascontiguousarray(v)).double().requires_grad_(not k.endswith("orthonormal_matrix"))
+           for k, v in sd.items()}
+    y = torch.from_numpy(d["y"][:24])
+    traj = torch.from_numpy(d["traj"][:24])
+    zo, lo = O.model_forward(sdg, spec, y.double(), O.feature_forward(sdg, spec, traj.double()))
+    loss64 = O.inn_nll_loss(zo, lo)
+    loss64.backward()
+    vf, gf = _nll_and_grads(m, y.to(DEV), traj.to(DEV), True)
+    vu, gu = _nll_and_grads(m, y.to(DEV), traj.to(DEV), False)
+    ok, err = close(vf[:1], loss64.detach().reshape(1))
+    assert ok, ("loss", err)
+    assert set(gf) == set(gu) and len(gf) == sum(1 for k in sd if not k.endswith("orthonormal_matrix"))
+    for name in gf:
+        ok, err = close(gf[name], sdg[name].grad, rtol=1e-4, floor=1e-4)
+        assert ok, (name, "vs fp64", err)
+        ok, err = close(gf[name], gu[name], rtol=1e-4, floor=1e-4)
+        assert ok, (name, "vs unfolded", err)
+
+
+def test_fc_large_folded_training_mode_equals_unfolded(fc_large):
+    """Training mode (feature dropout 0.111, coupling dropout 0.407): the folded and unfolded launches draw the same
+    masks from the same torch / Philox states and agree on the loss and every gradient."""
+    m, _, d = fc_large
+    y = torch.from_numpy(d["y"]).to(DEV)
+    traj = torch.from_numpy(d["traj"]).to(DEV)
+    m.train()
+    try:
+        st = m.fused.rng_state().clone()
+        torch.manual_seed(11)
+        vf, gf = _nll_and_grads(m, y, traj, True)
+        m.fused.rng_state().copy_(st)
+        torch.manual_seed(11)
+        vu, gu = _nll_and_grads(m, y, traj, False)
+    finally:
+        m.eval()
+    ok, err = close(vf, vu, rtol=1e-5, floor=1e-5)
+    assert ok, ("vals", err)
+    for name in gf:
+        ok, err = close(gf[name], gu[name], rtol=1e-4, floor=1e-4)
+        assert ok, (name, err)
+
+
+def test_lstm_large_pool_dim1_folded_nll_equals_unfolded():
+    """pool_dim=1 LSTM_large: mean over time commutes with the last Linear (280 -> 1360), which folds into the
+    projection; loss and every gradient (LSTM included) agree with the unfolded launch."""
+    d = load_golden("g10_lstm_large.npz")
+    m, _ = _build(LSTM_LARGE_CFG, SEED + 12, SEED + 13, pool_dim=1)
+    m.to(DEV).eval()
+    y, traj = torch.from_numpy(d["y1"]).to(DEV), torch.from_numpy(d["traj1"]).to(DEV)
+    vf, gf = _nll_and_grads(m, y, traj, True)
+    vu, gu = _nll_and_grads(m, y, traj, False)
+    ok, err = close(vf, vu, rtol=1e-5, floor=1e-5)
+    assert ok, ("vals", err)
+    assert set(gf) == set(gu)
+    for name in gf:
+        ok, err = close(gf[name], gu[name], rtol=1e-4, floor=1e-4)
+        assert ok, (name, err)
