@@ -62,6 +62,7 @@ struct WideLayout {
   // packed buffer (floats)
   long long pk_w0h;             // [nv * HP][Cp]    row v*HP + n = W0_v[n][nin_v + c], rows n >= H and c >= C zero
   long long pk_hid;             // [nv][NH-1][HP][HP]  W_l (l = 1..NH-1), zero beyond H
+  long long pk_hidT;            // [nv][NH-1][HP][HP]  W_l^T (the backward chain's K-contiguous operand)
   long long pk_w0y;             // [nv][WY][HP]     W0_v[n][j] transposed
   long long pk_wl;              // [nv][WL][HP]     last Linear, zero beyond H
   long long pk_q;               // [nb-1][D][D]
@@ -134,6 +135,7 @@ int wide_layout(const BcnfStackDesc* d, WideLayout* L) {
   long long o = 0;
   L->pk_w0h = o; o += pad4l((long long)L->nv * L->HP * L->Cp);
   L->pk_hid = o; o += pad4l((long long)L->nv * (L->NH - 1) * L->HP * L->HP);
+  L->pk_hidT = o; o += pad4l((long long)L->nv * (L->NH - 1) * L->HP * L->HP);
   L->pk_w0y = o; o += pad4l((long long)L->nv * L->WY * L->HP);
   L->pk_wl = o;  o += pad4l((long long)L->nv * L->WL * L->HP);
   L->pk_q = o;   o += pad4l((long long)(L->nb - 1) * L->D * L->D);
@@ -160,6 +162,7 @@ __global__ __launch_bounds__(WWG) void k_wpack(const WideLayout L, const float* 
         v = prm[vbase(L, vb) + L.lin_w[sd][0] + (long long)n * L.in0[sd] + L.nin[sd] + c];
       }
     } else if (e < L.pk_w0y) {
+      if (e >= L.pk_hidT) continue;           // the transposed copy: k_wtranspose, after this launch
       const long long i = e - L.pk_hid;
       const long long per = (long long)L.HP * L.HP;
       const long long kl = i / per;
@@ -194,6 +197,35 @@ __global__ __launch_bounds__(WWG) void k_wpack(const WideLayout L, const float* 
       if (i < (long long)(L.nb - 1) * L.D * L.D) v = q[i];
     }
     pk[e] = v;
+  }
+}
+
+// pk_hidT[kl] = pk_hid[kl]^T (HP x HP each), 32 x 32 tiles through LDS (coalesced on both sides).
+__global__ __launch_bounds__(256) void k_wtranspose(const WideLayout L, float* __restrict__ pk) {
+  __shared__ float t[32][33];
+  const long long off = (long long)blockIdx.z * L.HP * L.HP;
+  const float* __restrict__ src = pk + L.pk_hid + off;
+  float* __restrict__ dst = pk + L.pk_hidT + off;
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int r = ty; r < 32; r += 8)
+    if (r0 + r < L.HP && c0 + tx < L.HP) t[r][tx] = src[(long long)(r0 + r) * L.HP + c0 + tx];
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8)
+    if (c0 + r < L.HP && r0 + tx < L.HP) dst[(long long)(c0 + r) * L.HP + r0 + tx] = t[tx][r];
+}
+
+// out[m][n] = sum_p part[p][m][n] in p order (split-K partials; deterministic)
+__global__ __launch_bounds__(WWG) void k_wsum_parts(const float* __restrict__ part, long long pstride, int np, int M,
+                                                    int N4, long long ldp, float* __restrict__ out, long long ldo) {
+  const long long n = (long long)M * N4;
+  for (long long e = (long long)blockIdx.x * WWG + threadIdx.x; e < n; e += (long long)gridDim.x * WWG) {
+    const int m = (int)(e / N4), c = 4 * (int)(e - (long long)m * N4);
+    floatx4 a = *reinterpret_cast<const floatx4*>(part + (long long)m * ldp + c);
+    for (int p = 1; p < np; ++p) {
+      const floatx4 b = *reinterpret_cast<const floatx4*>(part + p * pstride + (long long)m * ldp + c);
+      a = floatx4{a[0] + b[0], a[1] + b[1], a[2] + b[2], a[3] + b[3]};
+    }
+    *reinterpret_cast<floatx4*>(out + (long long)m * ldo + c) = a;
   }
 }
 
@@ -263,6 +295,7 @@ __device__ __forceinline__ void st4(float* p, floatx4 v) { *reinterpret_cast<flo
 // tilings.
 template <int BM, int BN, int BK, bool AKC, bool BKC, int NT = WWG>
 struct TileIO {
+  static constexpr int BKT = BK;
   static constexpr int ASZ = AKC ? BM * (BK + 4) : BK * (BM + 4);
   static constexpr int BSZ = BKC ? BN * (BK + 4) : BK * (BN + 4);
   static constexpr int AV = (BM * BK / 4 + NT - 1) / NT, BV = (BN * BK / 4 + NT - 1) / NT;
@@ -324,13 +357,14 @@ struct TileIO {
 // Operands the epilogue of a 4-row group needs from memory (EPI_GRAD: the G factors; EPI_ACT: the column's bias),
 // fetched before the K loop so their latency hides behind it.
 template <int EPI>
-__device__ __forceinline__ void epi_pre(const GemmArgs& g, const float* __restrict__ Xg, int rbase, int col, float pre[4]) {
+__device__ __forceinline__ void epi_pre(const GemmArgs& g, const float* __restrict__ Xg, int rbase, int col, float pre[4],
+                                        int rs = 1) {
   pre[0] = pre[1] = pre[2] = pre[3] = 0.f;
   if (col >= g.N) return;
   if (EPI == EPI_GRAD) {
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr)
-      if (rbase + rr < g.M) pre[rr] = Xg[(long long)(rbase + rr) * g.ldaux + col];
+      if (rbase + rs * rr < g.M) pre[rr] = Xg[(long long)(rbase + rs * rr) * g.ldaux + col];
   } else if (EPI == EPI_ACT) {
     if (col < g.n_real) pre[0] = g.bias[col];
   }
@@ -338,11 +372,11 @@ __device__ __forceinline__ void epi_pre(const GemmArgs& g, const float* __restri
 
 template <int EPI>
 __device__ __forceinline__ void epi4(const GemmArgs& g, float* __restrict__ Cg, float* __restrict__ Xg, int rbase,
-                                     int col, const float v[4], uint4 rnd, const float pre[4]) {
+                                     int col, const float v[4], uint4 rnd, const float pre[4], int rs = 1) {
   const int M = g.M, N = g.N;
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
-    const int row = rbase + rr;
+    const int row = rbase + rs * rr;
     if (row >= M || col >= N) continue;
     if (EPI == EPI_STORE) {
       Cg[(long long)row * g.ldc + col] = v[rr];
@@ -438,6 +472,34 @@ __device__ __forceinline__ TileId tile_id() {
   return t;
 }
 
+// The K loop of both tilings: two LDS buffers and two register staging sets, loads issued TWO K tiles ahead of the
+// MFMAs (a tile's global loads have two tiles of MFMA work to land in, not one: at M = 2048, N = K = 528 a tile's
+// MFMA phase is ~1.3 us, below one loaded L2/HBM round trip). Hand-unrolled by two so each staging set is a fixed
+// register range: the store of set s waits only for s's loads (vmcnt counts the newer set's loads as in flight).
+// The prefetch index is clamped instead of predicated (a redundant reload of the last tile) for the same reason.
+template <class IO, class F>
+__device__ __forceinline__ void k_loop(const GemmArgs& g, const float* __restrict__ A, const float* __restrict__ B,
+                                       int m0, int n0, float* lds, F&& tile) {
+  constexpr int BK = IO::BKT, STG = IO::ASZ + IO::BSZ;
+  const int nk = (g.K + BK - 1) / BK;
+  IO s0, s1;
+  s0.load(g, A, B, m0, n0, 0);
+  s1.load(g, A, B, m0, n0, (nk > 1 ? 1 : 0) * BK);
+  s0.store(lds, lds + IO::ASZ);
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += 2) {
+    s0.load(g, A, B, m0, n0, min(kt + 2, nk - 1) * BK);
+    tile(lds);
+    s1.store(lds + STG, lds + STG + IO::ASZ);
+    __syncthreads();
+    if (kt + 1 >= nk) break;
+    s1.load(g, A, B, m0, n0, min(kt + 3, nk - 1) * BK);
+    tile(lds + STG);
+    s0.store(lds, lds + IO::ASZ);
+    __syncthreads();
+  }
+}
+
 // Tiling A: v_mfma_f32_32x32x2_f32, 2 x 2 waves, each (BM/2) x (BN/2) as 32x32 accumulators. Inside a K tile
 // lane half h consumes k = h*BK/2 + s at MFMA step s.
 template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI>
@@ -453,7 +515,6 @@ __global__ __launch_bounds__(WWG, 2) void k_wgemm(const GemmArgs g) {
   const float* __restrict__ A = g.A + g1 * g.sA1 + g0 * g.sA0;
   const float* __restrict__ B = g.B + g1 * g.sB1 + g0 * g.sB0;
   const int m0 = tl.y * BM, n0 = tl.x * BN;
-  IO io;
   const EpiCtx e = epi_ctx<EPI>(g, g1, g0);
   float pre[TI][TJ][4][4];
 #pragma unroll
@@ -470,15 +531,8 @@ __global__ __launch_bounds__(WWG, 2) void k_wgemm(const GemmArgs g) {
     for (int j = 0; j < TJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  const int nk = (g.K + BK - 1) / BK;
-  io.load(g, A, B, m0, n0, 0);
-  io.store(lds, lds + IO::ASZ);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const float* As = lds + (kt & 1) * (IO::ASZ + IO::BSZ);
+  auto tile = [&](const float* As) {
     const float* Bs = As + IO::ASZ;
-    const bool more = kt + 1 < nk;
-    if (more) io.load(g, A, B, m0, n0, (kt + 1) * BK);
 #pragma unroll
     for (int sq = 0; sq < BK / 8; ++sq) {
       const int kb = hh * (BK / 2) + 4 * sq;
@@ -495,12 +549,8 @@ __global__ __launch_bounds__(WWG, 2) void k_wgemm(const GemmArgs g) {
           for (int j = 0; j < TJ; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
     }
-    if (more) {
-      float* An = lds + ((kt + 1) & 1) * (IO::ASZ + IO::BSZ);
-      io.store(An, An + IO::ASZ);
-    }
-    __syncthreads();
-  }
+  };
+  k_loop<IO>(g, A, B, m0, n0, lds, tile);
   // accumulator element r of lane (c32, hh): row = (r & 3) + 8 (r >> 2) + 4 hh, col = c32
 #pragma unroll
   for (int i = 0; i < TI; ++i)
@@ -534,7 +584,6 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_wgemm16(const Gemm
   const float* __restrict__ A = g.A + g1 * g.sA1 + g0 * g.sA0;
   const float* __restrict__ B = g.B + g1 * g.sB1 + g0 * g.sB0;
   const int m0 = tl.y * BM, n0 = tl.x * BN;
-  IO io;
   const EpiCtx e = epi_ctx<EPI>(g, g1, g0);
   float pre[TI][TJ][4];
 #pragma unroll
@@ -546,15 +595,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_wgemm16(const Gemm
   for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int nk = (g.K + BK - 1) / BK;
-  io.load(g, A, B, m0, n0, 0);
-  io.store(lds, lds + IO::ASZ);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const float* As = lds + (kt & 1) * (IO::ASZ + IO::BSZ);
+  auto tile = [&](const float* As) {
     const float* Bs = As + IO::ASZ;
-    const bool more = kt + 1 < nk;
-    if (more) io.load(g, A, B, m0, n0, (kt + 1) * BK);
 #pragma unroll
     for (int kc = 0; kc < BK / 16; ++kc) {
       const int kb = 16 * kc + 4 * qq;
@@ -571,12 +613,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_wgemm16(const Gemm
           for (int j = 0; j < TJ; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
     }
-    if (more) {
-      float* An = lds + ((kt + 1) & 1) * (IO::ASZ + IO::BSZ);
-      io.store(An, An + IO::ASZ);
-    }
-    __syncthreads();
-  }
+  };
+  k_loop<IO>(g, A, B, m0, n0, lds, tile);
   // accumulator element r of lane (c16, qq): row = 4 qq + r, col = c16
 #pragma unroll
   for (int i = 0; i < TI; ++i)
@@ -586,6 +624,217 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_wgemm16(const Gemm
       const int rbase = m0 + wave * WM + 16 * i + 4 * qq;
       const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       epi4<EPI>(g, e.C, e.X, rbase, col, v, epi_rnd<EPI>(g, e, rbase, col), pre[i][j]);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Tiling C: LDS-DMA staging (global_load_lds_dwordx4), the gfx950 GEMM pipeline (cdna_hip_programming.md §5).
+// Register-staged tilings A / B serialise each K tile on one global round trip: their staging registers are
+// loop-carried, so hipcc drains vmcnt at the loop head (tools: .s of k_wgemm16), and at M = 2048, N = K = 528 the
+// chain GEMMs sit at ~23 us for ~8 us of MFMA work per CU. Here a K tile (BK = 64) of both operands is copied
+// global -> LDS with no VGPR destination, S stages deep: tile kt + S - 1 is issued right after the barrier that
+// retires tile kt, the wait is a counted `s_waitcnt vmcnt(NI x tiles still ahead)` (NI = DMA instructions per wave
+// per tile), the barrier is a raw s_barrier (a __syncthreads() fence would drain the in-flight DMA), and all LDS is
+// one dynamic array.
+//   * K-contiguous operand (KC): image [row][64 floats], 16-B chunk q of row r stored in slot q ^ (r & 15) -- the
+//     swizzle is applied to the DMA's per-lane SOURCE address (the LDS side of a DMA is lane-linear) and undone on
+//     the read; a fragment is one ds_read_b128 of 4 consecutive k, conflict-free over each 16-lane group.
+//   * otherwise: image [64 k][R] linear; lane c reads the float4 of columns 4c..4c+3 at one k, i.e. one k-step's
+//     operand for FOUR 16-wide tiles, so such an operand's wave extent is 64 (4 tiles) with tile t holding the
+//     rows / columns {4c + t} (undone in the epilogue: row stride 4).
+//   * out-of-range rows / columns read clamped (finite, never stored); the K tail beyond K is zeroed in registers.
+// Requirements as tilings A / B (checked by the host); rows read as float4 up to roundup4 of their length <= ld.
+// ------------------------------------------------------------------------------------------------
+template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, int S, int KS>
+struct GlCfg {
+  static constexpr int BK = 64, NT = WGM * WGN, NW = NT * KS;   // output-tile waves x K halves
+  static constexpr int WM = BM / WGM, WN = BN / WGN, TI = WM / 16, TJ = WN / 16;
+  static constexpr int ACH = BM * BK / 4, BCH = BN * BK / 4;   // 16-B chunks of one stage
+  static constexpr int NI = (ACH + BCH) / 64 / NW;              // DMA instructions per wave per stage
+  static constexpr int STG = (BM + BN) * BK;                    // floats per stage
+  static_assert(WM % 16 == 0 && WN % 16 == 0, "16-row MFMA tiles");
+  static_assert(AKC || TI == 4, "non-K-contiguous A: 64 rows per wave");
+  static_assert(BKC || TJ == 4, "non-K-contiguous B: 64 columns per wave");
+  static_assert(ACH % 64 == 0 && BCH % 64 == 0 && (ACH + BCH) % (64 * NW) == 0, "whole DMA instructions per wave");
+  static_assert(2 * NI <= 63, "vmcnt range");
+};
+
+// per-lane source of 16-B chunk e of an operand stage (KC: R rows x 64 k; else 64 k x R columns)
+template <bool KC, int R>
+__device__ __forceinline__ const float* gl_src(const float* __restrict__ X, long long ld, int e, int mn0, int k0, int MN,
+                                               int K) {
+  if (KC) {
+    const int r = e >> 4, q = (e & 15) ^ (r & 15);
+    const int gm = min(mn0 + r, MN - 1);
+    int gk = k0 + 4 * q;
+    if (gk >= K) gk = 0;
+    return X + (long long)gm * ld + gk;
+  } else {
+    const int kr = e / (R / 4), c = e - kr * (R / 4);
+    int gk = k0 + kr, gm = mn0 + 4 * c;
+    if (gk >= K) gk = 0;
+    if (gm >= MN) gm = 0;
+    return X + (long long)gk * ld + gm;
+  }
+}
+
+template <class T, bool AKC, bool BKC, int BM, int BN>
+__device__ __forceinline__ void gl_issue(const float* __restrict__ A, long long lda, const float* __restrict__ B,
+                                         long long ldb, int M, int N, int K, int m0, int n0, int k0, float* buf,
+                                         int wave, int lane) {
+#pragma unroll
+  for (int t = 0; t < T::NI; ++t) {
+    const int ins = wave + T::NW * t;                 // wave-uniform
+    const int e = ins * 64 + lane;
+    const float* src = (ins * 64 < T::ACH) ? gl_src<AKC, BM>(A, lda, e, m0, k0, M, K)
+                                           : gl_src<BKC, BN>(B, ldb, e - T::ACH, n0, k0, N, K);
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(buf + ins * 256), 16,
+                                     0, 0);
+  }
+}
+
+// fragments of one 16-deep k chunk: KC -> f[t] = 4 consecutive k of row t; else f[s] = tiles 0..3 at k-step s
+template <bool KC, int R, int T4>
+__device__ __forceinline__ void gl_frag(const float* __restrict__ Sx, int base, int kc, int c16, int qq, floatx4 f[4]) {
+  if (KC) {
+#pragma unroll
+    for (int t = 0; t < T4; ++t) f[t] = ld4(Sx + (base + 16 * t + c16) * 64 + 4 * ((4 * kc + qq) ^ c16));
+  } else {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) f[s] = ld4(Sx + (16 * kc + 4 * qq + s) * R + base + 4 * c16);
+  }
+}
+
+template <class T, bool AKC, bool BKC, int BM, int BN, int KS, bool TAIL>
+__device__ __forceinline__ void gl_tile(const float* __restrict__ As, floatx4 (&acc)[T::TI][T::TJ], int am, int bn,
+                                        int c16, int qq, int kh, int kvalid) {
+  const float* Bs = As + BM * 64;
+#pragma unroll
+  for (int kq = 0; kq < 4 / KS; ++kq) {
+    const int kc = kh * (4 / KS) + kq;
+    floatx4 a[4], b[4];
+    gl_frag<AKC, BM, T::TI>(As, am, kc, c16, qq, a);
+    gl_frag<BKC, BN, T::TJ>(Bs, bn, kc, c16, qq, b);
+    if (TAIL) {   // k >= K: zero (a K-contiguous operand implies K % 4 == 0, so its float4 is all in or all out)
+      const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bool out_t = 16 * kc + 4 * qq + t >= kvalid, out_q = 16 * kc + 4 * qq >= kvalid;
+        if (AKC ? out_q : out_t) a[t] = zero;
+        if (BKC ? out_q : out_t) b[t] = zero;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < T::TI; ++i)
+#pragma unroll
+        for (int j = 0; j < T::TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(AKC ? a[i][s] : a[s][i], BKC ? b[j][s] : b[s][j],
+                                                           acc[i][j], 0, 0, 0);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// KS = 2: each output tile's K chunks are split between two waves (k chunks 0-1 / 2-3 of every K tile), whose
+// partial accumulators meet in LDS after the loop: twice the waves per SIMD to cover LDS and MFMA latency, and
+// tile shapes whose output waves do not divide evenly over the 4 SIMDs (96 x 48 = 6 waves) balance at 12.
+template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, int EPI, int S, int KS>
+__global__ __launch_bounds__(64 * WGM * WGN * KS, 1) void k_wgl(const GemmArgs g) {
+  using T = GlCfg<BM, BN, WGM, WGN, AKC, BKC, S, KS>;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kh = wave / T::NT, wt = wave - kh * T::NT;
+  const int wm = wt / WGN, wn = wt - (wt / WGN) * WGN;
+  const int c16 = lane & 15, qq = lane >> 4;
+  const TileId tl = tile_id();
+  const int z = tl.z, g1 = z / g.G0, g0 = z - g1 * g.G0;
+  const float* __restrict__ A = g.A + g1 * g.sA1 + g0 * g.sA0;
+  const float* __restrict__ B = g.B + g1 * g.sB1 + g0 * g.sB0;
+  const int m0 = tl.y * BM, n0 = tl.x * BN;
+  const EpiCtx e = epi_ctx<EPI>(g, g1, g0);
+  // output rows / columns of accumulator tile (i, j), element r: KC A -> rows am0 + 16 i + 4 qq + r; else
+  // am0 + 16 qq + 4 r + i (row stride 4). KC B -> column bn0 + 16 j + c16; else bn0 + 4 c16 + j.
+  const int am0 = m0 + wm * T::WM, bn0 = n0 + wn * T::WN;
+  auto rbase = [&](int i) { return AKC ? am0 + 16 * i + 4 * qq : am0 + 16 * qq + i; };
+  auto colof = [&](int j) { return BKC ? bn0 + 16 * j + c16 : bn0 + 4 * c16 + j; };
+  constexpr int RS = AKC ? 1 : 4;
+  float pre[T::TI][T::TJ][4];
+  if (kh == 0) {
+#pragma unroll
+    for (int i = 0; i < T::TI; ++i)
+#pragma unroll
+      for (int j = 0; j < T::TJ; ++j) epi_pre<EPI>(g, e.X, rbase(i), colof(j), pre[i][j], RS);
+  }
+  floatx4 acc[T::TI][T::TJ];
+#pragma unroll
+  for (int i = 0; i < T::TI; ++i)
+#pragma unroll
+    for (int j = 0; j < T::TJ; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (g.K + T::BK - 1) / T::BK;
+#pragma unroll
+  for (int st = 0; st < S - 1; ++st)
+    if (st < nk)
+      gl_issue<T, AKC, BKC, BM, BN>(A, g.lda, B, g.ldb, g.M, g.N, g.K, m0, n0, st * T::BK, lds + st * T::STG, wave,
+                                    lane);
+  int rd = 0, wr = S - 1;       // stage read at kt / stage written by the issue of tile kt + S - 1
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = min(nk - 1 - kt, S - 2);
+    if (S > 3 && ahead >= 2) vm_wait<2 * T::NI>();
+    else if (S > 2 && ahead >= 1) vm_wait<T::NI>();
+    else vm_wait<0>();
+    raw_barrier();
+    if (kt + S - 1 < nk)
+      gl_issue<T, AKC, BKC, BM, BN>(A, g.lda, B, g.ldb, g.M, g.N, g.K, m0, n0, (kt + S - 1) * T::BK,
+                                    lds + wr * T::STG, wave, lane);
+    const float* As = lds + rd * T::STG;
+    const int am = AKC ? wm * T::WM : wm * 64, bn = BKC ? wn * T::WN : wn * 64;
+    if (kt == nk - 1 && (g.K & (T::BK - 1)))
+      gl_tile<T, AKC, BKC, BM, BN, KS, true>(As, acc, am, bn, c16, qq, kh, g.K - kt * T::BK);
+    else
+      gl_tile<T, AKC, BKC, BM, BN, KS, false>(As, acc, am, bn, c16, qq, kh, T::BK);
+    rd = rd + 1 == S ? 0 : rd + 1;
+    wr = wr + 1 == S ? 0 : wr + 1;
+  }
+  if (KS > 1) {   // K halves meet: the upper half's partials through LDS (the staging ring is idle now)
+    static_assert(KS == 2, "two K halves");
+    static_assert(T::NT * T::TI * T::TJ * 256 <= S * T::STG, "partials fit the staging ring");
+    raw_barrier();
+    float* part = lds + (wt * T::TI * T::TJ) * 256 + lane * 4;
+    if (kh == 1) {
+#pragma unroll
+      for (int i = 0; i < T::TI; ++i)
+#pragma unroll
+        for (int j = 0; j < T::TJ; ++j) st4(part + (i * T::TJ + j) * 256, acc[i][j]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+    if (kh == 1) return;
+#pragma unroll
+    for (int i = 0; i < T::TI; ++i)
+#pragma unroll
+      for (int j = 0; j < T::TJ; ++j) {
+        const floatx4 p = ld4(part + (i * T::TJ + j) * 256);
+        acc[i][j] = floatx4{acc[i][j][0] + p[0], acc[i][j][1] + p[1], acc[i][j][2] + p[2], acc[i][j][3] + p[3]};
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < T::TI; ++i)
+#pragma unroll
+    for (int j = 0; j < T::TJ; ++j) {
+      const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      epi4<EPI>(g, e.C, e.X, rbase(i), colof(j), v, epi_rnd<EPI>(g, e, rbase(i), colof(j)), pre[i][j], RS);
     }
 }
 
@@ -1262,6 +1511,26 @@ int launch_cfg16(const GemmArgs& g, int groups, hipStream_t st) {
   return bcnf_rt::launched();
 }
 
+template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, int EPI, int S, int KS = 2>
+int launch_gl(const GemmArgs& g, int groups, hipStream_t st) {
+  using T = GlCfg<BM, BN, WGM, WGN, AKC, BKC, S, KS>;
+  constexpr int bytes = S * T::STG * 4;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)k_wgl<BM, BN, WGM, WGN, AKC, BKC, EPI, S, KS>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
+      return BCNF_ERR_HIP;
+    attr = true;
+  }
+  dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, groups);
+  hipLaunchKernelGGL((k_wgl<BM, BN, WGM, WGN, AKC, BKC, EPI, S, KS>), grid, dim3(64 * T::NW), bytes, st, g);
+  return bcnf_rt::launched();
+}
+
+// LDS-DMA tilings per operand layout (tiling C): 5 = auto, 6 = the large-tile variant forced
+template <bool AKC, bool BKC, int EPI>
+int gemm_gl(const GemmArgs& g, int groups, hipStream_t st, bool large);
+
 constexpr int N_CU = 256;
 // Modelled time of a tiling: rounds of one workgroup per CU (MI355X: 256 CUs) x tile area / relative efficiency.
 double tile_cost(const GemmArgs& g, int groups, int BM, int BN, double eff) {
@@ -1270,7 +1539,7 @@ double tile_cost(const GemmArgs& g, int groups, int BM, int BN, double eff) {
 }
 
 int g_force_tiling = -1;   // test hook: 0 = 128x128, 1 = 64x64, 2 = 128x48 (16x16 MFMA), 3 = 128x48 on 8 waves,
-                           // 4 = 96x48 on 6 waves
+                           // 4 = 96x48 on 6 waves, 5 = LDS-DMA (tiling C, the default), 6 = tiling C large tiles
 
 template <bool AKC, bool BKC, int EPI>
 int gemm(const GemmArgs& g, int groups, hipStream_t st) {
@@ -1278,6 +1547,11 @@ int gemm(const GemmArgs& g, int groups, hipStream_t st) {
   if ((g.lda & 3) || (g.ldb & 3) || (!aligned16(g.A)) || (!aligned16(g.B))) return BCNF_ERR_ARG;
   if ((AKC || BKC) && (g.K & 3)) return BCNF_ERR_ARG;
   int pick = g_force_tiling;
+  // LDS-DMA tiling C for K-contiguous x K-contiguous operands (the chain GEMMs, the projections, the row-mapped
+  // condition gradient); the register-staged tilings keep the strided layouts, where tiling C's permuted
+  // 64-wide wave tiles measured slower (tools/gemm_bench.py t6 / t7, profiles/r02t_gemm_tilings.txt)
+  if (pick < 0 && AKC && BKC) pick = 5;
+  if (pick >= 5) return gemm_gl<AKC, BKC, EPI>(g, groups, st, pick == 6);
   if (pick < 0) {
     // relative efficiencies per operand layout, measured at 4096^3 on MI355X (tools/gemm_bench.py)
     const double e1 = AKC ? (BKC ? 1.06 : 0.88) : 0.78, e2 = AKC ? (BKC ? 0.86 : 0.70) : 0.60;
@@ -1296,6 +1570,44 @@ int gemm(const GemmArgs& g, int groups, hipStream_t st) {
   if (pick == 3) return launch_cfg16<128, 48, 64, AKC, BKC, EPI, 8>(g, groups, st);
   if (pick == 4) return launch_cfg16<96, 48, 64, AKC, BKC, EPI, 6>(g, groups, st);
   return launch_cfg<64, 64, 64, AKC, BKC, EPI>(g, groups, st);
+}
+
+template <bool AKC, bool BKC, int EPI>
+int gemm_gl(const GemmArgs& g, int groups, hipStream_t st, bool large) {
+  const long long t128 = (long long)((g.M + 127) / 128) * ((g.N + 127) / 128) * groups;
+  if (AKC && BKC) {
+    if (large || t128 >= 2 * N_CU) return launch_gl<128, 128, 2, 2, true, true, EPI, 2>(g, groups, st);
+    return launch_gl<96, 48, 6, 1, true, true, EPI, 4>(g, groups, st);
+  }
+  if (!AKC && !BKC) return launch_gl<128, 128, 2, 2, false, false, EPI, 2>(g, groups, st);
+  if (AKC) return launch_gl<64, 128, 2, 2, true, false, EPI, 3>(g, groups, st);
+  return launch_gl<128, 64, 2, 2, false, true, EPI, 3>(g, groups, st);
+}
+
+// C = A B with K split into np equal chunks (grouped launch into `part`, then a fixed-order sum): tall-K GEMMs whose
+// M x N grid alone cannot fill the chip (the folded condition gradients, K = nv * HP). Falls back to one GEMM when
+// K does not split evenly or the scratch is too small.
+template <bool AKC, bool BKC>
+int gemm_splitk(const GemmArgs& g, int np, float* part, long long part_floats, hipStream_t st) {
+  const int kc = np > 0 ? g.K / np : 0;
+  const long long ldp = (g.N + 3) & ~3LL;
+  if (np < 2 || kc * np != g.K || ((AKC || BKC) && (kc & 3)) || (g.N & 3) || (g.ldc & 3) || !aligned16(g.C) ||
+      (long long)np * g.M * ldp > part_floats)
+    return gemm<AKC, BKC, EPI_STORE>(g, 1, st);
+  GemmArgs p = g;
+  p.K = kc;
+  p.C = part;
+  p.ldc = ldp;
+  p.G0 = 1;
+  p.sA1 = AKC ? kc : (long long)kc * g.lda;
+  p.sB1 = BKC ? kc : (long long)kc * g.ldb;
+  p.sC1 = (long long)g.M * ldp;
+  const int rc = gemm<AKC, BKC, EPI_STORE>(p, np, st);
+  if (rc) return rc;
+  const long long n4 = (long long)g.M * (g.N / 4);
+  const int grid = (int)std::min<long long>((n4 + WWG - 1) / WWG, 2048);
+  hipLaunchKernelGGL(k_wsum_parts, dim3(grid), dim3(WWG), 0, st, part, p.sC1, np, g.M, g.N / 4, ldp, g.C, g.ldc);
+  return bcnf_rt::launched();
 }
 
 struct WideWs {       // workspace carve-up (floats)
@@ -1563,10 +1875,10 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
       const float* din = dZptr(vb, l, &ldi);
       float* dout = dZptr(vb, l - 1, &ldo);
       GemmArgs g = gemm_args((int)B, L.HP, L.HP, din, ldi,
-                             pk + L.pk_hid + ((long long)vb * (L.NH - 1) + (l - 1)) * L.HP * L.HP, L.HP, dout, ldo);
+                             pk + L.pk_hidT + ((long long)vb * (L.NH - 1) + (l - 1)) * L.HP * L.HP, L.HP, dout, ldo);
       g.aux = Gptr(vb, l - 1);
       g.ldaux = L.HP;
-      WCHK((gemm<true, false, EPI_GRAD>(g, 1, st)));
+      WCHK((gemm<true, true, EPI_GRAD>(g, 1, st)));
     }
   }
   int rc = BCNF_OK;
@@ -1649,13 +1961,15 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
     }
   }
   if (fold) {
+    // split K = nv * HP per virtual block; partials in the G region (dead once the chain has run)
+    const long long gfl = (long long)L.nv * L.NH * slab;
     if (fold->dwfb) {   // [dWf | dbf] = W0h_all^T Gx
       GemmArgs g = gemm_args(L.C, fold->Xp, L.nv * L.HP, pk + L.pk_w0h, L.Cp, fold->gx, fold->Xp, fold->dwfb, fold->Xp);
-      WCHK((gemm<false, false, EPI_STORE>(g, 1, st)));
+      WCHK((gemm_splitk<false, false>(g, L.nv, w.G, gfl, st)));
     }
     if (fold->dx) {     // dL/dx = dZ0_all Wcb
       GemmArgs g = gemm_args((int)B, fold->Xp, L.nv * L.HP, w.dZ0, ld0, fold->wcb, fold->Xp, fold->dx, fold->Xp);
-      WCHK((gemm<true, false, EPI_STORE>(g, 1, st)));
+      WCHK((gemm_splitk<true, false>(g, L.nv, w.G, gfl, st)));
     }
   } else if (dh) {   // dh = dZ0_all W0h_all
     GemmArgs g = gemm_args((int)B, L.C, L.nv * L.HP, w.dZ0, ld0, pk + L.pk_w0h, L.Cp, dh, L.C);
@@ -1769,6 +2083,11 @@ int bcnf_wide_pack(const BcnfStackDesc* desc, const float* params, const float* 
   const int grid = (int)std::min<long long>((n + WWG - 1) / WWG, 4096);
   hipLaunchKernelGGL(k_wpack, dim3(grid), dim3(WWG), 0, st, L, params, qmats, (float*)packed);
   WCHK(bcnf_rt::launched());
+  if (L.NH > 1) {
+    const int t = (L.HP + 31) / 32;
+    hipLaunchKernelGGL(k_wtranspose, dim3(t, t, L.nv * (L.NH - 1)), dim3(256), 0, st, L, (float*)packed);
+    WCHK(bcnf_rt::launched());
+  }
   hipLaunchKernelGGL(k_wpack_ldc, dim3(1), dim3(((L.nb + 63) / 64) * 64), 0, st, L, params, (float*)packed);
   WCHK(bcnf_rt::launched());
   hipLaunchKernelGGL(k_wpack_b0, dim3(L.nv), dim3(WWG), 0, st, L, params, (float*)packed);
@@ -1886,15 +2205,15 @@ int bcnf_wide_debug_phases(unsigned long long* dbg) {
   return BCNF_OK;
 }
 
-// Tiling override for every wide GEMM launch (-1 = the cost model's choice; 0 = 128x128, 1 = 64x64, 2 = 128x48).
+// Tiling override for every wide GEMM launch (-1 = the default, LDS-DMA tiling C; 0..6 as g_force_tiling).
 int bcnf_wide_force_tiling(int32_t tiling) {
   const int prev = g_force_tiling;
-  g_force_tiling = (tiling >= 0 && tiling <= 4) ? tiling : -1;
+  g_force_tiling = (tiling >= 0 && tiling <= 6) ? tiling : -1;
   return prev;
 }
 
 // Test hook: one plain GEMM through the tile machinery. layout: 0 = NT (A[m][k], B[n][k]), 1 = NN (A[m][k], B[k][n]),
-// 2 = TN (A[k][m], B[k][n]).
+// 2 = TN (A[k][m], B[k][n]), 3 = TT (A[k][m], B[n][k]).
 int bcnf_wide_gemm_test(int32_t layout, int32_t M, int32_t N, int32_t K, const float* A, int64_t lda, const float* B,
                         int64_t ldb, float* C, int64_t ldc, void* stream) {
   GemmArgs g = gemm_args(M, N, K, A, lda, B, ldb, C, ldc);
@@ -1909,6 +2228,7 @@ int bcnf_wide_gemm_test(int32_t layout, int32_t M, int32_t N, int32_t K, const f
   if (layout == 0) return gemm<true, true, EPI_STORE>(g, 1, st);
   if (layout == 1) return gemm<true, false, EPI_STORE>(g, 1, st);
   if (layout == 2) return gemm<false, false, EPI_STORE>(g, 1, st);
+  if (layout == 3) return gemm<false, true, EPI_STORE>(g, 1, st);
   return BCNF_ERR_ARG;
 }
 

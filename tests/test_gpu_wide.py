@@ -26,14 +26,14 @@ def _lib():
 
 
 # ------------------------------------------------------------------------------------------ GEMM tiles
-@pytest.mark.parametrize("tiling", [0, 1, 2, 3, 4, 5])
-@pytest.mark.parametrize("layout", [0, 1, 2])
+@pytest.mark.parametrize("tiling", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("layout", [0, 1, 2, 3])
 @pytest.mark.parametrize("mnk", [(64, 64, 32), (100, 70, 36), (2048, 528, 528), (18, 527, 300), (1030, 1360, 64),
-                                 (3, 5, 4)])
+                                 (3, 5, 4), (300, 200, 2052)])
 def test_wide_gemm_layouts_vs_fp64(layout, mnk, tiling):
     """C = A B through the MFMA tile machinery (tiling 0 = the dispatcher's choice, 1 = 128x128 32x32-MFMA,
-    2 = 64x64, 3 = 128x48 16x16-MFMA, 4 = the same on 8 waves, 5 = 96x48 on 6 waves; ragged M / N / K tails) vs
-    fp64."""
+    2 = 64x64, 3 = 128x48 16x16-MFMA, 4 = the same on 8 waves, 5 = 96x48 on 6 waves, 6 = LDS-DMA tiling C,
+    7 = tiling C large tiles; every operand layout; ragged M / N / K tails) vs fp64."""
     import ctypes
     N = _lib()
     M, Nn, K = mnk
@@ -42,21 +42,18 @@ def test_wide_gemm_layouts_vs_fp64(layout, mnk, tiling):
     B = torch.randn(K, Nn, generator=g, dtype=torch.float64)
     ref = A @ B
     pad = lambda n: (n + 3) // 4 * 4  # noqa: E731
-    if layout == 0:      # A[m][k], B[n][k]
+    if layout in (0, 1):  # A[m][k]
         Ad = torch.zeros(M, pad(K), dtype=torch.float32)
         Ad[:, :K] = A.float()
+    else:                 # A[k][m]
+        Ad = torch.zeros(pad(K), pad(M), dtype=torch.float32)
+        Ad[:K, :M] = A.t().float()
+    if layout in (0, 3):  # B[n][k]
         Bd = torch.zeros(Nn, pad(K), dtype=torch.float32)
         Bd[:, :K] = B.t().float()
-    elif layout == 1:    # A[m][k], B[k][n]
-        Ad = torch.zeros(M, pad(K), dtype=torch.float32)
-        Ad[:, :K] = A.float()
-        Bd = torch.zeros(K, pad(Nn), dtype=torch.float32)
-        Bd[:, :Nn] = B.float()
-    else:                # A[k][m], B[k][n]
-        Ad = torch.zeros(K, pad(M), dtype=torch.float32)
-        Ad[:, :M] = A.t().float()
-        Bd = torch.zeros(K, pad(Nn), dtype=torch.float32)
-        Bd[:, :Nn] = B.float()
+    else:                 # B[k][n]
+        Bd = torch.zeros(pad(K), pad(Nn), dtype=torch.float32)
+        Bd[:K, :Nn] = B.float()
     Ad, Bd = Ad.to(DEV), Bd.to(DEV)
     C = torch.full((M, pad(Nn)), float("nan"), device=DEV)
     Kp = pad(K) if layout != 2 else K
@@ -116,7 +113,8 @@ WIDE_SHAPES = [
 ]
 
 
-@pytest.fixture(params=[-1, 0, 1, 2, 3, 4], ids=["auto", "t128x128", "t64x64", "t128x48", "t128x48w8", "t96x48w6"])
+@pytest.fixture(params=[-1, 0, 1, 2, 3, 4, 6], ids=["auto", "t128x128", "t64x64", "t128x48", "t128x48w8", "t96x48w6",
+                                                   "glds_large"])
 def tiling(request):
     N = _lib()
     prev = N.lib().bcnf_wide_force_tiling(request.param)

@@ -124,7 +124,7 @@ def test_wide_family_routing_and_layout_queries():
     HP, nb, NH, B = 528, 26, 5, 2048
     pk = N.query_i64(lib.bcnf_wide_packed_bytes, ctypes.byref(big))
     r4 = lambda n: (n + 3) // 4 * 4  # noqa: E731
-    assert pk == 4 * (r4(nb * HP * 1360) + r4(nb * (NH - 1) * HP * HP) + r4(nb * 10 * HP) + r4(nb * 18 * HP)
+    assert pk == 4 * (r4(nb * HP * 1360) + 2 * r4(nb * (NH - 1) * HP * HP) + r4(nb * 10 * HP) + r4(nb * 18 * HP)
                       + r4(25 * 19 * 19) + r4(nb) + nb * HP)
     ws = N.query_i64(lib.bcnf_wide_workspace_bytes, ctypes.byref(big), ctypes.c_int64(B), ctypes.c_int32(1))
     slab = B * HP

@@ -37,7 +37,7 @@ def main():
             C = torch.empty(M, Nn, device=dev)
             st = N.stream_handle(dev)
             res = []
-            for t in (1, 2, 3, 4, 5):
+            for t in (1, 2, 3, 4, 5, 6, 7):
                 def f():
                     L.bcnf_wide_gemm_test(layout | (t << 4), M, Nn, K, N.ptr(A), A.shape[1], N.ptr(B), B.shape[1],
                                           N.ptr(C), Nn, st)

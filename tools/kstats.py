@@ -1,12 +1,16 @@
-"""Print a rocprofv3 kernel_stats.csv as per-step milliseconds (usage: kstats.py <csv> [steps])."""
-import csv
+"""Per-kernel summary of one rocprofv3 results db: calls, avg us, total ms, grid (first dispatch).
+Usage: python tools/kstats.py gpurun_out/prof_x/<name>_results.db [top]"""
+import sqlite3
 import sys
 
-rows = list(csv.DictReader(open(sys.argv[1])))
-steps = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
-tot = sum(float(r["TotalDurationNs"]) for r in rows)
-for r in rows[:int(sys.argv[3]) if len(sys.argv) > 3 else 22]:
-    n = r["Name"].replace("(anonymous namespace)::", "")[:100]
-    print(f"{float(r['TotalDurationNs']) / 1e6 / steps:8.3f} ms/step {int(r['Calls']) / steps:7.1f} calls "
-          f"avg {float(r['AverageNs']) / 1e3:8.1f} us {float(r['Percentage']):5.1f}%  {n}")
-print(f"total {tot / 1e6 / steps:.3f} ms/step")
+c = sqlite3.connect(sys.argv[1])
+top = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+q = """select s.display_name, count(*), avg(d.end-d.start), sum(d.end-d.start), min(d.grid_size_x), min(d.grid_size_y),
+       min(d.grid_size_z), min(d.workgroup_size_x)
+       from rocpd_kernel_dispatch d join rocpd_info_kernel_symbol s on d.kernel_id=s.id group by s.display_name
+       order by sum(d.end-d.start) desc"""
+rows = list(c.execute(q))
+tot = sum(r[3] for r in rows)
+for r in rows[:top]:
+    print(f"{r[3] / 1e6:9.2f}ms {r[1]:6d} {r[2] / 1e3:9.1f}us {100 * r[3] / tot:5.1f}% grid=({r[4]},{r[5]},{r[6]}) "
+          f"wg={r[7]} {r[0][:110]}")
