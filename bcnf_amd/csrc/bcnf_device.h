@@ -93,7 +93,11 @@ struct AdamScalars {
   float step_size, bc2s, omb1, omb2, b2, eps, wd;
 };
 
+// Contraction off: every caller (k_adam's vector / element paths, the fused Adam of the folded backward tail)
+// rounds each operation exactly like this, whatever fma shapes the surrounding code lets hipcc pick -- the
+// run_epoch == per-step-loop bit-equality rests on it.
 __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamScalars& a) {
+#pragma clang fp contract(off)
   if (a.wd != 0.f) g = fmaf(a.wd, p, g);
   m = m + a.omb1 * (g - m);                          // lerp, |weight| < 0.5 branch
   v = v * a.b2 + a.omb2 * (g * g);

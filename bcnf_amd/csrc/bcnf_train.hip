@@ -71,19 +71,43 @@ __global__ __launch_bounds__(BCNF_WG) void k_adam(TList T, const float* __restri
   // every operand load is issued first: none depends on the guard, the step count or the bias corrections,
   // so their round trip overlaps the scalar loads and thread 0's double pow
   const long long total = T.start[T.n];
+  // thread x owns the EPT = 4 consecutive elements i0..i0+3: one 16-B load / store per array when they lie in one
+  // tensor at a 16-B aligned offset (the whole flat coupling buffer), element-wise at tensor seams
+  const long long i0 = (long long)blockIdx.x * CHUNK + EPT * threadIdx.x;
+  const int t0 = find_tensor(T, i0 < total ? i0 : total - 1);
+  const long long o0 = i0 - T.start[t0];
+  const bool vec = i0 + EPT <= T.start[t0 + 1] &&
+                   ((((uintptr_t)(T.p[t0] + o0)) | ((uintptr_t)(T.g[t0] + o0)) | ((uintptr_t)(T.m[t0] + o0)) |
+                     ((uintptr_t)(T.v[t0] + o0))) & 15) == 0;
   float g[EPT], p[EPT], m[EPT], v[EPT];
   int t[EPT];
   long long o[EPT];
+  if (vec) {
+    const floatx4 g4 = *reinterpret_cast<const floatx4*>(T.g[t0] + o0);
+    const floatx4 p4 = *reinterpret_cast<const floatx4*>(T.p[t0] + o0);
+    const floatx4 m4 = *reinterpret_cast<const floatx4*>(T.m[t0] + o0);
+    const floatx4 v4 = *reinterpret_cast<const floatx4*>(T.v[t0] + o0);
 #pragma unroll
-  for (int e = 0; e < EPT; ++e) {
-    long long i = (long long)blockIdx.x * CHUNK + e * BCNF_WG + threadIdx.x;
-    i = i < total ? i : total - 1;
-    t[e] = find_tensor(T, i);
-    o[e] = i - T.start[t[e]];
-    g[e] = T.g[t[e]][o[e]];
-    p[e] = T.p[t[e]][o[e]];
-    m[e] = T.m[t[e]][o[e]];
-    v[e] = T.v[t[e]][o[e]];
+    for (int e = 0; e < EPT; ++e) {
+      g[e] = g4[e];
+      p[e] = p4[e];
+      m[e] = m4[e];
+      v[e] = v4[e];
+      t[e] = t0;
+      o[e] = o0 + e;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      long long i = i0 + e;
+      i = i < total ? i : total - 1;
+      t[e] = find_tensor(T, i);
+      o[e] = i - T.start[t[e]];
+      g[e] = T.g[t[e]][o[e]];
+      p[e] = T.p[t[e]][o[e]];
+      m[e] = T.m[t[e]][o[e]];
+      v[e] = T.v[t[e]][o[e]];
+    }
   }
   if (guard && guard[BCNF_GUARD_HALTED]) return;   // a halted step (see nll_finalize) leaves all state
   // bookkeeping: the logged values go out from workgroup 0 at the start (it reads the cursor before its own
@@ -93,14 +117,23 @@ __global__ __launch_bounds__(BCNF_WG) void k_adam(TList T, const float* __restri
   float ss = 0.f;
 #pragma unroll
   for (int e = 0; e < EPT; ++e) {
-    const long long i = (long long)blockIdx.x * CHUNK + e * BCNF_WG + threadIdx.x;
-    if (i < total) {
+    if (i0 + e < total) {
       ss = fmaf(g[e], g[e], ss);
       adam_elem(p[e], g[e], m[e], v[e], as);
-      T.m[t[e]][o[e]] = m[e];
-      T.v[t[e]][o[e]] = v[e];
-      T.p[t[e]][o[e]] = p[e];
     }
+  }
+  if (vec) {
+    *reinterpret_cast<floatx4*>(T.m[t0] + o0) = floatx4{m[0], m[1], m[2], m[3]};
+    *reinterpret_cast<floatx4*>(T.v[t0] + o0) = floatx4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<floatx4*>(T.p[t0] + o0) = floatx4{p[0], p[1], p[2], p[3]};
+  } else {
+#pragma unroll
+    for (int e = 0; e < EPT; ++e)
+      if (i0 + e < total) {
+        T.m[t[e]][o[e]] = m[e];
+        T.v[t[e]][o[e]] = v[e];
+        T.p[t[e]][o[e]] = p[e];
+      }
   }
   const float s = wg_sum(ss, red);
   if (threadIdx.x == 0 && part) part[blockIdx.x] = s;
@@ -124,10 +157,12 @@ __global__ void k_advance(float* step, long long* cursor, long long n_batches, c
 __global__ __launch_bounds__(BCNF_WG) void k_sumsq(TList T, float* __restrict__ part) {
   __shared__ float red[BCNF_WG];
   const long long total = T.start[T.n];
+  // the same element order and fmaf chain as k_adam's partials (clip norms bit-identical either way)
+  const long long i0 = (long long)blockIdx.x * CHUNK + EPT * threadIdx.x;
   float ss = 0.f;
 #pragma unroll
   for (int e = 0; e < EPT; ++e) {
-    const long long i = (long long)blockIdx.x * CHUNK + e * BCNF_WG + threadIdx.x;
+    const long long i = i0 + e;
     if (i < total) {
       const int t = find_tensor(T, i);
       const float g = T.g[t][i - T.start[t]];

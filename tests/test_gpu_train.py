@@ -248,8 +248,10 @@ def test_run_epoch_equals_per_step_loop(g1, unroll):
     (v0, p0, s0, r0, c0, g0), (v1, p1, s1, r1, c1, gr1) = res
     assert v0 == v1 and len(v1) == 4
     assert c0 == c1 == 0 and torch.equal(r0, r1)
-    for a, b in zip(p0 + s0 + g0, p1 + s1 + gr1):
-        assert torch.equal(a, b)
+    names = [f"param{i}" for i in range(len(p0))] + [f"state{i}" for i in range(len(s0))] + \
+        [f"grad{i}" for i in range(len(g0))]
+    for n, a, b in zip(names, p0 + s0 + g0, p1 + s1 + gr1):
+        assert torch.equal(a, b), (n, float((a.float() - b.float()).abs().max()))
 
 
 def test_run_epoch_divergence_halts_like_the_trainer(g1):

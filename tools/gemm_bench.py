@@ -25,10 +25,16 @@ def main():
     dev = torch.device("cuda")
     L = N.lib()
     shapes = [(2048, 528, 528), (1024, 528, 528), (2048, 13728, 1360), (2048, 1360, 13728), (528, 528, 2048)]
-    if len(sys.argv) > 1:
+    tilings = (1, 2, 3, 4, 5, 6, 7)
+    if len(sys.argv) > 1 and "x" in sys.argv[1]:      # explicit shapes MxNxK[,MxNxK...] [tilings t,t,...] [layouts]
+        shapes = [tuple(int(v) for v in a.split("x")) for a in sys.argv[1].split(",")]
+        if len(sys.argv) > 2:
+            tilings = tuple(int(t) for t in sys.argv[2].split(","))
+    elif len(sys.argv) > 1:
         shapes = shapes[:int(sys.argv[1])]
+    layouts = (0, 1, 2) if len(sys.argv) <= 3 else tuple(int(v) for v in sys.argv[3].split(","))
     for (M, Nn, K) in shapes:
-        for layout in (0, 1, 2):
+        for layout in layouts:
             if layout == 2:
                 A = torch.randn(K, M, device=dev)
             else:
@@ -37,7 +43,7 @@ def main():
             C = torch.empty(M, Nn, device=dev)
             st = N.stream_handle(dev)
             res = []
-            for t in (1, 2, 3, 4, 5, 6, 7):
+            for t in tilings:
                 def f():
                     L.bcnf_wide_gemm_test(layout | (t << 4), M, Nn, K, N.ptr(A), A.shape[1], N.ptr(B), B.shape[1],
                                           N.ptr(C), Nn, st)
