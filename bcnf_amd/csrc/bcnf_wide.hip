@@ -750,7 +750,7 @@ __device__ __forceinline__ void raw_barrier() {
 // partial accumulators meet in LDS after the loop: twice the waves per SIMD to cover LDS and MFMA latency, and
 // tile shapes whose output waves do not divide evenly over the 4 SIMDs (96 x 48 = 6 waves) balance at 12.
 template <int BM, int BN, int WGM, int WGN, bool AKC, bool BKC, int EPI, int S, int KS>
-__global__ __launch_bounds__(64 * WGM * WGN * KS, 1) void k_wgl(const GemmArgs g) {
+__global__ __launch_bounds__(64 * WGM * WGN * KS, (S * (BM + BN) * 64 * 4 <= 80 * 1024) ? 2 : 1) void k_wgl(const GemmArgs g) {
   using T = GlCfg<BM, BN, WGM, WGN, AKC, BKC, S, KS>;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -807,7 +807,7 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS, 1) void k_wgl(const GemmArgs g
     rd = rd + 1 == S ? 0 : rd + 1;
     wr = wr + 1 == S ? 0 : wr + 1;
   }
-  if (KS > 1) {   // K halves meet: the upper half's partials through LDS (the staging ring is idle now)
+  if constexpr (KS > 1) {   // K halves meet: the upper half's partials through LDS (the staging ring is idle now)
     static_assert(KS == 2, "two K halves");
     static_assert(T::NT * T::TI * T::TJ * 256 <= S * T::STG, "partials fit the staging ring");
     raw_barrier();
@@ -1539,7 +1539,8 @@ double tile_cost(const GemmArgs& g, int groups, int BM, int BN, double eff) {
 }
 
 int g_force_tiling = -1;   // test hook: 0 = 128x128, 1 = 64x64, 2 = 128x48 (16x16 MFMA), 3 = 128x48 on 8 waves,
-                           // 4 = 96x48 on 6 waves, 5 = LDS-DMA (tiling C, the default), 6 = tiling C large tiles
+                           // 4 = 96x48 on 6 waves, 5 = LDS-DMA (tiling C, the default; 96 x 48 for K-contiguous
+                           // operands), 6 = tiling C large tiles, 7 = tiling C 48 x 48
 
 template <bool AKC, bool BKC, int EPI>
 int gemm(const GemmArgs& g, int groups, hipStream_t st) {
@@ -1577,6 +1578,11 @@ int gemm_gl(const GemmArgs& g, int groups, hipStream_t st, bool large) {
   const long long t128 = (long long)((g.M + 127) / 128) * ((g.N + 127) / 128) * groups;
   if (AKC && BKC) {
     if (large || t128 >= 2 * N_CU) return launch_gl<128, 128, 2, 2, true, true, EPI, 2>(g, groups, st);
+    // 96 x 48 on one workgroup per CU while that grid covers most CUs (M = 2048, N = 528: 242 tiles); below,
+    // 48 x 48 workgroups two per CU (M = 1024, the LSTM_large chain: 13.3 vs 17.6 us, tools/gemm_bench.py)
+    const long long t96 = (long long)((g.M + 95) / 96) * ((g.N + 47) / 48) * groups;
+    if (g_force_tiling == 7 || (g_force_tiling != 5 && t96 < 3 * N_CU / 4))
+      return launch_gl<48, 48, 3, 1, true, true, EPI, 3>(g, groups, st);
     return launch_gl<96, 48, 6, 1, true, true, EPI, 4>(g, groups, st);
   }
   if (!AKC && !BKC) return launch_gl<128, 128, 2, 2, false, false, EPI, 2>(g, groups, st);
@@ -2208,7 +2214,7 @@ int bcnf_wide_debug_phases(unsigned long long* dbg) {
 // Tiling override for every wide GEMM launch (-1 = the default, LDS-DMA tiling C; 0..6 as g_force_tiling).
 int bcnf_wide_force_tiling(int32_t tiling) {
   const int prev = g_force_tiling;
-  g_force_tiling = (tiling >= 0 && tiling <= 6) ? tiling : -1;
+  g_force_tiling = (tiling >= 0 && tiling <= 7) ? tiling : -1;
   return prev;
 }
 
