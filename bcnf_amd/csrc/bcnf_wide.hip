@@ -31,6 +31,7 @@
 #include <algorithm>
 
 #include "bcnf_amd.h"
+#include <cstdlib>
 #include "bcnf_device.h"
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -1915,7 +1916,13 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
       g.sC0 = (L.NH > 2) ? (L.lin_w[0][2] - L.lin_w[0][1]) : 0;
       g.wcols = L.H;
       g.boff = (long long)L.H * L.H;
-      WCHK((gemm<false, false, EPI_LINGRAD>(g, L.nv * (L.NH - 1), st)));
+      // experiment knob: BCNF_LINGRAD_TILING = g_force_tiling value for this launch only
+      static const int lt = getenv("BCNF_LINGRAD_TILING") ? atoi(getenv("BCNF_LINGRAD_TILING")) : -1;
+      const int saved = g_force_tiling;
+      if (lt >= 0 && saved < 0) g_force_tiling = lt;
+      const int rc_l = gemm<false, false, EPI_LINGRAD>(g, L.nv * (L.NH - 1), st);
+      g_force_tiling = saved;
+      WCHK(rc_l);
     }
     for (int sd = 0; sd < L.S; ++sd) {
       {   // last Linear of every block's side-sd half: [dW | db] = dO^T [A_{NH-1} | 1]
