@@ -147,33 +147,16 @@ int wide_layout(const BcnfStackDesc* d, WideLayout* L) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Packing: padded, GEMM-friendly copies of the weights (one launch per parameter update).
+// Packing: padded, GEMM-friendly copies of the weights (k_wpack_rows + k_wpack + k_wtranspose + ldc / b0 per
+// parameter update).
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(WWG) void k_wpack(const WideLayout L, const float* __restrict__ prm,
                                                const float* __restrict__ q, float* __restrict__ pk) {
   const long long stride = (long long)gridDim.x * WWG;
-  for (long long e = (long long)blockIdx.x * WWG + threadIdx.x; e < L.pk_ldc; e += stride) {
+  for (long long e = L.pk_w0y + (long long)blockIdx.x * WWG + threadIdx.x; e < L.pk_ldc; e += stride) {
     float v = 0.f;
-    if (e < L.pk_hid) {
-      const long long r = e / L.Cp;
-      const int c = (int)(e - r * L.Cp);
-      const int vb = (int)(r / L.HP), n = (int)(r - (long long)vb * L.HP);
-      if (vb < L.nv && n < L.H && c < L.C) {
-        const int sd = vb % L.S;
-        v = prm[vbase(L, vb) + L.lin_w[sd][0] + (long long)n * L.in0[sd] + L.nin[sd] + c];
-      }
-    } else if (e < L.pk_w0y) {
-      if (e >= L.pk_hidT) continue;           // the transposed copy: k_wtranspose, after this launch
-      const long long i = e - L.pk_hid;
-      const long long per = (long long)L.HP * L.HP;
-      const long long kl = i / per;
-      const long long rem = i - kl * per;
-      const int n = (int)(rem / L.HP), kk = (int)(rem - (long long)n * L.HP);
-      if (L.NH > 1 && kl < (long long)L.nv * (L.NH - 1) && n < L.H && kk < L.H) {
-        const int vb = (int)(kl / (L.NH - 1)), l = (int)(kl % (L.NH - 1)) + 1;
-        v = prm[vbase(L, vb) + L.lin_w[vb % L.S][l] + (long long)n * L.H + kk];
-      }
-    } else if (e < L.pk_wl) {
+    // W0h_all and the hidden W (and W^T) are written by k_wpack_rows / k_wtranspose; this loop starts at pk_w0y
+    if (e < L.pk_wl) {
       const long long i = e - L.pk_w0y;
       const long long per = (long long)L.WY * L.HP;
       const int vb = (int)(i / per);
@@ -198,6 +181,47 @@ __global__ __launch_bounds__(WWG) void k_wpack(const WideLayout L, const float* 
       if (i < (long long)(L.nb - 1) * L.D * L.D) v = q[i];
     }
     pk[e] = v;
+  }
+}
+
+// The two big packed regions (W0h_all: nv*HP x Cp, hidden W: nv*(NH-1)*HP x HP; 96% of the packed floats) by
+// row: blockIdx.y walks rows, each thread 4 consecutive columns (one float4 store, 4 coalesced parameter loads) --
+// no per-element 64-bit division, which bounds k_wpack's element loop (247 us at FC_large).
+__global__ __launch_bounds__(WWG) void k_wpack_rows(const WideLayout L, const float* __restrict__ prm,
+                                                    float* __restrict__ pk) {
+  const long long rows_w0h = (long long)L.nv * L.HP;
+  const long long rows_hid = (long long)L.nv * (L.NH - 1) * L.HP;
+  for (long long r = blockIdx.y; r < rows_w0h + rows_hid; r += gridDim.y) {
+    const bool w0h = r < rows_w0h;
+    const int cols = w0h ? L.Cp : L.HP;
+    const int c = 4 * (blockIdx.x * WWG + threadIdx.x);
+    if (c >= cols) continue;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    long long dst;
+    if (w0h) {
+      const int vb = (int)(r / L.HP), n = (int)(r - (long long)vb * L.HP);
+      dst = L.pk_w0h + r * L.Cp + c;
+      if (n < L.H) {
+        const int sd = vb % L.S;
+        const float* src = prm + vbase(L, vb) + L.lin_w[sd][0] + (long long)n * L.in0[sd] + L.nin[sd];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (c + e < L.C) v[e] = src[c + e];
+      }
+    } else {
+      const long long rh = r - rows_w0h;
+      const long long kl = rh / L.HP;
+      const int n = (int)(rh - kl * L.HP);
+      dst = L.pk_hid + rh * L.HP + c;
+      if (n < L.H) {
+        const int vb = (int)(kl / (L.NH - 1)), l = (int)(kl % (L.NH - 1)) + 1;
+        const float* src = prm + vbase(L, vb) + L.lin_w[vb % L.S][l] + (long long)n * L.H;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (c + e < L.H) v[e] = src[c + e];
+      }
+    }
+    *reinterpret_cast<floatx4*>(pk + dst) = floatx4{v[0], v[1], v[2], v[3]};
   }
 }
 
@@ -2092,8 +2116,15 @@ int bcnf_wide_pack(const BcnfStackDesc* desc, const float* params, const float* 
   WCHK(wide_layout(desc, &L));
   if (!params || !packed || (L.nb > 1 && !qmats) || !aligned16(packed)) return BCNF_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
-  const long long n = L.pk_ldc;
+  const long long n = L.pk_ldc - L.pk_w0y;
   const int grid = (int)std::min<long long>((n + WWG - 1) / WWG, 4096);
+  {
+    const int cx = (std::max(L.Cp, L.HP) / 4 + WWG - 1) / WWG;
+    const long long rows = (long long)L.nv * L.HP * L.NH;   // W0h_all rows + hidden rows
+    hipLaunchKernelGGL(k_wpack_rows, dim3(cx, (unsigned)std::min<long long>(rows, 8192)), dim3(WWG), 0, st, L, params,
+                       (float*)packed);
+    WCHK(bcnf_rt::launched());
+  }
   hipLaunchKernelGGL(k_wpack, dim3(grid), dim3(WWG), 0, st, L, params, qmats, (float*)packed);
   WCHK(bcnf_rt::launched());
   if (L.NH > 1) {
