@@ -795,13 +795,16 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS, (S * (BM + BN) * 64 * 4 <= 80 
   auto rbase = [&](int i) { return AKC ? am0 + 16 * i + 4 * qq : am0 + 16 * qq + i; };
   auto colof = [&](int j) { return BKC ? bn0 + 16 * j + c16 : bn0 + 4 * c16 + j; };
   constexpr int RS = AKC ? 1 : 4;
+  // with KS = 2 the two K halves split the epilogue: half 0 finalises accumulator tiles f = i * TJ + j < NF0, half 1
+  // the rest (the GELU / Philox / G epilogue is a third of a chain GEMM's time at M = 2048)
+  constexpr int NF0 = (T::TI * T::TJ + 1) / 2;
+  auto mine = [&](int f) { return KS == 1 || (kh == 0 ? f < NF0 : f >= NF0); };
   float pre[T::TI][T::TJ][4];
-  if (kh == 0) {
 #pragma unroll
-    for (int i = 0; i < T::TI; ++i)
+  for (int i = 0; i < T::TI; ++i)
 #pragma unroll
-      for (int j = 0; j < T::TJ; ++j) epi_pre<EPI>(g, e.X, rbase(i), colof(j), pre[i][j], RS);
-  }
+    for (int j = 0; j < T::TJ; ++j)
+      if (mine(i * T::TJ + j)) epi_pre<EPI>(g, e.X, rbase(i), colof(j), pre[i][j], RS);
   floatx4 acc[T::TI][T::TJ];
 #pragma unroll
   for (int i = 0; i < T::TI; ++i)
@@ -832,35 +835,35 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS, (S * (BM + BN) * 64 * 4 <= 80 
     rd = rd + 1 == S ? 0 : rd + 1;
     wr = wr + 1 == S ? 0 : wr + 1;
   }
-  if constexpr (KS > 1) {   // K halves meet: the upper half's partials through LDS (the staging ring is idle now)
+  if constexpr (KS > 1) {   // K halves meet: each hands the other the partials of the tiles the other finalises
     static_assert(KS == 2, "two K halves");
     static_assert(T::NT * T::TI * T::TJ * 256 <= S * T::STG, "partials fit the staging ring");
     raw_barrier();
     float* part = lds + (wt * T::TI * T::TJ) * 256 + lane * 4;
-    if (kh == 1) {
-#pragma unroll
-      for (int i = 0; i < T::TI; ++i)
-#pragma unroll
-        for (int j = 0; j < T::TJ; ++j) st4(part + (i * T::TJ + j) * 256, acc[i][j]);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    raw_barrier();
-    if (kh == 1) return;
 #pragma unroll
     for (int i = 0; i < T::TI; ++i)
 #pragma unroll
-      for (int j = 0; j < T::TJ; ++j) {
-        const floatx4 p = ld4(part + (i * T::TJ + j) * 256);
-        acc[i][j] = floatx4{acc[i][j][0] + p[0], acc[i][j][1] + p[1], acc[i][j][2] + p[2], acc[i][j][3] + p[3]};
-      }
+      for (int j = 0; j < T::TJ; ++j)
+        if (!mine(i * T::TJ + j)) st4(part + (i * T::TJ + j) * 256, acc[i][j]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+#pragma unroll
+    for (int i = 0; i < T::TI; ++i)
+#pragma unroll
+      for (int j = 0; j < T::TJ; ++j)
+        if (mine(i * T::TJ + j)) {
+          const floatx4 p = ld4(part + (i * T::TJ + j) * 256);
+          acc[i][j] = floatx4{acc[i][j][0] + p[0], acc[i][j][1] + p[1], acc[i][j][2] + p[2], acc[i][j][3] + p[3]};
+        }
   }
 #pragma unroll
   for (int i = 0; i < T::TI; ++i)
 #pragma unroll
-    for (int j = 0; j < T::TJ; ++j) {
-      const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      epi4<EPI>(g, e.C, e.X, rbase(i), colof(j), v, epi_rnd<EPI>(g, e, rbase(i), colof(j)), pre[i][j], RS);
-    }
+    for (int j = 0; j < T::TJ; ++j)
+      if (mine(i * T::TJ + j)) {
+        const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        epi4<EPI>(g, e.C, e.X, rbase(i), colof(j), v, epi_rnd<EPI>(g, e, rbase(i), colof(j)), pre[i][j], RS);
+      }
 }
 
 // ------------------------------------------------------------------------------------------------
