@@ -737,6 +737,9 @@ __device__ __forceinline__ void gl_tile(const float* __restrict__ As, floatx4 (&
 #pragma unroll
   for (int kq = 0; kq < 4 / KS; ++kq) {
     const int kc = kh * (4 / KS) + kq;
+    // a 16-deep chunk wholly past K contributes nothing (K = 528 at BK = 64: 3 of the last tile's 4 chunks); kc and
+    // kvalid are wave-uniform, so the skip is a scalar branch
+    if (TAIL && 16 * kc >= kvalid) continue;
     floatx4 a[4], b[4];
     gl_frag<AKC, BM, T::TI>(As, am, kc, c16, qq, a);
     gl_frag<BKC, BN, T::TJ>(Bs, bn, kc, c16, qq, b);
@@ -1568,7 +1571,8 @@ double tile_cost(const GemmArgs& g, int groups, int BM, int BN, double eff) {
 
 int g_force_tiling = -1;   // test hook: 0 = 128x128, 1 = 64x64, 2 = 128x48 (16x16 MFMA), 3 = 128x48 on 8 waves,
                            // 4 = 96x48 on 6 waves, 5 = LDS-DMA (tiling C, the default; 96 x 48 for K-contiguous
-                           // operands), 6 = tiling C large tiles, 7 = tiling C 48 x 48
+                           // operands), 6 = tiling C large tiles, 7 = tiling C 48 x 48, 8 = 176 x 176 on 11 waves
+                           // (strided x strided operands only; the dispatcher's choice otherwise)
 
 template <bool AKC, bool BKC, int EPI>
 int gemm(const GemmArgs& g, int groups, hipStream_t st) {
@@ -1580,7 +1584,15 @@ int gemm(const GemmArgs& g, int groups, hipStream_t st) {
   // condition gradient); the register-staged tilings keep the strided layouts, where tiling C's permuted
   // 64-wide wave tiles measured slower (tools/gemm_bench.py t6 / t7, profiles/r02t_gemm_tilings.txt)
   if (pick < 0 && AKC && BKC) pick = 5;
-  if (pick >= 5) return gemm_gl<AKC, BKC, EPI>(g, groups, st, pick == 6);
+  if (pick >= 5 && pick <= 7) return gemm_gl<AKC, BKC, EPI>(g, groups, st, pick == 6);
+  // strided x strided (the grouped Linear gradients, M = H + 1, N = H at H = 526): 176 x 176 tiles cover 528 x 528
+  // exactly (the 64 x 64 / 128 x 128 grids compute 1.19x / 1.47x the area) and re-read each operand 3 times instead
+  // of 9; 11 waves of 16 x 176
+  if constexpr (!AKC && !BKC) {
+    if (pick == 8 || (pick < 0 && g.M > 352 && g.M <= 528 && g.N > 352 && g.N <= 528))
+      return launch_cfg16<176, 176, 32, AKC, BKC, EPI, 11>(g, groups, st);
+  }
+  if (pick == 8) pick = -1;
   if (pick < 0) {
     // relative efficiencies per operand layout, measured at 4096^3 on MI355X (tools/gemm_bench.py)
     const double e1 = AKC ? (BKC ? 1.06 : 0.88) : 0.78, e2 = AKC ? (BKC ? 0.86 : 0.70) : 0.60;
@@ -2255,7 +2267,7 @@ int bcnf_wide_debug_phases(unsigned long long* dbg) {
 // Tiling override for every wide GEMM launch (-1 = the default, LDS-DMA tiling C; 0..6 as g_force_tiling).
 int bcnf_wide_force_tiling(int32_t tiling) {
   const int prev = g_force_tiling;
-  g_force_tiling = (tiling >= 0 && tiling <= 7) ? tiling : -1;
+  g_force_tiling = (tiling >= 0 && tiling <= 8) ? tiling : -1;
   return prev;
 }
 
