@@ -1131,7 +1131,7 @@ __global__ __launch_bounds__(FWD_WG) void k_forward(BcnfLayout L, const float* _
 #pragma unroll
       for (int t = 0; t < HP_SMAX; ++t) wb[t] = (t < S) ? wcol[(long long)4 * t * P.NKp + 16 * k] : 0.f;
       uint32_t bits = 0xffu;
-      if (DROP) bits = dropout_bits(L, seed, off, bc, k, j, 0u);
+      if (DROP && !(BCNF_EXP & 16384)) bits = dropout_bits(L, seed, off, bc, k, j, 0u);   // 16384: no helper Philox
       const float bias = (hw == 0) ? P.b1c[16 * k + lr] : 0.f;
       floatx4 acc = {bias, bias, bias, bias};
 #pragma unroll

@@ -119,3 +119,46 @@ for x in grid[::3]:
     worst_abs = max(worst_abs, e)
     worst_ulp = max(worst_ulp, e / ulp)
 print(f"tanh: max abs err {worst_abs:.3e}, max ulp {worst_ulp:.2f}")
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# gelu_fit (bcnf_device.h gelu_tail, r02x): erfc(z) = t exp(-z^2) Q(t), t = 1 / (1 + p z), Q of degree 7, fitted
+# with relative weights on z in [0, 7] (Chebyshev nodes in t), p scanned; then the fp32 evaluation as the kernel
+# does it (p / sqrt2 on |x|, the 1/2 folded into Q, exp2 of -x^2 log2(e) / 2) against the fp64 GELU / GELU'.
+def gelu_fit(deg=7, zmax=7.0, n=8000):
+    from scipy.special import ndtr
+
+    def fit(p):
+        tmin = 1 / (1 + p * zmax)
+        tt = (np.cos(np.pi * (np.arange(n) + 0.5) / n) * 0.5 + 0.5) * (1 - tmin) + tmin
+        z = (1 / tt - 1) / p
+        y = erfc(z) * np.exp(z * z) / tt
+        w = np.ones_like(tt)
+        for _ in range(60):
+            c = fit_poly(tt, y, deg, w)
+            err = np.abs(np.polyval(c, tt) - y) / y
+            w = w * (1 + 0.5 * err / err.max())
+            w /= w.mean()
+        return c, err.max()
+
+    e, p = min((fit(p)[1], p) for p in np.linspace(0.28, 0.40, 25))
+    c, _ = fit(p)
+    ps, C = f32(p / np.sqrt(2)), [f32(0.5 * v) for v in c]
+    x = np.linspace(-12, 12, 2000001).astype(f32)
+    t = f32(1) / fma(ps, np.abs(x), f32(1))
+    q = np.full_like(x, C[0])
+    for cc in C[1:]:
+        q = fma(q, t, cc)
+    ez = f32(np.exp2(np.float64(f32(f32(x * x) * f32(-0.5 * np.log2(np.e))))))
+    h = f32(f32(t * q) * ez)
+    cdf = np.where(x < 0, h, f32(1) - h)
+    g, dg = f32(x * cdf), fma(x, f32(ez * f32(1 / np.sqrt(2 * np.pi))), cdf)
+    xd = x.astype(np.float64)
+    phi = ndtr(xd)
+    print(f"gelu_fit: p = {p:.4f}, fit max rel {e:.2e}; fp32 |GELU err| {np.abs(g - xd * phi).max():.2e}, "
+          f"|GELU' err| {np.abs(dg - (phi + xd * np.exp(-xd * xd / 2) / np.sqrt(2 * np.pi))).max():.2e}")
+    print("  p / sqrt2 =", f"{ps:.9e}", " Q / 2 (highest first):", ", ".join(f"{v:.9e}" for v in C))
+
+
+if __name__ == "__main__":
+    gelu_fit()
