@@ -166,11 +166,11 @@ __device__ float rec_f(const BcnfLayout& L, const float* P, const float* Q, int 
   const int Da = L.Da, Db = L.Db, D = L.D, NH = L.NH;
   const bool has_an = L.act_norm && k < L.nb - 1;
   const int anb = k * L.blk_stride;
-  if (e < 4) {
+  if (e < 4) {   // ActNorm scale / bias; the inverse record holds 1 / scale (the inverse multiplies, no fp32 divide)
     switch (e) {
-      case 0: return (j < Da) ? (has_an ? P[anb + j] : 1.f) : 0.f;
+      case 0: return (j < Da) ? (has_an ? (inverse ? 1.f / P[anb + j] : P[anb + j]) : 1.f) : 0.f;
       case 1: return (j < Da && has_an) ? P[anb + D + j] : 0.f;
-      case 2: return (j < Db) ? (has_an ? P[anb + Da + j] : 1.f) : 0.f;
+      case 2: return (j < Db) ? (has_an ? (inverse ? 1.f / P[anb + Da + j] : P[anb + Da + j]) : 1.f) : 0.f;
       default: return (j < Db && has_an) ? P[anb + D + Da + j] : 0.f;
     }
   }
@@ -1309,8 +1309,8 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse(BcnfLayout L, const float* 
     mlp_forward<NH, false>(L, rr, za, hpk, bits, DROP, T, Sp, nullptr, nullptr);
     const float S = tanh_bf(Sp);
     const float ybn = (zb - T) * exp_fast(-S);         // cnf.py:205
-    ya = (j < Da) ? (za - rr[1]) / rr[0] : 0.f;        // ActNorm inverse (cnf.py:353-354); identity where none
-    yb = (j < Db) ? (ybn - rr[3]) / rr[2] : 0.f;
+    ya = (j < Da) ? (za - rr[1]) * rr[0] : 0.f;        // ActNorm inverse (cnf.py:353-354), rr[0] = 1 / scale;
+    yb = (j < Db) ? (ybn - rr[3]) * rr[2] : 0.f;       // identity where none
     sr.store(rec + (cur ^ 1) * RING);
     __syncthreads();
   }
