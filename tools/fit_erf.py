@@ -122,10 +122,10 @@ print(f"tanh: max abs err {worst_abs:.3e}, max ulp {worst_ulp:.2f}")
 
 
 # ---------------------------------------------------------------------------------------------------------------
-# gelu_fit (bcnf_device.h gelu_tail, r02x): erfc(z) = t exp(-z^2) Q(t), t = 1 / (1 + p z), Q of degree 7, fitted
+# gelu_fit (bcnf_device.h gelu_tail, r02x): erfc(z) = t exp(-z^2) Q(t), t = 1 / (1 + p z), Q of degree 6, fitted
 # with relative weights on z in [0, 7] (Chebyshev nodes in t), p scanned; then the fp32 evaluation as the kernel
 # does it (p / sqrt2 on |x|, the 1/2 folded into Q, exp2 of -x^2 log2(e) / 2) against the fp64 GELU / GELU'.
-def gelu_fit(deg=7, zmax=7.0, n=8000):
+def gelu_fit(deg=6, zmax=7.0, n=8000):
     from scipy.special import ndtr
 
     def fit(p):
