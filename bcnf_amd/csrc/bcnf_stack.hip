@@ -633,12 +633,20 @@ __global__ __launch_bounds__(BCNF_WG) void k_dh(BcnfLayout L, const float* __res
   dh_body(L, pk, d1, B, dh, blockIdx.x, blockIdx.y, smem);
 }
 
+// BCNF_EXP & 32768: per-workgroup s_memrealtime stamps of the split-K (start, operands loaded, LDS staged, MFMAs done,
+// stored) -> g_sk[workgroup][5] (bcnf_debug_splitk)
+__device__ unsigned long long g_sk[1024 * 5];
+
 // dW1h split-K partials: 64 kj (4 blocks, one per wave) x all columns over one split of KC rows.
 // grid = (ceil(nb/4), splits); work[s][k][16][Cp]
 template <bool VEC, int BPW = 4>
 __device__ __forceinline__ void dw1h_body(const BcnfLayout& L, const float* __restrict__ d1, const float* __restrict__ h,
                                           long long B, int rows_per_split, float* __restrict__ work, int bx, int by,
                                           float* __restrict__ smem, int ones = -1) {
+  const int sk_wg = (int)(blockIdx.x + gridDim.x * blockIdx.y);
+#define SKS(i)                                                                                   \
+  if ((BCNF_EXP & 32768) && threadIdx.x == 0 && sk_wg < 1024) g_sk[sk_wg * 5 + (i)] = __builtin_amdgcn_s_memrealtime();
+  SKS(0)
   const int hs = bstride16(L.Cp);
   // BPW blocks per workgroup: 4 (one per wave, every column tile) or 2 (two waves per block, half the column
   // tiles each: twice the workgroups, LDS for two resident per CU)
@@ -669,6 +677,10 @@ __device__ __forceinline__ void dw1h_body(const BcnfLayout& L, const float* __re
     floatx4 rv[2][8];
 #pragma unroll
     for (int half = 0; half < 2; ++half) load_rows64<VEC>(h, m1, L.C, L.ldh, m0 + 64 * half, 0, rv[half], ones);
+    if (BCNF_EXP & 32768) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      SKS(1)
+    }
 #pragma unroll
     for (int kk = 0; kk < BPW; ++kk) {
       const float m = (ok && k0 + kk < L.nb) ? 1.f : 0.f;
@@ -700,6 +712,7 @@ __device__ __forceinline__ void dw1h_body(const BcnfLayout& L, const float* __re
     }
   }
   __syncthreads();
+  SKS(2)
   const int kw = BPW == 4 ? wave : wave >> 1;
   const int k = k0 + kw;
   const int nh = BPW == 4 ? NC16 : (NC16 + 1) >> 1;
@@ -721,11 +734,17 @@ __device__ __forceinline__ void dw1h_body(const BcnfLayout& L, const float* __re
       }
     }
     acc += acc1;
+    if ((BCNF_EXP & 32768) && n == n_hi - 1) SKS(3)
     if (k < L.nb) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) o[(long long)(4 * lq + i) * L.Cp + 16 * n + lr] = acc[i];
     }
   }
+  if (BCNF_EXP & 32768) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    SKS(4)
+  }
+#undef SKS
 }
 
 template <bool VEC>
@@ -2291,6 +2310,12 @@ const char* bcnf_status_string(int status) {
 }
 
 int bcnf_last_hip_error(void) { return bcnf_rt::last_hip; }
+
+#if BCNF_EXP & 32768
+int bcnf_debug_splitk(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sk), sizeof(g_sk)) == hipSuccess ? 0 : 3;
+}
+#endif
 
 #if BCNF_EXP & 256
 int bcnf_debug_phases(unsigned long long* out) {
