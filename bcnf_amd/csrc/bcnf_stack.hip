@@ -1339,6 +1339,118 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse(BcnfLayout L, const float* 
   }
 }
 
+// Whole-stack inverse on the matrix cores (eval / no dropout: sampling, cnf.py:499-506 via _sample), 16 samples
+// per wave. A feature vector of the wave's samples is 4 registers per lane: lane (q = l >> 4, s = l & 15) holds
+// features 4q .. 4q+3 of sample s -- exactly the v_mfma_f32_16x16x4f32 output layout D[4q + r][s] of out = W x
+// (rows = out features, columns = samples). Contracting the 16 inputs in 4 MFMA steps with input feature 4q + t
+// in K-slot q of step t makes the B operand of step t the lane's own register t, so a dense 16 x 16 layer is 4
+// MFMAs with no data movement; the A operand (W[s][4q + t]) is one LDS read per step from the same pre-rotated
+// inverse record k_inverse uses (entry (o - c) & 15 of out-row o). Mix, Linear 1 (condition part + bias from k_hp
+// as the accumulator), hidden layers and the T / S heads run on the matrix pipe; the VALU keeps GELU, tanh, exp
+// and the coupling / ActNorm inverse (row-layout k_inverse: ~380 VALU instructions per block per 4 samples, 95% of
+// VALU issue in profiles/r02y_k_inverse_pmc_insts.csv). Same sums as k_inverse in a different association order.
+constexpr int INV_M_SPW = 16;                       // samples per wave
+constexpr int INV_M_SPB = INV_M_SPW * (BCNF_WG / 64);
+
+template <int NH>
+__device__ __forceinline__ floatx4 inv_mv(floatx4 acc, const float* __restrict__ slot, const int (&aoff)[4], int off,
+                                          const floatx4& x) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc = mfma4(slot[aoff[t] + off], x[t], acc);
+  return acc;
+}
+
+template <int NH>
+__global__ __launch_bounds__(BCNF_WG) void k_inverse_mfma(BcnfLayout L, const float* __restrict__ pk,
+                                                          const float* __restrict__ zin, const float* __restrict__ hp,
+                                                          long long R, const int64_t* __restrict__ cond_index,
+                                                          long long N, float* __restrict__ yout) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  using F = RecF<NH>;
+  const int RFL = 16 * L.RF, RF = L.RF;
+  float* rec = smem;
+  const int l = threadIdx.x & 63, q = l >> 4, s = l & 15;
+  const long long b = (long long)blockIdx.x * INV_M_SPB + (threadIdx.x >> 6) * INV_M_SPW + s;
+  const long long bc = b < N ? b : N - 1;
+  const int D = L.D, Da = L.Da, Db = L.Db, nb = L.nb;
+  const float* pi = pk + L.pi_off;
+  const long long hr = cond_index ? (long long)cond_index[bc] : bc;
+  const floatx4* hpl = reinterpret_cast<const floatx4*>(hp + hr * 16 + 4 * q);   // HP[k][hr][4q..4q+3]
+  const long long hps4 = R * 4;
+  int aoff[4];                                      // A operand of step t: W[s][4q + t] at row s, entry (s-4q-t)&15
+#pragma unroll
+  for (int t = 0; t < 4; ++t) aoff[t] = s * RF + ((s - 4 * q - t) & 15);
+  const int f0 = 4 * q;                             // this lane's features f0 + r
+
+  floatx4 ya, yb;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    ya[r] = (f0 + r < Da) ? zin[bc * D + f0 + r] : 0.f;
+    yb[r] = (f0 + r < Db) ? zin[bc * D + Da + f0 + r] : 0.f;
+  }
+  const int kl = nb - 1;
+  floatx4 hp_n = hpl[kl * hps4];
+  {
+    Stage<STAGE_REC> sr;
+    sr.load(pi + (long long)kl * RFL, RFL);
+    sr.store(rec + (kl & 1) * RING);
+  }
+  __syncthreads();
+
+  for (int k = kl; k >= 0; --k) {
+    const int cur = k & 1;
+    const int k1 = k >= 1 ? k - 1 : 0;
+    Stage<STAGE_REC> sr;
+    sr.load(pi + (long long)k1 * RFL, RFL);
+    const floatx4 hpk = hp_n;
+    hp_n = hpl[k1 * hps4];
+    const float* slot = rec + cur * RING;
+    const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
+    // z @ Q^T (cnf.py:339): quadrants [a->a | b->a | a->b | b->b]; identity for the last block
+    const floatx4 za = inv_mv<NH>(inv_mv<NH>(zero, slot, aoff, F::Q, ya), slot, aoff, F::Q + 16, yb);
+    const floatx4 zb = inv_mv<NH>(inv_mv<NH>(zero, slot, aoff, F::Q + 32, ya), slot, aoff, F::Q + 48, yb);
+    // nested MLP (cnf.py:98-107): Linear 1 on za with the condition projection + b1 as the accumulator
+    floatx4 a = inv_mv<NH>(hpk, slot, aoff, F::W1, za);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a[r] = gelu_f(a[r]);
+#pragma unroll
+    for (int h = 2; h <= NH; ++h) {
+      const int off = F::HID + 17 * (h - 2);
+      floatx4 bias;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bias[r] = slot[(f0 + r) * RF + off + 16];
+      a = inv_mv<NH>(bias, slot, aoff, off, a);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[r] = gelu_f(a[r]);
+    }
+    floatx4 T, Sp;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      T[r] = slot[(f0 + r) * RF + F::T + 16];
+      Sp[r] = slot[(f0 + r) * RF + F::S + 16];
+    }
+    T = inv_mv<NH>(T, slot, aoff, F::T, a);
+    Sp = inv_mv<NH>(Sp, slot, aoff, F::S, a);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const floatx4 an = *reinterpret_cast<const floatx4*>(slot + (f0 + r) * RF);   // [1/sa ba 1/sb bb]
+      const float S = tanh_bf(Sp[r]);
+      const float ybn = (zb[r] - T[r]) * exp_fast(-S);                            // cnf.py:205
+      ya[r] = (f0 + r < Da) ? (za[r] - an[1]) * an[0] : 0.f;                       // ActNorm inverse (cnf.py:353-354)
+      yb[r] = (f0 + r < Db) ? (ybn - an[3]) * an[2] : 0.f;
+    }
+    sr.store(rec + (cur ^ 1) * RING);
+    __syncthreads();
+  }
+  if (b < N) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (f0 + r < Da) yout[b * D + f0 + r] = ya[r];
+      if (f0 + r < Db) yout[b * D + Da + f0 + r] = yb[r];
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Backward
 // ------------------------------------------------------------------------------------------------
@@ -1880,9 +1992,16 @@ template <int NH>
 int inv_dispatch(const BcnfLayout& L, const float* pk, const float* zin, const float* hp, long long R,
                  const int64_t* ci, long long N, float* y, bool drop, const uint64_t* rng, hipStream_t st) {
   if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
+  int rc;
+  if (!drop && !(BCNF_EXP & 262144)) {               // eval: matrix-core inverse (BCNF_EXP & 262144: row layout)
+    size_t lds_m = sizeof(float) * (size_t)(2 * RING);
+    if ((rc = launch_lds(k_inverse_mfma<NH>, lds_m))) return rc;
+    hipLaunchKernelGGL((k_inverse_mfma<NH>), dim3((unsigned)((N + INV_M_SPB - 1) / INV_M_SPB)), dim3(BCNF_WG), lds_m,
+                       st, L, pk, zin, hp, R, ci, N, y);
+    return check_launch();
+  }
   const dim3 grid((unsigned)((N + 15) / 16));
   size_t lds = fwd_lds_bytes(L);
-  int rc;
   if (drop) {
     rc = launch_lds(k_inverse<NH, true>, lds);
     if (rc) return rc;
