@@ -1350,24 +1350,70 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse(BcnfLayout L, const float* 
 // and the coupling / ActNorm inverse (row-layout k_inverse: ~380 VALU instructions per block per 4 samples, 95% of
 // VALU issue in profiles/r02y_k_inverse_pmc_insts.csv). Same sums as k_inverse in a different association order.
 constexpr int INV_M_SPW = 16;                       // samples per wave
-constexpr int INV_M_SPB = INV_M_SPW * (BCNF_WG / 64);
+constexpr int INV_M_WG = 512;                       // 8 waves share one record ring (2 x 16 KB): 4 workgroups per CU
+constexpr int INV_M_SPB = INV_M_SPW * (INV_M_WG / 64);
+template <int NH>
+constexpr int inv_m_rf() {                          // L.RF of this NH (round_rec of the record end), compile-time so
+  int n = (RecF<NH>::Q + 64 + 3) & ~3;              // every LDS address is a lane base + an immediate offset
+  if (((n / 4) & 1) == 0) n += 4;
+  return n;
+}
+
+// gelu_f on a pair of values with packed fp32 arithmetic (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth per
+// instruction); the same operations per element as gelu_f, so the same results.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_f2(f32x2 x) {
+  const f32x2 ax = {fabsf(x.x), fabsf(x.y)};
+  const f32x2 den = __builtin_elementwise_fma(ax, f32x2{2.616295218e-01f, 2.616295218e-01f}, f32x2{1.0f, 1.0f});
+  const f32x2 t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+  f32x2 q = {-7.295463979e-02f, -7.295463979e-02f};
+  q = __builtin_elementwise_fma(q, t, f32x2{2.239411026e-01f, 2.239411026e-01f});
+  q = __builtin_elementwise_fma(q, t, f32x2{-1.021702215e-01f, -1.021702215e-01f});
+  q = __builtin_elementwise_fma(q, t, f32x2{1.654430181e-01f, 1.654430181e-01f});
+  q = __builtin_elementwise_fma(q, t, f32x2{7.358670980e-02f, 7.358670980e-02f});
+  q = __builtin_elementwise_fma(q, t, f32x2{1.080111340e-01f, 1.080111340e-01f});
+  q = __builtin_elementwise_fma(q, t, f32x2{1.041427255e-01f, 1.041427255e-01f});
+  const f32x2 e = (x * x) * f32x2{-0.72134752044448170368f, -0.72134752044448170368f};
+  const f32x2 ez = {__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+  const f32x2 h = (t * q) * ez;
+  const f32x2 g = f32x2{1.0f, 1.0f} - h;
+  const f32x2 cdf = {x.x < 0.f ? h.x : g.x, x.y < 0.f ? h.y : g.y};
+  return x * cdf;
+}
+__device__ __forceinline__ void gelu4(floatx4& a) {
+  const f32x2 lo = gelu_f2(f32x2{a[0], a[1]}), hi = gelu_f2(f32x2{a[2], a[3]});
+  a[0] = lo.x;
+  a[1] = lo.y;
+  a[2] = hi.x;
+  a[3] = hi.y;
+}
 
 template <int NH>
 __device__ __forceinline__ floatx4 inv_mv(floatx4 acc, const float* __restrict__ slot, const int (&aoff)[4], int off,
                                           const floatx4& x) {
+  if (BCNF_EXP & 524288) {                          // two accumulator chains (t = 0, 1 | t = 2, 3)
+    floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
+    acc = mfma4(slot[aoff[0] + off], x[0], acc);
+    acc1 = mfma4(slot[aoff[2] + off], x[2], acc1);
+    acc = mfma4(slot[aoff[1] + off], x[1], acc);
+    acc1 = mfma4(slot[aoff[3] + off], x[3], acc1);
+    return acc + acc1;
+  }
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc = mfma4(slot[aoff[t] + off], x[t], acc);
   return acc;
 }
+constexpr int INV_M_OCC = (BCNF_EXP & 1048576) ? 5 : (BCNF_EXP & 2097152) ? 8 : 6;   // min waves per SIMD (80 VGPRs, no spills)
 
 template <int NH>
-__global__ __launch_bounds__(BCNF_WG) void k_inverse_mfma(BcnfLayout L, const float* __restrict__ pk,
+__global__ __launch_bounds__(INV_M_WG, INV_M_OCC) void k_inverse_mfma(BcnfLayout L, const float* __restrict__ pk,
                                                           const float* __restrict__ zin, const float* __restrict__ hp,
                                                           long long R, const int64_t* __restrict__ cond_index,
                                                           long long N, float* __restrict__ yout) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   using F = RecF<NH>;
-  const int RFL = 16 * L.RF, RF = L.RF;
+  constexpr int RF = inv_m_rf<NH>();                // == L.RF (checked by the dispatch)
+  const int RFL = 16 * RF;
   float* rec = smem;
   const int l = threadIdx.x & 63, q = l >> 4, s = l & 15;
   const long long b = (long long)blockIdx.x * INV_M_SPB + (threadIdx.x >> 6) * INV_M_SPW + s;
@@ -1390,18 +1436,27 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse_mfma(BcnfLayout L, const fl
   }
   const int kl = nb - 1;
   floatx4 hp_n = hpl[kl * hps4];
-  {
-    Stage<STAGE_REC> sr;
-    sr.load(pi + (long long)kl * RFL, RFL);
-    sr.store(rec + (kl & 1) * RING);
-  }
+  // record staging by LDS-DMA (global_load_lds_dwordx4, no staging registers): wave w copies 1 KB chunks
+  // w, w + 8 of block k's record into a ring slot; chunks past the record re-read its start (slot slack)
+  const int wv = threadIdx.x >> 6;
+  static_assert(RING % (INV_M_WG * 4) == 0, "ring chunks per wave");
+  auto stage = [&](int k, float* dst) {
+#pragma unroll
+    for (int c = 0; c < RING / (INV_M_WG * 4); ++c) {
+      const int ch = wv + (INV_M_WG / 64) * c, e = ch * 256 + 4 * l;
+      const float* src = pi + (long long)k * RFL + (e < RFL ? e : 0);
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(dst + ch * 256), 16,
+                                       0, 0);
+    }
+  };
+  stage(kl, rec + (kl & 1) * RING);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   for (int k = kl; k >= 0; --k) {
     const int cur = k & 1;
     const int k1 = k >= 1 ? k - 1 : 0;
-    Stage<STAGE_REC> sr;
-    sr.load(pi + (long long)k1 * RFL, RFL);
+    stage(k1, rec + (cur ^ 1) * RING);               // slot cur ^ 1 was last read before the previous barrier
     const floatx4 hpk = hp_n;
     hp_n = hpl[k1 * hps4];
     const float* slot = rec + cur * RING;
@@ -1411,8 +1466,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse_mfma(BcnfLayout L, const fl
     const floatx4 zb = inv_mv<NH>(inv_mv<NH>(zero, slot, aoff, F::Q + 32, ya), slot, aoff, F::Q + 48, yb);
     // nested MLP (cnf.py:98-107): Linear 1 on za with the condition projection + b1 as the accumulator
     floatx4 a = inv_mv<NH>(hpk, slot, aoff, F::W1, za);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) a[r] = gelu_f(a[r]);
+    gelu4(a);
 #pragma unroll
     for (int h = 2; h <= NH; ++h) {
       const int off = F::HID + 17 * (h - 2);
@@ -1420,8 +1474,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse_mfma(BcnfLayout L, const fl
 #pragma unroll
       for (int r = 0; r < 4; ++r) bias[r] = slot[(f0 + r) * RF + off + 16];
       a = inv_mv<NH>(bias, slot, aoff, off, a);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) a[r] = gelu_f(a[r]);
+      gelu4(a);
     }
     floatx4 T, Sp;
 #pragma unroll
@@ -1439,7 +1492,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse_mfma(BcnfLayout L, const fl
       ya[r] = (f0 + r < Da) ? (za[r] - an[1]) * an[0] : 0.f;                       // ActNorm inverse (cnf.py:353-354)
       yb[r] = (f0 + r < Db) ? (ybn - an[3]) * an[2] : 0.f;
     }
-    sr.store(rec + (cur ^ 1) * RING);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next record has landed in LDS
     __syncthreads();
   }
   if (b < N) {
@@ -1993,10 +2046,10 @@ int inv_dispatch(const BcnfLayout& L, const float* pk, const float* zin, const f
                  const int64_t* ci, long long N, float* y, bool drop, const uint64_t* rng, hipStream_t st) {
   if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
   int rc;
-  if (!drop && !(BCNF_EXP & 262144)) {               // eval: matrix-core inverse (BCNF_EXP & 262144: row layout)
+  if (!drop && L.RF == inv_m_rf<NH>() && !(BCNF_EXP & 262144)) {               // eval: matrix-core inverse (BCNF_EXP & 262144: row layout)
     size_t lds_m = sizeof(float) * (size_t)(2 * RING);
     if ((rc = launch_lds(k_inverse_mfma<NH>, lds_m))) return rc;
-    hipLaunchKernelGGL((k_inverse_mfma<NH>), dim3((unsigned)((N + INV_M_SPB - 1) / INV_M_SPB)), dim3(BCNF_WG), lds_m,
+    hipLaunchKernelGGL((k_inverse_mfma<NH>), dim3((unsigned)((N + INV_M_SPB - 1) / INV_M_SPB)), dim3(INV_M_WG), lds_m,
                        st, L, pk, zin, hp, R, ci, N, y);
     return check_launch();
   }
