@@ -678,6 +678,10 @@ def main_sample(args, n_draws=500):
     if rank == 0:
         flop = FWD_FLOP_PER_SAMPLE * rows
         achieved = flop / (inv_us * 1e-6) / 1e12
+        # the reference repeats each condition per draw, so its per-row MLP includes the condition projection
+        # (nb x 16 x C MACs); here k_hp computes it once per condition and k_inverse_mfma runs the rest
+        proj_macs = 32 * 16 * 80
+        flop_exec = 2 * ((FWD_FLOP_PER_SAMPLE // 2 - proj_macs) * rows + proj_macs * (b - a))
         line = {
             "metric": "posterior draws/sec (inverse sampling, 500 draws x 1024 conditions), trajectory_FC_small",
             "value": round(value, 1), "unit": "draws/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -690,7 +694,12 @@ def main_sample(args, n_draws=500):
                        "output": tuple(out.shape)},
             "roofline": {"bound": "mfma", "kernel": "k_inverse (this rank's rows)", "achieved": round(achieved, 3),
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                         "traffic": None, "avg_us": round(inv_us, 2), "flop_per_launch": flop},
+                         "traffic": None, "avg_us": round(inv_us, 2), "flop_per_launch": flop,
+                         "flop_executed_per_launch": flop_exec,
+                         "frac_executed": round(flop_exec / (inv_us * 1e-6) / 1e12 / PEAK_FP32_TFLOPS, 4),
+                         "note": "flop_per_launch counts the reference's per-row work (condition projection "
+                                 "repeated per draw); flop_executed: projection once per condition (k_hp) + "
+                                 "k_inverse_mfma (fp32 MFMA dense layers, VALU GELU / tanh / coupling)"},
         }
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline_sample()
