@@ -1349,7 +1349,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse(BcnfLayout L, const float* 
 // as the accumulator), hidden layers and the T / S heads run on the matrix pipe; the VALU keeps GELU, tanh, exp
 // and the coupling / ActNorm inverse (row-layout k_inverse: ~380 VALU instructions per block per 4 samples, 95% of
 // VALU issue in profiles/r02y_k_inverse_pmc_insts.csv). Same sums as k_inverse in a different association order.
-constexpr int INV_M_SPW = 16;                       // samples per wave
+constexpr int INV_M_SPW = 16 * ((BCNF_EXP & 4194304) ? 2 : 1);   // samples per wave
 constexpr int INV_M_WG = 512;                       // 8 waves share one record ring (2 x 16 KB): 4 workgroups per CU
 constexpr int INV_M_SPB = INV_M_SPW * (INV_M_WG / 64);
 template <int NH>
@@ -1403,7 +1403,21 @@ __device__ __forceinline__ floatx4 inv_mv(floatx4 acc, const float* __restrict__
   for (int t = 0; t < 4; ++t) acc = mfma4(slot[aoff[t] + off], x[t], acc);
   return acc;
 }
-constexpr int INV_M_OCC = (BCNF_EXP & 1048576) ? 5 : (BCNF_EXP & 2097152) ? 8 : 6;   // min waves per SIMD (80 VGPRs, no spills)
+constexpr int INV_M_OCC = (BCNF_EXP & 1048576) ? 5 : (BCNF_EXP & 2097152) ? 8 : (BCNF_EXP & 4194304) ? 3 : 6;   // min waves per SIMD (80 VGPRs, no spills)
+
+// G independent 16-sample groups per wave (BCNF_EXP & 4194304: G = 2) interleave their MFMA chains and GELUs.
+constexpr int INV_M_G = (BCNF_EXP & 4194304) ? 2 : 1;
+
+template <int G>
+__device__ __forceinline__ void inv_mv_g(floatx4 (&acc)[G], const float* __restrict__ slot, const int (&aoff)[4],
+                                         int off, const floatx4 (&x)[G]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const float w = slot[aoff[t] + off];            // shared by the groups
+#pragma unroll
+    for (int g = 0; g < G; ++g) acc[g] = mfma4(w, x[g][t], acc[g]);
+  }
+}
 
 template <int NH>
 __global__ __launch_bounds__(INV_M_WG, INV_M_OCC) void k_inverse_mfma(BcnfLayout L, const float* __restrict__ pk,
@@ -1412,30 +1426,38 @@ __global__ __launch_bounds__(INV_M_WG, INV_M_OCC) void k_inverse_mfma(BcnfLayout
                                                           long long N, float* __restrict__ yout) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   using F = RecF<NH>;
+  constexpr int G = INV_M_G;
   constexpr int RF = inv_m_rf<NH>();                // == L.RF (checked by the dispatch)
   const int RFL = 16 * RF;
   float* rec = smem;
   const int l = threadIdx.x & 63, q = l >> 4, s = l & 15;
-  const long long b = (long long)blockIdx.x * INV_M_SPB + (threadIdx.x >> 6) * INV_M_SPW + s;
-  const long long bc = b < N ? b : N - 1;
   const int D = L.D, Da = L.Da, Db = L.Db, nb = L.nb;
   const float* pi = pk + L.pi_off;
-  const long long hr = cond_index ? (long long)cond_index[bc] : bc;
-  const floatx4* hpl = reinterpret_cast<const floatx4*>(hp + hr * 16 + 4 * q);   // HP[k][hr][4q..4q+3]
+  long long b[G];
+  const floatx4* hpl[G];
   const long long hps4 = R * 4;
+  const int f0 = 4 * q;                             // this lane's features f0 + r
+  floatx4 ya[G], yb[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    b[g] = (long long)blockIdx.x * INV_M_SPB + (threadIdx.x >> 6) * INV_M_SPW + 16 * g + s;
+    const long long bc = b[g] < N ? b[g] : N - 1;
+    const long long hr = cond_index ? (long long)cond_index[bc] : bc;
+    hpl[g] = reinterpret_cast<const floatx4*>(hp + hr * 16 + 4 * q);   // HP[k][hr][4q..4q+3]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      ya[g][r] = (f0 + r < Da) ? zin[bc * D + f0 + r] : 0.f;
+      yb[g][r] = (f0 + r < Db) ? zin[bc * D + Da + f0 + r] : 0.f;
+    }
+  }
   int aoff[4];                                      // A operand of step t: W[s][4q + t] at row s, entry (s-4q-t)&15
 #pragma unroll
   for (int t = 0; t < 4; ++t) aoff[t] = s * RF + ((s - 4 * q - t) & 15);
-  const int f0 = 4 * q;                             // this lane's features f0 + r
 
-  floatx4 ya, yb;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    ya[r] = (f0 + r < Da) ? zin[bc * D + f0 + r] : 0.f;
-    yb[r] = (f0 + r < Db) ? zin[bc * D + Da + f0 + r] : 0.f;
-  }
   const int kl = nb - 1;
-  floatx4 hp_n = hpl[kl * hps4];
+  floatx4 hp_n[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) hp_n[g] = hpl[g][kl * hps4];
   // record staging by LDS-DMA (global_load_lds_dwordx4, no staging registers): wave w copies 1 KB chunks
   // w, w + 8 of block k's record into a ring slot; chunks past the record re-read its start (slot slack)
   const int wv = threadIdx.x >> 6;
@@ -1457,49 +1479,74 @@ __global__ __launch_bounds__(INV_M_WG, INV_M_OCC) void k_inverse_mfma(BcnfLayout
     const int cur = k & 1;
     const int k1 = k >= 1 ? k - 1 : 0;
     stage(k1, rec + (cur ^ 1) * RING);               // slot cur ^ 1 was last read before the previous barrier
-    const floatx4 hpk = hp_n;
-    hp_n = hpl[k1 * hps4];
+    floatx4 a[G], za[G], zb[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      a[g] = hp_n[g];                                // Linear 1 accumulator: condition projection + b1 (k_hp)
+      hp_n[g] = hpl[g][k1 * hps4];
+      za[g] = floatx4{0.f, 0.f, 0.f, 0.f};
+      zb[g] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
     const float* slot = rec + cur * RING;
-    const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
     // z @ Q^T (cnf.py:339): quadrants [a->a | b->a | a->b | b->b]; identity for the last block
-    const floatx4 za = inv_mv<NH>(inv_mv<NH>(zero, slot, aoff, F::Q, ya), slot, aoff, F::Q + 16, yb);
-    const floatx4 zb = inv_mv<NH>(inv_mv<NH>(zero, slot, aoff, F::Q + 32, ya), slot, aoff, F::Q + 48, yb);
-    // nested MLP (cnf.py:98-107): Linear 1 on za with the condition projection + b1 as the accumulator
-    floatx4 a = inv_mv<NH>(hpk, slot, aoff, F::W1, za);
-    gelu4(a);
+    inv_mv_g<G>(za, slot, aoff, F::Q, ya);
+    inv_mv_g<G>(zb, slot, aoff, F::Q + 32, ya);
+    inv_mv_g<G>(za, slot, aoff, F::Q + 16, yb);
+    inv_mv_g<G>(zb, slot, aoff, F::Q + 48, yb);
+    // nested MLP (cnf.py:98-107): Linear 1 on za, then the hidden layers
+    inv_mv_g<G>(a, slot, aoff, F::W1, za);
+#pragma unroll
+    for (int g = 0; g < G; ++g) gelu4(a[g]);
 #pragma unroll
     for (int h = 2; h <= NH; ++h) {
       const int off = F::HID + 17 * (h - 2);
-      floatx4 bias;
+      floatx4 bias, x[G];
 #pragma unroll
       for (int r = 0; r < 4; ++r) bias[r] = slot[(f0 + r) * RF + off + 16];
-      a = inv_mv<NH>(bias, slot, aoff, off, a);
-      gelu4(a);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        x[g] = a[g];
+        a[g] = bias;
+      }
+      inv_mv_g<G>(a, slot, aoff, off, x);
+#pragma unroll
+      for (int g = 0; g < G; ++g) gelu4(a[g]);
     }
-    floatx4 T, Sp;
+    floatx4 T[G], Sp[G], tb, sb;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      T[r] = slot[(f0 + r) * RF + F::T + 16];
-      Sp[r] = slot[(f0 + r) * RF + F::S + 16];
+      tb[r] = slot[(f0 + r) * RF + F::T + 16];
+      sb[r] = slot[(f0 + r) * RF + F::S + 16];
     }
-    T = inv_mv<NH>(T, slot, aoff, F::T, a);
-    Sp = inv_mv<NH>(Sp, slot, aoff, F::S, a);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      T[g] = tb;
+      Sp[g] = sb;
+    }
+    inv_mv_g<G>(T, slot, aoff, F::T, a);
+    inv_mv_g<G>(Sp, slot, aoff, F::S, a);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const floatx4 an = *reinterpret_cast<const floatx4*>(slot + (f0 + r) * RF);   // [1/sa ba 1/sb bb]
-      const float S = tanh_bf(Sp[r]);
-      const float ybn = (zb[r] - T[r]) * exp_fast(-S);                            // cnf.py:205
-      ya[r] = (f0 + r < Da) ? (za[r] - an[1]) * an[0] : 0.f;                       // ActNorm inverse (cnf.py:353-354)
-      yb[r] = (f0 + r < Db) ? (ybn - an[3]) * an[2] : 0.f;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const float S = tanh_bf(Sp[g][r]);
+        const float ybn = (zb[g][r] - T[g][r]) * exp_fast(-S);                    // cnf.py:205
+        ya[g][r] = (f0 + r < Da) ? (za[g][r] - an[1]) * an[0] : 0.f;               // ActNorm inverse (cnf.py:353-354)
+        yb[g][r] = (f0 + r < Db) ? (ybn - an[3]) * an[2] : 0.f;
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next record has landed in LDS
     __syncthreads();
   }
-  if (b < N) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (f0 + r < Da) yout[b * D + f0 + r] = ya[r];
-      if (f0 + r < Db) yout[b * D + Da + f0 + r] = yb[r];
+  for (int g = 0; g < G; ++g) {
+    if (b[g] < N) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (f0 + r < Da) yout[b[g] * D + f0 + r] = ya[g][r];
+        if (f0 + r < Db) yout[b[g] * D + Da + f0 + r] = yb[g][r];
+      }
     }
   }
 }
