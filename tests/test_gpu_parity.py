@@ -168,6 +168,23 @@ def test_ragged_batches_vs_oracle(model_g1, g1, B):
     assert ok, err
 
 
+def test_inverse_row_position_invariant(model_g1, g1):
+    """The matrix-core inverse (k_inverse_mfma: 16 samples per wave, 128 per workgroup) gives a row the same bits
+    wherever it sits in the launch: shifted batches, a single row and batches across workgroup edges agree."""
+    gen = torch.Generator().manual_seed(11)
+    B = 300
+    z = torch.randn(B, 19, generator=gen).to(DEV)
+    traj = (3.0 * torch.randn(B, 30, 3, generator=gen)).to(DEV)
+    with torch.no_grad():
+        full = model_g1.inverse(z, traj)
+        for lo in (1, 7, 127, 129):
+            part = model_g1.inverse(z[lo:], traj[lo:])
+            assert torch.equal(full[lo:], part), lo
+        one = model_g1.inverse(z[200:201], traj[200:201])
+    assert torch.equal(full[200:201], one)
+    assert torch.isfinite(full).all()
+
+
 def test_empty_batch(model_g1):
     """The reference's own FC feature net cannot view() an empty batch; the stack itself handles B=0."""
     from bcnf_amd.fused import stack_forward, stack_inverse
