@@ -1408,25 +1408,30 @@ constexpr int INV_M_OCC = (BCNF_EXP & 1048576) ? 5 : (BCNF_EXP & 2097152) ? 8 : 
 // G independent 16-sample groups per wave (BCNF_EXP & 4194304: G = 2) interleave their MFMA chains and GELUs.
 constexpr int INV_M_G = (BCNF_EXP & 4194304) ? 2 : 1;
 
-template <int G>
-__device__ __forceinline__ void inv_mv_g(floatx4 (&acc)[G], const float* __restrict__ slot, const int (&aoff)[4],
-                                         int off, const floatx4 (&x)[G]) {
+template <int G, int KS>
+__device__ __forceinline__ void inv_mv_g(floatx4 (&acc)[G], const float* __restrict__ slot, const int* ao, int off,
+                                         const floatx4 (&x)[G]) {
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const float w = slot[aoff[t] + off];            // shared by the groups
+  for (int t = 0; t < KS; ++t) {
+    const float w = slot[ao[t] + off];              // shared by the groups
 #pragma unroll
     for (int g = 0; g < G; ++g) acc[g] = mfma4(w, x[g][t], acc[g]);
   }
 }
 
-template <int NH>
-__global__ __launch_bounds__(INV_M_WG, INV_M_OCC) void k_inverse_mfma(BcnfLayout L, const float* __restrict__ pk,
+// PERM (D_a, D_b <= 12): the y / z half-vectors hold feature 3q + r in register r < 3 of lane (q, s) (register 3
+// stays 0), so every product with a half-vector input contracts in 3 MFMA steps instead of 4 (mix 16 -> 12 and
+// Linear 1 4 -> 3 MFMAs per block) and the coupling / ActNorm inverse runs on 3 registers. Rows of a permuted
+// output with no feature read entry 0 of lane record 15, which is zero in the mix, T and S rows when D_a, D_b < 15.
+template <int NH, bool PERM>
+__global__ __launch_bounds__(INV_M_WG, PERM ? INV_M_OCC - 1 : INV_M_OCC) void k_inverse_mfma(BcnfLayout L, const float* __restrict__ pk,
                                                           const float* __restrict__ zin, const float* __restrict__ hp,
                                                           long long R, const int64_t* __restrict__ cond_index,
                                                           long long N, float* __restrict__ yout) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   using F = RecF<NH>;
   constexpr int G = INV_M_G;
+  constexpr int KA = PERM ? 3 : 4;                  // MFMA steps over a half-vector input
   constexpr int RF = inv_m_rf<NH>();                // == L.RF (checked by the dispatch)
   const int RFL = 16 * RF;
   float* rec = smem;
@@ -1436,7 +1441,8 @@ __global__ __launch_bounds__(INV_M_WG, INV_M_OCC) void k_inverse_mfma(BcnfLayout
   long long b[G];
   const floatx4* hpl[G];
   const long long hps4 = R * 4;
-  const int f0 = 4 * q;                             // this lane's features f0 + r
+  // half-vector feature of register r (15: none -- a zero row of the mix / T / S records)
+  auto feat = [&](int r) { return PERM ? (r < 3 ? 3 * q + r : 15) : 4 * q + r; };
   floatx4 ya[G], yb[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -1446,13 +1452,25 @@ __global__ __launch_bounds__(INV_M_WG, INV_M_OCC) void k_inverse_mfma(BcnfLayout
     hpl[g] = reinterpret_cast<const floatx4*>(hp + hr * 16 + 4 * q);   // HP[k][hr][4q..4q+3]
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      ya[g][r] = (f0 + r < Da) ? zin[bc * D + f0 + r] : 0.f;
-      yb[g][r] = (f0 + r < Db) ? zin[bc * D + Da + f0 + r] : 0.f;
+      const int f = feat(r);
+      ya[g][r] = (f < Da) ? zin[bc * D + f] : 0.f;
+      yb[g][r] = (f < Db) ? zin[bc * D + Da + f] : 0.f;
     }
   }
-  int aoff[4];                                      // A operand of step t: W[s][4q + t] at row s, entry (s-4q-t)&15
+  // A operands: row o = s of the (possibly permuted) output, K-slot q of step t = input 4q + t (or 3q + t)
+  int aoff[4], aPP[4], aUP[4], aPU[4];
+  {
+    const bool none = PERM && (s & 3) == 3;                                    // permuted row with no feature
+    const int fo = PERM ? 3 * (s >> 2) + (s & 3) : s;                          // output feature of row s
 #pragma unroll
-  for (int t = 0; t < 4; ++t) aoff[t] = s * RF + ((s - 4 * q - t) & 15);
+    for (int t = 0; t < 4; ++t) {
+      const int ch = PERM ? 3 * q + t : 4 * q + t, cu = 4 * q + t;
+      aoff[t] = s * RF + ((s - cu) & 15);                                       // hidden layers
+      aPP[t] = none ? 15 * RF : fo * RF + ((fo - ch) & 15);                     // mix: half -> half
+      aUP[t] = s * RF + ((s - ch) & 15);                                        // Linear 1: half -> hidden
+      aPU[t] = none ? 15 * RF : fo * RF + ((fo - cu) & 15);                     // T / S: hidden -> half
+    }
+  }
 
   const int kl = nb - 1;
   floatx4 hp_n[G];
@@ -1489,12 +1507,12 @@ __global__ __launch_bounds__(INV_M_WG, INV_M_OCC) void k_inverse_mfma(BcnfLayout
     }
     const float* slot = rec + cur * RING;
     // z @ Q^T (cnf.py:339): quadrants [a->a | b->a | a->b | b->b]; identity for the last block
-    inv_mv_g<G>(za, slot, aoff, F::Q, ya);
-    inv_mv_g<G>(zb, slot, aoff, F::Q + 32, ya);
-    inv_mv_g<G>(za, slot, aoff, F::Q + 16, yb);
-    inv_mv_g<G>(zb, slot, aoff, F::Q + 48, yb);
+    inv_mv_g<G, KA>(za, slot, aPP, F::Q, ya);
+    inv_mv_g<G, KA>(zb, slot, aPP, F::Q + 32, ya);
+    inv_mv_g<G, KA>(za, slot, aPP, F::Q + 16, yb);
+    inv_mv_g<G, KA>(zb, slot, aPP, F::Q + 48, yb);
     // nested MLP (cnf.py:98-107): Linear 1 on za, then the hidden layers
-    inv_mv_g<G>(a, slot, aoff, F::W1, za);
+    inv_mv_g<G, KA>(a, slot, aUP, F::W1, za);
 #pragma unroll
     for (int g = 0; g < G; ++g) gelu4(a[g]);
 #pragma unroll
@@ -1502,38 +1520,39 @@ __global__ __launch_bounds__(INV_M_WG, INV_M_OCC) void k_inverse_mfma(BcnfLayout
       const int off = F::HID + 17 * (h - 2);
       floatx4 bias, x[G];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) bias[r] = slot[(f0 + r) * RF + off + 16];
+      for (int r = 0; r < 4; ++r) bias[r] = slot[(4 * q + r) * RF + off + 16];
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         x[g] = a[g];
         a[g] = bias;
       }
-      inv_mv_g<G>(a, slot, aoff, off, x);
+      inv_mv_g<G, 4>(a, slot, aoff, off, x);
 #pragma unroll
       for (int g = 0; g < G; ++g) gelu4(a[g]);
     }
     floatx4 T[G], Sp[G], tb, sb;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      tb[r] = slot[(f0 + r) * RF + F::T + 16];
-      sb[r] = slot[(f0 + r) * RF + F::S + 16];
+      tb[r] = slot[feat(r) * RF + F::T + 16];
+      sb[r] = slot[feat(r) * RF + F::S + 16];
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       T[g] = tb;
       Sp[g] = sb;
     }
-    inv_mv_g<G>(T, slot, aoff, F::T, a);
-    inv_mv_g<G>(Sp, slot, aoff, F::S, a);
+    inv_mv_g<G, 4>(T, slot, aPU, F::T, a);
+    inv_mv_g<G, 4>(Sp, slot, aPU, F::S, a);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const floatx4 an = *reinterpret_cast<const floatx4*>(slot + (f0 + r) * RF);   // [1/sa ba 1/sb bb]
+    for (int r = 0; r < (PERM ? 3 : 4); ++r) {
+      const int f = feat(r);
+      const floatx4 an = *reinterpret_cast<const floatx4*>(slot + f * RF);         // [1/sa ba 1/sb bb]
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const float S = tanh_bf(Sp[g][r]);
         const float ybn = (zb[g][r] - T[g][r]) * exp_fast(-S);                    // cnf.py:205
-        ya[g][r] = (f0 + r < Da) ? (za[g][r] - an[1]) * an[0] : 0.f;               // ActNorm inverse (cnf.py:353-354)
-        yb[g][r] = (f0 + r < Db) ? (ybn - an[3]) * an[2] : 0.f;
+        ya[g][r] = (f < Da) ? (za[g][r] - an[1]) * an[0] : 0.f;                    // ActNorm inverse (cnf.py:353-354)
+        yb[g][r] = (f < Db) ? (ybn - an[3]) * an[2] : 0.f;
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next record has landed in LDS
@@ -1544,8 +1563,9 @@ __global__ __launch_bounds__(INV_M_WG, INV_M_OCC) void k_inverse_mfma(BcnfLayout
     if (b[g] < N) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        if (f0 + r < Da) yout[b[g] * D + f0 + r] = ya[g][r];
-        if (f0 + r < Db) yout[b[g] * D + Da + f0 + r] = yb[g][r];
+        const int f = feat(r);
+        if (f < Da) yout[b[g] * D + f] = ya[g][r];
+        if (f < Db) yout[b[g] * D + Da + f] = yb[g][r];
       }
     }
   }
@@ -2095,9 +2115,14 @@ int inv_dispatch(const BcnfLayout& L, const float* pk, const float* zin, const f
   int rc;
   if (!drop && L.RF == inv_m_rf<NH>() && !(BCNF_EXP & 262144)) {               // eval: matrix-core inverse (BCNF_EXP & 262144: row layout)
     size_t lds_m = sizeof(float) * (size_t)(2 * RING);
-    if ((rc = launch_lds(k_inverse_mfma<NH>, lds_m))) return rc;
-    hipLaunchKernelGGL((k_inverse_mfma<NH>), dim3((unsigned)((N + INV_M_SPB - 1) / INV_M_SPB)), dim3(INV_M_WG), lds_m,
-                       st, L, pk, zin, hp, R, ci, N, y);
+    const dim3 grid_m((unsigned)((N + INV_M_SPB - 1) / INV_M_SPB));
+    if (L.Da <= 12 && L.Db <= 12 && !(BCNF_EXP & 8388608)) {
+      if ((rc = launch_lds(k_inverse_mfma<NH, true>, lds_m))) return rc;
+      hipLaunchKernelGGL((k_inverse_mfma<NH, true>), grid_m, dim3(INV_M_WG), lds_m, st, L, pk, zin, hp, R, ci, N, y);
+    } else {
+      if ((rc = launch_lds(k_inverse_mfma<NH, false>, lds_m))) return rc;
+      hipLaunchKernelGGL((k_inverse_mfma<NH, false>), grid_m, dim3(INV_M_WG), lds_m, st, L, pk, zin, hp, R, ci, N, y);
+    }
     return check_launch();
   }
   const dim3 grid((unsigned)((N + 15) / 16));

@@ -183,7 +183,9 @@ int bcnf_grad_reduce(const BcnfStackDesc* desc, const void* slab, const float* h
 
 /* Inverse of the whole stack: y (N x D) from z (N x D). h has h_rows rows; row r uses feature row
  * cond_index[r] when cond_index != NULL (h_rows may then be anything), else row r (h_rows == N).
- * `scratch`: bcnf_inverse_scratch_bytes(h_rows) -- the projection is computed once per feature row. */
+ * `scratch`: bcnf_inverse_scratch_bytes(h_rows) -- the projection is computed once per feature row.
+ * Without dropout (eval, or p = 0) the stack runs on the matrix cores, 16 rows per wave;
+ * training mode with dropout keeps the row-layout kernel. A row's result does not depend on its position. */
 int bcnf_stack_inverse(const BcnfStackDesc* desc, const void* packed, const float* z, const float* h,
                        int64_t h_rows, const int64_t* cond_index, int64_t n_rows, float* y, int32_t training,
                        const uint64_t* rng_state, void* scratch, void* stream);
