@@ -692,7 +692,7 @@ def main_sample(args, n_draws=500):
             "config": {"workload": "CondRealNVP_v2.sample-equivalent draw (configs[4])", "conditions": args.batch,
                        "draws_per_condition": n_draws, "parallelism": f"condition shards x{world}",
                        "output": tuple(out.shape)},
-            "roofline": {"bound": "mfma", "kernel": "k_inverse (this rank's rows)", "achieved": round(achieved, 3),
+            "roofline": {"bound": "mfma", "kernel": "k_inverse_mfma (this rank's rows)", "achieved": round(achieved, 3),
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
                          "traffic": None, "avg_us": round(inv_us, 2), "flop_per_launch": flop,
                          "flop_executed_per_launch": flop_exec,
