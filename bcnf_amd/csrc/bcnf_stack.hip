@@ -1363,8 +1363,8 @@ constexpr int inv_m_rf() {                          // L.RF of this NH (round_re
 // instruction); the same operations per element as gelu_f, so the same results.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 gelu_f2(f32x2 x) {
-  const f32x2 ax = {fabsf(x.x), fabsf(x.y)};
-  const f32x2 den = __builtin_elementwise_fma(ax, f32x2{2.616295218e-01f, 2.616295218e-01f}, f32x2{1.0f, 1.0f});
+  // scalar FMAs here: VOP3 takes |x| as a free source modifier (VOP3P has none)
+  const f32x2 den = {fmaf(2.616295218e-01f, fabsf(x.x), 1.0f), fmaf(2.616295218e-01f, fabsf(x.y), 1.0f)};
   const f32x2 t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
   f32x2 q = {-7.295463979e-02f, -7.295463979e-02f};
   q = __builtin_elementwise_fma(q, t, f32x2{2.239411026e-01f, 2.239411026e-01f});
