@@ -134,7 +134,11 @@ class ConditionalNestedNeuralNetwork(nn.Module):
 def _coupling_path(layer: str, activation: str, layer_kwargs, activation_kwargs) -> str:
     """Which implementation runs a coupling stack: "fused" (Linear + GELU: the small or wide HIP kernel family),
     "fft" (LinearFFTEnriched + GELU: the wide family on the folded weights, bcnf_amd/fft_stack.py) or "layerwise"
-    (AnyGLU: the reference's layer sequence on the GPU, its Linear layers on the library's MFMA GEMMs)."""
+    (AnyGLU: the reference's layer sequence on the GPU, its Linear layers on the library's MFMA GEMMs).
+    AnyGLU runs whatever activation module LayerFactory builds (e.g. Identity in
+    trajectory_SFrExp_LSTM_SiGLU_2_large.yaml); only the fused and fft paths are tied to GELU."""
+    if layer == "AnyGLU":
+        return "layerwise"
     if activation != "GELU" or activation_kwargs:
         raise NotImplementedError(f"bcnf_amd's coupling kernels implement activation='GELU' (exact erf); got "
                                   f"activation={activation!r}")
@@ -142,8 +146,6 @@ def _coupling_path(layer: str, activation: str, layer_kwargs, activation_kwargs)
         return "fused"
     if layer == "LinearFFTEnriched" and not layer_kwargs:
         return "fft"
-    if layer == "AnyGLU":
-        return "layerwise"
     raise NotImplementedError(f"bcnf_amd: no coupling path implements layer={layer!r} with {layer_kwargs!r}")
 
 
@@ -380,6 +382,10 @@ class CondRealNVP_v2(ConditionalInvertibleLayer):
     def flat_parameters(self) -> list[nn.Parameter]:
         """Optimizer-friendly parameter list: ONE flat leaf for the whole coupling stack plus the feature
         network (and prediction head) parameters. Switches the stack to flat-gradient mode."""
+        if self._path == "layerwise":
+            raise NotImplementedError("bcnf_amd: flat_parameters() needs a fused coupling stack (Linear or "
+                                      "LinearFFTEnriched); AnyGLU stacks keep per-layer parameters -- use "
+                                      "model.parameters()")
         self._fused.grad_mode = "flat"
         out = [self._fused.flat_param]
         if self.n_conditions > 0:

@@ -78,7 +78,10 @@ class FFTWideStack(WideStack):
 
     # ------------------------------------------------------------------ canonical <-> effective
     def refresh(self):
-        """canonical (reference) parameters -> effective Linear-layout buffer: W_eff = W[:, :n] + W[:, n:] F."""
+        """canonical (reference) parameters -> effective Linear-layout buffer: W_eff = W[:, :n] + W[:, n:] F.
+        The fold GEMM reads raw device pointers, so the buffers are checked first: a model still on the CPU raises
+        the same RuntimeError as every other entry point instead of handing host pointers to the HIP kernel."""
+        self._check_device(self.canon)
         with torch.no_grad():
             groups = {}
             for (o, shape, e, n) in self._maps:
@@ -123,10 +126,12 @@ class FFTWideStack(WideStack):
 
     # ------------------------------------------------------------------ launches (fold before, unfold after)
     def launch_forward(self, y, h, training: bool, save: bool, want_logp: bool = False):
+        self._check_inputs(y, h, "forward")
         self.refresh()
         return super().launch_forward(y, h, training, save, want_logp)
 
     def launch_nll_forward(self, y, h, training: bool, finalize: bool = True):
+        self._check_inputs(y, h, "forward")
         self.refresh()
         return super().launch_nll_forward(y, h, training, finalize)
 
@@ -139,6 +144,7 @@ class FFTWideStack(WideStack):
         return dy, dh, self.unfold_grad(dparams)
 
     def launch_inverse(self, z, h, cond_index=None, training: bool = False):
+        self._check_inputs(z, h, "inverse")
         if not self._pack_frozen:
             self.refresh()
         return super().launch_inverse(z, h, cond_index, training)

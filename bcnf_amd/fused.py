@@ -432,7 +432,7 @@ class FusedStack:
         ldj = torch.empty(B, dtype=torch.float32, device=dev)
         rng = self.rng_state() if (training and self.cfg.dropout > 0.0) else None
         calls = {
-            "forward": lambda: L.bcnf_nll_forward(self._pdesc, N.ptr(pk), N.ptr(y), N.ptr(h), ctypes.c_int64(B), N.ptr(z),
+            "k_forward": lambda: L.bcnf_nll_forward(self._pdesc, N.ptr(pk), N.ptr(y), N.ptr(h), ctypes.c_int64(B), N.ptr(z),
                                                   N.ptr(ldj), ctypes.c_int32(int(training)), N.ptr(rng), N.ptr(ws),
                                                   ctypes.c_int32(0), N.ptr(vals), None, stream),
             "k_backward": lambda: L.bcnf_nll_backward(self._pdesc, N.ptr(pk), N.ptr(h), N.ptr(z), None, ctypes.c_int64(B),
@@ -477,9 +477,9 @@ class FusedStack:
         ldj = torch.empty(B, dtype=torch.float32, device=dev)
         rng = self.rng_state() if (training and self.cfg.dropout > 0.0) else None
         calls = {
-            "pack": lambda: L.bcnf_pack_params_fold(self._pdesc, N.ptr(self.flat), N.ptr(self.qflat), N.ptr(wf),
+            "k_pack_fold": lambda: L.bcnf_pack_params_fold(self._pdesc, N.ptr(self.flat), N.ptr(self.qflat), N.ptr(wf),
                                                     N.ptr(bf), ctypes.c_int32(X), N.ptr(pk), N.ptr(fold), None, stream),
-            "forward": lambda: L.bcnf_fold_nll_forward(self._pdesc, N.ptr(pk), N.ptr(fold), ctypes.c_int32(X),
+            "k_forward": lambda: L.bcnf_fold_nll_forward(self._pdesc, N.ptr(pk), N.ptr(fold), ctypes.c_int32(X),
                                                        N.ptr(y), N.ptr(x), ldx, ctypes.c_int64(B), N.ptr(z),
                                                        N.ptr(ldj), ctypes.c_int32(int(training)), N.ptr(rng),
                                                        N.ptr(ws), ctypes.c_int32(0), N.ptr(vals), None, stream),

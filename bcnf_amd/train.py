@@ -191,15 +191,16 @@ class TrainStep:
         N.check(N.lib().bcnf_guard_check_global(N.ptr(self._gvals), N.ptr(self._guard),
                                                 N.stream_handle(self._gvals.device)), "bcnf_guard_check_global")
 
-    def _update(self, vals=None, clip: bool = True):
+    def _update(self, vals=None, clip: bool = True, epoch_book: bool = True):
         """Adam, then clip_grad_norm_ after the step (trainer.py:273-275); the clip launch also advances the
         Adam step count and, in epoch mode, the batch cursor, and stores the logged values into the pinned
-        history (end-of-step bookkeeping, no extra launch)."""
+        history (end-of-step bookkeeping, no extra launch). epoch_book=False: a batch from outside the epoch
+        order (step_indexed while an order is set) -- no cursor advance and no history row."""
         if self.world > 1 and vals is not None:
             vals = self._gvals              # every rank logs the global values and halts on the same step
             self._check_global()
-        cursor = (self._epoch[1], self._epoch[2]) if self._epoch is not None else None
-        log = (vals, self._hist) if (vals is not None and self._hist is not None) else None
+        cursor = (self._epoch[1], self._epoch[2]) if (self._epoch is not None and epoch_book) else None
+        log = (vals, self._hist) if (vals is not None and self._hist is not None and epoch_book) else None
         if not clip:
             # a step inside a multi-step graph that the next step's backward follows: its clip-after-step
             # would only scale gradients that are overwritten before anyone can read them (the reference
@@ -220,13 +221,14 @@ class TrainStep:
                 dist.broadcast(p.data, src=src, group=self.pg)
 
     # ------------------------------------------------------------------ eager / graph
-    def eager_step(self, y, traj, gather=None):
+    def eager_step(self, y, traj, gather=None, epoch_book: bool = True):
         self._setup_bucket()
         vals = self._forward_backward(y, traj, gather)
         vals = self._allreduce(vals)
-        self._update(vals)
+        self._update(vals, epoch_book=epoch_book)
         self._rebind = self._graphs is not None     # .grad now holds this step's buffers, not a graph's
-        return vals
+        # world > 1: vals is a view of the bucket tail, which the next step overwrites
+        return vals.clone() if self.world > 1 else vals
 
     def _gather(self, defer: bool = False):
         """Pool rows of the current batch, both tensors in one native launch: the static index buffer, or
@@ -411,8 +413,13 @@ class TrainStep:
         """step(pool_y[idx], pool_traj[idx]) with the gather captured in the graph."""
         if self._pool is None:
             raise RuntimeError("step_indexed() needs set_pool()")
-        idx = idx.to(dtype=torch.int64).contiguous()
         self._check_indices(idx)
+        idx = idx.to(device=self._pool[0].device, dtype=torch.int64).contiguous()
+        if self._epoch is not None:
+            # a batch outside the epoch order (the ragged remainder of an epoch, drop_last=False): the epoch graphs
+            # walk the device cursor and write history rows, so this one runs eagerly on the same kernels and
+            # optimizer state without touching the cursor or the history
+            return tuple(self.eager_step(*self._pool_rows(idx), epoch_book=False).tolist())
         if not self.capture:
             self._static = (None, None, idx)
             return tuple(self.eager_step(*self._gather()).tolist())
@@ -426,10 +433,11 @@ class TrainStep:
 
     def _check_indices(self, idx):
         """Pool indices in range (the reference's DataLoader raises IndexError; the device gather would read out of
-        bounds). One host round trip, before anything is launched."""
+        bounds), before anything is launched. Host indices (a DataLoader's) are checked on the host, no device sync;
+        device-resident indices cost one host round trip."""
         if idx.numel() == 0:
             return
-        lo, hi = torch.aminmax(idx)
+        lo, hi = torch.aminmax(idx if idx.device.type == "cpu" else idx.to(torch.int64))
         n = self._pool[0].shape[0]
         if int(lo) < 0 or int(hi) >= n:
             raise IndexError(f"bcnf_amd TrainStep: batch index out of range [0, {n}) (got {int(lo)}..{int(hi)})")

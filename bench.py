@@ -41,13 +41,19 @@ FC_SMALL = {
     ],
 }
 # Algorithmic work per sample (recompute excluded). MAC counts for FC_small:
-#   forward flow  = 32 * (90*16 + 6*16*16 + 16*18) + 31 * 19*19 = 115,639 MAC
-#   backward flow = dX (115,639) + dW of every Linear (32 * 3,264 = 104,448)      = 220,087 MAC
+#   forward flow  = 32 * (90*16 + 6*16*16 + 16*18) + 31 * 19*19 = 115,639 MAC   (k_forward; the reference's count,
+#                   the condition projection included -- k_forward computes it on its helper waves)
+#   backward flow = dX (115,639) + dW of every Linear (32 * 3,264 = 104,448)      = 220,087 MAC for the whole backward;
+#                   k_backward's own share excludes the W1 condition columns (dW1h and dL/dh: 2 * 32 * 16 * 80 =
+#                   81,920 MAC, done by the tail's split-K): 138,167 MAC
 FWD_FLOP_PER_SAMPLE = 2 * 115_639
 BWD_FLOP_PER_SAMPLE = 2 * 220_087
-# Minimal HBM bytes per sample of the fused kernels (inputs + outputs + saved block inputs / masks):
-#   forward (train): y 76 + h 320 + z 76 + ldj 4 + ysave 32*128 + masks 8*64        = 5,164 B
-#   backward       : h 320 + dz 76 + dldj 4 + ysave 4,096 + masks 512 + dh 320 + slab share = 5,328 B + slab
+KBWD_FLOP_PER_SAMPLE = 2 * (220_087 - 81_920)
+# SURVEY §8d minimal HBM bytes per sample of per-block kernels (recompute in backward), nb = 32, D = 19, C = 80:
+#   forward  nb * 4 * (2D + C + 2)                         = 15,360 B   (y, h in; z, ldj out, per block)
+#   training nb * 4 * (5D + 4C + 2)                        = 53,376 B   -> backward share 53,376 - 15,360 = 38,016 B
+FWD_ALG_BYTES_PER_SAMPLE = 32 * 4 * (2 * 19 + 80 + 2)
+BWD_ALG_BYTES_PER_SAMPLE = 32 * 4 * (5 * 19 + 4 * 80 + 2) - FWD_ALG_BYTES_PER_SAMPLE
 # trajectory_FC_large / trajectory_LSTM_large (configs/runs/old/*.yaml): the wide-MLP family (bcnf_wide.hip)
 FC_LARGE = {
     "global": FC_SMALL["global"],
@@ -72,6 +78,8 @@ LSTM_LARGE = {
 #   flow forward = 26 * (1370*526 + 4*526*526 + 526*18) + 25 * 19*19 = 47,765,617 MAC
 WIDE_FWD_FLOP_PER_SAMPLE = 2 * 47_765_617
 WIDE_TRAIN_FLOP_PER_SAMPLE = 3 * WIDE_FWD_FLOP_PER_SAMPLE
+# SURVEY §8d per-block minimum for the training step, nb = 26, D = 19, C = 1360: nb * 4 * (5D + 4C + 2)
+WIDE_ALG_BYTES_PER_SAMPLE = 26 * 4 * (5 * 19 + 4 * 1360 + 2)
 WIDE_NAMES = {"fc_large": "trajectory_FC_large", "lstm_large": "trajectory_LSTM_large"}
 WORKLOADS = {"fc_small": (FC_SMALL, 4096), "fc_large": (FC_LARGE, 2048), "lstm_large": (LSTM_LARGE, 1024),
              "sample": (FC_SMALL, 1024)}
@@ -415,17 +423,9 @@ def main():
     kern = kernel_timing(model, data, args) if rank == 0 else {}
     if rank == 0:
         B = args.batch
-        dom = "k_backward"                       # the dominant kernel (forward incl. k_hp is ~half of it)
-        flop = BWD_FLOP_PER_SAMPLE * B
-        us = kern.get(dom, float("nan"))
-        achieved = flop / (us * 1e-6) / 1e12
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                traffic = json.load(f).get(dom)
-        util = pmc_utilisation(dom, us)
         lp_abs, lp_rel = log_prob_error(model, device)
+        per_kernel = fc_small_rooflines(kern, B)
+        dom = max(per_kernel, key=lambda k: per_kernel[k]["avg_us"])   # the longest single launch, measured
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "ranks_seen": seen,
@@ -438,24 +438,73 @@ def main():
             "log_prob_max_abs_err": lp_abs, "log_prob_max_rel_err": lp_rel,
             "log_prob_err_other_fixtures": log_prob_errors_more(device),
             "last_loss": losses[0] if losses else None,
-            "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
-                         "avg_us": round(us, 2), "flop_per_launch": flop,
-                         # both fractions -- the PMC HBM bytes of the same launch over its duration
-                         "hbm_achieved_GBps": round(traffic / (us * 1e3), 1) if traffic else None,
-                         "hbm_frac": round(traffic / (us * 1e3) / PEAK_HBM_GBS, 4) if traffic else None,
-                         **util,
-                         "note": "fp32 VALU (DPP rotations) + fp32 MFMA; peak is the fp32 vector = MFMA-f32 rate"},
+            "roofline": dict(per_kernel[dom], kernel=dom),
+            "roofline_kernels": per_kernel,
             "kernels_us": {k: round(v, 2) for k, v in kern.items()},
         }
         if not args.no_secondary and world == 1 and not (args.indexed or args.per_step_sync):
             line["secondary"] = secondary_figures(step, args, device)
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(args)
+        if not args.no_secondary and world == 1 and not (args.indexed or args.per_step_sync):
+            # configs[2], [3], [4] at their single-GPU sizes, each with its own roofline and cpu_baseline (bounded)
+            del step, model, data
+            torch.cuda.empty_cache()
+            sub = line.setdefault("secondary", {})
+            for wl, steps in (("fc_large", 8), ("lstm_large", 8), ("sample", 5)):
+                t_sub = time.perf_counter()
+                try:
+                    if wl == "sample":
+                        sub[wl] = run_sample(WORKLOADS[wl][1], steps, 2, 1, 0, device, cpu=not args.no_cpu_baseline)
+                    else:
+                        sub[wl] = run_wide(wl, WORKLOADS[wl][1], steps, 3, 1, 0, device, graph=not args.no_graph,
+                                           kernel_iters=3, cpu=not args.no_cpu_baseline,
+                                           cpu_batch=256 if wl == "fc_large" else 128, cpu_steps=2)
+                except Exception as e:           # a sub-line never takes the headline down with it
+                    sub[wl] = {"error": f"{type(e).__name__}: {e}"}
+                sub[wl]["bench_wall_s"] = round(time.perf_counter() - t_sub, 1)
+                torch.cuda.empty_cache()
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _pmc_traffic(kernel):
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(pmc):
+        return None
+    with open(pmc) as f:
+        return json.load(f).get(kernel)
+
+
+def fc_small_rooflines(kern, B):
+    """Per-kernel roofline entries of the two single-launch FC_small kernels: achieved = the kernel's ALGORITHMIC
+    FLOPs per launch (reference count) / its HIP-event duration; algorithmic_bytes = SURVEY §8d's per-block
+    minimum x B; traffic = PMC FETCH (x2, gfx950) + WRITE bytes per launch of the same build (profiles/pmc_traffic.json,
+    tools/profile_round.sh), traffic_ratio = traffic / algorithmic_bytes (> 1: bytes beyond the per-block minimum)."""
+    spec = {"k_forward": (FWD_FLOP_PER_SAMPLE, FWD_ALG_BYTES_PER_SAMPLE,
+                          "whole-stack forward: ActNorm, nested MLP (DPP-rotation VALU), coupling, log-det, mix; "
+                          "condition projection on fp32 MFMA helper waves; saves the activation records"),
+              "k_backward": (KBWD_FLOP_PER_SAMPLE, BWD_ALG_BYTES_PER_SAMPLE,
+                             "whole-stack backward from the saved records: dX chain (DPP VALU) + dW tiles (fp32 "
+                             "MFMA); the W1 condition-column gradients run in the tail (excluded from its FLOPs)")}
+    out = {}
+    for k, (fps, bps, what) in spec.items():
+        us = kern.get(k, float("nan"))
+        flop, alg = fps * B, bps * B
+        achieved = flop / (us * 1e-6) / 1e12
+        traffic = _pmc_traffic(k)
+        out[k] = {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                  "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic, "avg_us": round(us, 2),
+                  "flop_per_launch": flop, "algorithmic_bytes": alg,
+                  "traffic_ratio": round(traffic / alg, 3) if traffic else None,
+                  "hbm_achieved_GBps": round(traffic / (us * 1e3), 1) if traffic else None,
+                  "hbm_frac": round(traffic / (us * 1e3) / PEAK_HBM_GBS, 4) if traffic else None,
+                  "alg_hbm_frac": round(alg / (us * 1e3) / PEAK_HBM_GBS, 4),
+                  **pmc_utilisation(k, us), "what": what,
+                  "note": "fp32 VALU + fp32 MFMA; peak = the fp32 vector = MFMA-f32 rate (MI355X_MICROARCH.md)"}
+    return out
 
 
 def secondary_figures(step, args, device, n_loop=50, n_trainer=12):
@@ -525,8 +574,9 @@ def secondary_figures(step, args, device, n_loop=50, n_trainer=12):
     return out
 
 
-def cpu_baseline_wide(args, cfg, batch=256, steps=4):
-    """CPU oracle training step of the wide workload (FC_large shapes) on this host, bounded: B=256, a few steps."""
+def cpu_baseline_wide(workload, cfg, batch=256, steps=4):
+    """CPU oracle training step of the wide workload (FC_large / LSTM_large shapes; LSTM features through the oracle's
+    LSTM restatement, pool_dim = 1 as on the GPU) on this host, bounded: a few steps at a small batch."""
     from oracle import cnf_oracle as O
     threads = host_cores()
     torch.set_num_threads(threads)
@@ -534,11 +584,14 @@ def cpu_baseline_wide(args, cfg, batch=256, steps=4):
     from bcnf_amd import CondRealNVP_v2
     m = CondRealNVP_v2.from_config(cfg)
     kw = cfg["model"]["kwargs"]
-    fs = cfg["feature_networks"][1]["kwargs"]
+    fn = cfg["feature_networks"][1]
+    fk = fn["kwargs"]
+    extra = ({"lstm": (fk["input_size"], fk["hidden_size"], fk["num_layers"], fk["bidirectional"], fk["pool_dim"])}
+             if fn["type"] == "LSTM" else {"feature_sizes": fk["sizes"], "feature_dropout": fk["dropout"]})
     spec = O.StackSpec(size=19, nested_sizes=kw["nested_sizes"], n_blocks=kw["n_blocks"],
-                       n_conditions=kw["n_conditions"], dropout=kw["dropout"], act_norm=kw["act_norm"],
-                       feature_sizes=fs["sizes"], feature_dropout=fs["dropout"])
+                       n_conditions=kw["n_conditions"], dropout=kw["dropout"], act_norm=kw["act_norm"], **extra)
     sd = {k: v.detach().clone().requires_grad_(not k.endswith("orthonormal_matrix")) for k, v in m.state_dict().items()}
+    del m
     opt = torch.optim.Adam([v for v in sd.values() if v.requires_grad], lr=2e-4)
     g = torch.Generator().manual_seed(7)
     y = torch.randn(batch, 19, generator=g)
@@ -550,37 +603,35 @@ def cpu_baseline_wide(args, cfg, batch=256, steps=4):
         times.append(time.perf_counter() - t0)
     med = statistics.median(times[1:])
     return {"value": round(batch / med, 1), "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/cnf_oracle.train_step_cpu, {args.workload} B={batch}, dropout on, median of {steps} "
+            "sample": f"oracle/cnf_oracle.train_step_cpu, {workload} B={batch}, dropout on, median of {steps} "
                       f"steps after 1 warmup, {threads} threads, {med * 1e3:.0f} ms/step"}
 
 
-def main_wide(args):
-    """NLL-training samples/s of the wide workloads (trajectory_FC_large = configs[2], trajectory_LSTM_large =
-    configs[3]) per GPU, same step definition and timing contract as main()."""
-    world, rank, local = init_dist(args)
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
+def run_wide(workload, batch, steps, warmup, world, rank, device, graph=True, kernel_iters=20, cpu=True,
+             cpu_batch=256, cpu_steps=4):
+    """NLL-training samples/s of a wide workload (trajectory_FC_large = configs[2], trajectory_LSTM_large =
+    configs[3]) per GPU, same step definition and timing contract as main(). Returns rank 0's JSON object."""
     from bcnf_amd import CondRealNVP_v2
     from bcnf_amd.data import DeviceBatches
     from bcnf_amd.train import TrainStep
-    cfg = WORKLOADS[args.workload][0]
+    cfg = WORKLOADS[workload][0]
     torch.manual_seed(2024_03_25)
     model = CondRealNVP_v2.from_config(cfg).to(device)
     model.train()
     model.fused.set_seed(2024_03_25 + 7919 * rank)
-    data = DeviceBatches(max(16384, 4 * args.batch), args.batch, device, seed=2024_03_25 + rank)
-    step = TrainStep(model, lr=2e-4, capture=not args.no_graph)
+    data = DeviceBatches(max(16384, 4 * batch), batch, device, seed=2024_03_25 + rank)
+    step = TrainStep(model, lr=2e-4, capture=graph)
     step.broadcast_parameters()
     step.set_pool(data.y, data.traj)
-    batches = [data.next_indices() for _ in range(args.warmup + args.steps)]
-    step.set_epoch(torch.cat(batches), args.batch)
-    step.run_epoch(args.warmup)
-    step.prepare_epoch(args.steps)          # no graph capture inside the timed region
+    batches = [data.next_indices() for _ in range(warmup + steps)]
+    step.set_epoch(torch.cat(batches), batch)
+    step.run_epoch(warmup)
+    step.prepare_epoch(steps)          # no graph capture inside the timed region
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    vals = step.run_epoch(args.steps)
+    vals = step.run_epoch(steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -589,66 +640,87 @@ def main_wide(args):
         tt = torch.tensor([dt], device=device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-    value = world * args.batch * args.steps / dt
+    value = world * batch * steps / dt
     seen = ranks_seen(world, device)
-    kern = kernel_timing(model, data, args) if rank == 0 else {}
+    if rank != 0:
+        return None
+
+    class _A:                           # kernel_timing's argument shape
+        pass
+    ka = _A()
+    ka.kernel_iters = kernel_iters
+    kern = kernel_timing(model, data, ka)
+    B = batch
+    flop_step = WIDE_TRAIN_FLOP_PER_SAMPLE * B
+    achieved = flop_step / (dt / steps) / 1e12
+    fb_us = kern.get("forward", float("nan")) + kern.get("backward", float("nan"))
+    ach_fb = flop_step / (fb_us * 1e-6) / 1e12
+    alg = WIDE_ALG_BYTES_PER_SAMPLE * B
+    kw = cfg["model"]["kwargs"]
+    line = {
+        "metric": f"NLL-training samples/sec, {WIDE_NAMES[workload]}",
+        "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": steps,
+        "warmup": warmup, "ms_per_step": round(dt / steps * 1e3, 4), "ranks_seen": seen,
+        **({"shared_devices": True} if SHARED_DEVICES else {}),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic ballistic trajectories (bcnf_amd/data.py), device-resident",
+        "config": {"workload": f"{WIDE_NAMES[workload]} NLL training step", "batch_per_gpu": B,
+                   "global_batch": B * world, "parallelism": f"dp{world}", "hip_graph": graph,
+                   "n_blocks": kw["n_blocks"], "nested_sizes": kw["nested_sizes"],
+                   "n_conditions": kw["n_conditions"], "dropout": kw["dropout"]},
+        "last_loss": vals[-1][0] if vals else None,
+        "roofline": {"bound": "mfma", "kernel": "coupling stack forward + backward launches (fp32 MFMA GEMM chain + "
+                                                "link kernels; HIP events over each launch sequence)",
+                     "achieved": round(ach_fb, 3), "achieved_whole_step": round(achieved, 3),
+                     "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(ach_fb / PEAK_FP32_TFLOPS, 4),
+                     "frac_whole_step": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                     "avg_us": round(fb_us, 2), "flop_per_step": flop_step, "algorithmic_bytes": alg,
+                     "alg_hbm_frac": round(alg / (fb_us * 1e3) / PEAK_HBM_GBS, 4),
+                     "note": "flop = SURVEY §8d reference count (3 x forward flow, feature net excluded); the fold "
+                             "of the last feature Linear executes fewer condition-GEMM FLOPs than it counts"},
+        "kernels_us": {k: round(v, 2) for k, v in kern.items()},
+    }
+    del step, model, data
+    torch.cuda.empty_cache()
+    if cpu and world == 1:
+        line["cpu_baseline"] = cpu_baseline_wide(workload, cfg, batch=cpu_batch, steps=cpu_steps)
+    return line
+
+
+def main_wide(args):
+    world, rank, local = init_dist(args)
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    line = run_wide(args.workload, args.batch, args.steps, args.warmup, world, rank, device, graph=not args.no_graph,
+                    kernel_iters=args.kernel_iters, cpu=not args.no_cpu_baseline)
     if rank == 0:
-        B = args.batch
-        flop_step = WIDE_TRAIN_FLOP_PER_SAMPLE * B
-        achieved = flop_step / (dt / args.steps) / 1e12
-        fb_us = kern.get("forward", float("nan")) + kern.get("backward", float("nan"))
-        kw = cfg["model"]["kwargs"]
-        line = {
-            "metric": f"NLL-training samples/sec, {WIDE_NAMES[args.workload]}",
-            "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "ranks_seen": seen,
-            **({"shared_devices": True} if SHARED_DEVICES else {}),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic ballistic trajectories (bcnf_amd/data.py), device-resident",
-            "config": {"workload": f"trajectory_{args.workload} NLL training step", "batch_per_gpu": B,
-                       "global_batch": B * world, "parallelism": f"dp{world}", "hip_graph": not args.no_graph,
-                       "n_blocks": kw["n_blocks"], "nested_sizes": kw["nested_sizes"],
-                       "n_conditions": kw["n_conditions"], "dropout": kw["dropout"]},
-            "last_loss": vals[-1][0] if vals else None,
-            "roofline": {"bound": "mfma", "kernel": "coupling stack forward+backward (all launches)",
-                         "achieved": round(WIDE_TRAIN_FLOP_PER_SAMPLE * B / (fb_us * 1e-6) / 1e12, 3),
-                         "achieved_whole_step": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(WIDE_TRAIN_FLOP_PER_SAMPLE * B / (fb_us * 1e-6) / 1e12 / PEAK_FP32_TFLOPS, 4),
-                         "traffic": None, "flop_per_step": flop_step},
-            "kernels_us": {k: round(v, 2) for k, v in kern.items()},
-        }
-        if not args.no_cpu_baseline and world == 1 and args.workload == "fc_large":
-            line["cpu_baseline"] = cpu_baseline_wide(args, cfg)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def main_sample(args, n_draws=500):
-    """Posterior draws/s (BASELINE configs[4]): 500 draws for each of 1024 conditions (--batch) with trajectory_FC_small,
+def run_sample(n_cond, steps, warmup, world, rank, device, n_draws=500, cpu=True, cpu_conds=1024):
+    """Posterior draws/s (BASELINE configs[4]): 500 draws for each of `n_cond` conditions with trajectory_FC_small,
     the conditions sharded over the ranks (strong scaling of a fixed job; bcnf_amd/sampling.py), gathered at the end.
     One step = draw_sharded(500, all conditions) incl. feature net, device z draw, inverse, all-gather."""
-    world, rank, local = init_dist(args)
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
     from bcnf_amd import CondRealNVP_v2
     from bcnf_amd.data import simulate
     from bcnf_amd.sampling import draw_sharded, shard_range
     torch.manual_seed(2024_03_25)
     model = CondRealNVP_v2.from_config(FC_SMALL).to(device).eval()
-    _, traj = simulate(args.batch, seed=2024_03_25)
+    _, traj = simulate(n_cond, seed=2024_03_25)
     traj = torch.from_numpy(traj)
     traj = ((traj - traj.mean((0, 1))) / (traj.std((0, 1)) + 1e-6)).to(device)
     gen = torch.Generator(device=device).manual_seed(17 + rank)
     with model.fused.reuse_pack():
-        for _ in range(args.warmup):
+        for _ in range(warmup):
             draw_sharded(model, n_draws, traj, generator=gen)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(steps):
             out = draw_sharded(model, n_draws, traj, generator=gen)
         torch.cuda.synchronize()
         if world > 1:
@@ -659,7 +731,7 @@ def main_sample(args, n_draws=500):
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             dt = float(tt.item())
         # dominant kernel: the inverse of this rank's n_draws x N_local rows, HIP events on the launch stream
-        a, b = shard_range(args.batch, rank, world)
+        a, b = shard_range(n_cond, rank, world)
         with torch.no_grad():
             h = model.feature_network_stack(traj[a:b]).contiguous()
             rows = n_draws * (b - a)
@@ -673,36 +745,53 @@ def main_sample(args, n_draws=500):
             e1.record()
             torch.cuda.synchronize()
             inv_us = e0.elapsed_time(e1) * 1e3 / 5
-    value = n_draws * args.batch * args.steps / dt
+    value = n_draws * n_cond * steps / dt
     seen = ranks_seen(world, device)
+    if rank != 0:
+        return None
+    flop = FWD_FLOP_PER_SAMPLE * rows
+    achieved = flop / (inv_us * 1e-6) / 1e12
+    # the reference repeats each condition per draw, so its per-row MLP includes the condition projection
+    # (nb x 16 x C MACs); here k_hp computes it once per condition and k_inverse_mfma runs the rest
+    proj_macs = 32 * 16 * 80
+    flop_exec = 2 * ((FWD_FLOP_PER_SAMPLE // 2 - proj_macs) * rows + proj_macs * (b - a))
+    # per-block minimum of the eval inverse (z in, y out per block, projection read per row; SURVEY §8d forward form)
+    alg = FWD_ALG_BYTES_PER_SAMPLE * rows
+    line = {
+        "metric": "posterior draws/sec (inverse sampling, 500 draws x 1024 conditions), trajectory_FC_small",
+        "value": round(value, 1), "unit": "draws/s", "n_gpus": world, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(dt / steps * 1e3, 4), "ranks_seen": seen, "higher_is_better": True,
+        **({"shared_devices": True} if SHARED_DEVICES else {}),
+        "scaling": "strong",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic ballistic trajectories as conditions, device z",
+        "config": {"workload": "CondRealNVP_v2.sample-equivalent draw (configs[4])", "conditions": n_cond,
+                   "draws_per_condition": n_draws, "parallelism": f"condition shards x{world}",
+                   "output": tuple(out.shape)},
+        "roofline": {"bound": "mfma", "kernel": "k_inverse_mfma (this rank's rows)", "achieved": round(achieved, 3),
+                     "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                     "traffic": _pmc_traffic("k_inverse_mfma"), "avg_us": round(inv_us, 2), "flop_per_launch": flop,
+                     "flop_executed_per_launch": flop_exec, "algorithmic_bytes": alg,
+                     "alg_hbm_frac": round(alg / (inv_us * 1e3) / PEAK_HBM_GBS, 4),
+                     "frac_executed": round(flop_exec / (inv_us * 1e-6) / 1e12 / PEAK_FP32_TFLOPS, 4),
+                     **pmc_utilisation("k_inverse_mfma", inv_us),
+                     "note": "flop_per_launch counts the reference's per-row work (condition projection "
+                             "repeated per draw); flop_executed: projection once per condition (k_hp) + "
+                             "k_inverse_mfma (fp32 MFMA dense layers, VALU GELU / tanh / coupling)"},
+    }
+    del model
+    torch.cuda.empty_cache()
+    if cpu and world == 1:
+        line["cpu_baseline"] = cpu_baseline_sample(n_draws, cpu_conds)
+    return line
+
+
+def main_sample(args, n_draws=500):
+    world, rank, local = init_dist(args)
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    line = run_sample(args.batch, args.steps, args.warmup, world, rank, device, n_draws=n_draws,
+                      cpu=not args.no_cpu_baseline)
     if rank == 0:
-        flop = FWD_FLOP_PER_SAMPLE * rows
-        achieved = flop / (inv_us * 1e-6) / 1e12
-        # the reference repeats each condition per draw, so its per-row MLP includes the condition projection
-        # (nb x 16 x C MACs); here k_hp computes it once per condition and k_inverse_mfma runs the rest
-        proj_macs = 32 * 16 * 80
-        flop_exec = 2 * ((FWD_FLOP_PER_SAMPLE // 2 - proj_macs) * rows + proj_macs * (b - a))
-        line = {
-            "metric": "posterior draws/sec (inverse sampling, 500 draws x 1024 conditions), trajectory_FC_small",
-            "value": round(value, 1), "unit": "draws/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 4), "ranks_seen": seen, "higher_is_better": True,
-            **({"shared_devices": True} if SHARED_DEVICES else {}),
-            "scaling": "strong",
-            "vs_baseline": None, "dtype": "f32", "data": "synthetic ballistic trajectories as conditions, device z",
-            "config": {"workload": "CondRealNVP_v2.sample-equivalent draw (configs[4])", "conditions": args.batch,
-                       "draws_per_condition": n_draws, "parallelism": f"condition shards x{world}",
-                       "output": tuple(out.shape)},
-            "roofline": {"bound": "mfma", "kernel": "k_inverse_mfma (this rank's rows)", "achieved": round(achieved, 3),
-                         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                         "traffic": None, "avg_us": round(inv_us, 2), "flop_per_launch": flop,
-                         "flop_executed_per_launch": flop_exec,
-                         "frac_executed": round(flop_exec / (inv_us * 1e-6) / 1e12 / PEAK_FP32_TFLOPS, 4),
-                         "note": "flop_per_launch counts the reference's per-row work (condition projection "
-                                 "repeated per draw); flop_executed: projection once per condition (k_hp) + "
-                                 "k_inverse_mfma (fp32 MFMA dense layers, VALU GELU / tanh / coupling)"},
-        }
-        if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline_sample()
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

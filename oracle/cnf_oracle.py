@@ -39,6 +39,9 @@ class StackSpec:
     two_way: bool = False
     feature_sizes: list = field(default_factory=list)  # FullyConnected feature net sizes ([] = identity)
     feature_dropout: float = 0.0
+    # LSTM feature net (feature_network.py:148-178); lstm = (input_size, hidden_size, num_layers, bidirectional,
+    # pool_dim) replaces the FullyConnected one when set
+    lstm: tuple | None = None
 
     @property
     def Da(self):
@@ -122,7 +125,10 @@ def coupling_inverse(sd, prefix, spec, z, h, training=False, gen=None):
 
 
 def feature_forward(sd, spec, cond):
-    """FeatureNetworkStack with ConcatenateCondition + FullyConnectedFeatureNetwork (feature_network.py:46-145)."""
+    """FeatureNetworkStack with ConcatenateCondition + FullyConnectedFeatureNetwork (feature_network.py:46-145), or
+    + LSTMFeatureNetwork when spec.lstm is set."""
+    if spec.lstm is not None:
+        return lstm_feature_forward(sd, spec, cond)
     x = cond.reshape(cond.shape[0], -1)
     fs = spec.feature_sizes
     if len(fs) < 2:
@@ -136,6 +142,19 @@ def feature_forward(sd, spec, cond):
         if li < n - 1:
             x = F.gelu(x)
     return x
+
+
+def lstm_feature_forward(sd, spec, cond, prefix="feature_network_stack.feature_networks.1"):
+    """LSTMFeatureNetwork.forward (feature_network.py:167-178): batch_first LSTM -> Linear -> mean pooling over
+    `pool_dim` (the reference pools over dim 0, the batch axis; pool_dim=1 is the documented fix). The LSTM runs as
+    torch.nn.LSTM with the state_dict's tensors bound functionally, so gradients reach sd's leaves. Mean pooling only
+    (every shipped LSTM config)."""
+    inp, hid, nl, bi, pool_dim = spec.lstm
+    lstm = torch.nn.LSTM(inp, hid, num_layers=nl, bidirectional=bi, batch_first=True)
+    params = {k[len(prefix) + 6:]: v for k, v in sd.items() if k.startswith(prefix + ".lstm.")}
+    x, _ = torch.func.functional_call(lstm, params, (cond,))
+    x = F.linear(x, sd[prefix + ".linear.weight"], sd[prefix + ".linear.bias"])
+    return x.mean(dim=pool_dim)
 
 
 def model_forward(sd, spec, y, h, training=False, gen=None):

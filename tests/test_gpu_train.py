@@ -313,6 +313,40 @@ def test_captured_step_with_ragged_batches_equals_eager(g1):
         assert torch.equal(a, b)
 
 
+def test_epoch_with_ragged_remainder_equals_eager_loop(g1):
+    """An epoch order walked by run_epoch, then the epoch's ragged remainders (1 and 7 samples) through
+    step_indexed, then run_epoch again == an eager TrainStep fed the same batches one by one: the remainders run
+    eagerly without advancing the device cursor or writing an epoch history row (logged values, parameters, RNG
+    offset and cursor bit for bit)."""
+    from bcnf_amd.train import TrainStep
+    gen = torch.Generator().manual_seed(23)
+    py, pt = _epoch_pool(gen)
+    perm = torch.randperm(768, generator=gen)
+    order, rem1, rem7 = perm[:4 * 128].to(DEV), perm[600:601].to(DEV), perm[601:608]
+    res = []
+    for epoch in (False, True):
+        m = fresh_model(g1, train=True)
+        m.fused.set_seed(13)
+        st = TrainStep(m, lr=2e-4, capture=epoch)
+        st.set_pool(py, pt)
+        batches = list(order.view(4, 128))
+        if epoch:
+            st.set_epoch(order, 128)
+            vals = st.run_epoch()
+            vals += [st.step_indexed(rem1), st.step_indexed(rem7)]     # rem7 from the host: checked there
+            vals += st.run_epoch()
+            cursor = st._epoch[1].item()
+        else:
+            vals = [st.step_indexed(b) for b in batches + [rem1, rem7] + batches]
+            cursor = 0
+        res.append((vals, [p.detach().clone() for p in m.parameters()], m.fused.rng_state().clone(), cursor))
+    (v0, p0, r0, c0), (v1, p1, r1, c1) = res
+    assert len(v1) == 10 and v0 == v1
+    assert c0 == c1 == 0 and torch.equal(r0, r1)
+    for a, b in zip(p0, p1):
+        assert torch.equal(a, b)
+
+
 def test_step_indexed_rejects_out_of_range_indices(g1):
     from bcnf_amd.train import TrainStep
     m = fresh_model(g1, train=True)

@@ -54,8 +54,30 @@ def test_variant_models_build_with_reference_layout(name):
     assert all(np.array_equal(q.numpy(), ref[k]) for k, q in zip([k for k in ref if k.endswith("orthonormal_matrix")], qs))
 
 
-def test_variant_models_refuse_cpu_tensors():
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_variant_models_refuse_cpu_tensors(name):
+    """A model left on the CPU raises a clean RuntimeError on every path -- the FFT path included, whose weight fold
+    would otherwise hand host pointers to the HIP GEMM (no kernel runs here)."""
     from bcnf_amd import CondRealNVP_v2
-    m = CondRealNVP_v2.from_config(copy.deepcopy(CASES["anyglu"][0]))
+    m = CondRealNVP_v2.from_config(copy.deepcopy(CASES[name][0]))
     with pytest.raises(RuntimeError):
-        m.forward(torch.randn(3, 19), torch.randn(3, 12))
+        m.forward(torch.randn(3, 19), torch.randn(3, 12), log_det_J=True)
+    with pytest.raises(RuntimeError):
+        m.inverse(torch.randn(3, 19), torch.randn(3, 12))
+
+
+def test_anyglu_identity_activation_builds():
+    """trajectory_SFrExp_LSTM_SiGLU_2_large.yaml: layer AnyGLU with activation Identity -- the layerwise path runs
+    whatever activation module LayerFactory builds, so the model builds (only the fused / fft paths need GELU)."""
+    from bcnf_amd import CondRealNVP_v2
+    cfg = copy.deepcopy(CASES["anyglu"][0])
+    cfg["model"]["kwargs"]["activation"] = "Identity"
+    m = CondRealNVP_v2.from_config(cfg)
+    assert type(m.fused).__name__ == "_LayerwiseStack"
+    assert any(type(mod).__name__ == "Identity" for mod in m.modules())
+    with pytest.raises(NotImplementedError):
+        m.flat_parameters()
+    cfg["model"]["kwargs"]["layer"] = "Linear"
+    cfg["model"]["kwargs"].pop("layer_kwargs")
+    with pytest.raises(NotImplementedError):
+        CondRealNVP_v2.from_config(cfg)          # the fused Linear kernels implement GELU only
