@@ -20,12 +20,13 @@ LIB_PATH = os.environ.get("BCNF_AMD_LIB") or os.path.join(_HERE, "libbcnf_amd.so
 MAX_HIDDEN = 8
 
 OK, ERR_ARG, ERR_UNSUPPORTED, ERR_HIP = 0, 1, 2, 3
+ERR_HIP_BASE = 1000          # include/bcnf_amd.h: BCNF_ERR_HIP_BASE + hipError_t
 
 # Every symbol include/bcnf_amd.h declares (checked by tests/test_native_abi.py).
 EXPORTS = (
     "bcnf_stack_supported", "bcnf_param_count", "bcnf_packed_bytes", "bcnf_workspace_bytes",
     "bcnf_slab_bytes", "bcnf_pack_params", "bcnf_stack_forward", "bcnf_stack_backward",
-    "bcnf_stack_inverse", "bcnf_grad_reduce", "bcnf_status_string", "bcnf_last_hip_error",
+    "bcnf_stack_inverse", "bcnf_grad_reduce", "bcnf_status_string",
     "bcnf_nll_forward", "bcnf_nll_backward", "bcnf_grad_partials", "bcnf_adam_step", "bcnf_adam_step_bookkeep",
     "bcnf_grad_sumsq",
     "bcnf_clip_grad_norm", "bcnf_linear_forward", "bcnf_linear_work_bytes", "bcnf_linear_backward",
@@ -35,7 +36,7 @@ EXPORTS = (
     "bcnf_wide_supported", "bcnf_wide_param_count", "bcnf_wide_packed_bytes", "bcnf_wide_workspace_bytes", "bcnf_wide_inverse_scratch_bytes",
     "bcnf_wide_pack", "bcnf_wide_forward", "bcnf_wide_nll_finalize", "bcnf_wide_backward", "bcnf_wide_inverse",
     "bcnf_wide_fold_prepare", "bcnf_wide_fold_forward", "bcnf_wide_fold_backward", "bcnf_wide_proj_rows",
-    "bcnf_wide_gemm_test", "bcnf_wide_force_tiling", "bcnf_wide_debug_phases", "bcnf_rank_count",
+    "bcnf_wide_gemm_test", "bcnf_rank_count",
     "bcnf_guard_check_global",
 )
 MAX_TENSORS = 48
@@ -51,6 +52,7 @@ class BcnfStackDesc(ctypes.Structure):
         ("act_norm", ctypes.c_int32),
         ("two_way", ctypes.c_int32),
         ("dropout", ctypes.c_float),
+        ("gemm_tiling", ctypes.c_int32),      # wide family: 0 = cost model, t + 1 forces tiling t (per call)
     ]
 
 
@@ -173,12 +175,9 @@ def _bind(lib):
         "bcnf_wide_backward": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64, _vp, _vp, _vp, _vp,
                                       _vp]),
         "bcnf_wide_inverse": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i32, _vp, _vp, _vp]),
-        "bcnf_wide_force_tiling": (_i32, [_i32]),
-        "bcnf_wide_debug_phases": (_i32, [_vp]),
         "bcnf_rank_count": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _vp]),
         "bcnf_wide_gemm_test": (_i32, [_i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp]),
         "bcnf_status_string": (ctypes.c_char_p, [_i32]),
-        "bcnf_last_hip_error": (_i32, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -206,7 +205,7 @@ def check(rc: int, what: str) -> None:
     if rc != OK:
         L = lib()
         msg = L.bcnf_status_string(rc).decode()
-        extra = f" (hipError {L.bcnf_last_hip_error()})" if rc == ERR_HIP else ""
+        extra = f" (hipError {rc - ERR_HIP_BASE})" if rc >= ERR_HIP_BASE else ""
         raise RuntimeError(f"bcnf_amd: {what} failed: {msg}{extra}")
 
 

@@ -9,24 +9,19 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/bcnf_amd.h"
+
 #define BCNF_WG 256
 #define BCNF_ROWS 16           // samples per workgroup
 #define BCNF_TSTRIDE 17        // padded row stride of the [16 samples][16] LDS tiles (bank spread)
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-// Last HIP error seen by any entry point of the library (bcnf_last_hip_error), shared by all
-// translation units.
+// HIP failures travel in the status code only (BCNF_ERR_HIP_BASE + the hipError_t, include/bcnf_amd.h): the library
+// keeps no error state between calls.
 namespace bcnf_rt {
-extern thread_local int last_hip;
-inline int launched() {
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) {
-    last_hip = (int)e;
-    return 3;   // BCNF_ERR_HIP
-  }
-  return 0;
-}
+inline int hip_status(hipError_t e) { return e == hipSuccess ? 0 : BCNF_ERR_HIP_BASE + (int)e; }
+inline int launched() { return hip_status(hipGetLastError()); }
 }  // namespace bcnf_rt
 
 // dst0[r] = src0[idx[r]] (cols0 floats), dst1[r] = src1[idx[r]] (cols1 floats), one launch for both;
@@ -283,7 +278,7 @@ __device__ __forceinline__ float tanh_bf(float a) {
 // Branch-free; no cancellation for x < 0. In fp32: |GELU error| < 3.9e-7, |GELU' error| < 3.6e-7 against the
 // double-precision function (the fp32 0.5 x (1 + erf(x/sqrt2)) of the reference: < 4.5e-7). Replaces (r02x) the
 // Numerical Recipes erfcc form t exp(-z^2 + P9(t)), which took a second exp and three more FMAs per call: the
-// GELUs are ~18% of the FC_small forward's compute chain (BCNF_EXP & 2048: 64.4 -> 52.5 us without them).
+// GELUs are ~18% of the FC_small forward's compute chain (an r02 experiment build with GELU replaced by x/2: 64.4 -> 52.5 us).
 __device__ __forceinline__ float gelu_tail(float x, float& ez) {   // Phi(-|x|); ez = exp(-x^2 / 2)
   const float t = __builtin_amdgcn_rcpf(fmaf(2.616295218e-01f, fabsf(x), 1.0f));   // p / sqrt2
   float q = -7.295463979e-02f;

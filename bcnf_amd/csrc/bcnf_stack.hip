@@ -20,17 +20,14 @@
 
 #include <mutex>
 
-// Experiment switches for A/B timing only (tools/exp_variants.sh builds separate libraries; results of a
-// nonzero BCNF_EXP are NOT valid): 1 = records read by row 0 only, 8 = no dropout RNG in the forward, 2048 =
-// GELU -> x/2 in the forward, 4096 = no orthonormal mix in the forward, 8192 = no activation-record stores in
-// the forward.
-#ifndef BCNF_EXP
-#define BCNF_EXP 0
+// Phase stamps (s_memtime per phase of workgroup 0's first compute and helper waves) exist only in a diagnostic
+// build with -DBCNF_PHASE_STAMPS (tools/exp_variants.sh); the shipped library has no stamp code, no debug globals
+// and no debug exports.
+#ifdef BCNF_PHASE_STAMPS
+#define BCNF_STAMPS 1
+#else
+#define BCNF_STAMPS 0
 #endif
-
-namespace bcnf_rt {
-thread_local int last_hip = 0;
-}
 
 namespace {
 
@@ -633,20 +630,12 @@ __global__ __launch_bounds__(BCNF_WG) void k_dh(BcnfLayout L, const float* __res
   dh_body(L, pk, d1, B, dh, blockIdx.x, blockIdx.y, smem);
 }
 
-// BCNF_EXP & 32768: per-workgroup s_memrealtime stamps of the split-K (start, operands loaded, LDS staged, MFMAs done,
-// stored) -> g_sk[workgroup][5] (bcnf_debug_splitk)
-__device__ unsigned long long g_sk[1024 * 5];
-
 // dW1h split-K partials: 64 kj (4 blocks, one per wave) x all columns over one split of KC rows.
 // grid = (ceil(nb/4), splits); work[s][k][16][Cp]
 template <bool VEC, int BPW = 4>
 __device__ __forceinline__ void dw1h_body(const BcnfLayout& L, const float* __restrict__ d1, const float* __restrict__ h,
                                           long long B, int rows_per_split, float* __restrict__ work, int bx, int by,
                                           float* __restrict__ smem, int ones = -1) {
-  const int sk_wg = (int)(blockIdx.x + gridDim.x * blockIdx.y);
-#define SKS(i)                                                                                   \
-  if ((BCNF_EXP & 32768) && threadIdx.x == 0 && sk_wg < 1024) g_sk[sk_wg * 5 + (i)] = __builtin_amdgcn_s_memrealtime();
-  SKS(0)
   const int hs = bstride16(L.Cp);
   // BPW blocks per workgroup: 4 (one per wave, every column tile) or 2 (two waves per block, half the column
   // tiles each: twice the workgroups, LDS for two resident per CU)
@@ -677,10 +666,6 @@ __device__ __forceinline__ void dw1h_body(const BcnfLayout& L, const float* __re
     floatx4 rv[2][8];
 #pragma unroll
     for (int half = 0; half < 2; ++half) load_rows64<VEC>(h, m1, L.C, L.ldh, m0 + 64 * half, 0, rv[half], ones);
-    if (BCNF_EXP & 32768) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      SKS(1)
-    }
 #pragma unroll
     for (int kk = 0; kk < BPW; ++kk) {
       const float m = (ok && k0 + kk < L.nb) ? 1.f : 0.f;
@@ -712,7 +697,6 @@ __device__ __forceinline__ void dw1h_body(const BcnfLayout& L, const float* __re
     }
   }
   __syncthreads();
-  SKS(2)
   const int kw = BPW == 4 ? wave : wave >> 1;
   const int k = k0 + kw;
   const int nh = BPW == 4 ? NC16 : (NC16 + 1) >> 1;
@@ -734,17 +718,11 @@ __device__ __forceinline__ void dw1h_body(const BcnfLayout& L, const float* __re
       }
     }
     acc += acc1;
-    if ((BCNF_EXP & 32768) && n == n_hi - 1) SKS(3)
     if (k < L.nb) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) o[(long long)(4 * lq + i) * L.Cp + 16 * n + lr] = acc[i];
     }
   }
-  if (BCNF_EXP & 32768) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    SKS(4)
-  }
-#undef SKS
 }
 
 template <bool VEC>
@@ -1019,17 +997,6 @@ __device__ __forceinline__ void ld_rec(float* __restrict__ rr, const float* __re
   }
 }
 
-template <int LO, int HI>
-__device__ __forceinline__ void ld_rec_exp(float* __restrict__ rr, const float* __restrict__ R) {
-  if (BCNF_EXP & 1) {
-#pragma unroll
-    for (int i = LO; i < HI; ++i) rr[i] = 0.f;
-    if ((threadIdx.x & 48) == 0) ld_rec<LO, HI>(rr, R);
-  } else {
-    ld_rec<LO, HI>(rr, R);
-  }
-}
-
 // Nested MLP forward on the row layout (cnf.py:98-107) from a register-resident forward record.
 // Input x (layer-1 y-part operand) and hp (its condition part + bias, from k_hp); returns t and s'
 // (pre-tanh). KEEP: also the masked activations and masked GELU derivatives for the backward's record.
@@ -1044,10 +1011,7 @@ __device__ __forceinline__ void mlp_forward(const BcnfLayout& L, const float* __
     const float bias = (l == 1) ? hp : w[16];            // hp = h W1h^T + b1 (k_hp)
     const float pre = rot16(a, w, bias);
     const float m = drop ? (((bits >> (l - 1)) & 1u) ? L.keep_scale : 0.f) : 1.f;
-    if (BCNF_EXP & 2048) {
-      a = pre * 0.5f * m;
-      if (KEEP) { act[l - 1] = a; gd[l - 1] = 0.5f * m; }
-    } else if (KEEP) {
+    if (KEEP) {
       float g, dg;
       gelu_fg(pre, g, dg);
       a = g * m;
@@ -1074,7 +1038,9 @@ __device__ __forceinline__ void mix(const float* __restrict__ rq, float a, float
 // ------------------------------------------------------------------------------------------------
 // Forward
 // ------------------------------------------------------------------------------------------------
-__device__ unsigned long long g_phase[16];   // BCNF_EXP & 256 phase stamps (bcnf_debug_phases)
+#if BCNF_STAMPS
+__device__ unsigned long long g_phase[16];   // phase stamps (bcnf_debug_phases), diagnostic build only
+#endif
 
 // Condition projection operands of the forward (the y-independent part of Linear 1, cnf.py:98-107 with the
 // condition columns): HP[b][16k + j] = sum_c h[b][c] W1hC[c][16k + j] + b1c[16k + j]; on the folded path h = x and
@@ -1120,10 +1086,10 @@ __global__ __launch_bounds__(FWD_WG) void k_forward(BcnfLayout L, const float* _
   const long long bc = b < B ? b : B - 1;                       // rows past the batch replay the last sample
   uint64_t seed = 0, off = 0;
   if (DROP) { seed = rng[0]; off = rng[1]; }
-  // BCNF_EXP & 256: per-phase cycles of workgroup 0's wave 0 (compute) and wave 4 (helper) -> g_phase[8..]
-  unsigned long long ph_t = (BCNF_EXP & 256) ? __builtin_amdgcn_s_memtime() : 0ULL, ph_acc[3] = {0, 0, 0};
+  // diagnostic build: per-phase cycles of workgroup 0's wave 0 (compute) and wave 4 (helper) -> g_phase[8..]
+  unsigned long long ph_t = BCNF_STAMPS ? __builtin_amdgcn_s_memtime() : 0ULL, ph_acc[3] = {0, 0, 0};
 #define PHF(i)                                                                                   \
-  if (BCNF_EXP & 256) {                                                                          \
+  if (BCNF_STAMPS) {                                                                             \
     const unsigned long long _t = __builtin_amdgcn_s_memtime();                                  \
     ph_acc[i] += _t - ph_t;                                                                      \
     ph_t = _t;                                                                                   \
@@ -1150,7 +1116,7 @@ __global__ __launch_bounds__(FWD_WG) void k_forward(BcnfLayout L, const float* _
 #pragma unroll
       for (int t = 0; t < HP_SMAX; ++t) wb[t] = (t < S) ? wcol[(long long)4 * t * P.NKp + 16 * k] : 0.f;
       uint32_t bits = 0xffu;
-      if (DROP && !(BCNF_EXP & 16384)) bits = dropout_bits(L, seed, off, bc, k, j, 0u);   // 16384: no helper Philox
+      if (DROP) bits = dropout_bits(L, seed, off, bc, k, j, 0u);
       const float bias = (hw == 0) ? P.b1c[16 * k + lr] : 0.f;
       floatx4 acc = {bias, bias, bias, bias};
 #pragma unroll
@@ -1182,11 +1148,10 @@ __global__ __launch_bounds__(FWD_WG) void k_forward(BcnfLayout L, const float* _
     for (int k = 0; k < nb; ++k) {
       const int cur = k & 1;
       float rr[RecF<NH>::USED];
-      ld_rec_exp<0, RecF<NH>::USED>(rr, rec + cur * RING + j * L.RF);
+      ld_rec<0, RecF<NH>::USED>(rr, rec + cur * RING + j * L.RF);
       const float* hq = hpb + cur * 1024 + tid;
       const float hpk = ((hq[0] + hq[256]) + hq[512]) + hq[768];
-      uint32_t bits = bitb[cur * 256 + tid];
-      if (BCNF_EXP & 8) bits = 0xffu;
+      const uint32_t bits = bitb[cur * 256 + tid];
       const float xa = fmaf(rr[0], ya, rr[1]);          // ActNorm (cnf.py:349)
       const float xb = fmaf(rr[2], yb, rr[3]);
       float T, Sp;
@@ -1195,7 +1160,7 @@ __global__ __launch_bounds__(FWD_WG) void k_forward(BcnfLayout L, const float* _
       const float Sv = tanh_bf(Sp);                      // cnf.py:107
       const float zb = fmaf(exp_fast(Sv), xb, T);        // cnf.py:179
       ldj += Sv;                                         // cnf.py:190
-      if (SAVE && !(BCNF_EXP & 8192)) {                  // coalesced across the wave
+      if (SAVE) {                                         // coalesced across the wave
         ar[AR::S] = Sv;
         ar[AR::YA] = ya;
         ar[AR::YB] = yb;
@@ -1207,7 +1172,6 @@ __global__ __launch_bounds__(FWD_WG) void k_forward(BcnfLayout L, const float* _
 #pragma unroll
         for (int i = 0; i < AR::AR1; ++i) d1p[i * BCNF_WG] = ar[4 * AR::AR4 + i];
       }
-      if (BCNF_EXP & 4096) { ya = xa; yb = zb; } else
       mix(rr + RecF<NH>::Q, xa, zb, ya, yb);             // y @ Q (cnf.py:335); identity after the last block
       PHF(1)
       __syncthreads();
@@ -1221,8 +1185,10 @@ __global__ __launch_bounds__(FWD_WG) void k_forward(BcnfLayout L, const float* _
     if (logp && j == 0) logp[bc] = -(0.5f * q2 - ltot) - 0.5f * (float)D * 1.8378770664093454836f;
     if (nll_part && j == 0) rec[s] = (b < B) ? 0.5f * q2 - ltot : 0.f;   // rec: free after the last barrier
   }
-  if ((BCNF_EXP & 256) && SAVE && blockIdx.x == 0 && (threadIdx.x == 0 || threadIdx.x == BCNF_WG))
+#if BCNF_STAMPS
+  if (SAVE && blockIdx.x == 0 && (threadIdx.x == 0 || threadIdx.x == BCNF_WG))
     for (int i = 0; i < 3; ++i) g_phase[8 + (helper ? 4 : 0) + i] = ph_acc[i];
+#endif
 #undef PHF
   if (nll_part) {   // per-workgroup partial of inn_nll_loss (utils.py:40-46); reduced by nll_finalize
     __syncthreads();
@@ -1349,7 +1315,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse(BcnfLayout L, const float* 
 // as the accumulator), hidden layers and the T / S heads run on the matrix pipe; the VALU keeps GELU, tanh, exp
 // and the coupling / ActNorm inverse (row-layout k_inverse: ~380 VALU instructions per block per 4 samples, 95% of
 // VALU issue in profiles/r02y_k_inverse_pmc_insts.csv). Same sums as k_inverse in a different association order.
-constexpr int INV_M_SPW = 16 * ((BCNF_EXP & 4194304) ? 2 : 1);   // samples per wave
+constexpr int INV_M_SPW = 16;                       // samples per wave
 constexpr int INV_M_WG = 512;                       // 8 waves share one record ring (2 x 16 KB): 4 workgroups per CU
 constexpr int INV_M_SPB = INV_M_SPW * (INV_M_WG / 64);
 template <int NH>
@@ -1391,22 +1357,14 @@ __device__ __forceinline__ void gelu4(floatx4& a) {
 template <int NH>
 __device__ __forceinline__ floatx4 inv_mv(floatx4 acc, const float* __restrict__ slot, const int (&aoff)[4], int off,
                                           const floatx4& x) {
-  if (BCNF_EXP & 524288) {                          // two accumulator chains (t = 0, 1 | t = 2, 3)
-    floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
-    acc = mfma4(slot[aoff[0] + off], x[0], acc);
-    acc1 = mfma4(slot[aoff[2] + off], x[2], acc1);
-    acc = mfma4(slot[aoff[1] + off], x[1], acc);
-    acc1 = mfma4(slot[aoff[3] + off], x[3], acc1);
-    return acc + acc1;
-  }
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc = mfma4(slot[aoff[t] + off], x[t], acc);
   return acc;
 }
-constexpr int INV_M_OCC = (BCNF_EXP & 1048576) ? 5 : (BCNF_EXP & 2097152) ? 8 : (BCNF_EXP & 4194304) ? 3 : 6;   // min waves per SIMD (80 VGPRs, no spills)
+constexpr int INV_M_OCC = 6;   // min waves per SIMD (80 VGPRs, no spills; 5 and 8 measured slower)
 
-// G independent 16-sample groups per wave (BCNF_EXP & 4194304: G = 2) interleave their MFMA chains and GELUs.
-constexpr int INV_M_G = (BCNF_EXP & 4194304) ? 2 : 1;
+// G independent 16-sample groups per wave interleaving their MFMA chains and GELUs (G = 2 measured neutral).
+constexpr int INV_M_G = 1;
 
 template <int G, int KS>
 __device__ __forceinline__ void inv_mv_g(floatx4 (&acc)[G], const float* __restrict__ slot, const int* ao, int off,
@@ -1676,10 +1634,10 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
   const int t8 = (int)threadIdx.x & (BCNF_WG - 1);
   const int j = t8 & 15, s = t8 >> 4;
   const int tix = tile_ix(s, j);
-  // BCNF_EXP & 256: per-phase cycles of workgroup 0's wave 0 (compute) and wave 4 (helper) -> g_phase
-  unsigned long long ph_t = (BCNF_EXP & 256) ? __builtin_amdgcn_s_memtime() : 0ULL, ph_acc[4] = {0, 0, 0, 0};
+  // diagnostic build: per-phase cycles of workgroup 0's wave 0 (compute) and wave 4 (helper) -> g_phase
+  unsigned long long ph_t = BCNF_STAMPS ? __builtin_amdgcn_s_memtime() : 0ULL, ph_acc[4] = {0, 0, 0, 0};
 #define PHS(i)                                                                                   \
-  if (BCNF_EXP & 256) {                                                                          \
+  if (BCNF_STAMPS) {                                                                             \
     const unsigned long long _t = __builtin_amdgcn_s_memtime();                                  \
     ph_acc[i] += _t - ph_t;                                                                      \
     ph_t = _t;                                                                                   \
@@ -1756,7 +1714,7 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
       PHS(0)
       prep_load(Pnext, k >= 2 ? k - 2 : 0);             // unconditional (clamped): no branch around loads in flight
       PHS(1)
-      if (k + 1 < nb && !(BCNF_EXP & 32))
+      if (k + 1 < nb)
         bwd_grad_jobs<NH>(dT + ((k + 1) & 1) * J::ND * TILE, aT + ((k + 1) % 3) * J::NA * TILE,
                           slab + (long long)(k + 1) * J::BLK, hw);
       PHS(2)
@@ -1859,8 +1817,10 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
       if (j < Db) dy[b * D + Da + j] = gyb;
     }
   }
-  if ((BCNF_EXP & 256) && blockIdx.x == 0 && (threadIdx.x == 0 || threadIdx.x == BCNF_WG))
+#if BCNF_STAMPS
+  if (blockIdx.x == 0 && (threadIdx.x == 0 || threadIdx.x == BCNF_WG))
     for (int i = 0; i < 4; ++i) g_phase[(helper ? 4 : 0) + i] = ph_acc[i];
+#endif
 #undef PHS
   if (loss_out && blockIdx.x == 0) {                 // deferred NLL reduction of the forward
     __syncthreads();                                  // (the helpers' last jobs have read the tiles)
@@ -2039,10 +1999,7 @@ int launch_lds(K kernel, size_t& lds) {
   for (int i = 0; i < g_attr_n; ++i)
     if (g_attr_fn[i] == fn && g_attr_lds[i] >= lds) return BCNF_OK;
   const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) {
-    bcnf_rt::last_hip = (int)e;
-    return BCNF_ERR_HIP;
-  }
+  if (e != hipSuccess) return bcnf_rt::hip_status(e);
   int slot = -1;
   for (int i = 0; i < g_attr_n; ++i)
     if (g_attr_fn[i] == fn) slot = i;
@@ -2113,10 +2070,10 @@ int inv_dispatch(const BcnfLayout& L, const float* pk, const float* zin, const f
                  const int64_t* ci, long long N, float* y, bool drop, const uint64_t* rng, hipStream_t st) {
   if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
   int rc;
-  if (!drop && L.RF == inv_m_rf<NH>() && !(BCNF_EXP & 262144)) {               // eval: matrix-core inverse (BCNF_EXP & 262144: row layout)
+  if (!drop && L.RF == inv_m_rf<NH>()) {               // eval: matrix-core inverse
     size_t lds_m = sizeof(float) * (size_t)(2 * RING);
     const dim3 grid_m((unsigned)((N + INV_M_SPB - 1) / INV_M_SPB));
-    if (L.Da <= 12 && L.Db <= 12 && !(BCNF_EXP & 8388608)) {
+    if (L.Da <= 12 && L.Db <= 12) {
       if ((rc = launch_lds(k_inverse_mfma<NH, true>, lds_m))) return rc;
       hipLaunchKernelGGL((k_inverse_mfma<NH, true>), grid_m, dim3(INV_M_WG), lds_m, st, L, pk, zin, hp, R, ci, N, y);
     } else {
@@ -2548,22 +2505,14 @@ const char* bcnf_status_string(int status) {
     case BCNF_OK: return "ok";
     case BCNF_ERR_ARG: return "invalid argument";
     case BCNF_ERR_UNSUPPORTED: return "unsupported stack shape for the fused kernel family";
-    case BCNF_ERR_HIP: return "HIP launch error";
-    default: return "unknown status";
+    default: return status >= BCNF_ERR_HIP_BASE ? hipGetErrorString((hipError_t)(status - BCNF_ERR_HIP_BASE))
+                                                 : "unknown status";
   }
 }
 
-int bcnf_last_hip_error(void) { return bcnf_rt::last_hip; }
-
-#if BCNF_EXP & 32768
-int bcnf_debug_splitk(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sk), sizeof(g_sk)) == hipSuccess ? 0 : 3;
-}
-#endif
-
-#if BCNF_EXP & 256
-int bcnf_debug_phases(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(g_phase)) == hipSuccess ? 0 : 3;
+#if BCNF_STAMPS
+int bcnf_debug_phases(unsigned long long* out) {   // diagnostic build only (not in include/bcnf_amd.h)
+  return bcnf_rt::hip_status(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(g_phase)));
 }
 #endif
 
@@ -2583,8 +2532,7 @@ int backward_impl(const BcnfStackDesc* desc, const void* packed, const float* h,
   if (batch < 0 || !packed || !h || !workspace || !slab) return BCNF_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   if (batch == 0) {
-    if (dparams && hipMemsetAsync(dparams, 0, sizeof(float) * (size_t)L.n_trainable, st) != hipSuccess)
-      return BCNF_ERR_HIP;
+    if (dparams) return bcnf_rt::hip_status(hipMemsetAsync(dparams, 0, sizeof(float) * (size_t)L.n_trainable, st));
     return BCNF_OK;
   }
   // `training` must match the forward call that filled the workspace: it says whether dropout masks

@@ -545,8 +545,10 @@ int bcnf_linear_backward(const float* x, const float* weight, const float* dy, i
   hipStream_t st = (hipStream_t)stream;
   const int K = in_features, N = out_features;
   if (rows == 0) {
-    if (dweight && hipMemsetAsync(dweight, 0, sizeof(float) * (size_t)N * K, st) != hipSuccess) return BCNF_ERR_HIP;
-    if (dbias && hipMemsetAsync(dbias, 0, sizeof(float) * (size_t)N, st) != hipSuccess) return BCNF_ERR_HIP;
+    if (dweight)
+      if (const int rc = bcnf_rt::hip_status(hipMemsetAsync(dweight, 0, sizeof(float) * (size_t)N * K, st))) return rc;
+    if (dbias)
+      if (const int rc = bcnf_rt::hip_status(hipMemsetAsync(dbias, 0, sizeof(float) * (size_t)N, st))) return rc;
     return BCNF_OK;
   }
   if (!dy) return BCNF_ERR_ARG;

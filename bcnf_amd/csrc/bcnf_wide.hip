@@ -70,6 +70,7 @@ struct WideLayout {
   long long pk_ldc;             // [nb]             sum_i log|scale_k,i| (0 without ActNorm)
   long long pk_b0;              // [nv][HP]         Linear-1 bias, zero beyond H
   long long total;
+  int tiling;                   // BcnfStackDesc.gemm_tiling of this call (0 = each GEMM's cost-model tiling)
 };
 
 __host__ __device__ inline long long wcb(const WideLayout& L, int k) {
@@ -91,6 +92,8 @@ int wide_layout(const BcnfStackDesc* d, WideLayout* L) {
   for (int i = 1; i < d->n_hidden; ++i)
     if (d->hidden[i] != d->hidden[0]) return BCNF_ERR_UNSUPPORTED;     // equal widths (every shipped config)
   if (d->size > DM || d->n_conditions < 1 || d->hidden[0] > 8192) return BCNF_ERR_UNSUPPORTED;
+  if (d->gemm_tiling < 0 || d->gemm_tiling > 9) return BCNF_ERR_ARG;
+  L->tiling = d->gemm_tiling;
   L->D = d->size;
   L->Da = (d->size + 1) / 2;
   L->Db = d->size / 2;
@@ -311,6 +314,7 @@ struct GemmArgs {
   // EPI_ROWMAP: row r -> virtual block v = r / rm_hp, n = r % rm_hp (skipped when >= rm_h):
   //   C + cb(v) + rm_off[side] + n * rm_ld[side] + col
   int rm_hp, rm_h; long long rm_off[2], rm_ld[2];
+  int tiling;                   // host-side dispatch only: BcnfStackDesc.gemm_tiling of the call (0 = cost model)
 };
 
 __device__ __forceinline__ floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
@@ -966,11 +970,16 @@ struct LinkArgs {
   unsigned long long* dbg;      // phase timestamps of workgroup 0 (bcnf_wide_debug_phases), nullable
 };
 
+// Phase stamps of the forward link: diagnostic build only (-DBCNF_PHASE_STAMPS, tools/exp_variants.sh).
+#ifdef BCNF_PHASE_STAMPS
 #define LINK_STAMP(i)                                                                          \
   do {                                                                                         \
     if (a.dbg && a.vt >= 0 && a.vh >= 0 && blockIdx.x == 0 && threadIdx.x == 0)                \
       a.dbg[i] = __builtin_amdgcn_s_memtime();                                                 \
   } while (0)
+#else
+#define LINK_STAMP(i) do {} while (0)
+#endif
 
 // Dropout mask for a float4 group (4 consecutive columns n..n+3 of one row).
 __device__ __forceinline__ uint4 drop4(uint64_t seed, uint64_t offs, long long row, int n, uint32_t tag) {
@@ -1525,10 +1534,11 @@ __global__ __launch_bounds__(WWG) void k_wnll_finalize(const float* __restrict__
 // ------------------------------------------------------------------------------------------------
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-GemmArgs gemm_args(int M, int N, int K, const float* A, long long lda, const float* B, long long ldb, float* C,
-                   long long ldc) {
+GemmArgs gemm_args(int tiling, int M, int N, int K, const float* A, long long lda, const float* B, long long ldb,
+                   float* C, long long ldc) {
   GemmArgs g;
   memset(&g, 0, sizeof(g));
+  g.tiling = tiling;
   g.M = M;
   g.N = N;
   g.K = K;
@@ -1564,9 +1574,9 @@ int launch_gl(const GemmArgs& g, int groups, hipStream_t st) {
   constexpr int bytes = S * T::STG * 4;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)k_wgl<BM, BN, WGM, WGN, AKC, BKC, EPI, S, KS>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
-      return BCNF_ERR_HIP;
+    if (const int rc = bcnf_rt::hip_status(hipFuncSetAttribute((const void*)k_wgl<BM, BN, WGM, WGN, AKC, BKC, EPI, S, KS>,
+                                                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes)))
+      return rc;
     attr = true;
   }
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, groups);
@@ -1585,17 +1595,17 @@ double tile_cost(const GemmArgs& g, int groups, int BM, int BN, double eff) {
   return (double)((wgs + N_CU - 1) / N_CU) * BM * BN / eff;
 }
 
-int g_force_tiling = -1;   // test hook: 0 = 128x128, 1 = 64x64, 2 = 128x48 (16x16 MFMA), 3 = 128x48 on 8 waves,
-                           // 4 = 96x48 on 6 waves, 5 = LDS-DMA (tiling C, the default; 96 x 48 for K-contiguous
-                           // operands), 6 = tiling C large tiles, 7 = tiling C 48 x 48, 8 = 176 x 176 on 11 waves
-                           // (strided x strided operands only; the dispatcher's choice otherwise)
+// Forced tilings (GemmArgs.tiling = t + 1, from BcnfStackDesc.gemm_tiling; 0 = the cost model): 0 = 128x128,
+// 1 = 64x64, 2 = 128x48 (16x16 MFMA), 3 = 128x48 on 8 waves, 4 = 96x48 on 6 waves, 5 = LDS-DMA (tiling C, the default;
+// 96 x 48 for K-contiguous operands), 6 = tiling C large tiles, 7 = tiling C 48 x 48, 8 = 176 x 176 on 11 waves
+// (strided x strided operands only; the dispatcher's choice otherwise)
 
 template <bool AKC, bool BKC, int EPI>
 int gemm(const GemmArgs& g, int groups, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0 || groups <= 0) return BCNF_OK;
   if ((g.lda & 3) || (g.ldb & 3) || (!aligned16(g.A)) || (!aligned16(g.B))) return BCNF_ERR_ARG;
   if ((AKC || BKC) && (g.K & 3)) return BCNF_ERR_ARG;
-  int pick = g_force_tiling;
+  int pick = g.tiling - 1;
   // LDS-DMA tiling C for K-contiguous x K-contiguous operands (the chain GEMMs, the projections, the row-mapped
   // condition gradient); the register-staged tilings keep the strided layouts, where tiling C's permuted
   // 64-wide wave tiles measured slower (tools/gemm_bench.py t6 / t7, profiles/r02t_gemm_tilings.txt)
@@ -1637,7 +1647,7 @@ int gemm_gl(const GemmArgs& g, int groups, hipStream_t st, bool large) {
     // 96 x 48 on one workgroup per CU while that grid covers most CUs (M = 2048, N = 528: 242 tiles); below,
     // 48 x 48 workgroups two per CU (M = 1024, the LSTM_large chain: 13.3 vs 17.6 us, tools/gemm_bench.py)
     const long long t96 = (long long)((g.M + 95) / 96) * ((g.N + 47) / 48) * groups;
-    if (g_force_tiling == 7 || (g_force_tiling != 5 && t96 < 3 * N_CU / 4))
+    if (g.tiling - 1 == 7 || (g.tiling - 1 != 5 && t96 < 3 * N_CU / 4))
       return launch_gl<48, 48, 3, 1, true, true, EPI, 3>(g, groups, st);
     return launch_gl<96, 48, 6, 1, true, true, EPI, 4>(g, groups, st);
   }
@@ -1744,11 +1754,17 @@ void link_dispatch(int ts, int hs, dim3 grid, size_t lds, hipStream_t st, const 
   else hipLaunchKernelGGL((k_wlink<INV, DD, 1, 0>), grid, dim3(WWG), lds, st, L, a);
 }
 
-unsigned long long* g_link_dbg = nullptr;   // bcnf_wide_debug_phases
+#ifdef BCNF_PHASE_STAMPS
+unsigned long long* g_link_dbg = nullptr;   // bcnf_wide_debug_phases (diagnostic build)
+#endif
 
 int link_launch(const WideLayout& L, const LinkArgs& a_in, bool inv, hipStream_t st) {
   LinkArgs a = a_in;
+#ifdef BCNF_PHASE_STAMPS
   a.dbg = g_link_dbg;
+#else
+  a.dbg = nullptr;
+#endif
   dim3 grid((unsigned)((a.B + LR - 1) / LR));
   const size_t lds = (size_t)link_lds_floats(L, a.vt >= 0, a.vh >= 0) * sizeof(float);
   const int ts = a.vt >= 0 ? a.vt % L.S : 1 - (a.vh % L.S);
@@ -1814,14 +1830,14 @@ const float* padded_h(const WideLayout& L, const float* h, long long rows, float
 
 // P = h W0h_all^T  (rows x nv*HP), h with row stride Cp
 int projection(const WideLayout& L, const float* pk, const float* hp, long long rows, float* P, hipStream_t st) {
-  GemmArgs g = gemm_args((int)rows, L.nv * L.HP, L.Cp, hp, L.Cp, pk + L.pk_w0h, L.Cp, P, (long long)L.nv * L.HP);
+  GemmArgs g = gemm_args(L.tiling, (int)rows, L.nv * L.HP, L.Cp, hp, L.Cp, pk + L.pk_w0h, L.Cp, P, (long long)L.nv * L.HP);
   return gemm<true, true, EPI_STORE>(g, 1, st);
 }
 
 // hidden Linear l (1..NH-1) of virtual block v: A_l = dropout(GELU(A_{l-1} W_l^T + b_l)), G_l
 int hidden_fwd(const WideLayout& L, const float* prm, const float* pk, int v, int l, long long B, const float* Ain,
                float* Aout, float* Gout, const uint64_t* rng, hipStream_t st) {
-  GemmArgs g = gemm_args((int)B, L.HP, L.HP, Ain, L.HP, pk + L.pk_hid + ((long long)v * (L.NH - 1) + (l - 1)) * L.HP * L.HP,
+  GemmArgs g = gemm_args(L.tiling, (int)B, L.HP, L.HP, Ain, L.HP, pk + L.pk_hid + ((long long)v * (L.NH - 1) + (l - 1)) * L.HP * L.HP,
                          L.HP, Aout, L.HP);
   g.bias = prm + vbase(L, v) + L.lin_b[v % L.S][l];
   g.aux = Gout;
@@ -1849,7 +1865,7 @@ struct WideFold {
 };
 
 int fold_prepare(const WideLayout& L, const float* pk, const float* wfb, int Xp, float* wcb, hipStream_t st) {
-  GemmArgs g = gemm_args(L.nv * L.HP, Xp, L.C, pk + L.pk_w0h, L.Cp, wfb, Xp, wcb, Xp);
+  GemmArgs g = gemm_args(L.tiling, L.nv * L.HP, Xp, L.C, pk + L.pk_w0h, L.Cp, wfb, Xp, wcb, Xp);
   return gemm<true, false, EPI_STORE>(g, 1, st);
 }
 
@@ -1863,7 +1879,7 @@ int wide_forward(const WideLayout& L, const float* prm, const float* pk, const f
   const long long slab = B * L.HP;
   int rc;
   if (fold) {
-    GemmArgs g = gemm_args((int)B, L.nv * L.HP, fold->Xp, fold->x1, fold->Xp, fold->wcb, fold->Xp, w.P,
+    GemmArgs g = gemm_args(L.tiling, (int)B, L.nv * L.HP, fold->Xp, fold->x1, fold->Xp, fold->wcb, fold->Xp, w.P,
                            (long long)L.nv * L.HP);
     WCHK((gemm<true, true, EPI_STORE>(g, 1, st)));
   } else {
@@ -1962,7 +1978,7 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
       long long ldi, ldo;
       const float* din = dZptr(vb, l, &ldi);
       float* dout = dZptr(vb, l - 1, &ldo);
-      GemmArgs g = gemm_args((int)B, L.HP, L.HP, din, ldi,
+      GemmArgs g = gemm_args(L.tiling, (int)B, L.HP, L.HP, din, ldi,
                              pk + L.pk_hidT + ((long long)vb * (L.NH - 1) + (l - 1)) * L.HP * L.HP, L.HP, dout, ldo);
       g.aux = Gptr(vb, l - 1);
       g.ldaux = L.HP;
@@ -1973,7 +1989,7 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
   const float* hp = fold ? nullptr : padded_h(L, h, B, w.Hp, st, &rc);
   WCHK(rc);
   if (fold) {   // Gx = dZ0_all^T x1 (the condition-side gradients below all go through it)
-    GemmArgs g = gemm_args(L.nv * L.HP, fold->Xp, (int)B, w.dZ0, ld0, fold->x1, fold->Xp, fold->gx, fold->Xp);
+    GemmArgs g = gemm_args(L.tiling, L.nv * L.HP, fold->Xp, (int)B, w.dZ0, ld0, fold->x1, fold->Xp, fold->gx, fold->Xp);
     WCHK((gemm<false, false, EPI_STORE>(g, 1, st)));
   }
   // ---- parameter gradients (canonical flat, every element written exactly once) ----
@@ -1985,7 +2001,7 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
       g.cb_nb = L.nb;
     };
     if (L.NH > 1) {   // hidden Linears of every virtual block in one grouped launch: [dW_l | db_l] = dZ_l^T [A_{l-1} | 1]
-      GemmArgs g = gemm_args(L.H, L.H + 1, (int)B, w.dZ, L.HP, w.A, L.HP, dprm + L.lin_w[0][1], L.H);
+      GemmArgs g = gemm_args(L.tiling, L.H, L.H + 1, (int)B, w.dZ, L.HP, w.A, L.HP, dprm + L.lin_w[0][1], L.H);
       g.G0 = L.NH - 1;
       g.sA1 = (long long)(L.NH - 1) * slab;
       g.sA0 = slab;
@@ -1997,17 +2013,11 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
       g.sC0 = (L.NH > 2) ? (L.lin_w[0][2] - L.lin_w[0][1]) : 0;
       g.wcols = L.H;
       g.boff = (long long)L.H * L.H;
-      // experiment knob: BCNF_LINGRAD_TILING = g_force_tiling value for this launch only
-      static const int lt = getenv("BCNF_LINGRAD_TILING") ? atoi(getenv("BCNF_LINGRAD_TILING")) : -1;
-      const int saved = g_force_tiling;
-      if (lt >= 0 && saved < 0) g_force_tiling = lt;
-      const int rc_l = gemm<false, false, EPI_LINGRAD>(g, L.nv * (L.NH - 1), st);
-      g_force_tiling = saved;
-      WCHK(rc_l);
+      WCHK((gemm<false, false, EPI_LINGRAD>(g, L.nv * (L.NH - 1), st)));
     }
     for (int sd = 0; sd < L.S; ++sd) {
       {   // last Linear of every block's side-sd half: [dW | db] = dO^T [A_{NH-1} | 1]
-        GemmArgs g = gemm_args(2 * L.nout[sd], L.H + 1, (int)B, w.O + (long long)sd * B * L.OP, L.OP,
+        GemmArgs g = gemm_args(L.tiling, 2 * L.nout[sd], L.H + 1, (int)B, w.O + (long long)sd * B * L.OP, L.OP,
                                w.A + ((long long)sd * L.NH + L.NH - 1) * slab, L.HP,
                                dprm + (sd ? L.mlp[0] : 0) + L.lin_w[sd][L.NH], L.H);
         g.sA1 = (long long)L.S * B * L.OP;
@@ -2018,7 +2028,7 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
         WCHK(lingrad_splitk(g, L.nb, w.G, w.G ? (long long)L.nv * L.NH * slab : 0, st));
       }
       {   // Linear-1, input columns + bias: [dW0[:, :nin] | db0] = dZ_0^T [u_in | 1]
-        GemmArgs g = gemm_args(L.H, L.nin[sd] + 1, (int)B, w.dZ0 + (long long)sd * L.HP, ld0,
+        GemmArgs g = gemm_args(L.tiling, L.H, L.nin[sd] + 1, (int)B, w.dZ0 + (long long)sd * L.HP, ld0,
                                w.U + (long long)sd * B * L.UP, L.UP, dprm + (sd ? L.mlp[0] : 0) + L.lin_w[sd][0],
                                L.in0[sd]);
         g.sA1 = (long long)L.S * L.HP;
@@ -2030,8 +2040,8 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
       }
     }
     {   // Linear-1, condition columns of every virtual block in one GEMM: dW0h_all = dZ0_all^T h (folded: Gx wfb^T)
-      GemmArgs g = fold ? gemm_args(L.nv * L.HP, L.C, fold->Xp, fold->gx, fold->Xp, fold->wfb, fold->Xp, dprm, 0)
-                        : gemm_args(L.nv * L.HP, L.C, (int)B, w.dZ0, ld0, hp, L.Cp, dprm, 0);
+      GemmArgs g = fold ? gemm_args(L.tiling, L.nv * L.HP, L.C, fold->Xp, fold->gx, fold->Xp, fold->wfb, fold->Xp, dprm, 0)
+                        : gemm_args(L.tiling, L.nv * L.HP, L.C, (int)B, w.dZ0, ld0, hp, L.Cp, dprm, 0);
       g.cb_stride = L.blk_stride;
       g.cb_an = L.an;
       g.cb_nb = L.nb;
@@ -2058,15 +2068,15 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
     // split K = nv * HP per virtual block; partials in the G region (dead once the chain has run)
     const long long gfl = (long long)L.nv * L.NH * slab;
     if (fold->dwfb) {   // [dWf | dbf] = W0h_all^T Gx
-      GemmArgs g = gemm_args(L.C, fold->Xp, L.nv * L.HP, pk + L.pk_w0h, L.Cp, fold->gx, fold->Xp, fold->dwfb, fold->Xp);
+      GemmArgs g = gemm_args(L.tiling, L.C, fold->Xp, L.nv * L.HP, pk + L.pk_w0h, L.Cp, fold->gx, fold->Xp, fold->dwfb, fold->Xp);
       WCHK((gemm_splitk<false, false>(g, L.nv, w.G, gfl, st)));
     }
     if (fold->dx) {     // dL/dx = dZ0_all Wcb
-      GemmArgs g = gemm_args((int)B, fold->Xp, L.nv * L.HP, w.dZ0, ld0, fold->wcb, fold->Xp, fold->dx, fold->Xp);
+      GemmArgs g = gemm_args(L.tiling, (int)B, fold->Xp, L.nv * L.HP, w.dZ0, ld0, fold->wcb, fold->Xp, fold->dx, fold->Xp);
       WCHK((gemm_splitk<true, false>(g, L.nv, w.G, gfl, st)));
     }
   } else if (dh) {   // dh = dZ0_all W0h_all
-    GemmArgs g = gemm_args((int)B, L.C, L.nv * L.HP, w.dZ0, ld0, pk + L.pk_w0h, L.Cp, dh, L.C);
+    GemmArgs g = gemm_args(L.tiling, (int)B, L.C, L.nv * L.HP, w.dZ0, ld0, pk + L.pk_w0h, L.Cp, dh, L.C);
     WCHK((gemm<true, false, EPI_STORE>(g, 1, st)));
   }
   return BCNF_OK;
@@ -2210,8 +2220,7 @@ int bcnf_wide_forward(const BcnfStackDesc* desc, const float* params, const void
                     save != 0, st));
   if (nll_part) {
     const WideWs w = carve(L, batch, save != 0, (float*)workspace);
-    if (hipMemcpyAsync(nll_part, w.nllp, batch * sizeof(float), hipMemcpyDeviceToDevice, st) != hipSuccess)
-      return bcnf_rt::launched() ? BCNF_ERR_HIP : BCNF_ERR_HIP;
+    return bcnf_rt::hip_status(hipMemcpyAsync(nll_part, w.nllp, batch * sizeof(float), hipMemcpyDeviceToDevice, st));
   }
   return BCNF_OK;
 }
@@ -2300,31 +2309,20 @@ int bcnf_wide_inverse(const BcnfStackDesc* desc, const float* params, const void
                       (float*)scratch, (hipStream_t)stream);
 }
 
-// Debug: phase timestamps (s_memtime) of workgroup 0 of every forward link launch into dbg[0..6] (nullptr = off).
+#ifdef BCNF_PHASE_STAMPS
+// Diagnostic build only: phase timestamps (s_memtime) of workgroup 0 of every forward link launch into dbg[0..6].
 int bcnf_wide_debug_phases(unsigned long long* dbg) {
   g_link_dbg = dbg;
   return BCNF_OK;
 }
-
-// Tiling override for every wide GEMM launch (-1 = the default, LDS-DMA tiling C; 0..6 as g_force_tiling).
-int bcnf_wide_force_tiling(int32_t tiling) {
-  const int prev = g_force_tiling;
-  g_force_tiling = (tiling >= 0 && tiling <= 8) ? tiling : -1;
-  return prev;
-}
+#endif
 
 // Test hook: one plain GEMM through the tile machinery. layout: 0 = NT (A[m][k], B[n][k]), 1 = NN (A[m][k], B[k][n]),
 // 2 = TN (A[k][m], B[k][n]), 3 = TT (A[k][m], B[n][k]).
 int bcnf_wide_gemm_test(int32_t layout, int32_t M, int32_t N, int32_t K, const float* A, int64_t lda, const float* B,
                         int64_t ldb, float* C, int64_t ldc, void* stream) {
-  GemmArgs g = gemm_args(M, N, K, A, lda, B, ldb, C, ldc);
-  const int prev = g_force_tiling;
-  if (layout >> 4) g_force_tiling = (layout >> 4) - 1;      // layout bits 4..: tiling + 1 (0 = current choice)
+  GemmArgs g = gemm_args(layout >> 4, M, N, K, A, lda, B, ldb, C, ldc);
   layout &= 15;
-  struct Reset {
-    int p;
-    ~Reset() { g_force_tiling = p; }
-  } reset{prev};
   hipStream_t st = (hipStream_t)stream;
   if (layout == 0) return gemm<true, true, EPI_STORE>(g, 1, st);
   if (layout == 1) return gemm<true, false, EPI_STORE>(g, 1, st);

@@ -49,8 +49,11 @@ enum {
   BCNF_OK = 0,
   BCNF_ERR_ARG = 1,          /* invalid descriptor / null pointer / bad size */
   BCNF_ERR_UNSUPPORTED = 2,  /* shape outside this kernel family (see bcnf_stack_supported) */
-  BCNF_ERR_HIP = 3           /* a HIP launch failed; see bcnf_last_hip_error */
+  BCNF_ERR_HIP = 3           /* reserved (a HIP failure returns BCNF_ERR_HIP_BASE + its hipError_t)       */
 };
+/* A HIP runtime failure (launch, attribute, memset / copy) returns BCNF_ERR_HIP_BASE + the hipError_t it produced;
+ * bcnf_status_string names it. The library keeps no error state between calls. */
+#define BCNF_ERR_HIP_BASE 1000
 
 /* Mirrors CondRealNVP_v2.__init__ kwargs (cnf.py:358-375) for the coupling stack. */
 typedef struct BcnfStackDesc {
@@ -62,6 +65,9 @@ typedef struct BcnfStackDesc {
   int32_t act_norm;                  /* 0/1                                    */
   int32_t two_way;                   /* 0/1 (small family: 0 only; wide: both) */
   float dropout;                     /* p of every nn.Dropout in the nested MLP */
+  int32_t gemm_tiling;               /* wide family only: 0 = each GEMM's cost-model tiling (use this); t + 1 forces
+                                        tiling t on every GEMM of the call (tests / A-B timing; see
+                                        bcnf_wide_gemm_test). Per call: the library holds no such setting. */
 } BcnfStackDesc;
 
 /* 1 if this descriptor runs on the fused small-width kernel family, else 0. */
@@ -364,22 +370,15 @@ int bcnf_wide_inverse(const BcnfStackDesc* desc, const float* params, const void
 int bcnf_rank_count(const float* y_hat, const float* y, int64_t n_draws, int64_t n_rows, int32_t dim, uint32_t* counts,
                     void* stream);
 
-/* Debug knob: device buffer of 8 uint64 receiving s_memtime stamps of workgroup 0's phases in every forward link
- * launch (0 start, 1 staged, 2 tail dot products, 3 tail reduction, 4 coupling, 5 head vector, 6 end); NULL = off. */
-int bcnf_wide_debug_phases(unsigned long long* dbg);
-
-/* Debug / test knob: force the tiling of every wide GEMM launch (-1 = the cost model's choice, 0 = 128x128 and
- * 1 = 64x64 with v_mfma_f32_32x32x2_f32, 2 = 128x48 with v_mfma_f32_16x16x4_f32). Returns the previous setting.
- * Process-wide; not for concurrent use. */
-int bcnf_wide_force_tiling(int32_t tiling);
 /* Test hook for the GEMM tiles: C (M x N) = A B with (layout & 15) 0 = A[m][k] B[n][k], 1 = A[m][k] B[k][n],
- * 2 = A[k][m] B[k][n]; layout >> 4 forces a tiling (0 = the dispatcher's choice, 1 = 128x128, 2 = 64x64,
- * 3 = 128x48); leading dimensions and K multiples of 4, 16-byte aligned bases. */
+ * 2 = A[k][m] B[k][n], 3 = A[k][m] B[n][k]; layout >> 4 forces a tiling as BcnfStackDesc.gemm_tiling (0 = the
+ * dispatcher's choice, t + 1 = tiling t: 0 = 128x128 and 1 = 64x64 on v_mfma_f32_32x32x2_f32, 2 = 128x48, 3 = 128x48
+ * on 8 waves, 4 = 96x48 on 6 waves (v_mfma_f32_16x16x4_f32), 5 / 6 / 7 = LDS-DMA tiling C auto / large / 48x48,
+ * 8 = 176x176 on 11 waves); leading dimensions and K multiples of 4, 16-byte aligned bases. */
 int bcnf_wide_gemm_test(int32_t layout, int32_t M, int32_t N, int32_t K, const float* A, int64_t lda, const float* B,
                         int64_t ldb, float* C, int64_t ldc, void* stream);
 
 const char* bcnf_status_string(int status);
-int bcnf_last_hip_error(void);
 
 #ifdef __cplusplus
 }

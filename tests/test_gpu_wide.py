@@ -117,10 +117,9 @@ WIDE_SHAPES = [
                 ids=["auto", "t128x128", "t64x64", "t128x48", "t128x48w8", "t96x48w6", "glds96x48", "glds_large",
                      "glds48x48", "t176x176w11"])
 def tiling(request):
-    N = _lib()
-    prev = N.lib().bcnf_wide_force_tiling(request.param)
-    yield request.param
-    N.lib().bcnf_wide_force_tiling(prev)
+    """A forced GEMM tiling travels in the model's descriptor (BcnfStackDesc.gemm_tiling = t + 1): per call, no
+    library-global setting."""
+    return request.param
 
 
 @pytest.mark.parametrize("shape", WIDE_SHAPES)
@@ -132,6 +131,7 @@ def test_wide_shapes_vs_oracle(shape, B, tiling):
     if tiling >= 0 and B == 1:
         pytest.skip("B = 1 covered by the auto tiling")
     m = _model(shape)
+    m.fused.desc.gemm_tiling = tiling + 1
     _perturb(m)
     sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
     spec = _spec(shape)

@@ -27,6 +27,24 @@ def test_library_exports_every_header_symbol():
     assert lib.bcnf_status_string(0) == b"ok"
 
 
+def test_boundary_has_no_global_state():
+    """stateless entry points. The header declares no process-global setter, no last-error query and no
+    debug hook; HIP failures come back in the status code (BCNF_ERR_HIP_BASE + hipError_t); the shipped library
+    exports no debug symbols (they exist only in the -DBCNF_PHASE_STAMPS diagnostic build)."""
+    from bcnf_amd import _native as N
+    names = header_functions()
+    for n in names:
+        assert not re.search(r"force|set_|debug|last_|_error$", n), n
+    src = open(HEADER).read()
+    assert "BCNF_ERR_HIP_BASE 1000" in src and N.ERR_HIP_BASE == 1000
+    lib = N.lib()
+    for n in ("bcnf_last_hip_error", "bcnf_wide_force_tiling", "bcnf_debug_phases", "bcnf_wide_debug_phases"):
+        assert not hasattr(lib, n), n
+    assert lib.bcnf_status_string(1000 + 98).decode() not in ("ok", "unknown status")   # hipErrorInvalidImage
+    for d in ("bcnf_stack.hip", "bcnf_wide.hip", "bcnf_train.hip", "bcnf_device.h"):
+        assert "BCNF_EXP" not in open(os.path.join(ROOT, "bcnf_amd", "csrc", d)).read(), d
+
+
 def test_layout_queries_match_module_tree():
     from bcnf_amd import CondRealNVP_v2
     from bcnf_amd import _native as N

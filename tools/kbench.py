@@ -60,7 +60,7 @@ def main():
 
 
 def phases():
-    """Per-phase cycles of the backward loop, workgroup 0 (experiment build with BCNF_EXP & 256)."""
+    """Per-phase cycles of the backward loop, workgroup 0 (diagnostic build: bash tools/exp_variants.sh stamps)."""
     import ctypes
     from bcnf_amd import _native as N
     L = N.lib()
