@@ -158,6 +158,7 @@ struct BcnfLayout {
   float p, keep_scale;
   uint32_t thresh16;    // drop if u16 < thresh16
   int RF, RB;           // per-lane record floats (forward/inverse, backward)
+  int PMB;              // floats per block of the matrix-core inverse's operand-ordered record (k_inverse_mfma)
   // record offsets (floats, per lane)
   int rf_b1, rf_w1, rf_hid, rf_t, rf_s, rf_q;
   int rb_w1t, rb_hid, rb_tt, rb_st, rb_qt, rb_an;
@@ -165,7 +166,7 @@ struct BcnfLayout {
   // W1 condition part, two contiguous copies for the projection GEMMs (NKp = nb*16 rounded up to 64):
   //   W1hC [Cp][NKp]  (c, k*16+j)   W1hR [NKp][Cp]  (k*16+j, c)   b1c [NKp]
   int NKp;
-  long long pf_off, pb_off, pi_off, w1c_off, w1r_off, b1c_off, ldc_off, total;
+  long long pf_off, pb_off, pi_off, w1c_off, w1r_off, b1c_off, ldc_off, pm_off, total;
   int ldh;              // row stride (floats) of the projection input: C for h, ldx for the folded path's x
 };
 

@@ -103,14 +103,15 @@ int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
   L->rf_s = L->rf_t + 17;
   L->rf_q = (L->rf_s + 17 + 3) & ~3;
   L->RF = round_rec(L->rf_q + 64);
-  // backward record: [W1T:16][hidden^T l: 16 ...][Tout^T:16][Sout^T:16][Q^T:64]
-  L->rb_w1t = 0;
-  L->rb_hid = 16;
-  L->rb_tt = 16 + 16 * (L->NH > 0 ? L->NH - 1 : 0);
-  L->rb_st = L->rb_tt + 16;
-  L->rb_qt = L->rb_st + 16;
-  L->rb_an = L->rb_qt + 64;                    // ActNorm [sa ba sb bb] (the backward needs no forward record)
-  L->RB = round_rec(L->rb_an + 4);
+  // backward record, in the order the backward consumes it (so its LDS reads are waited for piecewise, not all at
+  // once): [ActNorm sa ba sb bb][Q^T:64][Tout^T:16][Sout^T:16][hidden^T l = NH .. 2: 16 each][W1T:16]
+  L->rb_an = 0;
+  L->rb_qt = 4;
+  L->rb_tt = 68;
+  L->rb_st = 84;
+  L->rb_hid = 100;                             // hidden layer l at rb_hid + 16 (NH - l)
+  L->rb_w1t = 100 + 16 * (L->NH > 0 ? L->NH - 1 : 0);
+  L->RB = round_rec(L->rb_w1t + 16);
   long long nbl = L->nb;
   L->pf_off = 0;
   L->pb_off = L->pf_off + nbl * 16 * L->RF;
@@ -120,15 +121,19 @@ int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
   L->w1r_off = L->w1c_off + (long long)L->Cp * L->NKp;
   L->b1c_off = L->w1r_off + (long long)L->NKp * L->Cp;
   L->ldc_off = L->b1c_off + L->NKp;
-  L->total = L->ldc_off + 4;
+  // matrix-core inverse record in MFMA A-operand order (k_inverse_mfma, inv_mo_*): NH + 6 matrices x 64 lanes x 4
+  // steps, hidden / T / S biases as [4 q][4 r], ActNorm inverse [4 q][4 r][4]
+  L->PMB = (L->NH + 6) * 256 + (L->NH - 1) * 16 + 32 + 64;
+  L->pm_off = L->ldc_off + 4;
+  L->total = L->pm_off + nbl * L->PMB;
   return BCNF_OK;
 }
 
 size_t fwd_lds_bytes(const BcnfLayout& L) {   // forward / inverse record ring (2 blocks)
   return sizeof(float) * (size_t)(2 * RING);
 }
-size_t fwd2_lds_bytes(const BcnfLayout& L) {  // forward: record ring, projection partials, dropout bits (2 slots)
-  return sizeof(float) * (size_t)(2 * RING + 2 * 4 * 256 + 2 * 256);
+size_t fwd2_lds_bytes(const BcnfLayout& L) {  // k_forward: record ring, projection partials, dropout masks (3 slots)
+  return sizeof(float) * (size_t)(3 * RING + 3 * 4 * 256 + 3 * 8 * 256);
 }
 size_t bwd_lds_bytes(const BcnfLayout& L) {   // backward record ring, delta tiles (2), activation tiles (3), derivative slots (2)
   return sizeof(float) * (size_t)(2 * RING + 2 * (L.NH + 6) * TILE + 3 * (L.NH + 1) * TILE + 2 * 3 * 4 * 256);
@@ -217,21 +222,64 @@ __device__ float rec_f(const BcnfLayout& L, const float* P, const float* Q, int 
 // PB record entry (transposed weight rows for the backward).
 __device__ float rec_b(const BcnfLayout& L, const float* P, const float* Q, int k, int j, int e) {
   const int NH = L.NH, Db = L.Db;
-  if (e < 16) {
-    const int src = (j - e) & 15;
+  if (e >= L.rb_w1t && e < L.rb_w1t + 16) {
+    const int src = (j - (e - L.rb_w1t)) & 15;
     return (j < L.Da && src < L.H[1]) ? cW(L, P, k, 1, src, j) : 0.f;
   }
-  if (e >= L.rb_hid && e < L.rb_tt) {
-    const int l = 2 + (e - L.rb_hid) / 16, r = (e - L.rb_hid) % 16, src = (j - r) & 15;
+  if (e >= L.rb_hid && e < L.rb_w1t) {
+    const int l = NH - (e - L.rb_hid) / 16, r = (e - L.rb_hid) % 16, src = (j - r) & 15;
     return (j < L.H[l - 1] && src < L.H[l]) ? cW(L, P, k, l, src, j) : 0.f;
   }
-  if (e >= L.rb_tt && e < L.rb_qt) {
+  if (e >= L.rb_tt && e < L.rb_tt + 32) {
     const int half = (e - L.rb_tt) / 16, r = (e - L.rb_tt) % 16, src = (j - r) & 15;
     return (j < L.H[NH] && src < Db) ? cW(L, P, k, NH + 1, half * Db + src, j) : 0.f;
   }
   if (e >= L.rb_qt && e < L.rb_qt + 64) return rec_f(L, P, Q, k, j, L.rf_q + (e - L.rb_qt), true);
   if (e >= L.rb_an && e < L.rb_an + 4) return rec_f(L, P, Q, k, j, e - L.rb_an, false);
   return 0.f;
+}
+
+// Matrix-core inverse record of block k in MFMA A-operand order, entry e (k_inverse_mfma): matrix m's lane l = (q, s)
+// reads ONE float4 at m * 256 + 4 l -- its A operands of the layer's 4 K-steps t -- instead of 4 scalar reads of the
+// row-layout inverse record at lane-dependent offsets (bank conflicts: DESIGN 3e). Values are PI-record entries
+// (rec_f, inverse = true): m = 0..3 the mix quadrants qi (half -> half), 4 Linear 1 (half -> hidden), 5 .. NH + 3
+// the hidden layers, NH + 4 / NH + 5 the T / S heads (hidden -> half). PERM (D_a, D_b <= 12): half-vector feature
+// 3q + r in register r < 3; rows with no feature read lane 15's zero entry.
+__device__ float rec_pm(const BcnfLayout& L, const float* P, const float* Q, int k, int e) {
+  const int NH = L.NH, nm = NH + 6;
+  const bool perm = L.Da <= 12 && L.Db <= 12;
+  auto feat = [&](int q, int r) { return perm ? (r < 3 ? 3 * q + r : 15) : 4 * q + r; };
+  if (e < nm * 256) {
+    const int m = e >> 8, l = (e >> 2) & 63, t = e & 3, q = l >> 4, s = l & 15;
+    const bool none = perm && (s & 3) == 3;
+    const int fo = perm ? 3 * (s >> 2) + (s & 3) : s;
+    const int ch = perm ? 3 * q + t : 4 * q + t, cu = 4 * q + t;
+    if (m < 4) {                                                           // mix quadrant qi = m
+      if (perm && t == 3) return 0.f;
+      const int off = L.rf_q + 16 * m;
+      return none ? rec_f(L, P, Q, k, 15, off, true) : rec_f(L, P, Q, k, fo, off + ((fo - ch) & 15), true);
+    }
+    if (m == 4) {                                                          // Linear 1, y-part
+      if (perm && t == 3) return 0.f;
+      return rec_f(L, P, Q, k, s, L.rf_w1 + ((s - ch) & 15), true);
+    }
+    if (m < NH + 4) return rec_f(L, P, Q, k, s, L.rf_hid + 17 * (m - 5) + ((s - cu) & 15), true);
+    const int off = (m == NH + 4) ? L.rf_t : L.rf_s;
+    return none ? rec_f(L, P, Q, k, 15, off, true) : rec_f(L, P, Q, k, fo, off + ((fo - cu) & 15), true);
+  }
+  e -= nm * 256;
+  if (e < (NH - 1) * 16) {                                                 // hidden biases, row 4q + r
+    const int h = e >> 4, q = (e >> 2) & 3, r = e & 3;
+    return rec_f(L, P, Q, k, 4 * q + r, L.rf_hid + 17 * h + 16, true);
+  }
+  e -= (NH - 1) * 16;
+  if (e < 32) {                                                            // T / S biases, row feat(q, r)
+    const int half = e >> 4, q = (e >> 2) & 3, r = e & 3;
+    return rec_f(L, P, Q, k, feat(q, r), (half ? L.rf_s : L.rf_t) + 16, true);
+  }
+  e -= 32;                                                                 // ActNorm inverse [1/sa ba 1/sb bb]
+  const int q = e >> 4, r = (e >> 2) & 3, i = e & 3;
+  return rec_f(L, P, Q, k, feat(q, r), i, true);
 }
 
 // Grid: 1 workgroup that computes the ActNorm log|det| constant  sum_k sum_i log|scale_k,i|  (cnf.py:350) in a
@@ -264,7 +312,8 @@ __device__ __forceinline__ void pack_body(const BcnfLayout& L, const float* __re
   const int n_pf = L.nb * 16 * L.RF;
   const int n_pb = L.nb * 16 * L.RB;
   const int n_w = L.Cp * L.NKp;                       // each of W1hC, W1hR
-  const int total = 2 * n_pf + n_pb + 2 * n_w + L.NKp;
+  const int n_pm = L.nb * L.PMB;
+  const int total = 2 * n_pf + n_pb + 2 * n_w + L.NKp + n_pm;
   for (int i = (bx - 1) * BCNF_WG + threadIdx.x; i < total; i += npw * BCNF_WG) {
     float v;
     long long o;
@@ -292,10 +341,15 @@ __device__ __forceinline__ void pack_body(const BcnfLayout& L, const float* __re
       const int kj = ii / L.Cp, c = ii - kj * L.Cp, k = kj >> 4, j = kj & 15;
       v = (k < L.nb && j < L.H[1] && c < L.C) ? cW(L, P, k, 1, j, L.Da + c) : 0.f;
       o = L.w1r_off + ii;
-    } else {                                          // b1c [kj]
+    } else if (i < 2 * n_pf + n_pb + 2 * n_w + L.NKp) {   // b1c [kj]
       const int kj = i - 2 * n_pf - n_pb - 2 * n_w, k = kj >> 4, j = kj & 15;
       v = (k < L.nb && j < L.H[1]) ? cB(L, P, k, 1, j) : 0.f;
       o = L.b1c_off + kj;
+    } else {                                          // PM (matrix-core inverse, operand order)
+      const int ii = i - 2 * n_pf - n_pb - 2 * n_w - L.NKp;
+      const int k = ii / L.PMB, e = ii - k * L.PMB;
+      v = rec_pm(L, P, Q, k, e);
+      o = L.pm_off + ii;
     }
     out[o] = v;
   }
@@ -309,7 +363,8 @@ __global__ __launch_bounds__(BCNF_WG) void k_pack(BcnfLayout L, const float* __r
 
 // Record workgroups of a pack launch (the log-det workgroup not included).
 int pack_wgs(const BcnfLayout& L) {
-  const long long total = 2LL * L.nb * 16 * L.RF + (long long)L.nb * 16 * L.RB + 2LL * L.Cp * L.NKp + L.NKp;
+  const long long total = 2LL * L.nb * 16 * L.RF + (long long)L.nb * 16 * L.RB + 2LL * L.Cp * L.NKp + L.NKp +
+                          (long long)L.nb * L.PMB;
   const long long w = (total + BCNF_WG - 1) / BCNF_WG;
   return (int)(w < PACK_WG_MAX ? (w > 0 ? w : 1) : PACK_WG_MAX);
 }
@@ -968,9 +1023,9 @@ struct RecF {
   static constexpr int Q = (S + 17 + 3) & ~3, MLP_END = (S + 17 + 3) & ~3, USED = Q + 64;
 };
 template <int NH>
-struct RecB {
-  static constexpr int W1T = 0, HID = 16, TT = 16 + 16 * (NH - 1), ST = TT + 16, QT = ST + 16, AN = QT + 64;
-  static constexpr int USED = AN + 4;
+struct RecB {   // consumption order (make_layout): ActNorm, Q^T, T / S heads, hidden l = NH .. 2, W1^T
+  static constexpr int AN = 0, QT = 4, TT = 68, ST = 84, HID = 100, W1T = 100 + 16 * (NH - 1);
+  static constexpr int USED = W1T + 16;
 };
 // Activation record a training forward saves per (block, sample, lane) for the backward, so the backward never
 // recomputes the MLP: masked activations, masked GELU derivatives, tanh(s) and the block input, 2 NH + 3 floats
@@ -1026,6 +1081,32 @@ __device__ __forceinline__ void mlp_forward(const BcnfLayout& L, const float* __
   rot16x2(a, rr + F::T, T, a, rr + F::S, Sp);
 }
 
+// The same with the dropout multipliers as floats (msk[l - 1] = keep_scale or 0 for hidden layer l, drawn by
+// k_forward's helper waves): no bit extraction on the compute wave's chain.
+template <int NH, bool KEEP, bool DROP>
+__device__ __forceinline__ void mlp_forward_m(const float* __restrict__ rr, float x, float hp,
+                                              const float* __restrict__ msk, float& T, float& Sp, float* act, float* gd) {
+  using F = RecF<NH>;
+  float a = x;
+#pragma unroll
+  for (int l = 1; l <= NH; ++l) {
+    const float* w = (l == 1) ? rr + F::W1 : rr + F::HID + 17 * (l - 2);
+    const float pre = rot16(a, w, (l == 1) ? hp : w[16]);
+    if (KEEP) {
+      float g, dg;
+      gelu_fg(pre, g, dg);
+      a = DROP ? g * msk[l - 1] : g;
+      act[l - 1] = a;
+      gd[l - 1] = DROP ? dg * msk[l - 1] : dg;
+    } else {
+      a = DROP ? gelu_f(pre) * msk[l - 1] : gelu_f(pre);
+    }
+  }
+  T = rr[F::T + 16];
+  Sp = rr[F::S + 16];
+  rot16x2(a, rr + F::T, T, a, rr + F::S, Sp);
+}
+
 // Row-layout orthonormal mix: (na, nb) = (a, b) @ M with the four pre-rotated quadrants at rq
 // (register-resident): [a->a | b->a | a->b | b->b].
 __device__ __forceinline__ void mix(const float* __restrict__ rq, float a, float b, float& na, float& nbv) {
@@ -1054,29 +1135,37 @@ struct ProjArgs {
 };
 constexpr int FWD_WG = 2 * BCNF_WG;
 constexpr int HP_SMAX = 16;            // K-steps of 4 per helper wave: Cp / 16 <= 16 (Cp <= 256)
-constexpr int FWD_HP = 2 * 4 * 256;    // LDS: [2 slots][4 helper waves][16 samples][16] partial HP tiles
-constexpr int FWD_BITS = 2 * 256;      // LDS: [2 slots][256] dropout keep-bits (u32)
+constexpr int FWD_SLOTS = 3;           // ring depth: the helpers prepare block k + 2 while block k runs
+constexpr int FWD_HP = FWD_SLOTS * 4 * 256;   // LDS: [slot][4 helper waves][16 samples][16] partial HP tiles
+constexpr int FWD_HEAD = 24;           // record floats the compute waves prefetch one block ahead (ActNorm, b1, W1y)
 
 // Whole-stack forward, one launch, 512 threads = two roles per SIMD (waves w and w + 4 share a SIMD):
 //  * compute waves 0..3 (4 samples each, row layout): ActNorm -> nested MLP (GELU, dropout) -> affine coupling ->
-//    log-det -> orthonormal mix of block k, reading its record, condition projection and dropout bits from LDS;
-//  * helper waves 4..7, in the same interval, prepare block k+1: stage its forward record into the LDS ring,
-//    compute its condition projection for the workgroup's 16 samples on fp32 MFMA (one K-quarter per helper
-//    wave; the compute lanes add the four partials in a fixed order), and draw its dropout bits (Philox).
-// The projection therefore needs no separate GEMM launch and no HBM round trip, and the compute waves' loop
-// issues no global loads (the record stores of SAVE are its only VMEM traffic).
+//    log-det -> orthonormal mix of block k, reading its record, condition projection and dropout multipliers from
+//    LDS;
+//  * helper waves 4..7 prepare block k + 2 in the same interval (a 3-slot ring): stage its forward record into LDS,
+//    compute its condition projection for the workgroup's 16 samples on fp32 MFMA (one K-quarter per helper wave;
+//    the compute lanes add the four partials in a fixed order), and draw its dropout multipliers (Philox -> floats).
+// With the ring one block deeper, the compute waves read block k + 1's record head, projection partials and
+// multipliers at the end of block k (its slot is complete since the previous barrier), so a block starts without
+// an LDS round trip: a lone wave per SIMD is issue-bound (tools/probe_issue.py: ~8 s_memtime ticks per VALU
+// instruction against ~5.5 per wave with two waves per SIMD, profiles/r03b_probe.txt), and the old block start
+// waited for 27 record reads of all four compute waves.
+// The projection needs no separate GEMM launch and no HBM round trip, and the compute waves' loop issues no global
+// loads (the record stores of SAVE are its only VMEM traffic).
 template <int NH, bool DROP, bool SAVE>
-__global__ __launch_bounds__(FWD_WG) void k_forward(BcnfLayout L, const float* __restrict__ pk,
+__global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const float* __restrict__ pk,
                                                     const float* __restrict__ y, ProjArgs P,
                                                     long long B, float* __restrict__ z, float* __restrict__ ldj_out,
                                                     float* __restrict__ logp, const uint64_t* rng,
                                                     float* __restrict__ arec, float* __restrict__ nll_part) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int RFL = 16 * L.RF;
-  float* rec = smem;                          // [2][16*RF]
-  float* hpb = rec + 2 * RING;                // [2][4][16][16]
-  uint32_t* bitb = reinterpret_cast<uint32_t*>(hpb + FWD_HP);   // [2][256]
+  float* rec = smem;                          // [3][16*RF]
+  float* hpb = rec + FWD_SLOTS * RING;        // [3][4][16][16]
+  floatx4* mkb = reinterpret_cast<floatx4*>(hpb + FWD_HP);   // [3][2][256] dropout multipliers of layers 1..8
   using AR = ActRec<NH>;
+  static_assert(NH <= 8, "two float4 of dropout multipliers");
   const int nb = L.nb;
   const float* pf = pk + L.pf_off;
   const bool helper = threadIdx.x >= BCNF_WG;
@@ -1108,31 +1197,39 @@ __global__ __launch_bounds__(FWD_WG) void k_forward(BcnfLayout L, const float* _
       xa[t] = (t < S && kk < P.C) ? hrow[kk < P.C ? kk : 0] : 0.f;
     }
     const float* wcol = P.w1c + (long long)(4 * hw * S + lq) * P.NKp + lr;   // + 4 t NKp + 16 k
-    // block k's projection partial, dropout bits and record -> slot k & 1
-    auto prepare = [&](int k) {
+    // block k's projection partial, dropout multipliers and record -> slot sl
+    auto prepare = [&](int k, int sl) {
       Stage<STAGE_REC> sr;
       sr.load_t(pf + (long long)k * RFL, RFL, t8);
       float wb[HP_SMAX];
 #pragma unroll
       for (int t = 0; t < HP_SMAX; ++t) wb[t] = (t < S) ? wcol[(long long)4 * t * P.NKp + 16 * k] : 0.f;
-      uint32_t bits = 0xffu;
-      if (DROP) bits = dropout_bits(L, seed, off, bc, k, j, 0u);
+      if (DROP) {
+        const uint32_t bits = dropout_bits(L, seed, off, bc, k, j, 0u);
+        float m[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) m[i] = ((bits >> i) & 1u) ? L.keep_scale : 0.f;
+        mkb[(2 * sl) * BCNF_WG + t8] = floatx4{m[0], m[1], m[2], m[3]};
+        mkb[(2 * sl + 1) * BCNF_WG + t8] = floatx4{m[4], m[5], m[6], m[7]};
+      }
       const float bias = (hw == 0) ? P.b1c[16 * k + lr] : 0.f;
       floatx4 acc = {bias, bias, bias, bias};
 #pragma unroll
       for (int t = 0; t < HP_SMAX; ++t)
         if (t < S) acc = mfma4(xa[t], wb[t], acc);
-      float* hd = hpb + (k & 1) * 1024 + hw * 256 + 64 * lq + lr;
+      float* hd = hpb + sl * 1024 + hw * 256 + 64 * lq + lr;
 #pragma unroll
       for (int r = 0; r < 4; ++r) hd[16 * r] = acc[r];
-      bitb[(k & 1) * 256 + t8] = bits;
-      sr.store_t(rec + (k & 1) * RING, t8);
+      sr.store_t(rec + sl * RING, t8);
     };
-    prepare(0);
+    prepare(0, 0);
+    if (nb > 1) prepare(1, 1);
     __syncthreads();
     PHF(0)
+    int sl = 2;
     for (int k = 0; k < nb; ++k) {
-      if (k + 1 < nb) prepare(k + 1);
+      if (k + 2 < nb) prepare(k + 2, sl);
+      sl = sl == FWD_SLOTS - 1 ? 0 : sl + 1;
       PHF(1)
       __syncthreads();
       PHF(2)
@@ -1144,19 +1241,35 @@ __global__ __launch_bounds__(FWD_WG) void k_forward(BcnfLayout L, const float* _
     float yb = (j < Db) ? y[bc * D + Da + j] : 0.f;
     const float ldc = pk[L.ldc_off];
     __syncthreads();
+    // block k + 1's head: record floats [0, FWD_HEAD), the four projection partials, the dropout multipliers
+    float hd[FWD_HEAD], hq4[4];
+    floatx4 mk0 = {1.f, 1.f, 1.f, 1.f}, mk1 = {1.f, 1.f, 1.f, 1.f};
+    auto fetch_head = [&](int sl) {
+      ld_rec<0, FWD_HEAD>(hd, rec + sl * RING + j * L.RF);
+      const float* hq = hpb + sl * 1024 + tid;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) hq4[i] = hq[256 * i];
+      if (DROP) {
+        mk0 = mkb[(2 * sl) * BCNF_WG + tid];
+        mk1 = mkb[(2 * sl + 1) * BCNF_WG + tid];
+      }
+    };
+    fetch_head(0);
     float ldj = 0.f;
+    int cur = 0;
     for (int k = 0; k < nb; ++k) {
-      const int cur = k & 1;
+      const int nxt = cur == FWD_SLOTS - 1 ? 0 : cur + 1;
       float rr[RecF<NH>::USED];
-      ld_rec<0, RecF<NH>::USED>(rr, rec + cur * RING + j * L.RF);
-      const float* hq = hpb + cur * 1024 + tid;
-      const float hpk = ((hq[0] + hq[256]) + hq[512]) + hq[768];
-      const uint32_t bits = bitb[cur * 256 + tid];
+#pragma unroll
+      for (int i = 0; i < FWD_HEAD; ++i) rr[i] = hd[i];
+      ld_rec<FWD_HEAD, RecF<NH>::USED>(rr, rec + cur * RING + j * L.RF);   // the rest streams in behind layer 1
+      const float hpk = ((hq4[0] + hq4[1]) + hq4[2]) + hq4[3];
+      const float msk[8] = {mk0[0], mk0[1], mk0[2], mk0[3], mk1[0], mk1[1], mk1[2], mk1[3]};
       const float xa = fmaf(rr[0], ya, rr[1]);          // ActNorm (cnf.py:349)
       const float xb = fmaf(rr[2], yb, rr[3]);
       float T, Sp;
       float ar[AR::AR];                                   // activation record of this block (SAVE)
-      mlp_forward<NH, SAVE>(L, rr, xa, hpk, bits, DROP, T, Sp, ar + AR::ACT, ar + AR::GD);
+      mlp_forward_m<NH, SAVE, DROP>(rr, xa, hpk, msk, T, Sp, ar + AR::ACT, ar + AR::GD);
       const float Sv = tanh_bf(Sp);                      // cnf.py:107
       const float zb = fmaf(exp_fast(Sv), xb, T);        // cnf.py:179
       ldj += Sv;                                         // cnf.py:190
@@ -1172,16 +1285,22 @@ __global__ __launch_bounds__(FWD_WG) void k_forward(BcnfLayout L, const float* _
 #pragma unroll
         for (int i = 0; i < AR::AR1; ++i) d1p[i * BCNF_WG] = ar[4 * AR::AR4 + i];
       }
+      fetch_head(nxt);     // slot nxt is complete since the previous barrier (after the last block: unused, no
+                           // branch); the reads land while the mix runs
       mix(rr + RecF<NH>::Q, xa, zb, ya, yb);             // y @ Q (cnf.py:335); identity after the last block
+      cur = nxt;
       PHF(1)
-      __syncthreads();
+      // a bare barrier: the head reads stay in flight across it (nobody writes slot nxt in the next interval; the
+      // helpers write slot k % 3, whose reads this block's compute has consumed), so the wait for them lands on
+      // their first use in block k + 1, not here
+      asm volatile("s_barrier" ::: "memory");
       PHF(2)
     }
     const float ltot = row_sum16(ldj) + ldc;
+    const float q2 = row_sum16(ya * ya + yb * yb);
     if (j < Da) z[bc * D + j] = ya;
     if (j < Db) z[bc * D + Da + j] = yb;
     if (j == 0 && ldj_out) ldj_out[bc] = ltot;
-    const float q2 = row_sum16(ya * ya + yb * yb);
     if (logp && j == 0) logp[bc] = -(0.5f * q2 - ltot) - 0.5f * (float)D * 1.8378770664093454836f;
     if (nll_part && j == 0) rec[s] = (b < B) ? 0.5f * q2 - ltot : 0.f;   // rec: free after the last barrier
   }
@@ -1366,14 +1485,16 @@ constexpr int INV_M_OCC = 6;   // min waves per SIMD (80 VGPRs, no spills; 5 and
 // G independent 16-sample groups per wave interleaving their MFMA chains and GELUs (G = 2 measured neutral).
 constexpr int INV_M_G = 1;
 
+// One dense layer on the matrix cores: the lane's A operands of the KS K-steps are ONE float4 of the operand-ordered
+// record (rec_pm: matrix mat, lane l), conflict-free ds_read_b128.
 template <int G, int KS>
-__device__ __forceinline__ void inv_mv_g(floatx4 (&acc)[G], const float* __restrict__ slot, const int* ao, int off,
-                                         const floatx4 (&x)[G]) {
+__device__ __forceinline__ void inv_mv_mo(floatx4 (&acc)[G], const float* __restrict__ mat, int l,
+                                          const floatx4 (&x)[G]) {
+  const floatx4 w = *reinterpret_cast<const floatx4*>(mat + 4 * l);
 #pragma unroll
   for (int t = 0; t < KS; ++t) {
-    const float w = slot[ao[t] + off];              // shared by the groups
 #pragma unroll
-    for (int g = 0; g < G; ++g) acc[g] = mfma4(w, x[g][t], acc[g]);
+    for (int g = 0; g < G; ++g) acc[g] = mfma4(w[t], x[g][t], acc[g]);
   }
 }
 
@@ -1390,12 +1511,14 @@ __global__ __launch_bounds__(INV_M_WG, PERM ? INV_M_OCC - 1 : INV_M_OCC) void k_
   using F = RecF<NH>;
   constexpr int G = INV_M_G;
   constexpr int KA = PERM ? 3 : 4;                  // MFMA steps over a half-vector input
-  constexpr int RF = inv_m_rf<NH>();                // == L.RF (checked by the dispatch)
-  const int RFL = 16 * RF;
+  constexpr int NM = NH + 6;                         // matrices of the operand-ordered record (rec_pm)
+  constexpr int PMB = NM * 256 + (NH - 1) * 16 + 32 + 64;   // == L.PMB (checked by the dispatch)
+  constexpr int BIAS = NM * 256, TSB = BIAS + (NH - 1) * 16, ANB = TSB + 32;
+  static_assert(PMB <= RING, "operand-ordered record fits a ring slot");
   float* rec = smem;
   const int l = threadIdx.x & 63, q = l >> 4, s = l & 15;
   const int D = L.D, Da = L.Da, Db = L.Db, nb = L.nb;
-  const float* pi = pk + L.pi_off;
+  const float* pm = pk + L.pm_off;
   long long b[G];
   const floatx4* hpl[G];
   const long long hps4 = R * 4;
@@ -1415,20 +1538,6 @@ __global__ __launch_bounds__(INV_M_WG, PERM ? INV_M_OCC - 1 : INV_M_OCC) void k_
       yb[g][r] = (f < Db) ? zin[bc * D + Da + f] : 0.f;
     }
   }
-  // A operands: row o = s of the (possibly permuted) output, K-slot q of step t = input 4q + t (or 3q + t)
-  int aoff[4], aPP[4], aUP[4], aPU[4];
-  {
-    const bool none = PERM && (s & 3) == 3;                                    // permuted row with no feature
-    const int fo = PERM ? 3 * (s >> 2) + (s & 3) : s;                          // output feature of row s
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int ch = PERM ? 3 * q + t : 4 * q + t, cu = 4 * q + t;
-      aoff[t] = s * RF + ((s - cu) & 15);                                       // hidden layers
-      aPP[t] = none ? 15 * RF : fo * RF + ((fo - ch) & 15);                     // mix: half -> half
-      aUP[t] = s * RF + ((s - ch) & 15);                                        // Linear 1: half -> hidden
-      aPU[t] = none ? 15 * RF : fo * RF + ((fo - cu) & 15);                     // T / S: hidden -> half
-    }
-  }
 
   const int kl = nb - 1;
   floatx4 hp_n[G];
@@ -1442,7 +1551,7 @@ __global__ __launch_bounds__(INV_M_WG, PERM ? INV_M_OCC - 1 : INV_M_OCC) void k_
 #pragma unroll
     for (int c = 0; c < RING / (INV_M_WG * 4); ++c) {
       const int ch = wv + (INV_M_WG / 64) * c, e = ch * 256 + 4 * l;
-      const float* src = pi + (long long)k * RFL + (e < RFL ? e : 0);
+      const float* src = pm + (long long)k * PMB + (e < PMB ? e : 0);
       __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(dst + ch * 256), 16,
                                        0, 0);
     }
@@ -1465,46 +1574,41 @@ __global__ __launch_bounds__(INV_M_WG, PERM ? INV_M_OCC - 1 : INV_M_OCC) void k_
     }
     const float* slot = rec + cur * RING;
     // z @ Q^T (cnf.py:339): quadrants [a->a | b->a | a->b | b->b]; identity for the last block
-    inv_mv_g<G, KA>(za, slot, aPP, F::Q, ya);
-    inv_mv_g<G, KA>(zb, slot, aPP, F::Q + 32, ya);
-    inv_mv_g<G, KA>(za, slot, aPP, F::Q + 16, yb);
-    inv_mv_g<G, KA>(zb, slot, aPP, F::Q + 48, yb);
+    inv_mv_mo<G, KA>(za, slot, l, ya);                // quadrant 0: a -> a
+    inv_mv_mo<G, KA>(zb, slot + 2 * 256, l, ya);      // quadrant 2: a -> b
+    inv_mv_mo<G, KA>(za, slot + 1 * 256, l, yb);      // quadrant 1: b -> a
+    inv_mv_mo<G, KA>(zb, slot + 3 * 256, l, yb);      // quadrant 3: b -> b
     // nested MLP (cnf.py:98-107): Linear 1 on za, then the hidden layers
-    inv_mv_g<G, KA>(a, slot, aUP, F::W1, za);
+    inv_mv_mo<G, KA>(a, slot + 4 * 256, l, za);
 #pragma unroll
     for (int g = 0; g < G; ++g) gelu4(a[g]);
 #pragma unroll
     for (int h = 2; h <= NH; ++h) {
-      const int off = F::HID + 17 * (h - 2);
-      floatx4 bias, x[G];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bias[r] = slot[(4 * q + r) * RF + off + 16];
+      const floatx4 bias = *reinterpret_cast<const floatx4*>(slot + BIAS + 16 * (h - 2) + 4 * q);
+      floatx4 x[G];
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         x[g] = a[g];
         a[g] = bias;
       }
-      inv_mv_g<G, 4>(a, slot, aoff, off, x);
+      inv_mv_mo<G, 4>(a, slot + (5 + h - 2) * 256, l, x);
 #pragma unroll
       for (int g = 0; g < G; ++g) gelu4(a[g]);
     }
-    floatx4 T[G], Sp[G], tb, sb;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      tb[r] = slot[feat(r) * RF + F::T + 16];
-      sb[r] = slot[feat(r) * RF + F::S + 16];
-    }
+    floatx4 T[G], Sp[G];
+    const floatx4 tb = *reinterpret_cast<const floatx4*>(slot + TSB + 4 * q);
+    const floatx4 sb = *reinterpret_cast<const floatx4*>(slot + TSB + 16 + 4 * q);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       T[g] = tb;
       Sp[g] = sb;
     }
-    inv_mv_g<G, 4>(T, slot, aPU, F::T, a);
-    inv_mv_g<G, 4>(Sp, slot, aPU, F::S, a);
+    inv_mv_mo<G, 4>(T, slot + (NH + 4) * 256, l, a);
+    inv_mv_mo<G, 4>(Sp, slot + (NH + 5) * 256, l, a);
 #pragma unroll
     for (int r = 0; r < (PERM ? 3 : 4); ++r) {
       const int f = feat(r);
-      const floatx4 an = *reinterpret_cast<const floatx4*>(slot + f * RF);         // [1/sa ba 1/sb bb]
+      const floatx4 an = *reinterpret_cast<const floatx4*>(slot + ANB + 16 * q + 4 * r);   // [1/sa ba 1/sb bb]
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const float S = tanh_bf(Sp[g][r]);
@@ -1770,8 +1874,13 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
         }
       }
       float* Tt = dT + cur * J::ND * TILE + tix;
+      // the record streams in consumption order (RecB): ActNorm + Q^T + the heads now, then each stage issues the
+      // reads of a later one behind a scheduling barrier, so every wait covers a few reads, not the whole record
+      // (lgkmcnt counts at most 15 outstanding: a block-wide burst of 53 reads made the mix wait for ~40 of them)
+      const float* R = recB + cur * RING + j * L.RB;
       float rb[RBk::USED];
-      ld_rec<0, RBk::USED>(rb, recB + cur * RING + j * L.RB);
+      ld_rec<0, RBk::HID>(rb, R);                        // ActNorm, Q^T, T / S heads
+      __builtin_amdgcn_sched_barrier(0);
       const float* gd = gs;
       const float S = gs[NH], ya = gs[NH + 1], yb = gs[NH + 2];
       const float an_sa = rb[RBk::AN], an_sb = rb[RBk::AN + 2], an_bb = rb[RBk::AN + 3];
@@ -1779,6 +1888,8 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
       const float e = exp_fast(S);
       float gza, gzb;
       mix(rb + RBk::QT, gya, gyb, gza, gzb);            // g @ Q^T (identity for the last block)
+      ld16(rb + RBk::HID, R + RBk::HID);                 // hidden layer NH
+      __builtin_amdgcn_sched_barrier(0);
       const float dT_ = gzb;                             // z_b = exp(s) y_b + t
       const float dS = (j < Db) ? fmaf(gzb * e, xb, dl) : 0.f;
       const float dSp = dS * (1.f - S * S);
@@ -1790,9 +1901,11 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
       da += da2;
 #pragma unroll
       for (int l = NH; l >= 2; --l) {
+        ld16(rb + RBk::HID + 16 * (NH - l + 1), R + RBk::HID + 16 * (NH - l + 1));   // next layer (last: W1^T)
+        __builtin_amdgcn_sched_barrier(0);
         const float dpre = da * gd[l - 1];
         Tt[(l - 1) * TILE] = dpre;
-        da = rot16(dpre, rb + RBk::HID + 16 * (l - 2), 0.f);
+        da = rot16(dpre, rb + RBk::HID + 16 * (NH - l), 0.f);
       }
       const float dpre1 = da * gd[0];
       Tt[0] = dpre1;
@@ -2054,7 +2167,7 @@ int fwd_dispatch(const BcnfLayout& L, const float* pk, const float* y, const Pro
 #define BCNF_FWD(DR, SV)                                                                                    \
   rc = launch_lds(k_forward<NH, DR, SV>, lds);                                                              \
   if (rc) return rc;                                                                                        \
-  hipLaunchKernelGGL((k_forward<NH, DR, SV>), grid, dim3(FWD_WG), lds, st, L, pk, y, P, B, z, ldj, logp,     \
+  hipLaunchKernelGGL((k_forward<NH, DR, SV>), grid, dim3(2 * BCNF_WG), lds, st, L, pk, y, P, B, z, ldj, logp, \
                      rng, arec, no.part);
   if (drop) {
     if (save) { BCNF_FWD(true, true) } else { BCNF_FWD(true, false) }
@@ -2070,7 +2183,7 @@ int inv_dispatch(const BcnfLayout& L, const float* pk, const float* zin, const f
                  const int64_t* ci, long long N, float* y, bool drop, const uint64_t* rng, hipStream_t st) {
   if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
   int rc;
-  if (!drop && L.RF == inv_m_rf<NH>()) {               // eval: matrix-core inverse
+  if (!drop && L.RF == inv_m_rf<NH>() && L.PMB == (NH + 6) * 256 + (NH - 1) * 16 + 96) {   // eval: matrix cores
     size_t lds_m = sizeof(float) * (size_t)(2 * RING);
     const dim3 grid_m((unsigned)((N + INV_M_SPB - 1) / INV_M_SPB));
     if (L.Da <= 12 && L.Db <= 12) {
@@ -2096,6 +2209,8 @@ int inv_dispatch(const BcnfLayout& L, const float* pk, const float* zin, const f
   return check_launch();
 }
 
+long long slab_stride_of(const BcnfLayout& L) { return (long long)L.nb * L.sblk; }
+
 template <int NH>
 int bwd_dispatch(const BcnfLayout& L, const float* pk, const float* dz, const float* dldj, const float* dloss,
                  int nll, long long B, const float* arec, float* dy, float* d1, float* slab, long long stride,
@@ -2109,8 +2224,6 @@ int bwd_dispatch(const BcnfLayout& L, const float* pk, const float* dz, const fl
                      d1, slab, stride, part, loss_out, rng_w, guard);
   return check_launch();
 }
-
-long long slab_stride_of(const BcnfLayout& L) { return (long long)L.nb * L.sblk; }
 
 // split-K geometry of the W1 condition-part gradient
 int w1h_rows_per_split(long long) { return KC; }   // one LDS chunk of rows per split

@@ -46,6 +46,12 @@ __device__ __forceinline__ void body(float& a, float& b, float& c, float& d, flo
                  ADPP2(1) ADPP2(2) ADPP2(3) ADPP2(4) ADPP2(5) ADPP2(6) ADPP2(7) ADPP2(8) ADPP2(9) ADPP2(10)
                  ADPP2(11) ADPP2(12) ADPP2(13) ADPP2(14) ADPP2(15) ADPP2(1)
                  : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "v"(x), "v"(w));
+  } else if (KIND == 7) {   // 32 v_permlane16_swap_b32 (4 independent register pairs)
+#define PL4 "v_permlane16_swap_b32 %0, %1\n\tv_permlane16_swap_b32 %2, %3\n\tv_permlane16_swap_b32 %1, %0\n\tv_permlane16_swap_b32 %3, %2\n\t"
+    asm volatile(PL4 PL4 PL4 PL4 PL4 PL4 PL4 PL4 : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "v"(x), "v"(w));
+  } else if (KIND == 8) {   // the split-row combine, dependent: 8 x (2 add, nop, permlane16_swap, nop, add_dpp) = 32 VALU
+#define CMB "v_add_f32 %1, %0, %2\n\tv_add_f32 %3, %2, %0\n\ts_nop 1\n\tv_permlane16_swap_b32 %1, %3\n\ts_nop 1\n\tv_add_f32_dpp %0, %3, %1 row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+    asm volatile(CMB CMB CMB CMB CMB CMB CMB CMB : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "v"(x), "v"(w));
   } else if (KIND == 4) {   // 32 v_exp_f32 (independent)
     asm volatile(EXP4 EXP4 EXP4 EXP4 EXP4 EXP4 EXP4 EXP4 : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "v"(x), "v"(w));
   }
@@ -80,6 +86,8 @@ extern "C" int probe_run(int kind, int threads, int active, const float* in, uns
     case 4: hipLaunchKernelGGL(k_probe<4>, dim3(256), dim3(threads), 0, s, in, cyc, out, active); break;
     case 5: hipLaunchKernelGGL(k_probe<5>, dim3(256), dim3(threads), 0, s, in, cyc, out, active); break;
     case 6: hipLaunchKernelGGL(k_probe<6>, dim3(256), dim3(threads), 0, s, in, cyc, out, active); break;
+    case 7: hipLaunchKernelGGL(k_probe<7>, dim3(256), dim3(threads), 0, s, in, cyc, out, active); break;
+    case 8: hipLaunchKernelGGL(k_probe<8>, dim3(256), dim3(threads), 0, s, in, cyc, out, active); break;
     default: return -1;
   }
   return (int)hipGetLastError();

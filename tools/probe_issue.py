@@ -12,8 +12,11 @@ inp = torch.rand(128, device=dev) * 0.01
 cyc = torch.zeros(256 * 16, dtype=torch.int64, device=dev)
 out = torch.zeros(256 * 512, device=dev)
 st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-names = ["fmac x4 indep", "fmac_dpp 2 acc", "fmac_dpp 4 acc", "fmac dependent", "v_exp indep", "v_pk_fma indep", "add_dpp 2 acc"]
-for kind, name in enumerate(names):
+names = ["fmac x4 indep", "fmac_dpp 2 acc", "fmac_dpp 4 acc", "fmac dependent", "v_exp indep", "v_pk_fma indep", "add_dpp 2 acc", "permlane16_swap", "combine chain"]
+import sys
+kinds = [int(k) for k in sys.argv[1:]] or list(range(len(names)))
+for kind in kinds:
+    name = names[kind]
     for threads, active in ((256, 4), (512, 4), (512, 8)):
         for _ in range(3):
             cyc.zero_()
