@@ -451,11 +451,13 @@ def main():
             del step, model, data
             torch.cuda.empty_cache()
             sub = line.setdefault("secondary", {})
-            for wl, steps in (("fc_large", 8), ("lstm_large", 8), ("sample", 5)):
+            for wl, steps in (("fc_large", 8), ("lstm_large", 8), ("sample", 10)):
                 t_sub = time.perf_counter()
                 try:
                     if wl == "sample":
-                        sub[wl] = run_sample(WORKLOADS[wl][1], steps, 2, 1, 0, device, cpu=not args.no_cpu_baseline)
+                        # 10 warm-up draws (~20 ms): the first launches after the FC_large / LSTM_large sub-lines
+                        # run while the clocks settle (k_inverse_mfma 1.81 -> 1.57 ms over 13 launches, r03i trace)
+                        sub[wl] = run_sample(WORKLOADS[wl][1], steps, 10, 1, 0, device, cpu=not args.no_cpu_baseline)
                     else:
                         sub[wl] = run_wide(wl, WORKLOADS[wl][1], steps, 3, 1, 0, device, graph=not args.no_graph,
                                            kernel_iters=3, cpu=not args.no_cpu_baseline,
