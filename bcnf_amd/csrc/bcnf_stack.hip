@@ -1236,6 +1236,9 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
     }
   } else {
     const int tid = t8;
+#ifdef BCNF_PRIO_F
+    __builtin_amdgcn_s_setprio(BCNF_PRIO_F);
+#endif
     const int D = L.D, Da = L.Da, Db = L.Db;
     float ya = (j < Da) ? y[bc * D + j] : 0.f;
     float yb = (j < Db) ? y[bc * D + Da + j] : 0.f;
@@ -1748,6 +1751,9 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
   }
 
   if (helper) {
+#ifdef BCNF_PRIO_B
+    __builtin_amdgcn_s_setprio(BCNF_PRIO_B);
+#endif
     const int hw = __builtin_amdgcn_readfirstlane(t8 >> 6);
     float* slab = slab_all + (long long)blockIdx.x * slab_stride;
     // activation records [k][workgroup][AR/4][256 threads] float4 (k_forward)

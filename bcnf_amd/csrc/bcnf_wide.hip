@@ -311,6 +311,7 @@ struct GemmArgs {
   // flat-gradient group base (EPI_LINGRAD with use_cb, EPI_ROWMAP) of virtual block v = g1 (real block v / cb_S,
   // side v % cb_S): C + (v / cb_S) * cb_stride + (v / cb_S < cb_nb - 1 ? cb_an : 0) + (v % cb_S) * cb_side + g0 * sC0
   long long cb_stride, cb_side; int cb_an, cb_nb, cb_S, use_cb;
+  int cb_v0;                    // virtual block of group g1 = 0 / row 0 (a block range of the backward; else 0)
   // EPI_ROWMAP: row r -> virtual block v = r / rm_hp, n = r % rm_hp (skipped when >= rm_h):
   //   C + cb(v) + rm_off[side] + n * rm_ld[side] + col
   int rm_hp, rm_h; long long rm_off[2], rm_ld[2];
@@ -434,7 +435,7 @@ __device__ __forceinline__ void epi4(const GemmArgs& g, float* __restrict__ Cg, 
       if (col < g.wcols) Cg[(long long)row * g.ldc + col] = v[rr];
       else if (col == g.wcols) Cg[g.boff + row] = v[rr];
     } else {   // EPI_ROWMAP
-      const int vb = row / g.rm_hp, n = row - vb * g.rm_hp;
+      const int vr = row / g.rm_hp, n = row - vr * g.rm_hp, vb = vr + g.cb_v0;
       if (n < g.rm_h) {
         const int blk = vb / g.cb_S, sd = vb - blk * g.cb_S;
         Cg[(long long)blk * g.cb_stride + ((blk < g.cb_nb - 1) ? g.cb_an : 0) + sd * g.cb_side + g.rm_off[sd] +
@@ -456,7 +457,7 @@ __device__ __forceinline__ EpiCtx epi_ctx(const GemmArgs& g, int g1, int g0) {
   EpiCtx e;
   e.C = g.C;
   if (EPI == EPI_LINGRAD && g.use_cb) {
-    const int blk = g1 / g.cb_S, sd = g1 - blk * g.cb_S;
+    const int blk = (g1 + g.cb_v0) / g.cb_S, sd = (g1 + g.cb_v0) - blk * g.cb_S;
     e.C += blk * g.cb_stride + ((blk < g.cb_nb - 1) ? g.cb_an : 0) + sd * g.cb_side + g0 * g.sC0;
   } else if (EPI == EPI_ROWMAP) {
     // the row map carries the whole offset
@@ -1452,10 +1453,10 @@ __global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const Lin
 __global__ __launch_bounds__(WWG) void k_wactnorm_grad(const WideLayout L, const float* __restrict__ ANP, long long B,
                                                        const float* __restrict__ dldj, const float* __restrict__ zn,
                                                        const float* __restrict__ dvals, int nll,
-                                                       const float* __restrict__ prm, float* __restrict__ dprm) {
+                                                       const float* __restrict__ prm, float* __restrict__ dprm, int k0) {
   __shared__ float red[WWG];
   __shared__ float dsum_s;
-  const int k = blockIdx.x, tid = threadIdx.x;
+  const int k = k0 + (int)blockIdx.x, tid = threadIdx.x;
   const int ncol = 2 * L.D;
   const float* P = ANP + (long long)k * B * L.AP;
   // sum of dldj over the batch
@@ -1923,14 +1924,25 @@ int wide_forward(const WideLayout& L, const float* prm, const float* pk, const f
   return BCNF_OK;
 }
 
+// Real blocks [blo, bhi) of the backward: the chain iterations that complete them, then their parameter gradients
+// (canonical flat, every element written exactly once). The whole backward is [0, nb). A data-parallel caller may
+// split it into descending contiguous ranges, the first with bhi = nb, and reduce each range's gradient slice while
+// the next range runs (bcnf_wide_fold_backward_range); the range with blo = 0 also runs what needs every block (fold:
+// the feature-Linear gradients and dL/dx; else dL/dh). The chain iteration v finishes virtual block v (tail-B: dZ_0)
+// and starts v - 1 (head-B, then its hidden-layer chain), so a range runs v = (vhi == nv ? nv : vhi - 1) .. vlo.
+// Per-element results do not depend on the split: every GEMM keeps its K order, the split-K partials of the small
+// Linear gradients go to the finished range's G slots (dead once its chain has run).
 int wide_backward(const WideLayout& L, const float* prm, const float* pk, const float* h, const float* zn,
                   const float* dz, const float* dldj, const float* dvals, int nll, long long B, float* ws, float* dy,
-                  float* dh, float* dprm, hipStream_t st, const WideFold* fold = nullptr) {
+                  float* dh, float* dprm, hipStream_t st, const WideFold* fold = nullptr, int blo = 0, int bhi = -1) {
   if (B == 0) return BCNF_OK;
+  if (bhi < 0) bhi = L.nb;
+  if (blo < 0 || bhi > L.nb || blo >= bhi) return BCNF_ERR_ARG;
   ensure_lds_attrs();
   const WideWs w = carve(L, B, true, ws);
   const long long slab = B * L.HP;
   const long long ld0 = (long long)L.nv * L.HP;
+  const int vlo = blo * L.S, vhi = bhi * L.S, nvr = vhi - vlo;
   auto Gptr = [&](int v, int l) -> float* { return w.G + ((long long)v * L.NH + l) * slab; };
   // dZ_l (l = 1..NH-1) of virtual block v; dZ_0 of v is the column slice v*HP of dZ0_all
   auto dZptr = [&](int v, int l, long long* ld) -> float* {
@@ -1941,7 +1953,7 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
     *ld = L.HP;
     return w.dZ + ((long long)v * (L.NH - 1) + (l - 1)) * slab;
   };
-  for (int v = L.nv; v >= 0; --v) {
+  for (int v = vhi == L.nv ? L.nv : vhi - 1; v >= vlo; --v) {
     // link: tail-B(v) (v < nv), head-B(v-1)
     LinkBArgs a;
     memset(&a, 0, sizeof(a));
@@ -1988,11 +2000,14 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
   int rc = BCNF_OK;
   const float* hp = fold ? nullptr : padded_h(L, h, B, w.Hp, st, &rc);
   WCHK(rc);
-  if (fold) {   // Gx = dZ0_all^T x1 (the condition-side gradients below all go through it)
-    GemmArgs g = gemm_args(L.tiling, L.nv * L.HP, fold->Xp, (int)B, w.dZ0, ld0, fold->x1, fold->Xp, fold->gx, fold->Xp);
+  float* const gsc = Gptr(vlo, 0);                  // the range's G slots: split-K scratch once its chain has run
+  const long long gsc_floats = (long long)nvr * L.NH * slab;
+  if (fold) {   // Gx rows of the range = dZ0_all[:, range]^T x1 (the condition-side gradients below go through it)
+    GemmArgs g = gemm_args(L.tiling, nvr * L.HP, fold->Xp, (int)B, w.dZ0 + (long long)vlo * L.HP, ld0, fold->x1,
+                           fold->Xp, fold->gx + (long long)vlo * L.HP * fold->Xp, fold->Xp);
     WCHK((gemm<false, false, EPI_STORE>(g, 1, st)));
   }
-  // ---- parameter gradients (canonical flat, every element written exactly once) ----
+  // ---- parameter gradients of the range (canonical flat, every element written exactly once) ----
   if (dprm) {
     auto flat_groups = [&](GemmArgs& g) {   // group g1 = virtual block (or real block with S = 1 semantics)
       g.use_cb = 1;
@@ -2001,7 +2016,8 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
       g.cb_nb = L.nb;
     };
     if (L.NH > 1) {   // hidden Linears of every virtual block in one grouped launch: [dW_l | db_l] = dZ_l^T [A_{l-1} | 1]
-      GemmArgs g = gemm_args(L.tiling, L.H, L.H + 1, (int)B, w.dZ, L.HP, w.A, L.HP, dprm + L.lin_w[0][1], L.H);
+      GemmArgs g = gemm_args(L.tiling, L.H, L.H + 1, (int)B, w.dZ + (long long)vlo * (L.NH - 1) * slab, L.HP,
+                             w.A + (long long)vlo * L.NH * slab, L.HP, dprm + L.lin_w[0][1], L.H);
       g.G0 = L.NH - 1;
       g.sA1 = (long long)(L.NH - 1) * slab;
       g.sA0 = slab;
@@ -2009,43 +2025,50 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
       g.sB0 = slab;
       flat_groups(g);
       g.cb_S = L.S;
+      g.cb_v0 = vlo;
       g.cb_side = L.mlp[0] + (L.S == 2 ? L.lin_w[1][1] - L.lin_w[0][1] : 0);
       g.sC0 = (L.NH > 2) ? (L.lin_w[0][2] - L.lin_w[0][1]) : 0;
       g.wcols = L.H;
       g.boff = (long long)L.H * L.H;
-      WCHK((gemm<false, false, EPI_LINGRAD>(g, L.nv * (L.NH - 1), st)));
+      WCHK((gemm<false, false, EPI_LINGRAD>(g, nvr * (L.NH - 1), st)));
     }
     for (int sd = 0; sd < L.S; ++sd) {
       {   // last Linear of every block's side-sd half: [dW | db] = dO^T [A_{NH-1} | 1]
-        GemmArgs g = gemm_args(L.tiling, 2 * L.nout[sd], L.H + 1, (int)B, w.O + (long long)sd * B * L.OP, L.OP,
-                               w.A + ((long long)sd * L.NH + L.NH - 1) * slab, L.HP,
+        GemmArgs g = gemm_args(L.tiling, 2 * L.nout[sd], L.H + 1, (int)B,
+                               w.O + ((long long)blo * L.S + sd) * B * L.OP, L.OP,
+                               w.A + (((long long)blo * L.S + sd) * L.NH + L.NH - 1) * slab, L.HP,
                                dprm + (sd ? L.mlp[0] : 0) + L.lin_w[sd][L.NH], L.H);
         g.sA1 = (long long)L.S * B * L.OP;
         g.sB1 = (long long)L.S * L.NH * slab;
         flat_groups(g);
+        g.cb_v0 = blo;
         g.wcols = L.H;
         g.boff = (long long)2 * L.nout[sd] * L.H;
-        WCHK(lingrad_splitk(g, L.nb, w.G, w.G ? (long long)L.nv * L.NH * slab : 0, st));
+        WCHK(lingrad_splitk(g, bhi - blo, gsc, gsc_floats, st));
       }
       {   // Linear-1, input columns + bias: [dW0[:, :nin] | db0] = dZ_0^T [u_in | 1]
-        GemmArgs g = gemm_args(L.tiling, L.H, L.nin[sd] + 1, (int)B, w.dZ0 + (long long)sd * L.HP, ld0,
-                               w.U + (long long)sd * B * L.UP, L.UP, dprm + (sd ? L.mlp[0] : 0) + L.lin_w[sd][0],
-                               L.in0[sd]);
+        GemmArgs g = gemm_args(L.tiling, L.H, L.nin[sd] + 1, (int)B, w.dZ0 + ((long long)blo * L.S + sd) * L.HP, ld0,
+                               w.U + ((long long)blo * L.S + sd) * B * L.UP, L.UP,
+                               dprm + (sd ? L.mlp[0] : 0) + L.lin_w[sd][0], L.in0[sd]);
         g.sA1 = (long long)L.S * L.HP;
         g.sB1 = (long long)L.S * B * L.UP;
         flat_groups(g);
+        g.cb_v0 = blo;
         g.wcols = L.nin[sd];
         g.boff = (long long)L.H * L.in0[sd];
-        WCHK(lingrad_splitk(g, L.nb, w.G, w.G ? (long long)L.nv * L.NH * slab : 0, st));
+        WCHK(lingrad_splitk(g, bhi - blo, gsc, gsc_floats, st));
       }
     }
-    {   // Linear-1, condition columns of every virtual block in one GEMM: dW0h_all = dZ0_all^T h (folded: Gx wfb^T)
-      GemmArgs g = fold ? gemm_args(L.tiling, L.nv * L.HP, L.C, fold->Xp, fold->gx, fold->Xp, fold->wfb, fold->Xp, dprm, 0)
-                        : gemm_args(L.tiling, L.nv * L.HP, L.C, (int)B, w.dZ0, ld0, hp, L.Cp, dprm, 0);
+    {   // Linear-1, condition columns of the range's virtual blocks in one GEMM: dW0h = dZ0^T h (folded: Gx wfb^T)
+      GemmArgs g = fold ? gemm_args(L.tiling, nvr * L.HP, L.C, fold->Xp, fold->gx + (long long)vlo * L.HP * fold->Xp,
+                                    fold->Xp, fold->wfb, fold->Xp, dprm, 0)
+                        : gemm_args(L.tiling, nvr * L.HP, L.C, (int)B, w.dZ0 + (long long)vlo * L.HP, ld0, hp, L.Cp,
+                                    dprm, 0);
       g.cb_stride = L.blk_stride;
       g.cb_an = L.an;
       g.cb_nb = L.nb;
       g.cb_S = L.S;
+      g.cb_v0 = vlo;
       g.cb_side = L.mlp[0];
       g.rm_hp = L.HP;
       g.rm_h = L.H;
@@ -2059,11 +2082,14 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
       else
         WCHK((gemm<false, false, EPI_ROWMAP>(g, 1, st)));
     }
-    if (L.an && L.nb > 1) {
-      hipLaunchKernelGGL(k_wactnorm_grad, dim3(L.nb - 1), dim3(WWG), 0, st, L, w.ANP, B, dldj, zn, dvals, nll, prm, dprm);
+    const int an_hi = bhi < L.nb - 1 ? bhi : L.nb - 1;   // ActNorm k sits in real block k (the last block has none)
+    if (L.an && an_hi > blo) {
+      hipLaunchKernelGGL(k_wactnorm_grad, dim3(an_hi - blo), dim3(WWG), 0, st, L, w.ANP, B, dldj, zn, dvals, nll, prm,
+                         dprm, blo);
       WCHK(bcnf_rt::launched());
     }
   }
+  if (blo > 0) return BCNF_OK;
   if (fold) {
     // split K = nv * HP per virtual block; partials in the G region (dead once the chain has run)
     const long long gfl = (long long)L.nv * L.NH * slab;
@@ -2280,6 +2306,29 @@ int bcnf_wide_fold_backward(const BcnfStackDesc* desc, const float* params, cons
                        (float*)workspace, nullptr, nullptr, dparams, (hipStream_t)stream, &f);
 }
 
+int bcnf_wide_fold_backward_range(const BcnfStackDesc* desc, const float* params, const void* packed, const float* x1,
+                                  int32_t xp, const float* wfb, const float* wcb, const float* z, const float* dloss,
+                                  int64_t batch, void* workspace, float* gx_scratch, float* dparams, float* dwfb,
+                                  float* dx, int32_t block_lo, int32_t block_hi, void* stream) {
+  WideLayout L;
+  WCHK(wide_layout(desc, &L));
+  if (batch < 1 || !params || !packed || !x1 || !wfb || !wcb || !z || !workspace || !gx_scratch || !dparams ||
+      xp < 4 || (xp & 3) || !aligned16(x1) || !aligned16(wfb) || !aligned16(wcb) || !aligned16(gx_scratch) ||
+      (dwfb && !aligned16(dwfb)) || (dx && !aligned16(dx)) || block_lo < 0 || block_hi > L.nb || block_lo >= block_hi)
+    return BCNF_ERR_ARG;
+  WideFold f = {x1, wfb, wcb, gx_scratch, dwfb, dx, (int)xp};
+  return wide_backward(L, params, (const float*)packed, nullptr, z, nullptr, nullptr, dloss, 1, batch,
+                       (float*)workspace, nullptr, nullptr, dparams, (hipStream_t)stream, &f, block_lo, block_hi);
+}
+
+int bcnf_wide_block_offset(const BcnfStackDesc* desc, int32_t block, int64_t* offset) {
+  WideLayout L;
+  WCHK(wide_layout(desc, &L));
+  if (!offset || block < 0 || block > L.nb) return BCNF_ERR_ARG;
+  *offset = block == L.nb ? (int64_t)L.n_trainable : (int64_t)block * L.blk_stride;
+  return BCNF_OK;
+}
+
 int bcnf_wide_backward(const BcnfStackDesc* desc, const float* params, const void* packed, const float* h,
                        const float* z, const float* dz, const float* dldj, const float* dloss, int32_t nll,
                        int64_t batch, void* workspace, float* dy, float* dh, float* dparams, void* stream) {
@@ -2288,7 +2337,7 @@ int bcnf_wide_backward(const BcnfStackDesc* desc, const float* params, const voi
   if (batch < 0) return BCNF_ERR_ARG;
   if (!params || !packed || !h || !workspace || (nll && !z)) return BCNF_ERR_ARG;
   if (batch == 0) {
-    if (dparams) (void)hipMemsetAsync(dparams, 0, L.n_trainable * 4, (hipStream_t)stream);
+    if (dparams) return bcnf_rt::hip_status(hipMemsetAsync(dparams, 0, L.n_trainable * 4, (hipStream_t)stream));
     return BCNF_OK;
   }
   return wide_backward(L, params, (const float*)packed, h, z, dz, dldj, dloss, nll, batch, (float*)workspace, dy, dh,

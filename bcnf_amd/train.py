@@ -51,7 +51,7 @@ GUARD_CHECK, GUARD_DIVERGED, GUARD_HALTED, GUARD_CHECK_GLOBAL, GUARD_WORDS = 0, 
 
 class TrainStep:
     def __init__(self, model, lr: float = 2e-4, hybrid_weight: float = 0.0, capture: bool = True,
-                 max_norm: float = 1.0, process_group=None):
+                 max_norm: float = 1.0, process_group=None, overlap_ranges: int = 0):
         if getattr(model, "_path", "fused") != "fused":
             raise NotImplementedError(
                 f"bcnf_amd.TrainStep drives the fused Linear + GELU coupling kernels; a layer={model._fam[0]!r} model "
@@ -83,6 +83,16 @@ class TrainStep:
         self._gvals = None      # data parallel: the all-reduced (loss, nll, mse) -- a view of the bucket tail
         self._packed_inplace = False   # the last bucket pack found the gradients already in place
         self._host_cursor = 0   # host mirror of the epoch cursor (the history row of the next step)
+        # data parallel, wide family: the backward runs in `overlap_ranges` block ranges and each finished range's
+        # bucket slice is all-reduced (async) while the rest of the backward runs; eager steps (the collectives are
+        # issued between kernel launches, outside any captured graph), joined before the update
+        self.overlap_ranges = 0
+        self._works = []        # in-flight all-reduces of bucket slices, and the slices [lo, hi) they cover
+        self._reduced = []
+        from bcnf_amd.wide import WideStack
+        if self.world > 1 and overlap_ranges > 0 and isinstance(getattr(model, "fused", None), WideStack):
+            self.overlap_ranges = min(int(overlap_ranges), model.fused.cfg.n_blocks)
+            self.capture = False
         dev = self.params[0].device
         self._guard = None
         self._hist = None
@@ -114,20 +124,31 @@ class TrainStep:
         return torch.stack([loss.detach(), nll.detach(), mse.detach()])
 
     def _pack_grads(self):
-        """All gradients -> one contiguous bucket (one launch), so the data-parallel exchange is ONE collective
-        per step whatever the number of feature-network tensors (FC_large: 17, LSTM_large: 19)."""
+        """All gradients -> one contiguous bucket, so the data-parallel exchange is ONE collective per step whatever
+        the number of feature-network tensors (FC_large: 17, LSTM_large: 19). Gradients the backward already wrote
+        into their bucket slots (the folded backwards, FusedStack / WideStack.grad_bucket) are not copied."""
         grads = [p.grad for p in self.params]
         if any(g is None for g in grads):
             raise RuntimeError("bcnf_amd TrainStep: a parameter received no gradient")
         if self._bucket is None:
             self._alloc_bucket(grads[0].device)
-        base, off, inplace = self._bucket.data_ptr(), 0, True
-        for g in grads:                     # the folded backward wrote straight into the bucket (_setup_bucket)
-            inplace = inplace and g.is_contiguous() and g.data_ptr() == base + 4 * off
+        base, off, slots = self._bucket.data_ptr(), 0, []
+        for g in grads:
+            slots.append((g, off, g.is_contiguous() and g.data_ptr() == base + 4 * off))
             off += g.numel()
-        self._packed_inplace = inplace
-        if not inplace:
+        self._packed_inplace = all(ok for _, _, ok in slots)
+        if self._packed_inplace:
+            return
+        if not any(ok for _, _, ok in slots):
             torch.cat([g.reshape(-1) for g in grads], out=self._bucket[:self._n_grad])
+            return
+        for g, o, ok in slots:
+            if ok:
+                continue
+            if any(lo < o + g.numel() and o < hi for lo, hi in self._reduced):
+                raise RuntimeError("bcnf_amd TrainStep: a gradient of an already all-reduced bucket slice is not in "
+                                   "its slot")
+            self._bucket[o:o + g.numel()].copy_(g.reshape(-1))
 
     def _alloc_bucket(self, dev):
         """The gradient bucket + a 4-float tail holding the step's logged (loss, nll, mse): the one all-reduce of the
@@ -137,8 +158,10 @@ class TrainStep:
         self._gvals = self._bucket[self._n_grad:self._n_grad + 3]
 
     def _setup_bucket(self):
-        """Data parallel: allocate the gradient bucket up front and, when the model folds its feature Linear, let
-        the folded backward write its gradients into it (FusedStack.grad_bucket): no copy before the all-reduce."""
+        """Data parallel: allocate the gradient bucket up front and let the folded backwards write their gradients
+        into it (no copy before the all-reduce): the small family's (coupling + feature Linear,
+        FusedStack.grad_bucket), the wide family's coupling gradients (WideStack.grad_bucket), the latter range by
+        range when overlap_ranges is set."""
         if self.world == 1 or self._bucket is not None:
             return
         self._alloc_bucket(self.params[0].device)
@@ -150,6 +173,18 @@ class TrainStep:
             offs[id(p)] = off
             off += p.numel()
         fp = self.model.fused.flat_param
+        from bcnf_amd.wide import WideStack
+        if isinstance(self.model.fused, WideStack):
+            if id(fp) not in offs:
+                return
+            st = self.model.fused
+            st.grad_bucket = (self._bucket, offs[id(fp)])
+            if self.overlap_ranges > 0:
+                nb, r = st.cfg.n_blocks, self.overlap_ranges
+                cuts = [round(nb * i / r) for i in range(r + 1)]
+                st.range_blocks = [(cuts[i - 1], cuts[i]) for i in range(r, 0, -1) if cuts[i] > cuts[i - 1]]
+                st.on_range = self._reduce_range
+            return
         if len(self.params) != (3 if lin.bias is not None else 2) or id(fp) not in offs or id(lin.weight) not in offs:
             return
         self.model.fused.grad_bucket = (self._bucket, (offs[id(fp)], offs[id(lin.weight)],
@@ -165,8 +200,26 @@ class TrainStep:
 
     def _reduce_bucket(self):
         """Sum over ranks of the gradient bucket: ONE RCCL all-reduce per step (the 1/world scaling runs inside
-        the captured update segment, _scale_bucket)."""
-        dist.all_reduce(self._bucket, op=dist.ReduceOp.SUM, group=self.pg)
+        the captured update segment, _scale_bucket). With slices already in flight (overlap_ranges), the rest of the
+        bucket -- the feature-network gradients and the logged values -- then a join on every slice."""
+        if not self._works:
+            dist.all_reduce(self._bucket, op=dist.ReduceOp.SUM, group=self.pg)
+            return
+        lo = 0
+        for a, b in sorted(self._reduced) + [(self._bucket.numel(), self._bucket.numel())]:
+            if a > lo:
+                dist.all_reduce(self._bucket[lo:a], op=dist.ReduceOp.SUM, group=self.pg)
+            lo = max(lo, b)
+        for w in self._works:
+            w.wait()
+        self._works.clear()
+        self._reduced.clear()
+
+    def _reduce_range(self, lo: int, hi: int):
+        """A finished block range's bucket slice [lo, hi): its all-reduce runs while the backward continues
+        (WideStack.on_range); the update joins it (_reduce_bucket)."""
+        self._works.append(dist.all_reduce(self._bucket[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+        self._reduced.append((lo, hi))
 
     def _scale_bucket(self):
         self._bucket.mul_(1.0 / self.world)

@@ -193,6 +193,18 @@ class WideStack(FusedStack):
             self._finalize(ws, B, vals, training)
         return z, ldj, vals, (ws, pk, x1, wfb, wcb, xp, x.shape[1])
 
+    # Data parallel (TrainStep): (bucket, offset) -- the coupling gradients land in bucket[offset:offset + n], a view
+    # that autograd adopts as .grad; and, with range_blocks (descending real-block ranges covering [0, nb)), the
+    # backward runs range by range and calls on_range(lo, hi) with each finished range's bucket slice [lo, hi), so
+    # the slice's all-reduce overlaps the rest of the backward (bcnf_wide_fold_backward_range).
+    grad_bucket = None
+    range_blocks = None
+    on_range = None
+
+    def block_offset(self, block: int) -> int:
+        """Canonical flat offset of real block `block` (block = nb: the parameter count)."""
+        return N.query_i64(N.lib().bcnf_wide_block_offset, self._pdesc, ctypes.c_int32(block))
+
     def launch_fold_nll_backward(self, z, dvals, training: bool, saved, want_x: bool, finalize_into=None):
         ws, pk, x1, wfb, wcb, xp, X = saved
         B = z.shape[0]
@@ -200,14 +212,26 @@ class WideStack(FusedStack):
         if finalize_into is not None:
             self._finalize(ws, B, finalize_into, training)
         gx = torch.empty_like(wcb)
-        dparams = torch.empty_like(self.flat)
+        off = None
+        if self.grad_bucket is not None:
+            bucket, off = self.grad_bucket
+            dparams = bucket.narrow(0, off, self.flat.numel()).view_as(self.flat)
+        else:
+            dparams = torch.empty_like(self.flat)
         dwfb = torch.empty_like(wfb)
         dx = torch.empty((B, xp), dtype=torch.float32, device=dev) if want_x else None
-        rc = self._timed("k_backward", lambda: N.lib().bcnf_wide_fold_backward(
-            self._pdesc, N.ptr(self.flat), N.ptr(pk), N.ptr(x1), ctypes.c_int32(xp), N.ptr(wfb), N.ptr(wcb), N.ptr(z),
-            N.ptr(dvals), ctypes.c_int64(B), N.ptr(ws), N.ptr(gx), N.ptr(dparams), N.ptr(dwfb), N.ptr(dx),
-            N.stream_handle(dev)))
-        N.check(rc, "bcnf_wide_fold_backward")
+        L = N.lib()
+        stream = N.stream_handle(dev)
+        args = (self._pdesc, N.ptr(self.flat), N.ptr(pk), N.ptr(x1), ctypes.c_int32(xp), N.ptr(wfb), N.ptr(wcb), N.ptr(z),
+                N.ptr(dvals), ctypes.c_int64(B), N.ptr(ws), N.ptr(gx), N.ptr(dparams), N.ptr(dwfb), N.ptr(dx))
+        if self.range_blocks and self.on_range is not None and off is not None:
+            for lo, hi in self.range_blocks:
+                N.check(L.bcnf_wide_fold_backward_range(*args, ctypes.c_int32(lo), ctypes.c_int32(hi), stream),
+                        "bcnf_wide_fold_backward_range")
+                self.on_range(off + self.block_offset(lo), off + self.block_offset(hi))
+        else:
+            rc = self._timed("k_backward", lambda: L.bcnf_wide_fold_backward(*args, stream))
+            N.check(rc, "bcnf_wide_fold_backward")
         return dparams, dwfb[:, :X], dwfb[:, X], (dx[:, :X] if want_x else None)
 
     @torch.no_grad()

@@ -358,6 +358,20 @@ int bcnf_wide_fold_backward(const BcnfStackDesc* desc, const float* params, cons
                             int32_t xp, const float* wfb, const float* wcb, const float* z, const float* dloss,
                             int64_t batch, void* workspace, float* gx_scratch, float* dparams, float* dwfb, float* dx,
                             void* stream);
+/* bcnf_wide_fold_backward split over real blocks, for data parallelism that overlaps the gradient exchange with the
+ * rest of the backward (trainer.py:244-277 is the single-process step it splits): one call per
+ * contiguous block range [block_lo, block_hi), in descending order over one forward's workspace, the first with
+ * block_hi = nb and the last with block_lo = 0. A call runs the backward chain until blocks [block_lo, block_hi) are
+ * complete and writes their canonical parameter gradients, dparams[bcnf_wide_block_offset(block_lo) ..
+ * bcnf_wide_block_offset(block_hi)); the block_lo = 0 call also writes dwfb and dx. Results equal one
+ * bcnf_wide_fold_backward call bit for bit; calls out of that order leave the outputs undefined. */
+int bcnf_wide_fold_backward_range(const BcnfStackDesc* desc, const float* params, const void* packed, const float* x1,
+                                  int32_t xp, const float* wfb, const float* wcb, const float* z, const float* dloss,
+                                  int64_t batch, void* workspace, float* gx_scratch, float* dparams, float* dwfb,
+                                  float* dx, int32_t block_lo, int32_t block_hi, void* stream);
+/* Canonical flat offset of real block `block`'s first trainable parameter (its ActNorm, cnf.py:296-335 module order);
+ * block = nb gives the parameter count. Host-only. */
+int bcnf_wide_block_offset(const BcnfStackDesc* desc, int32_t block, int64_t* offset);
 /* Rows of the padded projection (nv*HP) of a wide stack. */
 int bcnf_wide_proj_rows(const BcnfStackDesc* desc, int64_t* rows);
 /* Inverse: as bcnf_stack_inverse (cond_index selects feature rows; scratch = bcnf_wide_inverse_scratch_bytes). */

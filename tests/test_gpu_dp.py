@@ -50,7 +50,9 @@ def _worker(rank, world, port, cfg, q, mode="step"):
     try:
         from bcnf_amd.train import TrainStep
         m = _model(cfg)
-        step = TrainStep(m, lr=1e-3, capture=True)
+        step = TrainStep(m, lr=1e-3, capture=True, overlap_ranges=2 if mode == "overlap" else 0)
+        if mode == "overlap":   # wide family: eager steps, the coupling gradient all-reduced in 2 block ranges
+            assert step.overlap_ranges == 2 and not step.capture
         step.broadcast_parameters()
         y, t = _data()
         n = y.shape[0] // world
@@ -88,8 +90,9 @@ def _worker(rank, world, port, cfg, q, mode="step"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["step", "epoch"])
-@pytest.mark.parametrize("cfg", [CFG, WIDE], ids=["small_family", "wide_family"])
+@pytest.mark.parametrize("mode,cfg", [("step", CFG), ("epoch", CFG), ("step", WIDE), ("epoch", WIDE),
+                                      ("overlap", WIDE)],
+                         ids=["small_step", "small_epoch", "wide_step", "wide_epoch", "wide_overlap_ranges"])
 def test_two_rank_step_equals_union_batch_step(cfg, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
