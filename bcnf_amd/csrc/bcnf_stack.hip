@@ -1447,9 +1447,15 @@ constexpr int inv_m_rf() {                          // L.RF of this NH (round_re
   return n;
 }
 
-// gelu_f on a pair of values with packed fp32 arithmetic (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth per
-// instruction); the same operations per element as gelu_f, so the same results.
+// gelu_f's approximation on a pair of values with packed fp32 arithmetic (v_pk_fma_f32 / v_pk_mul_f32: two lanes'
+// worth per instruction); the same erfc fit, combined as max(x, 0) - |x| h (one rounding fewer than x (1 - h)).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+// max(x, 0) as ONE v_max_f32 (fmaxf under IEEE mode adds a canonicalising max per operand)
+__device__ __forceinline__ float relu_f(float x) {
+  float r;
+  asm("v_max_f32_e32 %0, 0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
 __device__ __forceinline__ f32x2 gelu_f2(f32x2 x) {
   // scalar FMAs here: VOP3 takes |x| as a free source modifier (VOP3P has none)
   const f32x2 den = {fmaf(2.616295218e-01f, fabsf(x.x), 1.0f), fmaf(2.616295218e-01f, fabsf(x.y), 1.0f)};
@@ -1463,10 +1469,10 @@ __device__ __forceinline__ f32x2 gelu_f2(f32x2 x) {
   q = __builtin_elementwise_fma(q, t, f32x2{1.041427255e-01f, 1.041427255e-01f});
   const f32x2 e = (x * x) * f32x2{-0.72134752044448170368f, -0.72134752044448170368f};
   const f32x2 ez = {__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+  // x Phi(x) = max(x, 0) - |x| h with h = erfc(|x| / sqrt 2) / 2 = t Q(t) e^{-x^2/2}: one VOP3 FMA per element
+  // (|x| as a free source modifier) instead of the sign select, 1 - h and the product x cdf
   const f32x2 h = (t * q) * ez;
-  const f32x2 g = f32x2{1.0f, 1.0f} - h;
-  const f32x2 cdf = {x.x < 0.f ? h.x : g.x, x.y < 0.f ? h.y : g.y};
-  return x * cdf;
+  return f32x2{fmaf(-fabsf(x.x), h.x, relu_f(x.x)), fmaf(-fabsf(x.y), h.y, relu_f(x.y))};
 }
 __device__ __forceinline__ void gelu4(floatx4& a) {
   const f32x2 lo = gelu_f2(f32x2{a[0], a[1]}), hi = gelu_f2(f32x2{a[2], a[3]});

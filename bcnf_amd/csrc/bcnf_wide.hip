@@ -92,7 +92,7 @@ int wide_layout(const BcnfStackDesc* d, WideLayout* L) {
   for (int i = 1; i < d->n_hidden; ++i)
     if (d->hidden[i] != d->hidden[0]) return BCNF_ERR_UNSUPPORTED;     // equal widths (every shipped config)
   if (d->size > DM || d->n_conditions < 1 || d->hidden[0] > 8192) return BCNF_ERR_UNSUPPORTED;
-  if (d->gemm_tiling < 0 || d->gemm_tiling > 9) return BCNF_ERR_ARG;
+  if (d->gemm_tiling < 0 || d->gemm_tiling > 10) return BCNF_ERR_ARG;
   L->tiling = d->gemm_tiling;
   L->D = d->size;
   L->Da = (d->size + 1) / 2;
@@ -617,8 +617,15 @@ __global__ __launch_bounds__(WWG, 2) void k_wgemm(const GemmArgs g) {
 // k = 4q + s at MFMA step s. Finer N granularity than tiling A: e.g. BN = 48 tiles N = 528 exactly. NW = 8: two
 // waves per SIMD in one workgroup, so a wave's barrier / LDS / staging stalls run under its partner's MFMAs (the
 // small-M GEMMs of the wide family leave most CUs with one workgroup).
+// Two workgroups per CU only when the two LDS buffers fit twice in the CU's 160 KB (the 128 x 48 tile's 94 KB does
+// not: one workgroup per CU, declared as such).
+template <int BM, int BN, int BK, bool AKC, bool BKC, int NW>
+constexpr int wg16_occ() {
+  using IO = TileIO<BM, BN, BK, AKC, BKC, 64 * NW>;
+  return (NW == 4 && 2 * (IO::ASZ + IO::BSZ) * 4 <= 80 * 1024) ? 2 : 1;
+}
 template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI, int NW = 4>
-__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_wgemm16(const GemmArgs g) {
+__global__ __launch_bounds__(64 * NW, (wg16_occ<BM, BN, BK, AKC, BKC, NW>())) void k_wgemm16(const GemmArgs g) {
   using IO = TileIO<BM, BN, BK, AKC, BKC, 64 * NW>;
   constexpr int WM = BM / NW;
   constexpr int TI = WM / 16, TJ = BN / 16;
@@ -888,6 +895,139 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS, (S * (BM + BN) * 64 * 4 <= 80 
         const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         epi4<EPI>(g, e.C, e.X, rbase(i), colof(j), v, epi_rnd<EPI>(g, e, rbase(i), colof(j)), pre[i][j], RS);
       }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Tiling W: the workgroup's whole B band resident in LDS (K-contiguous A and B, K <= 768). On the chain shape
+// (M = 2048, N = K = 528) tiling C runs ~1.5 us per 64-deep K tile at ANY M (37 rows as at 2048): per-CU issue, not
+// bandwidth -- every K tile costs each SIMD 9 LDS-DMA pieces (60-185 issue cycles each beside MFMAs,
+// MI355X_MICROARCH.md) and a 12-wave barrier. Here the
+// 48-column B band (48 x K floats: 101 KB at K = 528) is copied into LDS ONCE by LDS-DMA at the start, one barrier,
+// and each wave then streams only its own 16 A rows straight into a P-deep register ring (one float4 per lane per
+// 16-deep K chunk; A rows are never shared between waves): inside the K loop there is no barrier, no DMA, and per
+// chunk one global load + 3 ds_read_b128 per 12 MFMAs. Band layout [column][S], S = K16 + 4 floats (S / 4 odd: the
+// 16 columns of a fragment read start on 16 distinct 4-bank groups, conflict-free). KS = 2 waves per output wave tile
+// split the chunks (contiguous halves) and meet in LDS after the loop as in tiling R (fixed order).
+// ------------------------------------------------------------------------------------------------
+constexpr int WB_KMAX = 768;   // K of the resident B band (48 x 772 floats = 148 KB of LDS)
+template <int WGM, int KS, int P, int KQ>
+struct WbCfg {
+  // KQ float4 per lane per chunk: a chunk is CK = 16 KQ deep and lane group q holds its k = 4 KQ q .. 4 KQ q + 4 KQ - 1
+  // (KQ = 2: each row's 128-B line is fetched by ONE load instruction instead of half a line per load, twice)
+  static constexpr int BM = 16 * WGM, BN = 48, TJ = 3, NT = WGM, NW = NT * KS, CK = 16 * KQ;
+  static constexpr int KMAX = WB_KMAX;
+  __host__ __device__ static constexpr int stride(int K) { return ((K + CK - 1) / CK) * CK + 4; }
+  __host__ __device__ static constexpr int band_floats(int K) { return (BN * stride(K) + 255) & ~255; }
+  __host__ __device__ static constexpr int lds_floats(int K) {
+    return band_floats(K) > NT * TJ * KS * 256 ? band_floats(K) : NT * TJ * KS * 256;
+  }
+};
+
+template <int WGM, int KS, int P, int KQ, int EPI>
+__global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const GemmArgs g) {
+  using T = WbCfg<WGM, KS, P, KQ>;
+  constexpr int CK = T::CK;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int kh = wave / T::NT, wm = wave - kh * T::NT;
+  const int c16 = lane & 15, qq = lane >> 4;
+  const TileId tl = tile_id();
+  const int z = tl.z, g1 = z / g.G0, g0 = z - g1 * g.G0;
+  const float* __restrict__ A = g.A + g1 * g.sA1 + g0 * g.sA0;
+  const float* __restrict__ B = g.B + g1 * g.sB1 + g0 * g.sB0;
+  const int am0 = tl.y * T::BM + wm * 16, n0 = tl.x * T::BN;
+  const EpiCtx e = epi_ctx<EPI>(g, g1, g0);
+  const int K = g.K, S = T::stride(K);
+  // 1. A: this wave's 16 rows, its contiguous share of the chunks, the first P chunks issued now. A float4 wholly
+  //    past K (K % 4 == 0) reads the row start instead and is zeroed before use.
+  const float* pa = A + (long long)min(am0 + c16, g.M - 1) * g.lda + 4 * KQ * qq;
+  const int nchunk = (K + CK - 1) / CK;
+  const int c_lo = kh * nchunk / KS, n = (kh + 1) * nchunk / KS - c_lo;
+  const int clast = min(c_lo + (n > 0 ? n - 1 : 0), nchunk - 1);
+  auto mine = [&](int j) { return KS == 1 || j % KS == kh; };
+  float pre[T::TJ][4];
+#pragma unroll
+  for (int j = 0; j < T::TJ; ++j)
+    if (mine(j)) epi_pre<EPI>(g, e.X, am0 + 4 * qq, n0 + 16 * j + c16, pre[j]);
+  floatx4 buf[P][KQ];
+  auto load = [&](int u, int c) {
+#pragma unroll
+    for (int h = 0; h < KQ; ++h)
+      buf[u][h] = ld4(pa + (CK * c + 4 * KQ * qq + 4 * h < K ? CK * c + 4 * h : 4 * h - 4 * KQ * qq));
+  };
+#pragma unroll
+  for (int u = 0; u < P; ++u) load(u, min(c_lo + u, clast));
+  // 2. the B band: piece p (1 KB) = LDS floats [256 p, 256 p + 256); lane l's float4 is column f / S, k = f % S
+  //    (k >= K: padding, any valid source)
+  {
+    const int np = T::band_floats(K) / 256;
+    for (int p = wave; p < np; p += T::NW) {     // wave-uniform trip count
+      const int f = 256 * p + 4 * lane, col = f / S, k = f - col * S;
+      const float* src = B + (long long)min(n0 + col, g.N - 1) * g.ldb + (k < K ? k : 0);
+      // the DMA as inline asm: hipcc's wait pass, seeing an LDS-DMA builtin before the K loop, puts a vmcnt(0) at
+      // the loop head (it cannot bound the DMA against the band reads there), draining the A ring every iteration;
+      // the explicit vmcnt(0) below retires these copies before anything reads the band
+      const uint32_t dst = (uint32_t)(uintptr_t)(lds + 256 * p);
+      uint32_t m0_saved;                          // m0 is reserved to the compiler: restored after the copy
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                   "s_mov_b32 m0, %0" : "=&s"(m0_saved) : "v"(src), "s"(dst) : "memory");
+    }
+  }
+  floatx4 acc[T::TJ];
+#pragma unroll
+  for (int j = 0; j < T::TJ; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // everything landed (every other wave's pieces too after the barrier)
+  __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0)
+  raw_barrier();
+  const float* bs = lds + c16 * S + 4 * KQ * qq;  // column 16 j + c16 at k = CK c + 4 KQ q: bs + 16 j S + CK c
+  for (int c = 0; c < n; c += P) {
+#pragma unroll
+    for (int u = 0; u < P; ++u) {
+      if (c + u < n) {
+        const int ck = c_lo + c + u;
+#pragma unroll
+        for (int h = 0; h < KQ; ++h) {
+          floatx4 a = buf[u][h], b[T::TJ];
+#pragma unroll
+          for (int j = 0; j < T::TJ; ++j) b[j] = ld4(bs + 16 * j * S + CK * ck + 4 * h);
+          if ((K % CK) && ck == nchunk - 1 && CK * ck + 4 * KQ * qq + 4 * h >= K) a = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int j = 0; j < T::TJ; ++j)
+              acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[j][s], acc[j], 0, 0, 0);
+        }
+      }
+      load(u, min(c_lo + c + u + P, clast));
+    }
+  }
+  if constexpr (KS > 1) {    // the band is dead once every wave has finished its MFMAs: partials reuse its LDS
+    raw_barrier();
+    float* part = lds + (wm * T::TJ) * KS * 256 + lane * 4;      // [wave tile][j][slice][64 lanes][4]
+#pragma unroll
+    for (int j = 0; j < T::TJ; ++j)
+      if (!mine(j)) st4(part + (j * KS + kh) * 256, acc[j]);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < T::TJ; ++j)
+      if (mine(j)) {
+        floatx4 s = kh == 0 ? acc[j] : ld4(part + (j * KS) * 256);
+#pragma unroll
+        for (int h = 1; h < KS; ++h) {
+          const floatx4 p = h == kh ? acc[j] : ld4(part + (j * KS + h) * 256);
+          s = floatx4{s[0] + p[0], s[1] + p[1], s[2] + p[2], s[3] + p[3]};
+        }
+        acc[j] = s;
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < T::TJ; ++j)
+    if (mine(j)) {
+      const float v[4] = {acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
+      const int rb = am0 + 4 * qq, col = n0 + 16 * j + c16;
+      epi4<EPI>(g, e.C, e.X, rb, col, v, epi_rnd<EPI>(g, e, rb, col), pre[j]);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1585,6 +1725,23 @@ int launch_gl(const GemmArgs& g, int groups, hipStream_t st) {
   return bcnf_rt::launched();
 }
 
+template <int WGM, int KS, int P, int KQ, int EPI>
+int launch_wb(const GemmArgs& g, int groups, hipStream_t st) {
+  using T = WbCfg<WGM, KS, P, KQ>;
+  const int bytes = T::lds_floats(g.K) * 4;
+  static bool attr = false;
+  if (!attr) {
+    if (const int rc = bcnf_rt::hip_status(hipFuncSetAttribute((const void*)k_wbr<WGM, KS, P, KQ, EPI>,
+                                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                               T::lds_floats(T::KMAX) * 4)))
+      return rc;
+    attr = true;
+  }
+  dim3 grid((g.N + T::BN - 1) / T::BN, (g.M + T::BM - 1) / T::BM, groups);
+  hipLaunchKernelGGL((k_wbr<WGM, KS, P, KQ, EPI>), grid, dim3(64 * T::NW), bytes, st, g);
+  return bcnf_rt::launched();
+}
+
 // LDS-DMA tilings per operand layout (tiling C): 5 = auto, 6 = the large-tile variant forced
 template <bool AKC, bool BKC, int EPI>
 int gemm_gl(const GemmArgs& g, int groups, hipStream_t st, bool large);
@@ -1599,7 +1756,8 @@ double tile_cost(const GemmArgs& g, int groups, int BM, int BN, double eff) {
 // Forced tilings (GemmArgs.tiling = t + 1, from BcnfStackDesc.gemm_tiling; 0 = the cost model): 0 = 128x128,
 // 1 = 64x64, 2 = 128x48 (16x16 MFMA), 3 = 128x48 on 8 waves, 4 = 96x48 on 6 waves, 5 = LDS-DMA (tiling C, the default;
 // 96 x 48 for K-contiguous operands), 6 = tiling C large tiles, 7 = tiling C 48 x 48, 8 = 176 x 176 on 11 waves
-// (strided x strided operands only; the dispatcher's choice otherwise)
+// (strided x strided operands only; the dispatcher's choice otherwise), 9 = tiling W (K-contiguous x K-contiguous,
+// K <= 768; the dispatcher's choice otherwise). Auto picks tiling W where tiling C would run 96 x 48.
 
 template <bool AKC, bool BKC, int EPI>
 int gemm(const GemmArgs& g, int groups, hipStream_t st) {
@@ -1612,6 +1770,9 @@ int gemm(const GemmArgs& g, int groups, hipStream_t st) {
   // 64-wide wave tiles measured slower (tools/gemm_bench.py t6 / t7, profiles/r02t_gemm_tilings.txt)
   if (pick < 0 && AKC && BKC) pick = 5;
   if (pick >= 5 && pick <= 7) return gemm_gl<AKC, BKC, EPI>(g, groups, st, pick == 6);
+  if constexpr (AKC && BKC) {   // tiling W forced
+    if (pick == 9 && g.K >= 4 && g.K <= WB_KMAX) return launch_wb<6, 2, 4, 1, EPI>(g, groups, st);
+  }
   // strided x strided (the grouped Linear gradients, M = H + 1, N = H at H = 526): 176 x 176 tiles cover 528 x 528
   // exactly (the 64 x 64 / 128 x 128 grids compute 1.19x / 1.47x the area) and re-read each operand 3 times instead
   // of 9; 11 waves of 16 x 176
@@ -1650,6 +1811,9 @@ int gemm_gl(const GemmArgs& g, int groups, hipStream_t st, bool large) {
     const long long t96 = (long long)((g.M + 95) / 96) * ((g.N + 47) / 48) * groups;
     if (g.tiling - 1 == 7 || (g.tiling - 1 != 5 && t96 < 3 * N_CU / 4))
       return launch_gl<48, 48, 3, 1, true, true, EPI, 3>(g, groups, st);
+    // the 96 x 48 grid: tiling W (B band resident in LDS, no per-K-tile DMA / barrier) when the band fits: the chain
+    // GEMMs 19.0 -> 17.8 us at M = 2048, N = K = 528 (tools/gemm_rd.py, profiles/r03l_gemm_wb2.txt)
+    if (g.tiling - 1 != 5 && g.K >= 4 && g.K <= WB_KMAX) return launch_wb<6, 2, 4, 1, EPI>(g, groups, st);
     return launch_gl<96, 48, 6, 1, true, true, EPI, 4>(g, groups, st);
   }
   if (!AKC && !BKC) return launch_gl<128, 128, 2, 2, false, false, EPI, 2>(g, groups, st);
