@@ -92,7 +92,7 @@ int wide_layout(const BcnfStackDesc* d, WideLayout* L) {
   for (int i = 1; i < d->n_hidden; ++i)
     if (d->hidden[i] != d->hidden[0]) return BCNF_ERR_UNSUPPORTED;     // equal widths (every shipped config)
   if (d->size > DM || d->n_conditions < 1 || d->hidden[0] > 8192) return BCNF_ERR_UNSUPPORTED;
-  if (d->gemm_tiling < 0 || d->gemm_tiling > 10) return BCNF_ERR_ARG;
+  if (d->gemm_tiling < 0 || d->gemm_tiling > 11) return BCNF_ERR_ARG;
   L->tiling = d->gemm_tiling;
   L->D = d->size;
   L->Da = (d->size + 1) / 2;
@@ -910,22 +910,22 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS, (S * (BM + BN) * 64 * 4 <= 80 
 // split the chunks (contiguous halves) and meet in LDS after the loop as in tiling R (fixed order).
 // ------------------------------------------------------------------------------------------------
 constexpr int WB_KMAX = 768;   // K of the resident B band (48 x 772 floats = 148 KB of LDS)
-template <int WGM, int KS, int P, int KQ>
+template <int WGM, int KS, int P, int KQ, int TI = 1>
 struct WbCfg {
   // KQ float4 per lane per chunk: a chunk is CK = 16 KQ deep and lane group q holds its k = 4 KQ q .. 4 KQ q + 4 KQ - 1
   // (KQ = 2: each row's 128-B line is fetched by ONE load instruction instead of half a line per load, twice)
-  static constexpr int BM = 16 * WGM, BN = 48, TJ = 3, NT = WGM, NW = NT * KS, CK = 16 * KQ;
+  static constexpr int BM = 16 * TI * WGM, BN = 48, TJ = 3, NF = TI * TJ, NT = WGM, NW = NT * KS, CK = 16 * KQ;
   static constexpr int KMAX = WB_KMAX;
   __host__ __device__ static constexpr int stride(int K) { return ((K + CK - 1) / CK) * CK + 4; }
   __host__ __device__ static constexpr int band_floats(int K) { return (BN * stride(K) + 255) & ~255; }
   __host__ __device__ static constexpr int lds_floats(int K) {
-    return band_floats(K) > NT * TJ * KS * 256 ? band_floats(K) : NT * TJ * KS * 256;
+    return band_floats(K) > NT * NF * KS * 256 ? band_floats(K) : NT * NF * KS * 256;
   }
 };
 
-template <int WGM, int KS, int P, int KQ, int EPI>
+template <int WGM, int KS, int P, int KQ, int TI, int EPI>
 __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const GemmArgs g) {
-  using T = WbCfg<WGM, KS, P, KQ>;
+  using T = WbCfg<WGM, KS, P, KQ, TI>;
   constexpr int CK = T::CK;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63;
@@ -936,25 +936,29 @@ __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const
   const int z = tl.z, g1 = z / g.G0, g0 = z - g1 * g.G0;
   const float* __restrict__ A = g.A + g1 * g.sA1 + g0 * g.sA0;
   const float* __restrict__ B = g.B + g1 * g.sB1 + g0 * g.sB0;
-  const int am0 = tl.y * T::BM + wm * 16, n0 = tl.x * T::BN;
+  const int am0 = tl.y * T::BM + wm * 16 * TI, n0 = tl.x * T::BN;
   const EpiCtx e = epi_ctx<EPI>(g, g1, g0);
   const int K = g.K, S = T::stride(K);
   // 1. A: this wave's 16 rows, its contiguous share of the chunks, the first P chunks issued now. A float4 wholly
   //    past K (K % 4 == 0) reads the row start instead and is zeroed before use.
-  const float* pa = A + (long long)min(am0 + c16, g.M - 1) * g.lda + 4 * KQ * qq;
+  const float* pa[TI];
+#pragma unroll
+  for (int i = 0; i < TI; ++i) pa[i] = A + (long long)min(am0 + 16 * i + c16, g.M - 1) * g.lda + 4 * KQ * qq;
   const int nchunk = (K + CK - 1) / CK;
   const int c_lo = kh * nchunk / KS, n = (kh + 1) * nchunk / KS - c_lo;
   const int clast = min(c_lo + (n > 0 ? n - 1 : 0), nchunk - 1);
-  auto mine = [&](int j) { return KS == 1 || j % KS == kh; };
-  float pre[T::TJ][4];
+  auto mine = [&](int f) { return KS == 1 || f % KS == kh; };     // accumulator tile f = i * TJ + j
+  float pre[T::NF][4];
 #pragma unroll
-  for (int j = 0; j < T::TJ; ++j)
-    if (mine(j)) epi_pre<EPI>(g, e.X, am0 + 4 * qq, n0 + 16 * j + c16, pre[j]);
-  floatx4 buf[P][KQ];
+  for (int f = 0; f < T::NF; ++f)
+    if (mine(f)) epi_pre<EPI>(g, e.X, am0 + 16 * (f / T::TJ) + 4 * qq, n0 + 16 * (f % T::TJ) + c16, pre[f]);
+  floatx4 buf[P][TI][KQ];
   auto load = [&](int u, int c) {
 #pragma unroll
-    for (int h = 0; h < KQ; ++h)
-      buf[u][h] = ld4(pa + (CK * c + 4 * KQ * qq + 4 * h < K ? CK * c + 4 * h : 4 * h - 4 * KQ * qq));
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int h = 0; h < KQ; ++h)
+        buf[u][i][h] = ld4(pa[i] + (CK * c + 4 * KQ * qq + 4 * h < K ? CK * c + 4 * h : 4 * h - 4 * KQ * qq));
   };
 #pragma unroll
   for (int u = 0; u < P; ++u) load(u, min(c_lo + u, clast));
@@ -974,9 +978,9 @@ __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const
                    "s_mov_b32 m0, %0" : "=&s"(m0_saved) : "v"(src), "s"(dst) : "memory");
     }
   }
-  floatx4 acc[T::TJ];
+  floatx4 acc[T::NF];
 #pragma unroll
-  for (int j = 0; j < T::TJ; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int f = 0; f < T::NF; ++f) acc[f] = floatx4{0.f, 0.f, 0.f, 0.f};
   // everything landed (every other wave's pieces too after the barrier)
   __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0)
   raw_barrier();
@@ -988,15 +992,21 @@ __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const
         const int ck = c_lo + c + u;
 #pragma unroll
         for (int h = 0; h < KQ; ++h) {
-          floatx4 a = buf[u][h], b[T::TJ];
+          floatx4 a[TI], b[T::TJ];
 #pragma unroll
           for (int j = 0; j < T::TJ; ++j) b[j] = ld4(bs + 16 * j * S + CK * ck + 4 * h);
-          if ((K % CK) && ck == nchunk - 1 && CK * ck + 4 * KQ * qq + 4 * h >= K) a = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int i = 0; i < TI; ++i) {
+            a[i] = buf[u][i][h];
+            if ((K % CK) && ck == nchunk - 1 && CK * ck + 4 * KQ * qq + 4 * h >= K) a[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+          }
 #pragma unroll
           for (int s = 0; s < 4; ++s)
 #pragma unroll
-            for (int j = 0; j < T::TJ; ++j)
-              acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[j][s], acc[j], 0, 0, 0);
+            for (int i = 0; i < TI; ++i)
+#pragma unroll
+              for (int j = 0; j < T::TJ; ++j)
+                acc[i * T::TJ + j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i * T::TJ + j], 0, 0, 0);
         }
       }
       load(u, min(c_lo + c + u + P, clast));
@@ -1004,29 +1014,29 @@ __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const
   }
   if constexpr (KS > 1) {    // the band is dead once every wave has finished its MFMAs: partials reuse its LDS
     raw_barrier();
-    float* part = lds + (wm * T::TJ) * KS * 256 + lane * 4;      // [wave tile][j][slice][64 lanes][4]
+    float* part = lds + (wm * T::NF) * KS * 256 + lane * 4;      // [wave tile][f][slice][64 lanes][4]
 #pragma unroll
-    for (int j = 0; j < T::TJ; ++j)
-      if (!mine(j)) st4(part + (j * KS + kh) * 256, acc[j]);
+    for (int f = 0; f < T::NF; ++f)
+      if (!mine(f)) st4(part + (f * KS + kh) * 256, acc[f]);
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < T::TJ; ++j)
-      if (mine(j)) {
-        floatx4 s = kh == 0 ? acc[j] : ld4(part + (j * KS) * 256);
+    for (int f = 0; f < T::NF; ++f)
+      if (mine(f)) {
+        floatx4 s = kh == 0 ? acc[f] : ld4(part + (f * KS) * 256);
 #pragma unroll
         for (int h = 1; h < KS; ++h) {
-          const floatx4 p = h == kh ? acc[j] : ld4(part + (j * KS + h) * 256);
+          const floatx4 p = h == kh ? acc[f] : ld4(part + (f * KS + h) * 256);
           s = floatx4{s[0] + p[0], s[1] + p[1], s[2] + p[2], s[3] + p[3]};
         }
-        acc[j] = s;
+        acc[f] = s;
       }
   }
 #pragma unroll
-  for (int j = 0; j < T::TJ; ++j)
-    if (mine(j)) {
-      const float v[4] = {acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
-      const int rb = am0 + 4 * qq, col = n0 + 16 * j + c16;
-      epi4<EPI>(g, e.C, e.X, rb, col, v, epi_rnd<EPI>(g, e, rb, col), pre[j]);
+  for (int f = 0; f < T::NF; ++f)
+    if (mine(f)) {
+      const float v[4] = {acc[f][0], acc[f][1], acc[f][2], acc[f][3]};
+      const int rb = am0 + 16 * (f / T::TJ) + 4 * qq, col = n0 + 16 * (f % T::TJ) + c16;
+      epi4<EPI>(g, e.C, e.X, rb, col, v, epi_rnd<EPI>(g, e, rb, col), pre[f]);
     }
 }
 
@@ -1725,20 +1735,20 @@ int launch_gl(const GemmArgs& g, int groups, hipStream_t st) {
   return bcnf_rt::launched();
 }
 
-template <int WGM, int KS, int P, int KQ, int EPI>
+template <int WGM, int KS, int P, int KQ, int EPI, int TI = 1>
 int launch_wb(const GemmArgs& g, int groups, hipStream_t st) {
-  using T = WbCfg<WGM, KS, P, KQ>;
+  using T = WbCfg<WGM, KS, P, KQ, TI>;
   const int bytes = T::lds_floats(g.K) * 4;
   static bool attr = false;
   if (!attr) {
-    if (const int rc = bcnf_rt::hip_status(hipFuncSetAttribute((const void*)k_wbr<WGM, KS, P, KQ, EPI>,
+    if (const int rc = bcnf_rt::hip_status(hipFuncSetAttribute((const void*)k_wbr<WGM, KS, P, KQ, TI, EPI>,
                                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                                T::lds_floats(T::KMAX) * 4)))
       return rc;
     attr = true;
   }
   dim3 grid((g.N + T::BN - 1) / T::BN, (g.M + T::BM - 1) / T::BM, groups);
-  hipLaunchKernelGGL((k_wbr<WGM, KS, P, KQ, EPI>), grid, dim3(64 * T::NW), bytes, st, g);
+  hipLaunchKernelGGL((k_wbr<WGM, KS, P, KQ, TI, EPI>), grid, dim3(64 * T::NW), bytes, st, g);
   return bcnf_rt::launched();
 }
 
@@ -1756,8 +1766,9 @@ double tile_cost(const GemmArgs& g, int groups, int BM, int BN, double eff) {
 // Forced tilings (GemmArgs.tiling = t + 1, from BcnfStackDesc.gemm_tiling; 0 = the cost model): 0 = 128x128,
 // 1 = 64x64, 2 = 128x48 (16x16 MFMA), 3 = 128x48 on 8 waves, 4 = 96x48 on 6 waves, 5 = LDS-DMA (tiling C, the default;
 // 96 x 48 for K-contiguous operands), 6 = tiling C large tiles, 7 = tiling C 48 x 48, 8 = 176 x 176 on 11 waves
-// (strided x strided operands only; the dispatcher's choice otherwise), 9 = tiling W (K-contiguous x K-contiguous,
-// K <= 768; the dispatcher's choice otherwise). Auto picks tiling W where tiling C would run 96 x 48.
+// (strided x strided operands only; the dispatcher's choice otherwise), 9 = tiling W 96 x 48, 10 = tiling W 48 x 48
+// (K-contiguous x K-contiguous, K <= 768; the dispatcher's choice otherwise). Auto: tiling W for K-contiguous
+// operands with K <= 768 unless the grid is large enough for tiling C's 128 x 128 tiles.
 
 template <bool AKC, bool BKC, int EPI>
 int gemm(const GemmArgs& g, int groups, hipStream_t st) {
@@ -1772,6 +1783,7 @@ int gemm(const GemmArgs& g, int groups, hipStream_t st) {
   if (pick >= 5 && pick <= 7) return gemm_gl<AKC, BKC, EPI>(g, groups, st, pick == 6);
   if constexpr (AKC && BKC) {   // tiling W forced
     if (pick == 9 && g.K >= 4 && g.K <= WB_KMAX) return launch_wb<6, 2, 4, 1, EPI>(g, groups, st);
+    if (pick == 10 && g.K >= 4 && g.K <= WB_KMAX) return launch_wb<3, 4, 4, 1, EPI>(g, groups, st);
   }
   // strided x strided (the grouped Linear gradients, M = H + 1, N = H at H = 526): 176 x 176 tiles cover 528 x 528
   // exactly (the 64 x 64 / 128 x 128 grids compute 1.19x / 1.47x the area) and re-read each operand 3 times instead
@@ -1806,14 +1818,20 @@ int gemm_gl(const GemmArgs& g, int groups, hipStream_t st, bool large) {
   const long long t128 = (long long)((g.M + 127) / 128) * ((g.N + 127) / 128) * groups;
   if (AKC && BKC) {
     if (large || t128 >= 2 * N_CU) return launch_gl<128, 128, 2, 2, true, true, EPI, 2>(g, groups, st);
-    // 96 x 48 on one workgroup per CU while that grid covers most CUs (M = 2048, N = 528: 242 tiles); below,
-    // 48 x 48 workgroups two per CU (M = 1024, the LSTM_large chain: 13.3 vs 17.6 us, tools/gemm_bench.py)
+    // tiling W (B band resident in LDS, one workgroup per CU) unless tiling C is forced: 48 x 48 tiles on 12 waves
+    // (K in 4 slices) while that grid fits one round of the CUs (M = 1024, the LSTM_large chain: 13.2 -> 10.9 us),
+    // else 96 x 48 on 12 waves (K halves; M = 2048, the FC_large chain: 17.9 -> 17.3 us; tools/gemm_rd.py,
+    // profiles/r03n_gemm_wbti.txt)
+    const int forced = g.tiling - 1;
+    const bool wb = g.K >= 4 && g.K <= WB_KMAX && forced != 5 && forced != 7;
+    const long long t48 = (long long)((g.M + 47) / 48) * ((g.N + 47) / 48) * groups;
+    if (wb && t48 <= N_CU) return launch_wb<3, 4, 4, 1, EPI>(g, groups, st);
+    if (wb) return launch_wb<6, 2, 4, 1, EPI>(g, groups, st);
+    // tiling C: 96 x 48 on one workgroup per CU while that grid covers most CUs (M = 2048, N = 528: 242 tiles); below,
+    // 48 x 48 workgroups two per CU (M = 1024: 13.3 vs 17.6 us, tools/gemm_bench.py)
     const long long t96 = (long long)((g.M + 95) / 96) * ((g.N + 47) / 48) * groups;
-    if (g.tiling - 1 == 7 || (g.tiling - 1 != 5 && t96 < 3 * N_CU / 4))
+    if (forced == 7 || (forced != 5 && t96 < 3 * N_CU / 4))
       return launch_gl<48, 48, 3, 1, true, true, EPI, 3>(g, groups, st);
-    // the 96 x 48 grid: tiling W (B band resident in LDS, no per-K-tile DMA / barrier) when the band fits: the chain
-    // GEMMs 19.0 -> 17.8 us at M = 2048, N = K = 528 (tools/gemm_rd.py, profiles/r03l_gemm_wb2.txt)
-    if (g.tiling - 1 != 5 && g.K >= 4 && g.K <= WB_KMAX) return launch_wb<6, 2, 4, 1, EPI>(g, groups, st);
     return launch_gl<96, 48, 6, 1, true, true, EPI, 4>(g, groups, st);
   }
   if (!AKC && !BKC) return launch_gl<128, 128, 2, 2, false, false, EPI, 2>(g, groups, st);
