@@ -37,7 +37,7 @@ EXPORTS = (
     "bcnf_wide_pack", "bcnf_wide_forward", "bcnf_wide_nll_finalize", "bcnf_wide_backward", "bcnf_wide_inverse",
     "bcnf_wide_fold_prepare", "bcnf_wide_fold_forward", "bcnf_wide_fold_backward", "bcnf_wide_proj_rows",
     "bcnf_wide_fold_backward_range", "bcnf_wide_block_offset",
-    "bcnf_wide_gemm_test", "bcnf_rank_count",
+    "bcnf_wide_gemm_test", "bcnf_rank_count", "bcnf_resimulate",
     "bcnf_guard_check_global",
 )
 MAX_TENSORS = 48
@@ -180,6 +180,8 @@ def _bind(lib):
                                       _vp]),
         "bcnf_wide_inverse": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i32, _vp, _vp, _vp]),
         "bcnf_rank_count": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _vp]),
+        "bcnf_resimulate": (_i32, [_vp, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _i32, ctypes.c_double, _i32,
+                                   ctypes.c_double, ctypes.c_double, _i32, _vp, _vp, _vp, _vp]),
         "bcnf_wide_gemm_test": (_i32, [_i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp]),
         "bcnf_status_string": (ctypes.c_char_p, [_i32]),
     }

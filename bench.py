@@ -82,7 +82,12 @@ WIDE_TRAIN_FLOP_PER_SAMPLE = 3 * WIDE_FWD_FLOP_PER_SAMPLE
 WIDE_ALG_BYTES_PER_SAMPLE = 26 * 4 * (5 * 19 + 4 * 1360 + 2)
 WIDE_NAMES = {"fc_large": "trajectory_FC_large", "lstm_large": "trajectory_LSTM_large"}
 WORKLOADS = {"fc_small": (FC_SMALL, 4096), "fc_large": (FC_LARGE, 2048), "lstm_large": (LSTM_LARGE, 1024),
-             "sample": (FC_SMALL, 1024)}
+             "sample": (FC_SMALL, 1024), "resimulate": (None, 1024)}
+# Re-simulation (simulation/resimulation.py:21-59, notebooks/resimulation.ipynb: T = 2, dt = 1/15, m_samples = 1000,
+# break_on_impact = True): executed fp64 work per Dormand-Prince attempt of bcnf_resim.hip, counted from its source:
+# 6 right-hand sides x 28 (sqrt and reciprocal as 1 each) + stage combinations 138 + error norm 59
+RESIM_FLOP_PER_ATTEMPT = 6 * 28 + 138 + 59
+PEAK_FP64_TFLOPS = 78.6        # MI355X fp64 vector, AMD's product figure (not in MI355X_MICROARCH.md)
 PEAK_FP32_TFLOPS = 157.3       # MI355X fp32 (vector = MFMA f32), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
 
@@ -364,6 +369,8 @@ def main():
         args.batch = WORKLOADS[args.workload][1]
     if args.workload == "sample":
         return main_sample(args)
+    if args.workload == "resimulate":
+        return main_resim(args)
     if args.workload != "fc_small":
         return main_wide(args)
     world, rank, local = init_dist(args)
@@ -451,10 +458,12 @@ def main():
             del step, model, data
             torch.cuda.empty_cache()
             sub = line.setdefault("secondary", {})
-            for wl, steps in (("fc_large", 8), ("lstm_large", 8), ("sample", 10)):
+            for wl, steps in (("fc_large", 8), ("lstm_large", 8), ("sample", 10), ("resimulate", 5)):
                 t_sub = time.perf_counter()
                 try:
-                    if wl == "sample":
+                    if wl == "resimulate":
+                        sub[wl] = run_resim(WORKLOADS[wl][1], steps, 2, 1, 0, device, cpu=not args.no_cpu_baseline)
+                    elif wl == "sample":
                         # 10 warm-up draws (~20 ms): the first launches after the FC_large / LSTM_large sub-lines
                         # run while the clocks settle (k_inverse_mfma 1.81 -> 1.57 ms over 13 launches, r03i trace)
                         sub[wl] = run_sample(WORKLOADS[wl][1], steps, 10, 1, 0, device, cpu=not args.no_cpu_baseline)
@@ -817,6 +826,117 @@ def cpu_baseline_sample(n_draws=500, n_cond=1024):
     return {"value": round(n_draws * n_cond / dt, 1), "unit": "draws/s", "cores": threads, "kind": "port",
             "sample": f"oracle.sample(outer=True, batch_size=100), {n_draws} draws x {n_cond} conditions, "
                       f"{threads} threads, {dt:.2f} s"}
+
+
+def resim_draws(n_traj, n_draws, seed=2024_03_25):
+    """(M, N, 19) float32 'posterior draws' of the FC_small parameters for N synthetic trajectories (bcnf_amd/data.py
+    priors), each parameter jittered by 5% per draw, + the data_dict with the parameters the model does not predict."""
+    from bcnf_amd.data import simulate
+    y, _ = simulate(n_traj, seed=seed, T=0.1, dt=0.067)
+    rng = np.random.Generator(np.random.PCG64(seed + 1))
+    yh = y[None] * (1 + 0.05 * rng.standard_normal((n_draws, n_traj, y.shape[1]))).astype(np.float32)
+    zeros = [0.0] * n_traj
+    data_dict = {"g_x": zeros, "g_y": zeros, "g_z": list(y[:, 6].astype(np.float64))}
+    return yh.astype(np.float32), data_dict
+
+
+def run_resim(n_traj, steps, warmup, world, rank, device, n_draws=1000, cpu=True, T=2.0, dt=1 / 15):
+    """Re-simulated trajectories/s (resimulate with y_hat given, resimulation.py:21-59; notebooks/resimulation.ipynb
+    sizes): n_draws x n_traj trajectories, the trajectories sharded over the ranks (independent, no collective).
+    One step = bcnf_resimulate over this rank's draws, y_hat resident in HBM, (N, M, 30, 3) float64 written."""
+    from bcnf_amd.resimulation import resimulate_device
+    from bcnf_amd.sampling import shard_range
+    from bcnf_amd.utils import ParameterIndexMapping
+    yh, data_dict = resim_draws(n_traj, n_draws)
+    a, b = shard_range(n_traj, rank, world)
+    pim = ParameterIndexMapping(FC_SMALL["global"]["parameter_selection"])
+    dd = {k: v[a:b] for k, v in data_dict.items()}
+    y = torch.from_numpy(yh[:, a:b]).to(device).contiguous()
+    st = torch.cuda.current_stream(device)
+    for _ in range(warmup):
+        out = resimulate_device(y, T, dt, dd, pim, break_on_impact=True, device=device)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = resimulate_device(y, T, dt, dd, pim, break_on_impact=True, device=device)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    # the kernel alone, HIP events on its launch stream; step attempts for the executed-work roofline
+    _, att, stat = resimulate_device(y, T, dt, dd, pim, break_on_impact=True, device=device, return_status=True)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(3):
+        resimulate_device(y, T, dt, dd, pim, break_on_impact=True, device=device)
+    e1.record(st)
+    torch.cuda.synchronize()
+    k_us = e0.elapsed_time(e1) * 1e3 / 3
+    value = n_draws * n_traj * steps / el
+    seen = ranks_seen(world, device)
+    if rank != 0:
+        return None
+    n_att = int(att.sum().item())
+    n_bad = int((stat != 0).sum().item())
+    flop = RESIM_FLOP_PER_ATTEMPT * n_att
+    ach = flop / (k_us * 1e-6) / 1e12
+    out_bytes = out.numel() * 8
+    line = {
+        "metric": "re-simulated trajectories/sec (resimulate, y_hat given: 1000 draws x 1024 trajectories, T=2, "
+                  "dt=1/15, break_on_impact)",
+        "value": round(value, 1), "unit": "trajectories/s", "n_gpus": world, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(el / steps * 1e3, 4), "ranks_seen": seen, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic draws: bcnf_amd/data.py priors jittered 5% per draw, device-resident",
+        "config": {"workload": "resimulate (simulation/resimulation.py:21-59), y_hat given", "trajectories": n_traj,
+                   "draws": n_draws, "steps_per_trajectory": int(out.shape[2]), "parallelism": f"trajectory shards x{world}",
+                   "output": list(out.shape)},
+        "roofline": {"bound": "valu-fp64", "kernel": "k_resim", "achieved": round(ach, 3), "peak": PEAK_FP64_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(ach / PEAK_FP64_TFLOPS, 4), "traffic": _pmc_traffic("k_resim"),
+                     "avg_us": round(k_us, 2), "flop_per_launch": flop, "attempts_per_trajectory":
+                     round(n_att / (n_draws * (b - a)), 2), "not_ok_trajectories": n_bad,
+                     "output_bytes": out_bytes, "hbm_floor_us": round(out_bytes / PEAK_HBM_GBS / 1e3, 2),
+                     "note": "adaptive integrator: FLOPs are the executed Dormand-Prince attempts x "
+                             f"{RESIM_FLOP_PER_ATTEMPT} (fp64 sqrt / division count 1 but are multi-instruction "
+                             "sequences); the float64 positions written set an HBM floor (hbm_floor_us)"},
+    }
+    if cpu and world == 1:
+        line["cpu_baseline"] = cpu_baseline_resim(yh, data_dict, pim.parameters, T, dt)
+    return line
+
+
+def main_resim(args):
+    world, rank, local = init_dist(args)
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    line = run_resim(args.batch, args.steps, args.warmup, world, rank, device, cpu=not args.no_cpu_baseline)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline_resim(yh, data_dict, names, T, dt, n_traj=4):
+    """The oracle (scipy odeint per (draw, trajectory), the reference's integrator) over all draws of the first
+    n_traj trajectories, one process (the reference maps the same tasks over a ProcessPoolExecutor)."""
+    import warnings
+    from oracle import resim_oracle as RO
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        t0 = time.perf_counter()
+        RO.resimulate(yh, list(names), data_dict, T, dt, True, traj=range(n_traj))
+        el = time.perf_counter() - t0
+    n = yh.shape[0] * n_traj
+    return {"value": round(n / el, 1), "unit": "trajectories/s", "cores": 1, "kind": "port",
+            "sample": f"oracle.resimulate (scipy odeint) over {yh.shape[0]} draws x {n_traj} trajectories, "
+                      f"1 process, {el:.2f} s"}
 
 
 if __name__ == "__main__":

@@ -32,6 +32,8 @@
  *                        <- nn.Linear of FullyConnectedFeatureNetwork (feature_network.py:114-145)
  *   bcnf_wide_*          <- the same stack interfaces for the wide-MLP shapes (FC_large / LSTM_large)
  *   bcnf_rank_count      <- the rank count of compute_y_hat_ranks (eval/calibration.py:42-46)
+ *   bcnf_resimulate      <- resimulate's per-draw physics_ODE_simulation map (simulation/resimulation.py:12-18,
+ *                           49-56 -> simulation/physics.py:53-160)
  */
 #ifndef BCNF_AMD_H
 #define BCNF_AMD_H
@@ -383,6 +385,26 @@ int bcnf_wide_inverse(const BcnfStackDesc* desc, const float* params, const void
  * dim) draws of sample(outer=True); counts is uint32 and accumulates, so draws can be fed in chunks. */
 int bcnf_rank_count(const float* y_hat, const float* y, int64_t n_draws, int64_t n_rows, int32_t dim, uint32_t* counts,
                     void* stream);
+
+/* ---- Re-simulation (simulation/resimulation.py:21-59 -> physics.py:53-160, physics_ODE_simulation per draw) -------
+ * Replaces the ProcessPoolExecutor map of resimulate_trajectory (resimulation.py:12-18, 49-56) over every (draw j,
+ * trajectory i). Physics parameter q (physics.py:53-72 order: x0_x x0_y x0_z v0_x v0_y v0_z g_x g_y g_z w_x w_y w_z
+ * b m rho r a_x a_y a_z) is y_hat[(j * n_traj + i) * dim + param_cols[q]] (float32, or float64 with y_hat_f64) when
+ * param_cols[q] >= 0 (the model predicts it: ParameterIndexMapping.dictify), else fixed[i * 19 + q] (the trajectory's
+ * data_dict value, resimulation.py:53). tgrid = np.arange(0, T, dt) (steps >= 1 entries). Output
+ * x[((i * n_draws + j) * steps + s) * 3 + c] (float64, = np.array(X_resimulation_list)). The velocity ODE is
+ * integrated in fp64 by an adaptive Dormand-Prince 5(4) pair at (rtol, atol) between grid times; max_attempts bounds
+ * the step attempts per trajectory. param_cols is a HOST array of 19; every other pointer is device memory.
+ * attempts / status (int32 per (i, j)) are optional; status is BCNF_RESIM_*; a
+ * trajectory that is not OK is NaN from the first grid time it could not reach. */
+#define BCNF_RESIM_NPARAM 19
+#define BCNF_RESIM_OK 0
+#define BCNF_RESIM_NONFINITE 1   /* non-finite right-hand side at t = 0 (e.g. zero wind: 0/0 in physics.py:42) */
+#define BCNF_RESIM_STEPS 2       /* step size underflow or max_attempts exhausted (divergent draw) */
+int bcnf_resimulate(const void* y_hat, int32_t y_hat_f64, int64_t n_draws, int64_t n_traj, int32_t dim,
+                    const int32_t* param_cols, const double* fixed, const double* tgrid, int32_t steps, double dt,
+                    int32_t break_on_impact, double rtol, double atol, int32_t max_attempts, double* x,
+                    int32_t* attempts, int32_t* status, void* stream);
 
 /* Test hook for the GEMM tiles: C (M x N) = A B with (layout & 15) 0 = A[m][k] B[n][k], 1 = A[m][k] B[k][n],
  * 2 = A[k][m] B[k][n], 3 = A[k][m] B[n][k]; layout >> 4 forces a tiling as BcnfStackDesc.gemm_tiling (0 = the

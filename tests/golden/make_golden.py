@@ -28,6 +28,10 @@ Fixtures:
   g12_fft_enriched.npz  layer="LinearFFTEnriched" coupling stack (dev config, test size): z, ldj, inverse, the
                      state_dict and every parameter gradient of the eval NLL (reference autograd)
   g13_anyglu.npz     layer="AnyGLU" (Sigmoid gate) two_way coupling stack (dev config, test size): the same
+  g14_resim.npz      physics_ODE_simulation (physics.py:53-160) on 40 parameter sets (priors of g9 + thrust, one zero
+                     wind) at (T=2, dt=1/15) with and without break_on_impact and at (T=10, dt=0.1); and
+                     resimulate(...) (resimulation.py:21-59) itself, y_hat given (M=6 draws x N=5 trajectories, the
+                     FC_small parameter_selection, g_x / g_y / g_z from data_dict), break_on_impact=True, 2 processes
 """
 import os
 import sys
@@ -386,12 +390,75 @@ def make_g13(cnf, utils):
     _variant_fixture(cnf, utils, GLU_DEV, SEED + 21, SEED + 22, SEED + 23, "g13_anyglu.npz")
 
 
+def _physics_draw(rng):
+    r_xy, phi = abs(rng.normal(0, 20)), rng.uniform(0, 2 * np.pi)
+    v_xy, vphi = abs(rng.normal(0, 15)), rng.uniform(0, 2 * np.pi)
+    w_xy, wphi = abs(rng.normal(0, 3)), rng.uniform(0, 2 * np.pi)
+    p = dict(x0_x=r_xy * np.cos(phi), x0_y=r_xy * np.sin(phi), x0_z=rng.uniform(0.1, 2.5),
+             v0_x=v_xy * np.cos(vphi), v0_y=v_xy * np.sin(vphi), v0_z=rng.normal(7, 5),
+             g_x=0.0, g_y=0.0, g_z=-rng.gamma(9.81, 1.0),
+             w_x=w_xy * np.cos(wphi), w_y=w_xy * np.sin(wphi), w_z=rng.normal(0, 1),
+             rho=rng.gamma(3.5, 0.35), r=rng.gamma(1.75, 0.05) + 1e-3, m=rng.gamma(2.0, 0.5) + 0.05,
+             a_x=rng.normal(0, 0.5), a_y=rng.normal(0, 0.5), a_z=rng.normal(0, 0.5))
+    p["b"] = 0.5 * p["rho"] * np.pi * p["r"] ** 2 * rng.gamma(2.0, 0.1)
+    return p
+
+
+PHYS = ("x0_x", "x0_y", "x0_z", "v0_x", "v0_y", "v0_z", "g_x", "g_y", "g_z", "w_x", "w_y", "w_z", "b", "m", "rho", "r",
+        "a_x", "a_y", "a_z")
+
+
+def make_g14(utils, physics):
+    import types
+    import warnings
+    from bcnf.simulation import resimulation
+    rng = np.random.Generator(np.random.PCG64(SEED + 24))
+    n = 40
+    P = np.zeros((n, len(PHYS)))
+    for k in range(n):
+        p = _physics_draw(rng)
+        if k == 7:                                   # zero wind: w^2 w / |w| = 0/0 (physics.py:42)
+            p.update(w_x=0.0, w_y=0.0, w_z=0.0)
+        if k == 11:                                  # heavy and draggy
+            p.update(m=0.06, b=0.02)
+        P[k] = [p[q] for q in PHYS]
+    out = {"params": P}
+    grids = {"a": (2.0, 1 / 15), "c": (10.0, 0.1)}
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for tag, brk in (("a", False), ("b", True), ("c", False)):
+            T, dt = grids.get(tag, grids["a"])
+            out["x_" + tag] = np.stack([physics.physics_ODE_simulation(**dict(zip(PHYS, P[k])), T=T, dt=dt,
+                                                                       break_on_impact=brk) for k in range(n)])
+        # resimulate itself, y_hat given: the FC_small parameter_selection (g_x / g_y / g_z are not predicted, 'g',
+        # 'A', 'Cd' are predicted but are no physics arguments)
+        names = FC_SMALL["global"]["parameter_selection"]
+        M, N = 6, 5
+        base = [_physics_draw(rng) for _ in range(N)]
+        data_dict = {q: [b[q] for b in base] for q in PHYS}
+        data_dict.update(g=[b["g_z"] for b in base], A=[np.pi * b["r"] ** 2 for b in base], Cd=[0.2] * N,
+                         trajectories=[np.zeros((30, 3)) for _ in range(N)])
+        y_hat = np.zeros((M, N, len(names)), dtype=np.float32)
+        for j in range(M):
+            for i in range(N):
+                for c, q in enumerate(names):
+                    v = data_dict[q][i] if q in data_dict else 0.0
+                    y_hat[j, i, c] = v * (1 + 0.05 * rng.standard_normal()) if q not in ("a_x", "a_y", "a_z") else v
+        model = types.SimpleNamespace(parameter_index_mapping=utils.ParameterIndexMapping(names))
+        X = resimulation.resimulate(model, 2, 1 / 15, data_dict, y_hat, break_on_impact=True, n_procs=2,
+                                    verbose=False)
+    fixed = np.array([[data_dict[q][i] for q in PHYS] for i in range(N)])
+    np.savez_compressed(os.path.join(OUT, "g14_resim.npz"), **out, y_hat=y_hat, names=np.array(names),
+                        fixed_phys=fixed, g_extra=np.array(data_dict["g"]), A_extra=np.array(data_dict["A"]),
+                        resim=X)
+
+
 def main():
     cnf, utils, physics = _import_reference()
     if len(sys.argv) > 1:                      # e.g. `make_golden.py g10 g11`: only those fixtures
         for name in sys.argv[1:]:
             {"g10": lambda: make_g10(cnf), "g11": lambda: make_g11(cnf), "g12": lambda: make_g12(cnf, utils),
-             "g13": lambda: make_g13(cnf, utils)}[name]()
+             "g13": lambda: make_g13(cnf, utils), "g14": lambda: make_g14(utils, physics)}[name]()
         return
     torch.set_num_threads(8)
     make_g1(cnf, utils)
@@ -404,6 +471,7 @@ def main():
     make_g11(cnf)
     make_g12(cnf, utils)
     make_g13(cnf, utils)
+    make_g14(utils, physics)
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

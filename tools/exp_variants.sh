@@ -9,6 +9,6 @@ mkdir -p build_exp
 name=${1:-stamps}
 shift || true
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -shared -fPIC -Iinclude -DBCNF_PHASE_STAMPS "$@" \
-  bcnf_amd/csrc/bcnf_stack.hip bcnf_amd/csrc/bcnf_train.hip bcnf_amd/csrc/bcnf_wide.hip bcnf_amd/csrc/bcnf_eval.hip \
+  bcnf_amd/csrc/bcnf_stack.hip bcnf_amd/csrc/bcnf_train.hip bcnf_amd/csrc/bcnf_wide.hip bcnf_amd/csrc/bcnf_eval.hip bcnf_amd/csrc/bcnf_resim.hip \
   -o build_exp/lib$name.so
 ls -la build_exp
