@@ -45,7 +45,7 @@ struct Phys {
 
 // ballistic_ODE (physics.py:42): (g - buoyancy) - kd (v^2 v / |v| - w^2 w / |w|) + a
 __device__ __forceinline__ void rhs(const Phys& P, const double v[3], double d[3]) {
-  const double inv = 1.0 / sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+  const double inv = rsqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);     // 1 / |v| (no fp64 division)
 #pragma unroll
   for (int c = 0; c < 3; ++c) d[c] = P.gb[c] - P.kd * (v[c] * v[c] * v[c] * inv - P.wt[c]) + P.a[c];
 }
@@ -126,16 +126,21 @@ __global__ __launch_bounds__(RWG) void k_resim(const ResimArgs a, const TY* __re
 #pragma unroll
       for (int c = 0; c < 3; ++c) vn[c] = v[c] + hh * (B1 * k1[c] + B3 * k3[c] + B4 * k4[c] + B5 * k5[c] + B6 * k6[c]);
       rhs(P, vn, k7);
-      double en = 0.0;
+      // squared RMS error norm in fp32: it only steers the step size (accept / shrink), so its rounding never
+      // reaches the solution beyond the tolerance it enforces; no fp64 division, square root or pow
+      float en2 = 0.f;
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         const double e = hh * (E1 * k1[c] + E3 * k3[c] + E4 * k4[c] + E5 * k5[c] + E6 * k6[c] + E7 * k7[c]);
         const double sc = a.atol + a.rtol * fmax(fabs(v[c]), fabs(vn[c]));
-        en += (e / sc) * (e / sc);
+        const float q = (float)e * __builtin_amdgcn_rcpf((float)sc);
+        en2 += q * q;
       }
-      en = sqrt(en * (1.0 / 3.0));
-      if (!(en <= 1.0) || !finite3(vn)) {      // reject (a NaN / inf error norm shrinks the step too)
-        h = hh * (isfinite(en) ? fmax(0.2, 0.9 * pow(en, -0.2)) : 0.2);
+      en2 *= 1.f / 3.f;
+      // 0.9 en^(-1/5) = 0.9 (en^2)^(-1/10)
+      const float fac0 = 0.9f * __builtin_amdgcn_exp2f(-0.1f * __builtin_amdgcn_logf(en2));
+      if (!(en2 <= 1.f) || !finite3(vn)) {     // reject (a NaN / inf error norm shrinks the step too)
+        h = hh * (double)(en2 < INFINITY ? fmaxf(0.2f, fac0) : 0.2f);
         if (!(h > 1e-13 * (fabs(t) + fabs(tend)))) { st = BCNF_RESIM_STEPS; break; }
         continue;
       }
@@ -146,7 +151,7 @@ __global__ __launch_bounds__(RWG) void k_resim(const ResimArgs a, const TY* __re
       }
       t = last ? tend : t + hh;
       reached = last;
-      const double fac = en > 0.0 ? fmin(5.0, fmax(0.2, 0.9 * pow(en, -0.2))) : 5.0;
+      const double fac = en2 > 0.f ? (double)fminf(5.f, fmaxf(0.2f, fac0)) : 5.0;
       if (!last || fac < 1.0) h = hh * fac;     // a step clipped to the grid keeps the controller's h
     }
     if (st != BCNF_RESIM_OK) break;

@@ -509,7 +509,13 @@ __device__ __forceinline__ TileId tile_id() {
   const unsigned gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
   const unsigned total = gx * gy * gz;
   unsigned lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-  if (total >= 16 && (total & 7u) == 0) lin = (lin & 7u) * (total >> 3) + (lin >> 3);
+  // the dispatcher sends workgroup `lin` to XCD lin % 8: give each XCD one contiguous range of tiles (x fastest, so an
+  // XCD's tiles share A row blocks and the whole B in its own L2), also when total is not a multiple of 8 (the
+  // 11 x 22 chain grids): XCD x takes q + (x < r) tiles starting at x q + min(x, r)
+  if (total >= 16) {
+    const unsigned q = total >> 3, r = total & 7u, x = lin & 7u;
+    lin = x * q + (x < r ? x : r) + (lin >> 3);
+  }
   TileId t;
   t.x = (int)(lin % gx);
   lin /= gx;
