@@ -7,7 +7,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 bash tools/profile_round.sh $TAG
-for w in fc_large lstm_large sample; do
+for w in fc_large lstm_large sample resimulate; do
   timeout -k 10 300 python bench.py --workload $w > gpurun_out/${TAG}_${w}_bench.json 2> gpurun_out/${TAG}_${w}_bench.err
   echo ${w}_ok
 done
@@ -16,3 +16,11 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU
   SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --output-format csv -d $OUT/inv -o inv -- \
   python bench.py --workload sample --steps 3 --warmup 1 --no-cpu-baseline > $OUT/inv.log 2>&1
 echo inv_ok
+# re-simulation: kernel trace + FETCH / WRITE passes of k_resim (summarize_profile.py merges them into pmc_traffic.json)
+RES="python bench.py --workload resimulate --steps 3 --warmup 1 --no-cpu-baseline"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_resim -o resim -- $RES > $OUT/resim_trace.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch/resim -o fetch -- $RES > $OUT/resim_fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write/resim -o write -- $RES > $OUT/resim_write.log 2>&1
+echo resim_prof_ok
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_sample -o sample -- python bench.py --workload sample --steps 5 --warmup 2 --no-cpu-baseline > $OUT/sample_trace.log 2>&1
+echo sample_trace_ok

@@ -24,11 +24,15 @@ stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursi
 if stats:
     shutil.copy(stats[0], os.path.join(dst, f"{tag}_kernel_stats.csv"))
     print("kernel stats:", stats[0])
+for wl in ("resim", "sample", "fc_large"):        # other workloads' --stats runs (tools/round_evidence.sh)
+    st2 = glob.glob(os.path.join(src, "trace_" + wl, "**", "*kernel_stats.csv"), recursive=True)
+    if st2:
+        shutil.copy(st2[0], os.path.join(dst, f"{tag}_{wl}_kernel_stats.csv"))
 
 
 def short(name):
     for k in ("k_forward", "k_backward", "k_inverse", "k_red_gx", "k_fold_splitk", "k_fold_finish", "k_pack_fold",
-              "k_bwd_tail", "k_adam", "k_clip", "k_pack", "k_hp"):
+              "k_bwd_tail", "k_adam", "k_clip", "k_pack", "k_hp", "k_resim"):
         if k in name:
             return k
     return None
