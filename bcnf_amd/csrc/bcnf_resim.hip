@@ -65,11 +65,57 @@ __device__ __forceinline__ bool finite3(const double v[3]) {
   return isfinite(v[0]) && isfinite(v[1]) && isfinite(v[2]);
 }
 
+// One Dormand-Prince attempt over [t, t + hh] from v (k1 = f(v), FSAL). Returns the squared RMS error norm and
+// writes vn and k7 = f(vn).
+__device__ __forceinline__ float dp_attempt(const Phys& P, const double v[3], const double k1[3], double hh,
+                                            double rtol, double atol, double vn[3], double k7[3]) {
+  double y[3], k2[3], k3[3], k4[3], k5[3], k6[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) y[c] = v[c] + hh * (A21 * k1[c]);
+  rhs(P, y, k2);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) y[c] = v[c] + hh * (A31 * k1[c] + A32 * k2[c]);
+  rhs(P, y, k3);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) y[c] = v[c] + hh * (A41 * k1[c] + A42 * k2[c] + A43 * k3[c]);
+  rhs(P, y, k4);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) y[c] = v[c] + hh * (A51 * k1[c] + A52 * k2[c] + A53 * k3[c] + A54 * k4[c]);
+  rhs(P, y, k5);
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+    y[c] = v[c] + hh * (A61 * k1[c] + A62 * k2[c] + A63 * k3[c] + A64 * k4[c] + A65 * k5[c]);
+  rhs(P, y, k6);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) vn[c] = v[c] + hh * (B1 * k1[c] + B3 * k3[c] + B4 * k4[c] + B5 * k5[c] + B6 * k6[c]);
+  rhs(P, vn, k7);
+  // squared RMS error norm in fp32: it only steers the step size (accept / shrink), so its rounding never reaches the
+  // solution beyond the tolerance it enforces; no fp64 division, square root or pow
+  float en2 = 0.f;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const double e = hh * (E1 * k1[c] + E3 * k3[c] + E4 * k4[c] + E5 * k5[c] + E6 * k6[c] + E7 * k7[c]);
+    const double sc = atol + rtol * fmax(fabs(v[c]), fabs(vn[c]));
+    const float q = (float)e * __builtin_amdgcn_rcpf((float)sc);
+    en2 += q * q;
+  }
+  return en2 * (1.f / 3.f);
+}
+
+// Positions go through LDS in chunks of RCH grid points: the workgroup's 128 trajectories are consecutive in x, so a
+// chunk is 128 runs of 3 RCH contiguous doubles, copied out by consecutive threads (a thread's own stores would hit
+// 64 different lines per wave instruction: 35% of the launch, measured by an experiment build without them).
+constexpr int RCH = 6;
+constexpr int RLD = 3 * RCH + 1;       // LDS row (doubles) per trajectory, odd: rows start on different banks
+
 template <typename TY>
 __global__ __launch_bounds__(RWG) void k_resim(const ResimArgs a, const TY* __restrict__ yhat) {
-  const long long o = (long long)blockIdx.x * RWG + threadIdx.x;
-  if (o >= a.M * a.N) return;
-  const long long i = o / a.M, j = o - i * a.M;
+  __shared__ double sx[RWG * RLD];
+  const long long n = a.M * a.N;
+  const long long o0 = (long long)blockIdx.x * RWG, o = o0 + threadIdx.x;
+  const bool live = o < n;
+  const long long oc = live ? o : n - 1;     // threads past the end compute a copy and store nothing
+  const long long i = oc / a.M, j = oc - i * a.M;
   double p[BCNF_RESIM_NPARAM];
 #pragma unroll
   for (int q = 0; q < BCNF_RESIM_NPARAM; ++q)
@@ -86,105 +132,75 @@ __global__ __launch_bounds__(RWG) void k_resim(const ResimArgs a, const TY* __re
   }
   P.kd = 0.5 * b / m;
   double x[3] = {p[0], p[1], p[2]}, v[3] = {p[3], p[4], p[5]};
-  double* out = a.x + o * (long long)a.steps * 3;
-  out[0] = x[0];
-  out[1] = x[1];
-  out[2] = x[2];
   double k1[3];
   rhs(P, v, k1);
+  // st != OK or `frozen`: the trajectory is finished and x holds what every later grid point repeats (the impact
+  // point, or NaN: a non-finite right-hand side, e.g. zero wind's 0/0 in physics.py:42, makes odeint's solution NaN
+  // from t[1] on, and a failed step size leaves the rest NaN as well)
   int st = finite3(k1) ? BCNF_RESIM_OK : BCNF_RESIM_NONFINITE;
+  bool frozen = false;
   int tries = 0;
   double h = a.steps > 1 ? (a.tgrid[1] - a.tgrid[0]) * 0.25 : 0.0;
-  int s = 1;
-  for (; s < a.steps && st == BCNF_RESIM_OK; ++s) {
-    // integrate v over [t[s-1], t[s]]
-    double t = a.tgrid[s - 1];
-    const double tend = a.tgrid[s];
-    bool reached = !(tend > t);
-    while (!reached) {
-      if (++tries > a.max_attempts) { st = BCNF_RESIM_STEPS; break; }
-      bool last = false;
-      double hh = h;
-      if (hh >= tend - t) { hh = tend - t; last = true; }
-      double y[3], k2[3], k3[3], k4[3], k5[3], k6[3], k7[3], vn[3];
+  double* row = sx + threadIdx.x * RLD;
+  for (int s0 = 0; s0 < a.steps; s0 += RCH) {             // uniform across the workgroup
+    const int s1 = s0 + RCH < a.steps ? s0 + RCH : a.steps;
+    for (int s = s0; s < s1; ++s) {
+      if (s > 0 && st == BCNF_RESIM_OK && !frozen) {
+        // integrate v over [t[s-1], t[s]]
+        double t = a.tgrid[s - 1];
+        const double tend = a.tgrid[s];
+        bool reached = !(tend > t);
+        while (!reached) {
+          if (++tries > a.max_attempts) { st = BCNF_RESIM_STEPS; break; }
+          bool last = false;
+          double hh = h;
+          if (hh >= tend - t) { hh = tend - t; last = true; }
+          double vn[3], k7[3];
+          const float en2 = dp_attempt(P, v, k1, hh, a.rtol, a.atol, vn, k7);
+          const float fac0 = 0.9f * __builtin_amdgcn_exp2f(-0.1f * __builtin_amdgcn_logf(en2));   // 0.9 en^(-1/5)
+          if (!(en2 <= 1.f) || !finite3(vn)) {     // reject (a NaN / inf error norm shrinks the step too)
+            h = hh * (double)(en2 < INFINITY ? fmaxf(0.2f, fac0) : 0.2f);
+            if (!(h > 1e-13 * (fabs(t) + fabs(tend)))) { st = BCNF_RESIM_STEPS; break; }
+            continue;
+          }
 #pragma unroll
-      for (int c = 0; c < 3; ++c) y[c] = v[c] + hh * (A21 * k1[c]);
-      rhs(P, y, k2);
+          for (int c = 0; c < 3; ++c) {
+            v[c] = vn[c];
+            k1[c] = k7[c];
+          }
+          t = last ? tend : t + hh;
+          reached = last;
+          const double fac = en2 > 0.f ? (double)fminf(5.f, fmaxf(0.2f, fac0)) : 5.0;
+          if (!last || fac < 1.0) h = hh * fac;     // a step clipped to the grid keeps the controller's h
+        }
+        if (st == BCNF_RESIM_OK) {
+          double xn[3];
 #pragma unroll
-      for (int c = 0; c < 3; ++c) y[c] = v[c] + hh * (A31 * k1[c] + A32 * k2[c]);
-      rhs(P, y, k3);
+          for (int c = 0; c < 3; ++c) xn[c] = x[c] + v[c] * a.dt;
+          if (a.break_on_impact && xn[2] < 0.0) {   // physics.py:154-159
+            const double ti = -x[2] / v[2];
 #pragma unroll
-      for (int c = 0; c < 3; ++c) y[c] = v[c] + hh * (A41 * k1[c] + A42 * k2[c] + A43 * k3[c]);
-      rhs(P, y, k4);
+            for (int c = 0; c < 3; ++c) xn[c] = x[c] + v[c] * ti;
+            frozen = true;
+          }
 #pragma unroll
-      for (int c = 0; c < 3; ++c) y[c] = v[c] + hh * (A51 * k1[c] + A52 * k2[c] + A53 * k3[c] + A54 * k4[c]);
-      rhs(P, y, k5);
-#pragma unroll
-      for (int c = 0; c < 3; ++c)
-        y[c] = v[c] + hh * (A61 * k1[c] + A62 * k2[c] + A63 * k3[c] + A64 * k4[c] + A65 * k5[c]);
-      rhs(P, y, k6);
-#pragma unroll
-      for (int c = 0; c < 3; ++c) vn[c] = v[c] + hh * (B1 * k1[c] + B3 * k3[c] + B4 * k4[c] + B5 * k5[c] + B6 * k6[c]);
-      rhs(P, vn, k7);
-      // squared RMS error norm in fp32: it only steers the step size (accept / shrink), so its rounding never
-      // reaches the solution beyond the tolerance it enforces; no fp64 division, square root or pow
-      float en2 = 0.f;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const double e = hh * (E1 * k1[c] + E3 * k3[c] + E4 * k4[c] + E5 * k5[c] + E6 * k6[c] + E7 * k7[c]);
-        const double sc = a.atol + a.rtol * fmax(fabs(v[c]), fabs(vn[c]));
-        const float q = (float)e * __builtin_amdgcn_rcpf((float)sc);
-        en2 += q * q;
+          for (int c = 0; c < 3; ++c) x[c] = xn[c];
+        }
       }
-      en2 *= 1.f / 3.f;
-      // 0.9 en^(-1/5) = 0.9 (en^2)^(-1/10)
-      const float fac0 = 0.9f * __builtin_amdgcn_exp2f(-0.1f * __builtin_amdgcn_logf(en2));
-      if (!(en2 <= 1.f) || !finite3(vn)) {     // reject (a NaN / inf error norm shrinks the step too)
-        h = hh * (double)(en2 < INFINITY ? fmaxf(0.2f, fac0) : 0.2f);
-        if (!(h > 1e-13 * (fabs(t) + fabs(tend)))) { st = BCNF_RESIM_STEPS; break; }
-        continue;
-      }
+      if (s > 0 && st != BCNF_RESIM_OK) x[0] = x[1] = x[2] = __builtin_nan("");
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        v[c] = vn[c];
-        k1[c] = k7[c];
-      }
-      t = last ? tend : t + hh;
-      reached = last;
-      const double fac = en2 > 0.f ? (double)fminf(5.f, fmaxf(0.2f, fac0)) : 5.0;
-      if (!last || fac < 1.0) h = hh * fac;     // a step clipped to the grid keeps the controller's h
+      for (int c = 0; c < 3; ++c) row[3 * (s - s0) + c] = x[c];
     }
-    if (st != BCNF_RESIM_OK) break;
-    double xn[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) xn[c] = x[c] + v[c] * a.dt;
-    if (a.break_on_impact && xn[2] < 0.0) {
-      const double ti = -x[2] / v[2];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) xn[c] = x[c] + v[c] * ti;
-      for (int u = s; u < a.steps; ++u) {
-        out[3 * u] = xn[0];
-        out[3 * u + 1] = xn[1];
-        out[3 * u + 2] = xn[2];
-      }
-      s = a.steps;
-      break;
+    __syncthreads();
+    const int w = 3 * (s1 - s0);
+    for (int e = threadIdx.x; e < RWG * w; e += RWG) {
+      const int tt = e / w, q = e - tt * w;
+      if (o0 + tt < n) a.x[(o0 + tt) * a.steps * 3 + 3 * s0 + q] = sx[tt * RLD + q];
     }
-    out[3 * s] = xn[0];
-    out[3 * s + 1] = xn[1];
-    out[3 * s + 2] = xn[2];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) x[c] = xn[c];
+    __syncthreads();
   }
-  // a non-finite right-hand side (e.g. zero wind: 0/0, physics.py:42) makes odeint's solution NaN from t[1] on;
-  // a failed step size leaves the rest of the trajectory NaN as well
-  for (; s < a.steps; ++s) {
-    out[3 * s] = __builtin_nan("");
-    out[3 * s + 1] = __builtin_nan("");
-    out[3 * s + 2] = __builtin_nan("");
-  }
-  if (a.attempts) a.attempts[o] = tries;
-  if (a.status) a.status[o] = st;
+  if (live && a.attempts) a.attempts[o] = tries;
+  if (live && a.status) a.status[o] = st;
 }
 
 }  // namespace
