@@ -105,7 +105,8 @@ __device__ __forceinline__ float dp_attempt(const Phys& P, const double v[3], co
 // Positions go through LDS in chunks of RCH grid points: the workgroup's 128 trajectories are consecutive in x, so a
 // chunk is 128 runs of 3 RCH contiguous doubles, copied out by consecutive threads (a thread's own stores would hit
 // 64 different lines per wave instruction: 35% of the launch, measured by an experiment build without them).
-constexpr int RCH = 6;
+constexpr int RCH = 6;          // 19.5 KB of LDS per workgroup (4 waves / SIMD, as the 107 VGPRs allow; 4 and 3 with
+                                // 5 waves / SIMD measured 2-15% slower, tools/ab_resim.sh)
 constexpr int RLD = 3 * RCH + 1;       // LDS row (doubles) per trajectory, odd: rows start on different banks
 
 template <typename TY>
