@@ -929,7 +929,9 @@ struct WbCfg {
   }
 };
 
-template <int WGM, int KS, int P, int KQ, int TI, int EPI>
+// KT: K has a partial last chunk (K % CK != 0). Without one (the chain GEMMs: K = 528) the A loads are a pointer plus
+// a chunk offset and nothing is zeroed: no per-chunk index selects or masks on the VALU.
+template <int WGM, int KS, int P, int KQ, int TI, int EPI, bool KT = true>
 __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const GemmArgs g) {
   using T = WbCfg<WGM, KS, P, KQ, TI>;
   constexpr int CK = T::CK;
@@ -964,7 +966,7 @@ __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const
     for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int h = 0; h < KQ; ++h)
-        buf[u][i][h] = ld4(pa[i] + (CK * c + 4 * KQ * qq + 4 * h < K ? CK * c + 4 * h : 4 * h - 4 * KQ * qq));
+        buf[u][i][h] = ld4(pa[i] + (!KT || CK * c + 4 * KQ * qq + 4 * h < K ? CK * c + 4 * h : 4 * h - 4 * KQ * qq));
   };
 #pragma unroll
   for (int u = 0; u < P; ++u) load(u, min(c_lo + u, clast));
@@ -991,6 +993,11 @@ __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const
   __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0)
   raw_barrier();
   const float* bs = lds + c16 * S + 4 * KQ * qq;  // column 16 j + c16 at k = CK c + 4 KQ q: bs + 16 j S + CK c
+  // B fragments one chunk ahead (bq): a chunk's MFMAs never wait for their own ds_reads
+  static_assert(KQ == 1, "the B prefetch holds one float4 per fragment and chunk");
+  floatx4 bq[T::TJ];
+#pragma unroll
+  for (int j = 0; j < T::TJ; ++j) bq[j] = ld4(bs + 16 * j * S + CK * c_lo);
   for (int c = 0; c < n; c += P) {
 #pragma unroll
     for (int u = 0; u < P; ++u) {
@@ -999,12 +1006,16 @@ __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const
 #pragma unroll
         for (int h = 0; h < KQ; ++h) {
           floatx4 a[TI], b[T::TJ];
+          const int cn = ck + 1 < c_lo + n ? ck + 1 : ck;
 #pragma unroll
-          for (int j = 0; j < T::TJ; ++j) b[j] = ld4(bs + 16 * j * S + CK * ck + 4 * h);
+          for (int j = 0; j < T::TJ; ++j) {
+            b[j] = bq[j];
+            bq[j] = ld4(bs + 16 * j * S + CK * cn);
+          }
 #pragma unroll
           for (int i = 0; i < TI; ++i) {
             a[i] = buf[u][i][h];
-            if ((K % CK) && ck == nchunk - 1 && CK * ck + 4 * KQ * qq + 4 * h >= K) a[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+            if (KT && ck == nchunk - 1 && CK * ck + 4 * KQ * qq + 4 * h >= K) a[i] = floatx4{0.f, 0.f, 0.f, 0.f};
           }
 #pragma unroll
           for (int s = 0; s < 4; ++s)
@@ -1754,6 +1765,18 @@ int launch_wb(const GemmArgs& g, int groups, hipStream_t st) {
     attr = true;
   }
   dim3 grid((g.N + T::BN - 1) / T::BN, (g.M + T::BM - 1) / T::BM, groups);
+  if (g.K % T::CK == 0) {
+    static bool attr2 = false;
+    if (!attr2) {
+      if (const int rc = bcnf_rt::hip_status(hipFuncSetAttribute((const void*)k_wbr<WGM, KS, P, KQ, TI, EPI, false>,
+                                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                                 T::lds_floats(T::KMAX) * 4)))
+        return rc;
+      attr2 = true;
+    }
+    hipLaunchKernelGGL((k_wbr<WGM, KS, P, KQ, TI, EPI, false>), grid, dim3(64 * T::NW), bytes, st, g);
+    return bcnf_rt::launched();
+  }
   hipLaunchKernelGGL((k_wbr<WGM, KS, P, KQ, TI, EPI>), grid, dim3(64 * T::NW), bytes, st, g);
   return bcnf_rt::launched();
 }
