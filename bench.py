@@ -458,7 +458,7 @@ def main():
             del step, model, data
             torch.cuda.empty_cache()
             sub = line.setdefault("secondary", {})
-            for wl, steps in (("fc_large", 8), ("lstm_large", 8), ("sample", 10), ("resimulate", 5)):
+            for wl, steps in (("fc_large", 8), ("lstm_large", 8), ("sample", 30), ("resimulate", 5)):
                 t_sub = time.perf_counter()
                 try:
                     if wl == "resimulate":
