@@ -1450,10 +1450,13 @@ constexpr int inv_m_rf() {                          // L.RF of this NH (round_re
 // gelu_f's approximation on a pair of values with packed fp32 arithmetic (v_pk_fma_f32 / v_pk_mul_f32: two lanes'
 // worth per instruction); the same erfc fit, combined as max(x, 0) - |x| h (one rounding fewer than x (1 - h)).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-// max(x, 0) as ONE v_max_f32 (fmaxf under IEEE mode adds a canonicalising max per operand)
-__device__ __forceinline__ float relu_f(float x) {
+// max(x, 0) as ONE v_max_f32 (fmaxf under IEEE mode adds a canonicalising max per operand). hipcc pads no hazard
+// inside an asm string, and x is usually an MFMA result (its D needs 12 wait states before any VALU read,
+// cdna_hip_programming.md, inline-asm rule 2): `after` is a value hipcc computed from x with the pad in front of it,
+// so the dependency places this read behind that pad.
+__device__ __forceinline__ float relu_f(float x, float after) {
   float r;
-  asm("v_max_f32_e32 %0, 0, %1" : "=v"(r) : "v"(x));
+  asm("v_max_f32_e32 %0, 0, %1" : "=v"(r) : "v"(x), "v"(after));
   return r;
 }
 __device__ __forceinline__ f32x2 gelu_f2(f32x2 x) {
@@ -1472,7 +1475,7 @@ __device__ __forceinline__ f32x2 gelu_f2(f32x2 x) {
   // x Phi(x) = max(x, 0) - |x| h with h = erfc(|x| / sqrt 2) / 2 = t Q(t) e^{-x^2/2}: one VOP3 FMA per element
   // (|x| as a free source modifier) instead of the sign select, 1 - h and the product x cdf
   const f32x2 h = (t * q) * ez;
-  return f32x2{fmaf(-fabsf(x.x), h.x, relu_f(x.x)), fmaf(-fabsf(x.y), h.y, relu_f(x.y))};
+  return f32x2{fmaf(-fabsf(x.x), h.x, relu_f(x.x, den.x)), fmaf(-fabsf(x.y), h.y, relu_f(x.y, den.y))};
 }
 __device__ __forceinline__ void gelu4(floatx4& a) {
   const f32x2 lo = gelu_f2(f32x2{a[0], a[1]}), hi = gelu_f2(f32x2{a[2], a[3]});
