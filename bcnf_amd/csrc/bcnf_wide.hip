@@ -854,7 +854,8 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS, (S * (BM + BN) * 64 * 4 <= 80 
       gl_issue<T, AKC, BKC, BM, BN>(A, g.lda, B, g.ldb, g.M, g.N, g.K, m0, n0, st * T::BK, lds + st * T::STG, wave,
                                     lane);
   int rd = 0, wr = S - 1;       // stage read at kt / stage written by the issue of tile kt + S - 1
-  for (int kt = 0; kt < nk; ++kt) {
+  const int am = AKC ? wm * T::WM : wm * 64, bn = BKC ? wn * T::WN : wn * 64;
+  auto ktile = [&](int kt) {    // wait for tile kt, issue tile kt + S - 1, return tile kt's stage
     const int ahead = min(nk - 1 - kt, S - 2);
     if (S > 3 && ahead >= 2) vm_wait<2 * T::NI>();
     else if (S > 2 && ahead >= 1) vm_wait<T::NI>();
@@ -864,14 +865,17 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS, (S * (BM + BN) * 64 * 4 <= 80 
       gl_issue<T, AKC, BKC, BM, BN>(A, g.lda, B, g.ldb, g.M, g.N, g.K, m0, n0, (kt + S - 1) * T::BK,
                                     lds + wr * T::STG, wave, lane);
     const float* As = lds + rd * T::STG;
-    const int am = AKC ? wm * T::WM : wm * 64, bn = BKC ? wn * T::WN : wn * 64;
-    if (kt == nk - 1 && (g.K & (T::BK - 1)))
-      gl_tile<T, AKC, BKC, BM, BN, KS, true>(As, acc, am, bn, c16, qq, kh, g.K - kt * T::BK);
-    else
-      gl_tile<T, AKC, BKC, BM, BN, KS, false>(As, acc, am, bn, c16, qq, kh, T::BK);
     rd = rd + 1 == S ? 0 : rd + 1;
     wr = wr + 1 == S ? 0 : wr + 1;
-  }
+    return As;
+  };
+  // the partial last K tile is peeled off the loop: with the tail variant inside it, hipcc kept two register
+  // homes for the accumulators and copied them (a v_mov_b64 per accumulator pair and path) every iteration
+  const bool tail = (g.K & (T::BK - 1)) != 0;
+  const int nfull = tail ? nk - 1 : nk;
+  for (int kt = 0; kt < nfull; ++kt)
+    gl_tile<T, AKC, BKC, BM, BN, KS, false>(ktile(kt), acc, am, bn, c16, qq, kh, T::BK);
+  if (tail) gl_tile<T, AKC, BKC, BM, BN, KS, true>(ktile(nk - 1), acc, am, bn, c16, qq, kh, g.K - (nk - 1) * T::BK);
   if constexpr (KS > 1) {   // K halves meet: each hands the other the partials of the tiles the other finalises
     static_assert(KS == 2, "two K halves");
     static_assert(T::NT * T::TI * T::TJ * 256 <= S * T::STG, "partials fit the staging ring");
