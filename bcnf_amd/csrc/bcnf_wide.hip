@@ -341,17 +341,12 @@ struct TileIO {
       const int gm = mn0 + row, gk = k0 + 4 * kq;
       if (gm < MN && gk < K) v = ld4(X + (long long)gm * ld + gk);
     } else {
+      // a whole float4 whenever gm < MN: a [K][MN] operand's rows are readable up to roundup4(MN) <= ld (ld % 4 == 0,
+      // host-checked), and the values past MN only reach output rows / columns that are never stored. The row offset
+      // splits into a loop-invariant part and k0 ld, so the K loop carries no 64-bit multiply and no edge branches.
       const int kr = e / (ROWS / 4), mq = e % (ROWS / 4);
       const int gk = k0 + kr, gm = mn0 + 4 * mq;
-      if (gk < K) {
-        const float* p = X + (long long)gk * ld + gm;
-        if (gm + 3 < MN) v = ld4(p);
-        else {
-          if (gm < MN) v.x = p[0];
-          if (gm + 1 < MN) v.y = p[1];
-          if (gm + 2 < MN) v.z = p[2];
-        }
-      }
+      if (gk < K && gm < MN) v = ld4(X + ((long long)kr * ld + gm) + (long long)k0 * ld);
     }
     return v;
   }
