@@ -914,6 +914,9 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS, (S * (BM + BN) * 64 * 4 <= 80 
 // 16 columns of a fragment read start on 16 distinct 4-bank groups, conflict-free). KS = 2 waves per output wave tile
 // split the chunks (contiguous halves) and meet in LDS after the loop as in tiling R (fixed order).
 // ------------------------------------------------------------------------------------------------
+#ifndef WB_P
+#define WB_P 2          // A-operand register ring depth of tiling W (chunks in flight per wave)
+#endif
 constexpr int WB_KMAX = 768;   // K of the resident B band (48 x 772 floats = 148 KB of LDS)
 template <int WGM, int KS, int P, int KQ, int TI = 1>
 struct WbCfg {
@@ -1810,8 +1813,8 @@ int gemm(const GemmArgs& g, int groups, hipStream_t st) {
   if (pick < 0 && AKC && BKC) pick = 5;
   if (pick >= 5 && pick <= 7) return gemm_gl<AKC, BKC, EPI>(g, groups, st, pick == 6);
   if constexpr (AKC && BKC) {   // tiling W forced
-    if (pick == 9 && g.K >= 4 && g.K <= WB_KMAX) return launch_wb<6, 2, 4, 1, EPI>(g, groups, st);
-    if (pick == 10 && g.K >= 4 && g.K <= WB_KMAX) return launch_wb<3, 4, 4, 1, EPI>(g, groups, st);
+    if (pick == 9 && g.K >= 4 && g.K <= WB_KMAX) return launch_wb<6, 2, WB_P, 1, EPI>(g, groups, st);
+    if (pick == 10 && g.K >= 4 && g.K <= WB_KMAX) return launch_wb<3, 4, WB_P, 1, EPI>(g, groups, st);
   }
   // strided x strided (the grouped Linear gradients, M = H + 1, N = H at H = 526): 176 x 176 tiles cover 528 x 528
   // exactly (the 64 x 64 / 128 x 128 grids compute 1.19x / 1.47x the area) and re-read each operand 3 times instead
@@ -1853,8 +1856,9 @@ int gemm_gl(const GemmArgs& g, int groups, hipStream_t st, bool large) {
     const int forced = g.tiling - 1;
     const bool wb = g.K >= 4 && g.K <= WB_KMAX && forced != 5 && forced != 7;
     const long long t48 = (long long)((g.M + 47) / 48) * ((g.N + 47) / 48) * groups;
-    if (wb && t48 <= N_CU) return launch_wb<3, 4, 4, 1, EPI>(g, groups, st);
-    if (wb) return launch_wb<6, 2, 4, 1, EPI>(g, groups, st);
+    // A ring 2 chunks deep (3: -0.8%, 4: -1.1%, 6: -2.3% on FC_large; tools/ab_wide.sh, profiles/r03zh_*)
+    if (wb && t48 <= N_CU) return launch_wb<3, 4, WB_P, 1, EPI>(g, groups, st);
+    if (wb) return launch_wb<6, 2, WB_P, 1, EPI>(g, groups, st);
     // tiling C: 96 x 48 on one workgroup per CU while that grid covers most CUs (M = 2048, N = 528: 242 tiles); below,
     // 48 x 48 workgroups two per CU (M = 1024: 13.3 vs 17.6 us, tools/gemm_bench.py)
     const long long t96 = (long long)((g.M + 95) / 96) * ((g.N + 47) / 48) * groups;
