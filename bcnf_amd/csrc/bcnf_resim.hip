@@ -25,7 +25,7 @@
 
 namespace {
 
-constexpr int RWG = 128;
+constexpr int RWG = 64;        // one wave per workgroup: the chunk barrier costs nothing (533 -> 521 us against 128)
 
 struct ResimArgs {
   int col[BCNF_RESIM_NPARAM];      // y_hat column of each physics parameter, -1 = fixed[i][q]
@@ -102,10 +102,10 @@ __device__ __forceinline__ float dp_attempt(const Phys& P, const double v[3], co
   return en2 * (1.f / 3.f);
 }
 
-// Positions go through LDS in chunks of RCH grid points: the workgroup's 128 trajectories are consecutive in x, so a
-// chunk is 128 runs of 3 RCH contiguous doubles, copied out by consecutive threads (a thread's own stores would hit
+// Positions go through LDS in chunks of RCH grid points: the workgroup's RWG trajectories are consecutive in x, so a
+// chunk is RWG runs of 3 RCH contiguous doubles, copied out by consecutive threads (a thread's own stores would hit
 // 64 different lines per wave instruction: 35% of the launch, measured by an experiment build without them).
-constexpr int RCH = 6;          // 19.5 KB of LDS per workgroup (4 waves / SIMD, as the 107 VGPRs allow; 4 and 3 with
+constexpr int RCH = 6;          // 9.7 KB of LDS per 64-thread workgroup (4 waves / SIMD, as the 107 VGPRs allow; 4 and 3 with
                                 // 5 waves / SIMD measured 2-15% slower, tools/ab_resim.sh)
 constexpr int RLD = 3 * RCH + 1;       // LDS row (doubles) per trajectory, odd: rows start on different banks
 
