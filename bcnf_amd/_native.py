@@ -38,8 +38,9 @@ EXPORTS = (
     "bcnf_wide_fold_prepare", "bcnf_wide_fold_forward", "bcnf_wide_fold_backward", "bcnf_wide_proj_rows",
     "bcnf_wide_fold_backward_range", "bcnf_wide_block_offset",
     "bcnf_wide_gemm_test", "bcnf_rank_count", "bcnf_resimulate",
-    "bcnf_guard_check_global",
+    "bcnf_guard_check_global", "bcnf_abi_version",
 )
+ABI_VERSION = 2          # include/bcnf_amd.h BCNF_AMD_ABI_VERSION (the struct layouts below)
 MAX_TENSORS = 48
 
 
@@ -184,6 +185,7 @@ def _bind(lib):
                                    ctypes.c_double, ctypes.c_double, _i32, _vp, _vp, _vp, _vp]),
         "bcnf_wide_gemm_test": (_i32, [_i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp]),
         "bcnf_status_string": (ctypes.c_char_p, [_i32]),
+        "bcnf_abi_version": (_i32, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -203,6 +205,9 @@ def lib():
                         "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950).")
                 handle = ctypes.CDLL(LIB_PATH)
                 _bind(handle)
+                if handle.bcnf_abi_version() != ABI_VERSION:
+                    raise RuntimeError(f"bcnf_amd: {LIB_PATH} has ABI version {handle.bcnf_abi_version()}, the "
+                                       f"bindings expect {ABI_VERSION}: rebuild the library")
                 _lib = handle
     return _lib
 

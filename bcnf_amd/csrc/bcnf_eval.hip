@@ -31,6 +31,9 @@ __global__ __launch_bounds__(EWG) void k_rank_count(const float* __restrict__ yh
 
 extern "C" {
 
+int bcnf_abi_version(void) { return BCNF_AMD_ABI_VERSION; }
+
+
 int bcnf_rank_count(const float* y_hat, const float* y, int64_t n_draws, int64_t n_rows, int32_t dim, uint32_t* counts,
                     void* stream) {
   if (n_draws < 0 || n_rows < 0 || dim < 1) return BCNF_ERR_ARG;

@@ -132,7 +132,23 @@ def resimulate(model, T: int, dt: float, data_dict: dict[str, list], y_hat=None,
     if M == 0:
         return np.array([[] for _ in range(N)])
     device = model.device if torch.device(model.device).type == "cuda" else None
-    x = resimulate_device(y_hat, T, dt, data_dict, model.parameter_index_mapping, break_on_impact=break_on_impact,
-                          device=device)
+    x, _, status = resimulate_device(y_hat, T, dt, data_dict, model.parameter_index_mapping,
+                                     break_on_impact=break_on_impact, device=device, return_status=True)
+    _warn_unfinished(status)
     return x.cpu().numpy()
+
+
+def _warn_unfinished(status) -> int:
+    """A trajectory the explicit Dormand-Prince pair could not finish (step-size underflow or the attempt bound:
+    a stiff or divergent draw) is NaN from the first grid time it missed. The reference's LSODA switches method
+    and returns values there (odeint warns when it struggles), so these rows are never silent: one warning with
+    their count. NONFINITE rows (a zero wind: 0/0 in the drag term) are NaN in the reference as well."""
+    n = int((status == STATUS_STEPS).sum().item()) if status is not None and status.numel() else 0
+    if n:
+        import warnings
+        warnings.warn(f"bcnf_amd.resimulate: {n} of {status.numel()} trajectories did not finish (stiff or divergent "
+                      f"draws: step-size underflow or the attempt bound); their positions are NaN from the first grid "
+                      f"time that was not reached (resimulate_device(..., return_status=True) names them)",
+                      RuntimeWarning, stacklevel=3)
+    return n
 

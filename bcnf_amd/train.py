@@ -37,10 +37,11 @@ MI355X specifics:
 """
 from __future__ import annotations
 
+import contextlib
+import math
+
 import torch
 import torch.distributed as dist
-
-import math
 
 from bcnf_amd.errors import TrainingDivergedError
 from bcnf_amd.optim import FusedAdam, clip_grad_norm_
@@ -89,6 +90,7 @@ class TrainStep:
         self.overlap_ranges = 0
         self._works = []        # in-flight all-reduces of bucket slices, and the slices [lo, hi) they cover
         self._reduced = []
+        self._hooks = None      # data parallel: the stack attributes _stack_hooks installs around each backward
         from bcnf_amd.wide import WideStack
         if self.world > 1 and overlap_ranges > 0 and isinstance(getattr(model, "fused", None), WideStack):
             self.overlap_ranges = min(int(overlap_ranges), model.fused.cfg.n_blocks)
@@ -103,6 +105,10 @@ class TrainStep:
 
     # ------------------------------------------------------------------ step pieces
     def _forward_backward(self, y, traj, gather=None, adam=None):
+        with self._stack_hooks():
+            return self._forward_backward_body(y, traj, gather, adam)
+
+    def _forward_backward_body(self, y, traj, gather=None, adam=None):
         self.opt.zero_grad(set_to_none=True)
         if self.fused_loss:
             # reduced in the backward launch; a deferred gather runs inside the pack launch
@@ -161,7 +167,8 @@ class TrainStep:
         """Data parallel: allocate the gradient bucket up front and let the folded backwards write their gradients
         into it (no copy before the all-reduce): the small family's (coupling + feature Linear,
         FusedStack.grad_bucket), the wide family's coupling gradients (WideStack.grad_bucket), the latter range by
-        range when overlap_ranges is set."""
+        range when overlap_ranges is set. The stack hooks are installed only around this step's own backward
+        (_stack_hooks), so a backward outside the TrainStep never writes into the bucket or issues collectives."""
         if self.world == 1 or self._bucket is not None:
             return
         self._alloc_bucket(self.params[0].device)
@@ -178,17 +185,45 @@ class TrainStep:
             if id(fp) not in offs:
                 return
             st = self.model.fused
-            st.grad_bucket = (self._bucket, offs[id(fp)])
+            hooks = {"grad_bucket": (self._bucket, offs[id(fp)])}
             if self.overlap_ranges > 0:
                 nb, r = st.cfg.n_blocks, self.overlap_ranges
                 cuts = [round(nb * i / r) for i in range(r + 1)]
-                st.range_blocks = [(cuts[i - 1], cuts[i]) for i in range(r, 0, -1) if cuts[i] > cuts[i - 1]]
-                st.on_range = self._reduce_range
+                hooks["range_blocks"] = [(cuts[i - 1], cuts[i]) for i in range(r, 0, -1) if cuts[i] > cuts[i - 1]]
+                hooks["on_range"] = self._reduce_range
+            self._hooks = hooks
             return
         if len(self.params) != (3 if lin.bias is not None else 2) or id(fp) not in offs or id(lin.weight) not in offs:
             return
-        self.model.fused.grad_bucket = (self._bucket, (offs[id(fp)], offs[id(lin.weight)],
-                                                       offs[id(lin.bias)] if lin.bias is not None else 0))
+        self._hooks = {"grad_bucket": (self._bucket, (offs[id(fp)], offs[id(lin.weight)],
+                                                      offs[id(lin.bias)] if lin.bias is not None else 0))}
+
+    @contextlib.contextmanager
+    def _stack_hooks(self):
+        """The bucket / range hooks on the fused stack for the duration of this step's forward + backward (eager or
+        being captured), removed afterwards even when the step raises."""
+        st = self.model.fused
+        if not self._hooks:
+            yield
+            return
+        for k, v in self._hooks.items():
+            setattr(st, k, v)
+        try:
+            yield
+        finally:
+            for k in self._hooks:
+                setattr(st, k, None)
+
+    def _drain_slices(self):
+        """Join and forget slice all-reduces a previous step left in flight (it raised between issuing them and the
+        update's join), so this step neither skips those slices nor waits on stale handles."""
+        works, self._works = self._works, []
+        self._reduced.clear()
+        for w in works:
+            try:
+                w.wait()
+            except Exception:       # the failed step's own error was already raised to the caller
+                pass
 
     def _bind_grads(self):
         """Every .grad becomes a view of the (reduced) bucket: Adam and the clip read it in place."""
@@ -275,6 +310,7 @@ class TrainStep:
 
     # ------------------------------------------------------------------ eager / graph
     def eager_step(self, y, traj, gather=None, epoch_book: bool = True):
+        self._drain_slices()
         self._setup_bucket()
         vals = self._forward_backward(y, traj, gather)
         vals = self._allreduce(vals)

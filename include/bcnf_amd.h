@@ -46,6 +46,11 @@ extern "C" {
 
 #define BCNF_MAX_HIDDEN 8
 #define BCNF_MAX_TENSORS 48
+/* Layout version of the structs below (2: BcnfStackDesc.gemm_tiling appended). bcnf_abi_version() returns the
+ * library's; a caller compares it with this macro before passing any struct. */
+#define BCNF_AMD_ABI_VERSION 2
+
+int bcnf_abi_version(void);
 
 enum {
   BCNF_OK = 0,
@@ -68,8 +73,10 @@ typedef struct BcnfStackDesc {
   int32_t two_way;                   /* 0/1 (small family: 0 only; wide: both) */
   float dropout;                     /* p of every nn.Dropout in the nested MLP */
   int32_t gemm_tiling;               /* wide family only: 0 = each GEMM's cost-model tiling (use this); t + 1 forces
-                                        tiling t on every GEMM of the call (tests / A-B timing; see
-                                        bcnf_wide_gemm_test). Per call: the library holds no such setting. */
+                                        tiling t (0 <= t <= 10, see bcnf_wide_gemm_test) on every GEMM of the call
+                                        (tests / A-B timing). Per call: the library holds no such setting. Appended
+                                        in ABI version 2 (BCNF_AMD_ABI_VERSION): C callers built against a version-1
+                                        header pass a shorter struct and must be rebuilt. */
 } BcnfStackDesc;
 
 /* 1 if this descriptor runs on the fused small-width kernel family, else 0. */
@@ -410,7 +417,11 @@ int bcnf_resimulate(const void* y_hat, int32_t y_hat_f64, int64_t n_draws, int64
  * 2 = A[k][m] B[k][n], 3 = A[k][m] B[n][k]; layout >> 4 forces a tiling as BcnfStackDesc.gemm_tiling (0 = the
  * dispatcher's choice, t + 1 = tiling t: 0 = 128x128 and 1 = 64x64 on v_mfma_f32_32x32x2_f32, 2 = 128x48, 3 = 128x48
  * on 8 waves, 4 = 96x48 on 6 waves (v_mfma_f32_16x16x4_f32), 5 / 6 / 7 = LDS-DMA tiling C auto / large / 48x48,
- * 8 = 176x176 on 11 waves); leading dimensions and K multiples of 4, 16-byte aligned bases. */
+ * 8 = 176x176 on 11 waves (strided x strided layouts only), 9 / 10 = tiling W 96x48 / 48x48 (layout 0 only, the B band
+ * resident in LDS, K <= 768); a forced tiling that does not apply to the layout / K runs as 64x64 (tiling 1);
+ * leading dimensions and K multiples of 4, 16-byte aligned bases. Strided operands ([K][M] / [K][N] rows) are read
+ * as whole float4 up to roundup4(M) / roundup4(N) columns in EVERY row, the last one included: allocate K * ld
+ * floats for them (a tight (K - 1) * ld + M buffer is read out of bounds). */
 int bcnf_wide_gemm_test(int32_t layout, int32_t M, int32_t N, int32_t K, const float* A, int64_t lda, const float* B,
                         int64_t ldb, float* C, int64_t ldc, void* stream);
 

@@ -107,7 +107,19 @@ def _overlap_worker(rank, world, port, q):
         assert len(step._works) == 2
         out = step._allreduce(vals)
         assert not step._works and not step._reduced
-        q.put((rank, [p.grad.detach().numpy().copy() for p in step.params], out.detach().numpy().copy(),
+        res = [p.grad.detach().numpy().copy() for p in step.params]
+        # a step that raised after handing a slice over: the next step joins and forgets it first (_drain_slices)
+        step._reduce_range(0, 10)
+        step._drain_slices()
+        assert not step._works and not step._reduced
+        # the stack hooks live only around a step's own backward, also when it raises
+        step._hooks = {"on_range": step._reduce_range, "range_blocks": [(0, 1)]}
+        with pytest.raises(ZeroDivisionError):
+            with step._stack_hooks():
+                assert m.fused.on_range is not None and m.fused.range_blocks == [(0, 1)]
+                1 / 0
+        assert m.fused.on_range is None and m.fused.range_blocks is None
+        q.put((rank, res, out.detach().numpy().copy(),
                step._packed_inplace))
     except Exception:
         q.put((rank, traceback.format_exc(), None, None))

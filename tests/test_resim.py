@@ -11,12 +11,14 @@ to ~100) are compared at rtol = atol = 2e-6.
 """
 import os
 import types
+import warnings
 
 import numpy as np
 import pytest
 import torch
 
-from bcnf_amd.resimulation import PHYSICS_PARAMETERS, _columns, resimulate, resimulate_device, time_grid
+from bcnf_amd.resimulation import (PHYSICS_PARAMETERS, STATUS_STEPS, _columns, _warn_unfinished, resimulate,
+                                   resimulate_device, time_grid)
 from bcnf_amd.utils import ParameterIndexMapping
 from oracle import resim_oracle as RO
 
@@ -77,6 +79,20 @@ def test_no_cpu_path():
     y = torch.zeros(2, 3, 19)
     with pytest.raises(RuntimeError, match="HIP device only"):
         resimulate_device(y, 2, 1 / 15, {}, ParameterIndexMapping(list(PHYSICS_PARAMETERS)), device="cpu")
+
+
+def test_unfinished_trajectories_warn():
+    """resimulate() never returns a silent NaN row for a trajectory the integrator could not finish."""
+    st = torch.zeros(3, 4, dtype=torch.int32)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        assert _warn_unfinished(st) == 0
+        st[0, 1] = 1                                   # NONFINITE (zero wind): NaN in the reference as well
+        assert _warn_unfinished(st) == 0
+    st[2, 3] = STATUS_STEPS
+    st[1, 0] = STATUS_STEPS
+    with pytest.warns(RuntimeWarning, match="2 of 12 trajectories did not finish"):
+        assert _warn_unfinished(st) == 2
 
 
 # ---------------------------------------------------------------------------------------------------------- GPU
@@ -165,3 +181,17 @@ def test_gpu_draw_major_layout_and_edges():
     model = types.SimpleNamespace(parameter_index_mapping=pim, device="cuda:0")
     assert resimulate(model, 2, 1 / 15, {}, np.zeros((0, 4, 19)), verbose=False).shape == (4, 0)
     assert resimulate(model, 2, 1 / 15, {}, np.zeros((3, 0, 19)), verbose=False).shape == (0,)
+
+
+@pytest.mark.gpu
+def test_gpu_attempt_bound_reports_steps_status():
+    """A trajectory stopped by the attempt bound is NaN from the first grid time it missed, with status STEPS."""
+    d = _g14()
+    y, pim = _all_from_draws(d["params"][:4])
+    x, att, st = resimulate_device(y, 2.0, 1 / 15, {}, pim, max_attempts=5, return_status=True)
+    st = st.cpu().numpy()[:, 0]
+    assert (st == STATUS_STEPS).all() and (att.cpu().numpy() == 6).all()
+    x = x.cpu().numpy()[:, 0]
+    assert not np.isnan(x[:, 0]).any() and np.isnan(x[:, -1]).all()
+    with pytest.warns(RuntimeWarning, match="4 of 4"):
+        _warn_unfinished(torch.from_numpy(st))
