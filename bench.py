@@ -101,6 +101,9 @@ def parse():
                     help="fc_small = the headline metric (configs[1]); fc_large / lstm_large = configs[2] / [3] per GPU")
     ap.add_argument("--batch", type=int, default=None, help="samples per GPU (weak scaling; default per workload)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--overlap-ranges", type=int, default=None,
+                    help="wide workloads at world > 1: block ranges of the overlapped gradient all-reduce (default "
+                         "4; 0 = one all-reduce after the backward, captured graphs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=12)
     ap.add_argument("--kernel-iters", type=int, default=20)
@@ -194,9 +197,10 @@ def launch_check(args):
     world, rank, _ = init_dist(args)
     dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0"))) if torch.cuda.is_available() else "cpu"
     seen = ranks_seen(world, dev)
+    sub = run_sublines(args, world, rank, dev, dry=True)
     if rank == 0:
         print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_seen": seen,
-                          "backend": dist.get_backend() if world > 1 else None}), flush=True)
+                          "backend": dist.get_backend() if world > 1 else None, "secondary": sub}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -428,6 +432,7 @@ def main():
     seen = ranks_seen(world, device)
 
     kern = kernel_timing(model, data, args) if rank == 0 else {}
+    line = None
     if rank == 0:
         B = args.batch
         lp_abs, lp_rel = log_prob_error(model, device)
@@ -453,32 +458,78 @@ def main():
             line["secondary"] = secondary_figures(step, args, device)
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(args)
-        if not args.no_secondary and world == 1 and not (args.indexed or args.per_step_sync):
-            # configs[2], [3], [4] at their single-GPU sizes, each with its own roofline and cpu_baseline (bounded)
-            del step, model, data
-            torch.cuda.empty_cache()
-            sub = line.setdefault("secondary", {})
-            for wl, steps in (("fc_large", 8), ("lstm_large", 8), ("sample", 30), ("resimulate", 5)):
-                t_sub = time.perf_counter()
-                try:
-                    if wl == "resimulate":
-                        sub[wl] = run_resim(WORKLOADS[wl][1], steps, 2, 1, 0, device, cpu=not args.no_cpu_baseline)
-                    elif wl == "sample":
-                        # 10 warm-up draws (~20 ms): the first launches after the FC_large / LSTM_large sub-lines
-                        # run while the clocks settle (k_inverse_mfma 1.81 -> 1.57 ms over 13 launches, r03i trace)
-                        sub[wl] = run_sample(WORKLOADS[wl][1], steps, 10, 1, 0, device, cpu=not args.no_cpu_baseline)
-                    else:
-                        sub[wl] = run_wide(wl, WORKLOADS[wl][1], steps, 3, 1, 0, device, graph=not args.no_graph,
-                                           kernel_iters=3, cpu=not args.no_cpu_baseline,
-                                           cpu_batch=256 if wl == "fc_large" else 128, cpu_steps=2)
-                except Exception as e:           # a sub-line never takes the headline down with it
-                    sub[wl] = {"error": f"{type(e).__name__}: {e}"}
-                sub[wl]["bench_wall_s"] = round(time.perf_counter() - t_sub, 1)
-                torch.cuda.empty_cache()
+    if not args.no_secondary and not (args.indexed or args.per_step_sync):
+        # configs[2], [3], [4] and re-simulation on every rank (the world's own scaling of each), each with its own
+        # roofline and, at world 1, its own cpu_baseline (bounded)
+        del step, model, data
+        torch.cuda.empty_cache()
+        sub = run_sublines(args, world, rank, device)
+        if rank == 0:
+            line.setdefault("secondary", {}).update(sub)
+    if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+# The sub-lines of the default run: (workload, timed steps). Per rank: FC_large 2048 / LSTM_large 1024 samples per step
+# (weak scaling; at world > 1 the backward's bucket slices are all-reduced while it runs, TrainStep overlap_ranges),
+# sampling's 1024 conditions and re-simulation's 1024 trajectories sharded over the ranks (strong scaling).
+SUBLINES = (("fc_large", 8), ("lstm_large", 8), ("sample", 30), ("resimulate", 5))
+OVERLAP_RANGES = 4
+
+
+def run_sublines(args, world, rank, device, dry=False):
+    """Every SUBLINES workload on every rank of the world (the collectives of each -- barriers, the max-over-ranks
+    clock, the gradient / draw exchange -- need all of them); returns rank 0's {workload: JSON object}. dry=True
+    (--launch-check, no GPU) walks the same sequence through the timing contract with an empty step."""
+    out = {}
+    cpu = not args.no_cpu_baseline and world == 1
+    for wl, steps in SUBLINES:
+        t_sub = time.perf_counter()
+        try:
+            if dry:
+                res = run_dry(wl, steps, world, rank, device)
+            elif wl == "resimulate":
+                res = run_resim(WORKLOADS[wl][1], steps, 2, world, rank, device, cpu=cpu)
+            elif wl == "sample":
+                # 10 warm-up draws (~20 ms): the first launches after the FC_large / LSTM_large sub-lines
+                # run while the clocks settle (k_inverse_mfma 1.81 -> 1.57 ms over 13 launches, r03i trace)
+                res = run_sample(WORKLOADS[wl][1], steps, 10, world, rank, device, cpu=cpu)
+            else:
+                res = run_wide(wl, WORKLOADS[wl][1], steps, 3, world, rank, device, graph=not args.no_graph,
+                               kernel_iters=3, cpu=cpu, cpu_batch=256 if wl == "fc_large" else 128, cpu_steps=2,
+                               overlap_ranges=(args.overlap_ranges if args.overlap_ranges is not None
+                                               else OVERLAP_RANGES) if world > 1 else 0)
+        except Exception as e:           # a sub-line never takes the headline down with it
+            res = {"error": f"{type(e).__name__}: {e}"}
+        if rank == 0:
+            res = res if res is not None else {"error": "rank 0 returned no line"}
+            res["bench_wall_s"] = round(time.perf_counter() - t_sub, 1)
+            out[wl] = res
+        if not dry:
+            torch.cuda.empty_cache()
+    return out
+
+
+def run_dry(workload, steps, world, rank, device):
+    """--launch-check: one sub-line's distributed plumbing without a GPU -- the barrier-bracketed timed region, the
+    max-over-ranks clock and ranks_seen -- so a CPU test can see that every sub-line runs on every rank."""
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    seen = ranks_seen(world, device)
+    if rank != 0:
+        return None
+    return {"metric": workload, "dry": True, "n_gpus": world, "steps": steps, "ranks_seen": seen}
 
 
 def _pmc_traffic(kernel):
@@ -619,7 +670,7 @@ def cpu_baseline_wide(workload, cfg, batch=256, steps=4):
 
 
 def run_wide(workload, batch, steps, warmup, world, rank, device, graph=True, kernel_iters=20, cpu=True,
-             cpu_batch=256, cpu_steps=4):
+             cpu_batch=256, cpu_steps=4, overlap_ranges=0):
     """NLL-training samples/s of a wide workload (trajectory_FC_large = configs[2], trajectory_LSTM_large =
     configs[3]) per GPU, same step definition and timing contract as main(). Returns rank 0's JSON object."""
     from bcnf_amd import CondRealNVP_v2
@@ -631,7 +682,9 @@ def run_wide(workload, batch, steps, warmup, world, rank, device, graph=True, ke
     model.train()
     model.fused.set_seed(2024_03_25 + 7919 * rank)
     data = DeviceBatches(max(16384, 4 * batch), batch, device, seed=2024_03_25 + rank)
-    step = TrainStep(model, lr=2e-4, capture=graph)
+    # world > 1: the backward in `overlap_ranges` block ranges, each range's gradient slice all-reduced while the
+    # rest runs (eager steps: the collectives sit between kernel launches)
+    step = TrainStep(model, lr=2e-4, capture=graph, overlap_ranges=overlap_ranges)
     step.broadcast_parameters()
     step.set_pool(data.y, data.traj)
     batches = [data.next_indices() for _ in range(warmup + steps)]
@@ -676,7 +729,8 @@ def run_wide(workload, batch, steps, warmup, world, rank, device, graph=True, ke
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic ballistic trajectories (bcnf_amd/data.py), device-resident",
         "config": {"workload": f"{WIDE_NAMES[workload]} NLL training step", "batch_per_gpu": B,
-                   "global_batch": B * world, "parallelism": f"dp{world}", "hip_graph": graph,
+                   "global_batch": B * world, "parallelism": f"dp{world}", "hip_graph": step.capture,
+                   "overlap_ranges": step.overlap_ranges,
                    "n_blocks": kw["n_blocks"], "nested_sizes": kw["nested_sizes"],
                    "n_conditions": kw["n_conditions"], "dropout": kw["dropout"]},
         "last_loss": vals[-1][0] if vals else None,
@@ -702,8 +756,9 @@ def main_wide(args):
     world, rank, local = init_dist(args)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
+    ov = args.overlap_ranges if args.overlap_ranges is not None else (OVERLAP_RANGES if world > 1 else 0)
     line = run_wide(args.workload, args.batch, args.steps, args.warmup, world, rank, device, graph=not args.no_graph,
-                    kernel_iters=args.kernel_iters, cpu=not args.no_cpu_baseline)
+                    kernel_iters=args.kernel_iters, cpu=not args.no_cpu_baseline, overlap_ranges=ov)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -878,6 +933,25 @@ def run_resim(n_traj, steps, warmup, world, rank, device, n_draws=1000, cpu=True
     e1.record(st)
     torch.cuda.synchronize()
     k_us = e0.elapsed_time(e1) * 1e3 / 3
+    # the reference-compatible resimulate() also hands the (N, M, steps, 3) float64 positions to the host as numpy:
+    # timed separately (same barrier / max-over-ranks contract), never part of `value`
+    import types
+    from bcnf_amd.resimulation import resimulate
+    host_model = types.SimpleNamespace(parameter_index_mapping=pim, device=device)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(2):
+        xh = resimulate(host_model, T, dt, dd, y, break_on_impact=True, verbose=False)
+    if world > 1:
+        dist.barrier()
+    el_host = (time.perf_counter() - t0) / 2
+    if world > 1:
+        tt = torch.tensor([el_host], device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el_host = float(tt.item())
+    host_bytes = xh.nbytes
+    del xh
     value = n_draws * n_traj * steps / el
     seen = ranks_seen(world, device)
     if rank != 0:
@@ -888,8 +962,8 @@ def run_resim(n_traj, steps, warmup, world, rank, device, n_draws=1000, cpu=True
     ach = flop / (k_us * 1e-6) / 1e12
     out_bytes = out.numel() * 8
     line = {
-        "metric": "re-simulated trajectories/sec (resimulate, y_hat given: 1000 draws x 1024 trajectories, T=2, "
-                  "dt=1/15, break_on_impact)",
+        "metric": "re-simulated trajectories/sec, device-resident (resimulate_device: y_hat in HBM, positions left "
+                  "in HBM; 1000 draws x 1024 trajectories, T=2, dt=1/15, break_on_impact)",
         "value": round(value, 1), "unit": "trajectories/s", "n_gpus": world, "steps": steps, "warmup": warmup,
         "ms_per_step": round(el / steps * 1e3, 4), "ranks_seen": seen, "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f64",
@@ -897,6 +971,10 @@ def run_resim(n_traj, steps, warmup, world, rank, device, n_draws=1000, cpu=True
         "config": {"workload": "resimulate (simulation/resimulation.py:21-59), y_hat given", "trajectories": n_traj,
                    "draws": n_draws, "steps_per_trajectory": int(out.shape[2]), "parallelism": f"trajectory shards x{world}",
                    "output": list(out.shape)},
+        "end_to_end": {"value": round(n_draws * n_traj / el_host, 1), "unit": "trajectories/s",
+                       "ms_per_call": round(el_host * 1e3, 2), "host_bytes_per_rank": host_bytes,
+                       "what": "resimulate() (the reference's signature and result): the same launch + the float64 "
+                               "positions copied to a host numpy array (pageable device-to-host copy)"},
         "roofline": {"bound": "valu-fp64", "kernel": "k_resim", "achieved": round(ach, 3), "peak": PEAK_FP64_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(ach / PEAK_FP64_TFLOPS, 4), "traffic": _pmc_traffic("k_resim"),
                      "avg_us": round(k_us, 2), "flop_per_launch": flop, "attempts_per_trajectory":

@@ -27,6 +27,13 @@ def test_gpus2_launches_two_ranks():
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout          # ONE JSON line, from rank 0
     assert lines[0]["n_gpus"] == 2 and lines[0]["ranks_seen"] == 2 and lines[0]["backend"] == "gloo"
+    # every sub-line of the default run (configs[2] - [4], re-simulation) runs on both ranks at world 2
+    from bench import SUBLINES
+    sub = lines[0]["secondary"]
+    assert list(sub) == [wl for wl, _ in SUBLINES]
+    for wl, res in sub.items():
+        assert "error" not in res, (wl, res)
+        assert res["ranks_seen"] == 2 and res["n_gpus"] == 2, (wl, res)
 
 
 @pytest.mark.timeout(120)

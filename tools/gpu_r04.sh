@@ -1,0 +1,35 @@
+# GPU box, one call (round 4): STEPS selects what runs, in this order, each under its own limit, the chain stopping at
+# the first failure:  tests = the full GPU suite; bench = the default bench line; bench2 = `bench.py --gpus 2` (two
+# ranks sharing the card over gloo: a plumbing rehearsal, not a scaling number); abk = same-box A/B of the FC_small
+# kernels against build_exp/libhead.so; prof = rocprofv3 kernel stats of the default bench.
+#   bash tools/gpu_r04.sh <tag> "tests bench bench2"
+set -e
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+T=${1:-r04}
+STEPS=${2:-"tests bench"}
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 540 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${T}_gpu_tests.log 2>&1 || { tail -40 gpurun_out/${T}_gpu_tests.log; exit 1; }
+      tail -2 gpurun_out/${T}_gpu_tests.log ;;
+    testsk)
+      timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "$TESTK" > gpurun_out/${T}_gpu_testsk.log 2>&1 || { tail -40 gpurun_out/${T}_gpu_testsk.log; exit 1; }
+      tail -2 gpurun_out/${T}_gpu_testsk.log ;;
+    bench)
+      timeout -k 10 420 python bench.py > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || { tail -20 gpurun_out/${T}_bench.err; exit 1; }
+      python tools/show_bench.py gpurun_out/${T}_bench.json ;;
+    bench2)
+      timeout -k 10 420 python bench.py --gpus 2 --no-cpu-baseline > gpurun_out/${T}_bench2.json 2> gpurun_out/${T}_bench2.err || { tail -20 gpurun_out/${T}_bench2.err; exit 1; }
+      python tools/show_bench.py gpurun_out/${T}_bench2.json ;;
+    abk)
+      for i in 1 2; do
+        timeout -k 10 120 python tools/abk.py
+        BCNF_AMD_LIB=build_exp/libhead.so timeout -k 10 120 python tools/abk.py
+      done 2>&1 | grep -v amdgpu.ids | tee gpurun_out/${T}_ab_kernels.txt ;;
+    prof)
+      cd /tmp && export TMPDIR=/tmp
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/${T}_prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --no-secondary --no-cpu-baseline --steps 40 > $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.log; exit 1; }
+      cd $GRAFT_REPO_ROOT ;;
+  esac
+done
