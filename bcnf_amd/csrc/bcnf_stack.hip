@@ -32,12 +32,19 @@
 namespace {
 
 constexpr int NC16_MAX = 16;           // C <= 256: register-resident column tiles of k_hp / k_dh / k_dw1h            // tiles: D_1..D_NH, D_T, D_S, A_0..A_NH, PA, GA, PB, GB
-// Backward LDS tile of [16 samples s][16 columns r]: element (s, r) at r * TPITCH + 4 (s & 3) + (s >> 2), so the MFMA
-// operand of lane (q, r) for the four K-steps t (sample 4 t + q) is ONE 16-B read at r * TPITCH + 4 q (pitch 24:
-// conflict-free ds_read_b128).
-constexpr int TPITCH = 24;
-constexpr int TILE = 16 * TPITCH;                // 384 floats
-__host__ __device__ constexpr int tile_ix(int s, int r) { return r * TPITCH + 4 * (s & 3) + (s >> 2); }
+// Backward LDS tile of [16 samples s][16 columns r], unpadded: the four samples 4 t + q (t = 0..3) of column r sit in
+// the 16-B slot tile_slot(r, q) = 4 r + ((q + (r >> 1)) & 3), so the MFMA operand of lane (q, r) for the four K-steps t
+// is ONE 16-B read at 4 tile_slot(r, q), and each ds_read_b128 lane group covers all 16 slot banks (conflict-free). The
+// rotation by r >> 1 also spreads the element stores: a compute / helper wave holds samples w + 4 i (sample_of) --
+// one q per wave, t = i -- so a 32-lane half stores to 16 distinct banks (2-way, which costs a ds_write_b32 nothing;
+// the padded pitch-24 rows were 4-way: 4.13M conflict cycles per k_backward launch).
+constexpr int TILE = 256;
+__host__ __device__ constexpr int tile_slot(int r, int q) { return 4 * r + ((q + (r >> 1)) & 3); }
+__host__ __device__ constexpr int tile_ix(int s, int r) { return 4 * tile_slot(r, s & 3) + (s >> 2); }
+// Sample (0..15) a forward / backward thread t8 (role-relative, 256 per role) works on: wave w = t8 >> 6 holds the
+// samples w + 4 i of its four 16-lane rows i (the activation records and the derivative slots are per t8, so both
+// kernels use the same map).
+__host__ __device__ constexpr int sample_of(int t8) { return (t8 >> 6) + 4 * ((t8 >> 4) & 3); }
 constexpr int STAGE_REC = 4;   // 16 * RF (RB) floats  <= 4 float4 per thread (RF, RB <= 256)
 constexpr int RING = STAGE_REC * BCNF_WG * 4;    // floats per record-ring slot: a Stage stores all of it
 // floats per lane of a block's activation record (ActRec); the AR1 single floats follow all the float4 parts
@@ -1170,7 +1177,7 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
   const float* pf = pk + L.pf_off;
   const bool helper = threadIdx.x >= BCNF_WG;
   const int t8 = (int)threadIdx.x & (BCNF_WG - 1);              // thread index within the role
-  const int j = t8 & 15, s = t8 >> 4;                           // (sample, lane) of a compute / Philox thread
+  const int j = t8 & 15, s = sample_of(t8);                     // (sample, lane) of a compute / Philox thread
   const long long b = (long long)blockIdx.x * 16 + s;
   const long long bc = b < B ? b : B - 1;                       // rows past the batch replay the last sample
   uint64_t seed = 0, off = 0;
@@ -1249,7 +1256,7 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
     floatx4 mk0 = {1.f, 1.f, 1.f, 1.f}, mk1 = {1.f, 1.f, 1.f, 1.f};
     auto fetch_head = [&](int sl) {
       ld_rec<0, FWD_HEAD>(hd, rec + sl * RING + j * L.RF);
-      const float* hq = hpb + sl * 1024 + tid;
+      const float* hq = hpb + sl * 1024 + 16 * s + j;            // [sample][neuron] partial tiles
 #pragma unroll
       for (int i = 0; i < 4; ++i) hq4[i] = hq[256 * i];
       if (DROP) {
@@ -1685,7 +1692,7 @@ __device__ __forceinline__ void bwd_grad_jobs(const float* __restrict__ Td, cons
   const int l64 = threadIdx.x & 63, q = l64 >> 4, r = l64 & 15;
   constexpr int UW = (J::NW + 3) / 4, US = (J::NS + 3) / 4;
   floatx4 a[UW], bv[UW], v[US];                            // lane (q, r): samples 4 t + q of column r, t = 0..3
-  const int o = r * TPITCH + 4 * q;
+  const int o = 4 * tile_slot(r, q);
 #pragma unroll
   for (int u = 0; u < UW; ++u) {                           // all operand reads first
     const int c = hw + 4 * u < J::NW ? hw + 4 * u : J::NW - 1;
@@ -1748,7 +1755,7 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
   const float* pbk = pk + L.pb_off;
   const bool helper = threadIdx.x >= BCNF_WG;
   const int t8 = (int)threadIdx.x & (BCNF_WG - 1);
-  const int j = t8 & 15, s = t8 >> 4;
+  const int j = t8 & 15, s = sample_of(t8);
   const int tix = tile_ix(s, j);
   // diagnostic build: per-phase cycles of workgroup 0's wave 0 (compute) and wave 4 (helper) -> g_phase
   unsigned long long ph_t = BCNF_STAMPS ? __builtin_amdgcn_s_memtime() : 0ULL, ph_acc[4] = {0, 0, 0, 0};
