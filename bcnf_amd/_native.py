@@ -30,6 +30,7 @@ EXPORTS = (
     "bcnf_nll_forward", "bcnf_nll_backward", "bcnf_grad_partials", "bcnf_adam_step", "bcnf_adam_step_bookkeep",
     "bcnf_grad_sumsq",
     "bcnf_clip_grad_norm", "bcnf_linear_forward", "bcnf_linear_work_bytes", "bcnf_linear_backward",
+    "bcnf_linear_gelu_forward", "bcnf_linear_gelu_backward",
     "bcnf_inverse_scratch_bytes", "bcnf_stack_dh", "bcnf_backward_tail", "bcnf_gather_rows2",
     "bcnf_gather_batch", "bcnf_advance_counters", "bcnf_fold_bytes", "bcnf_fold_slab_bytes",
     "bcnf_pack_params_fold", "bcnf_fold_nll_forward", "bcnf_fold_backward_tail",
@@ -161,6 +162,9 @@ def _bind(lib):
         "bcnf_linear_forward": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp]),
         "bcnf_linear_work_bytes": (_i64, [_i64, _i32, _i32]),
         "bcnf_linear_backward": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+        "bcnf_linear_gelu_forward": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, ctypes.c_float, _vp, _i32, _vp, _vp,
+                                            _vp]),
+        "bcnf_linear_gelu_backward": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
         "bcnf_wide_supported": (_i32, [_pdesc]),
         "bcnf_wide_param_count": (_i32, [_pdesc, _pi64, _pi64]),
         "bcnf_wide_packed_bytes": (_i32, [_pdesc, _pi64]),

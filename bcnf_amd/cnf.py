@@ -16,10 +16,12 @@ There is no CPU path for the coupling stack: CPU tensors raise.
 from __future__ import annotations
 
 import math
+import weakref
 from abc import abstractmethod
 from typing import Any
 
 import numpy as np
+
 import torch
 import torch.nn as nn
 
@@ -335,6 +337,10 @@ class CondRealNVP_v2(ConditionalInvertibleLayer):
         self.layers.append(ConditionalAffineCouplingLayer(self.size, self.nested_sizes, self.n_conditions,
                                                           **coupling_kwargs))
         self._build_fused()
+        if n_conditions > 0:       # the fused feature dropout draws from the coupling's device Philox state
+            for fn in self.feature_network_stack.feature_networks:
+                if isinstance(fn, FullyConnectedFeatureNetwork):
+                    fn._rng_owner = weakref.ref(self)
 
     # ------------------------------------------------------------------ fused stack plumbing
     def _canonical(self):
@@ -557,12 +563,10 @@ class CondRealNVP_v2(ConditionalInvertibleLayer):
             mods = list(fn.nn)
             if not mods or type(mods[-1]) not in (nn.Linear, HIPLinear):
                 return None
-            x = c.reshape(c.shape[0], -1)
-            for mod in mods[:-1]:
-                x = mod(x)
+            x = fn.run(c.reshape(c.shape[0], -1), upto=-1)     # the fused Linear + GELU + Dropout layers
             lin = mods[-1]
         elif isinstance(fn, LSTMFeatureNetwork) and fn.pooling == "mean" and fn.pool_dim == 1:
-            x = fn.lstm(c)[0].mean(dim=1)
+            x = fn.lstm_out(c).mean(dim=1)
             lin = fn.linear
         else:
             return None

@@ -256,19 +256,14 @@ __device__ __forceinline__ void ld16(float* __restrict__ w, const float* __restr
 // checks (overflow -> inf, underflow -> 0, which every caller tolerates).
 __device__ __forceinline__ float exp_fast(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896340736f); }
 
+// tanh(a) = 1 - 2 / (exp(2a) + 1): one v_exp_f32, one v_rcp_f32, branch-free, saturating to +-1 through inf / 0
+// (r04: replaces a two-region form -- odd polynomial below |a| = 0.625, this expression above, both evaluated and
+// selected -- that cost ~16 VALU instead of 5). Absolute error <= 1.9e-7 on [-12, 12] against float64 tanh
+// (emulated fp32, tools/fit_erf.py tanh_check); S = tanh(s') enters the coupling as exp(S) and the log-det as S, both
+// of which see absolute, not relative, error.
 __device__ __forceinline__ float tanh_bf(float a) {
-  const float t = fabsf(a), s = a * a;
-  float p = 2.321433276e-03f;                       // |a| < 0.625 : a + a^3 P(a^2)
-  p = fmaf(p, s, -8.373901248e-03f);
-  p = fmaf(p, s, 2.178018540e-02f);
-  p = fmaf(p, s, -5.396108329e-02f);
-  p = fmaf(p, s, 1.333331466e-01f);
-  p = fmaf(p, s, -3.333333433e-01f);
-  const float rs = fmaf(a * s, p, a);
-  const float e = exp_fast(2.0f * t);               // otherwise   : 1 - 2 / (exp(2t) + 1)
-  float rl = 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
-  rl = copysignf(rl, a);
-  return (t < 0.625f) ? rs : rl;
+  const float e = __builtin_amdgcn_exp2f(a * 2.88539008177792681472f);   // exp(2a)
+  return fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
 }
 
 // Exact-erf GELU as nn.GELU(approximate='none') (cnf.py:81 via LayerFactory): x Phi(x), with the normal
@@ -280,30 +275,38 @@ __device__ __forceinline__ float tanh_bf(float a) {
 // double-precision function (the fp32 0.5 x (1 + erf(x/sqrt2)) of the reference: < 4.5e-7). Replaces (r02x) the
 // Numerical Recipes erfcc form t exp(-z^2 + P9(t)), which took a second exp and three more FMAs per call: the
 // GELUs are ~18% of the FC_small forward's compute chain (an r02 experiment build with GELU replaced by x/2: 64.4 -> 52.5 us).
-__device__ __forceinline__ float gelu_tail(float x, float& ez) {   // Phi(-|x|); ez = exp(-x^2 / 2)
+// r04: the 1/2 and 1/sqrt(2 pi) live in the constants: the exponential is phi(x) = exp(-x^2/2) / sqrt(2 pi) itself
+// (exp2(x^2 (-log2(e)/2) + log2(1/sqrt(2 pi))): the derivative's phi costs nothing extra) and Q carries sqrt(2 pi)/2,
+// so h = Phi(-|x|) = t Q(t) phi(x).
+__device__ __forceinline__ float gelu_tq(float x, float& phi) {   // t Q(t); phi = phi(x)
   const float t = __builtin_amdgcn_rcpf(fmaf(2.616295218e-01f, fabsf(x), 1.0f));   // p / sqrt2
-  float q = -7.295463979e-02f;
-  q = fmaf(q, t, 2.239411026e-01f);
-  q = fmaf(q, t, -1.021702215e-01f);
-  q = fmaf(q, t, 1.654430181e-01f);
-  q = fmaf(q, t, 7.358670980e-02f);
-  q = fmaf(q, t, 1.080111340e-01f);
-  q = fmaf(q, t, 1.041427255e-01f);
-  ez = __builtin_amdgcn_exp2f((x * x) * -0.72134752044448170368f);                 // -log2(e) / 2
-  return (t * q) * ez;
+  float q = -1.828701629e-01f;                                                      // Q x sqrt(2 pi)
+  q = fmaf(q, t, 5.613370996e-01f);
+  q = fmaf(q, t, -2.561027660e-01f);
+  q = fmaf(q, t, 4.147041470e-01f);
+  q = fmaf(q, t, 1.844545274e-01f);
+  q = fmaf(q, t, 2.707437625e-01f);
+  q = fmaf(q, t, 2.610471003e-01f);
+  phi = __builtin_amdgcn_exp2f(fmaf(x * x, -0.72134752044448170368f, -1.32574806473615920f));
+  return t * q;
 }
-__device__ __forceinline__ float gelu_f(float x) {
-  float ez;
-  const float h = gelu_tail(x, ez);
-  return x * (x < 0.f ? h : 1.0f - h);
+__device__ __forceinline__ float gelu_f(float x) {          // x Phi(x) = max(x, 0) - |x| Phi(-|x|)
+  float phi;
+  const float h = gelu_tq(x, phi) * phi;
+  // max(x, 0) as ONE v_max_f32 (fmaxf under IEEE mode canonicalises an operand that comes out of inline asm); it reads
+  // x after h, whose computation from x carries any wait states an MFMA-produced x needs
+  float r;
+  asm("v_max_f32_e32 %0, 0, %1" : "=v"(r) : "v"(x), "v"(h));
+  return fmaf(-fabsf(x), h, r);
 }
-// GELU and its derivative Phi(x) + x phi(x) (phi from the same exp(-x^2/2)).
+// GELU and its derivative Phi(x) + x phi(x): Phi(x) = 1/2 + sign(x) (1/2 - Phi(-|x|)), the sign moved by one bit
+// and-or (v_and_or_b32) instead of a compare and a select.
 __device__ __forceinline__ void gelu_fg(float x, float& g, float& dg) {
-  float ez;
-  const float h = gelu_tail(x, ez);
-  const float cdf = x < 0.f ? h : 1.0f - h;
+  float phi;
+  const float hm = fmaf(-gelu_tq(x, phi), phi, 0.5f);                      // 1/2 - Phi(-|x|) >= 0
+  const float cdf = 0.5f + __uint_as_float(__float_as_uint(hm) | (__float_as_uint(x) & 0x80000000u));
   g = x * cdf;
-  dg = fmaf(x, ez * 0.39894228040143267794f, cdf);
+  dg = fmaf(x, phi, cdf);
 }
 
 // ---------------------------------------------------------------------------------------------

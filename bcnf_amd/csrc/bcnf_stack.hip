@@ -294,9 +294,12 @@ __device__ float rec_pm(const BcnfLayout& L, const float* P, const float* Q, int
 // one element, so the launch is one load round trip, not a chain of them).
 constexpr int PACK_WG_MAX = 4096;
 
+// train_only (the folded training step, bcnf_pack_params_fold): only what its forward, backward and tail read --
+// PF, PB, W1hR and the log-det constant -- not the inverse records PI / PM (the costliest entries: rec_pm calls
+// rec_f per element) nor the unfolded projection's W1hC / b1c: about half the elements of a full pack.
 __device__ __forceinline__ void pack_body(const BcnfLayout& L, const float* __restrict__ P,
                                           const float* __restrict__ Q, float* __restrict__ out, int bx, int npw,
-                                          float* __restrict__ part) {
+                                          float* __restrict__ part, bool train_only = false) {
   if (bx == 0) {
     float acc = 0.f;
     if (L.act_norm) {
@@ -320,10 +323,12 @@ __device__ __forceinline__ void pack_body(const BcnfLayout& L, const float* __re
   const int n_pb = L.nb * 16 * L.RB;
   const int n_w = L.Cp * L.NKp;                       // each of W1hC, W1hR
   const int n_pm = L.nb * L.PMB;
-  const int total = 2 * n_pf + n_pb + 2 * n_w + L.NKp + n_pm;
-  for (int i = (bx - 1) * BCNF_WG + threadIdx.x; i < total; i += npw * BCNF_WG) {
+  const int total = train_only ? n_pf + n_pb + n_w : 2 * n_pf + n_pb + 2 * n_w + L.NKp + n_pm;
+  for (int ii0 = (bx - 1) * BCNF_WG + threadIdx.x; ii0 < total; ii0 += npw * BCNF_WG) {
     float v;
     long long o;
+    // train_only: [PF | PB | W1hR] mapped onto the full pack's index space (PI and W1hC skipped)
+    const int i = (train_only && ii0 >= n_pf + n_pb) ? ii0 + n_pf + n_w : ii0;
     if (i < n_pf) {                                   // PF
       const int kj = i / L.RF, e = i - kj * L.RF;
       v = rec_f(L, P, Q, kj >> 4, kj & 15, e, false);
@@ -369,9 +374,10 @@ __global__ __launch_bounds__(BCNF_WG) void k_pack(BcnfLayout L, const float* __r
 }
 
 // Record workgroups of a pack launch (the log-det workgroup not included).
-int pack_wgs(const BcnfLayout& L) {
-  const long long total = 2LL * L.nb * 16 * L.RF + (long long)L.nb * 16 * L.RB + 2LL * L.Cp * L.NKp + L.NKp +
-                          (long long)L.nb * L.PMB;
+int pack_wgs(const BcnfLayout& L, bool train_only = false) {
+  const long long total = train_only ? (long long)L.nb * 16 * (L.RF + L.RB) + (long long)L.Cp * L.NKp
+                                     : 2LL * L.nb * 16 * L.RF + (long long)L.nb * 16 * L.RB + 2LL * L.Cp * L.NKp +
+                                           L.NKp + (long long)L.nb * L.PMB;
   const long long w = (total + BCNF_WG - 1) / BCNF_WG;
   return (int)(w < PACK_WG_MAX ? (w > 0 ? w : 1) : PACK_WG_MAX);
 }
@@ -462,7 +468,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_pack_fold(BcnfLayout L, const float
     gather2_rows(ga.idx, ga.n, ga.rpw, ga.s0, ga.c0, ga.d0, ga.s1, ga.c1, ga.d1, ga.cursor, bx);
     return;
   }
-  pack_body(L, P, Q, out, bx - ga.nwg, npw, smem);
+  pack_body(L, P, Q, out, bx - ga.nwg, npw, smem, true);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2499,7 +2505,7 @@ int bcnf_pack_params_fold(const BcnfStackDesc* desc, const float* params, const 
                         g.cols1, 0};
     gather2_plan(g.n, &ga.rpw, &ga.nwg);
   }
-  const int npw = pack_wgs(L);
+  const int npw = pack_wgs(L, true);
   const unsigned grid = (unsigned)(L.NKp / 16 * FOLD_SPLIT + ga.nwg + npw + 1);
   hipLaunchKernelGGL(k_pack_fold, dim3(grid), dim3(BCNF_WG), 0, (hipStream_t)stream, L, params, qmats, (float*)packed,
                      feat_weight, feat_bias, (int)in_features, fold, ga, npw);

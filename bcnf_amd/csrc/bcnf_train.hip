@@ -213,11 +213,24 @@ __global__ __launch_bounds__(BCNF_WG) void k_clip(TList T, const float* __restri
 // Small GEMMs for nn.Linear. One wave = one 16x16 output tile, v_mfma_f32_16x16x4f32 over the
 // reduction; lane l supplies A[l&15][l>>4] and B[l>>4][l&15] and owns D[4(l>>4)+i][l&15].
 // C[M][Nc] = A[M][K] * op(B) + bias; op(B)[k][n] = TB ? B[n*ldb + k] : B[k*ldb + n].
+// SA: every A element is multiplied by the same element of sa ([M][lda]) as it is loaded -- the backward of a fused
+// GELU + dropout layer, dL/dpre = dL/da * g, never stored.
+// ACT (feature MLP layer, feature_network.py:128-134: Linear -> GELU -> Dropout): the epilogue stores
+// a = mask GELU(pre) and, when G is given, g = mask GELU'(pre), mask = keep_scale or 0 from Philox4x32-10
+// (key = rng seed ^ salt, counter = (column, row / 4, rng offset)) when rng is given, else 1.
 // ------------------------------------------------------------------------------------------------
-template <bool TB>
+struct ActArgs {
+  float* G;
+  const uint64_t* rng;
+  uint32_t salt, thresh;
+  float keep;
+};
+
+template <bool TB, bool SA, bool ACT>
 __global__ __launch_bounds__(BCNF_WG) void k_gemm(const float* __restrict__ A, int lda, const float* __restrict__ Bm,
                                                   int ldb, const float* __restrict__ bias, float* __restrict__ C,
-                                                  int ldc, long long M, int Nc, int K) {
+                                                  int ldc, long long M, int Nc, int K, const float* __restrict__ sa,
+                                                  ActArgs act) {
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lq = l >> 4;
   const long long row0 = ((long long)blockIdx.x * 4 + wave) * 16;
   const int col0 = blockIdx.y * 16;
@@ -225,23 +238,26 @@ __global__ __launch_bounds__(BCNF_WG) void k_gemm(const float* __restrict__ A, i
   const long long ar = row0 + lr < M ? row0 + lr : M - 1;     // clamped rows: loaded, never stored
   const int bc = col0 + lr < Nc ? col0 + lr : Nc - 1;
   const float* a = A + ar * lda;
+  const float* as = SA ? sa + ar * lda : nullptr;
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
   int k0 = 0;
   for (; k0 + 32 <= K; k0 += 32) {              // 8 MFMA steps, all 16 loads issued first
-    float av[8], bv[8];
+    float av[8], bv[8], sv[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       const int k = k0 + 4 * t + lq;
       av[t] = a[k];
+      if (SA) sv[t] = as[k];
       bv[t] = TB ? Bm[(long long)bc * ldb + k] : Bm[(long long)k * ldb + bc];
     }
 #pragma unroll
-    for (int t = 0; t < 8; ++t) acc = mfma4(av[t], bv[t], acc);
+    for (int t = 0; t < 8; ++t) acc = mfma4(SA ? av[t] * sv[t] : av[t], bv[t], acc);
   }
   for (; k0 < K; k0 += 4) {
     const int k = k0 + lq;
     const int kc = k < K ? k : K - 1;
     float av = a[kc];
+    if (SA) av *= as[kc];
     float bv = TB ? Bm[(long long)bc * ldb + kc] : Bm[(long long)kc * ldb + bc];
     av = k < K ? av : 0.f;
     bv = k < K ? bv : 0.f;
@@ -250,19 +266,45 @@ __global__ __launch_bounds__(BCNF_WG) void k_gemm(const float* __restrict__ A, i
   const int col = col0 + lr;
   if (col < Nc) {
     const float bb = bias ? bias[col] : 0.f;
+    if (ACT) {
+      float m[4] = {1.f, 1.f, 1.f, 1.f};
+      if (act.rng) {
+        const uint64_t seed = act.rng[0], off = act.rng[1];
+        const uint4 r = philox4x32_10(make_uint4((uint32_t)col, (uint32_t)((row0 >> 2) + lq), (uint32_t)off,
+                                                 (uint32_t)(off >> 32)),
+                                      make_uint2((uint32_t)seed ^ act.salt, (uint32_t)(seed >> 32)));
+        m[0] = r.x >= act.thresh ? act.keep : 0.f;
+        m[1] = r.y >= act.thresh ? act.keep : 0.f;
+        m[2] = r.z >= act.thresh ? act.keep : 0.f;
+        m[3] = r.w >= act.thresh ? act.keep : 0.f;
+      }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const long long r = row0 + 4 * lq + i;
-      if (r < M) C[r * ldc + col] = acc[i] + bb;
+      for (int i = 0; i < 4; ++i) {
+        const long long rr = row0 + 4 * lq + i;
+        float g, dg;
+        gelu_fg(acc[i] + bb, g, dg);
+        if (rr < M) {
+          C[rr * ldc + col] = g * m[i];
+          if (act.G) act.G[rr * ldc + col] = dg * m[i];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long long r = row0 + 4 * lq + i;
+        if (r < M) C[r * ldc + col] = acc[i] + bb;
+      }
     }
   }
 }
 
 // Split-K weight gradient: work[s][n][k] = sum_{m in split s} dY[m][n] X[m][k],
 // bwork[s][n] = sum_{m in split s} dY[m][n]. grid = (tiles_n * tiles_k / 4 rounded up, splits).
+template <bool SA>
 __global__ __launch_bounds__(BCNF_WG) void k_gemm_wt(const float* __restrict__ X, const float* __restrict__ dY,
                                                      long long M, int N, int K, int rows_per_split,
-                                                     float* __restrict__ work, float* __restrict__ bwork) {
+                                                     float* __restrict__ work, float* __restrict__ bwork,
+                                                     const float* __restrict__ sg) {
   const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lq = l >> 4;
   const int tiles_k = (K + 15) / 16, tiles_n = (N + 15) / 16;
   const int tile = blockIdx.x * 4 + wave;
@@ -283,6 +325,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_gemm_wt(const float* __restrict__ X
     for (int t = 0; t < 8; ++t) {
       const long long m = m0 + 4 * t + lq;
       av[t] = dY[m * N + n];
+      if (SA) av[t] *= sg[m * N + n];     // dL/dpre = dL/da * g of a fused GELU + dropout layer
       bv[t] = X[m * K + k];
     }
 #pragma unroll
@@ -295,6 +338,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_gemm_wt(const float* __restrict__ X
     const long long m = m0 + lq;
     const long long mc = m < m_end ? m : m_end - 1;
     float av = dY[mc * N + n];          // A[n][m] = dY[m][n]
+    if (SA) av *= sg[mc * N + n];
     float bv = X[mc * K + k];           // B[m][k] = X[m][k]
     av = m < m_end ? av : 0.f;
     bv = m < m_end ? bv : 0.f;
@@ -528,8 +572,27 @@ int bcnf_linear_forward(const float* x, const float* weight, const float* bias, 
   if (rows == 0) return BCNF_OK;
   if (!x || !weight || !y) return BCNF_ERR_ARG;
   const dim3 grid((unsigned)((rows + 63) / 64), (unsigned)((out_features + 15) / 16));
-  hipLaunchKernelGGL(k_gemm<true>, grid, dim3(BCNF_WG), 0, (hipStream_t)stream, x, in_features, weight, in_features,
-                     bias, y, out_features, (long long)rows, out_features, in_features);
+  hipLaunchKernelGGL((k_gemm<true, false, false>), grid, dim3(BCNF_WG), 0, (hipStream_t)stream, x, in_features, weight,
+                     in_features, bias, y, out_features, (long long)rows, out_features, in_features,
+                     (const float*)nullptr, ActArgs{});
+  return launched();
+}
+
+int bcnf_linear_gelu_forward(const float* x, const float* weight, const float* bias, int64_t rows, int32_t in_features,
+                             int32_t out_features, float p, const uint64_t* rng, int32_t salt, float* a, float* g,
+                             void* stream) {
+  if (rows < 0 || in_features < 1 || out_features < 1 || !(p >= 0.f && p < 1.f)) return BCNF_ERR_ARG;
+  if (rows == 0) return BCNF_OK;
+  if (!x || !weight || !a) return BCNF_ERR_ARG;
+  ActArgs act{g, p > 0.f ? rng : nullptr, (uint32_t)salt * 0x9E3779B9u, 0u, 1.f};
+  if (act.rng) {
+    act.thresh = (uint32_t)fmin(4294967295.0, floor((double)p * 4294967296.0 + 0.5));   // keep iff u >= thresh
+    act.keep = (float)(1.0 / (1.0 - (double)p));
+  }
+  const dim3 grid((unsigned)((rows + 63) / 64), (unsigned)((out_features + 15) / 16));
+  hipLaunchKernelGGL((k_gemm<true, false, true>), grid, dim3(BCNF_WG), 0, (hipStream_t)stream, x, in_features, weight,
+                     in_features, bias, a, out_features, (long long)rows, out_features, in_features,
+                     (const float*)nullptr, act);
   return launched();
 }
 
@@ -539,11 +602,13 @@ int64_t bcnf_linear_work_bytes(int64_t rows, int32_t in_features, int32_t out_fe
   return (int64_t)splits * ((int64_t)out_features * in_features + out_features) * 4;
 }
 
-int bcnf_linear_backward(const float* x, const float* weight, const float* dy, int64_t rows, int32_t in_features,
-                         int32_t out_features, float* dx, float* dweight, float* dbias, void* work, void* stream) {
-  if (rows < 0 || in_features < 1 || out_features < 1) return BCNF_ERR_ARG;
-  hipStream_t st = (hipStream_t)stream;
-  const int K = in_features, N = out_features;
+}  // extern "C"
+
+namespace {
+// dL/dx, dL/dW, dL/db of y = x W^T + b from dy, or -- sg given -- of a fused GELU + dropout layer from dL/da = dy and
+// its saved g (dL/dpre = dy * g, formed as each operand element is loaded).
+int linear_backward(const float* x, const float* weight, const float* dy, const float* sg, int64_t rows, int K, int N,
+                    float* dx, float* dweight, float* dbias, void* work, hipStream_t st) {
   if (rows == 0) {
     if (dweight)
       if (const int rc = bcnf_rt::hip_status(hipMemsetAsync(dweight, 0, sizeof(float) * (size_t)N * K, st))) return rc;
@@ -555,8 +620,12 @@ int bcnf_linear_backward(const float* x, const float* weight, const float* dy, i
   if (dx) {   // dX[m][k] = sum_n dY[m][n] W[n][k]
     if (!weight) return BCNF_ERR_ARG;
     const dim3 grid((unsigned)((rows + 63) / 64), (unsigned)((K + 15) / 16));
-    hipLaunchKernelGGL(k_gemm<false>, grid, dim3(BCNF_WG), 0, st, dy, N, weight, K, (const float*)nullptr, dx, K,
-                       (long long)rows, K, N);
+    if (sg)
+      hipLaunchKernelGGL((k_gemm<false, true, false>), grid, dim3(BCNF_WG), 0, st, dy, N, weight, K,
+                         (const float*)nullptr, dx, K, (long long)rows, K, N, sg, ActArgs{});
+    else
+      hipLaunchKernelGGL((k_gemm<false, false, false>), grid, dim3(BCNF_WG), 0, st, dy, N, weight, K,
+                         (const float*)nullptr, dx, K, (long long)rows, K, N, (const float*)nullptr, ActArgs{});
     int rc = launched();
     if (rc) return rc;
   }
@@ -567,8 +636,13 @@ int bcnf_linear_backward(const float* x, const float* weight, const float* dy, i
     const int tiles = ((N + 15) / 16) * ((K + 15) / 16);
     float* w = (float*)work;
     float* bw = w + (long long)splits * N * K;
-    hipLaunchKernelGGL(k_gemm_wt, dim3((unsigned)((tiles + 3) / 4), (unsigned)splits), dim3(BCNF_WG), 0, st, x, dy,
-                       (long long)rows, N, K, rps, w, dbias ? bw : nullptr);
+    const dim3 grid((unsigned)((tiles + 3) / 4), (unsigned)splits);
+    if (sg)
+      hipLaunchKernelGGL(k_gemm_wt<true>, grid, dim3(BCNF_WG), 0, st, x, dy, (long long)rows, N, K, rps, w,
+                         dbias ? bw : nullptr, sg);
+    else
+      hipLaunchKernelGGL(k_gemm_wt<false>, grid, dim3(BCNF_WG), 0, st, x, dy, (long long)rows, N, K, rps, w,
+                         dbias ? bw : nullptr, (const float*)nullptr);
     int rc = launched();
     if (rc) return rc;
     const long long outs = (long long)N * K + (dbias ? N : 0);
@@ -577,6 +651,24 @@ int bcnf_linear_backward(const float* x, const float* weight, const float* dy, i
     return launched();
   }
   return BCNF_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int bcnf_linear_backward(const float* x, const float* weight, const float* dy, int64_t rows, int32_t in_features,
+                         int32_t out_features, float* dx, float* dweight, float* dbias, void* work, void* stream) {
+  if (rows < 0 || in_features < 1 || out_features < 1) return BCNF_ERR_ARG;
+  return linear_backward(x, weight, dy, nullptr, rows, in_features, out_features, dx, dweight, dbias, work,
+                         (hipStream_t)stream);
+}
+
+int bcnf_linear_gelu_backward(const float* x, const float* weight, const float* da, const float* g, int64_t rows,
+                              int32_t in_features, int32_t out_features, float* dx, float* dweight, float* dbias,
+                              void* work, void* stream) {
+  if (rows < 0 || in_features < 1 || out_features < 1 || (rows > 0 && !g)) return BCNF_ERR_ARG;
+  return linear_backward(x, weight, da, g, rows, in_features, out_features, dx, dweight, dbias, work,
+                         (hipStream_t)stream);
 }
 
 }  // extern "C"

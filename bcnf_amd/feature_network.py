@@ -12,6 +12,7 @@ Restated from the reference's behaviour (src/bcnf/models/feature_network.py); th
 """
 from __future__ import annotations
 
+import os
 from typing import Any, Type
 
 import torch
@@ -52,6 +53,48 @@ class _LinearFn(torch.autograd.Function):
                                              N.ptr(db), N.ptr(work), N.stream_handle(x.device)),
                 "bcnf_linear_backward")
         return dx, (dw if need_w else None), db
+
+
+class _LinearGeluFn(torch.autograd.Function):
+    """a = dropout(GELU(x W^T + b)) in ONE launch (bcnf_linear_gelu_forward), the backward from the saved
+    g = mask GELU'(pre) in the dX / dW GEMMs' operand loads (bcnf_linear_gelu_backward): no ATen GELU, dropout,
+    GELU-backward or masked-scale launches."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, p, rng, salt, need_g):
+        from bcnf_amd import _native as N
+        rows, k = x.shape
+        n = weight.shape[0]
+        a = torch.empty((rows, n), dtype=torch.float32, device=x.device)
+        g = torch.empty_like(a) if need_g else None
+        N.check(N.lib().bcnf_linear_gelu_forward(N.ptr(x), N.ptr(weight), N.ptr(bias), rows, k, n, float(p),
+                                                 N.ptr(rng), int(salt), N.ptr(a), N.ptr(g),
+                                                 N.stream_handle(x.device)), "bcnf_linear_gelu_forward")
+        ctx.save_for_backward(x, weight, g)
+        ctx.has_bias = bias is not None
+        return a
+
+    @staticmethod
+    def backward(ctx, da):
+        from bcnf_amd import _native as N
+        x, weight, g = ctx.saved_tensors
+        if g is None:
+            raise RuntimeError("bcnf_amd: fused Linear + GELU layer ran without saving its derivative")
+        da = da.contiguous()
+        rows, k = x.shape
+        n = weight.shape[0]
+        need_x, need_w, need_b = ctx.needs_input_grad[:3]
+        dx = torch.empty_like(x) if need_x else None
+        dw = torch.empty_like(weight) if (need_w or need_b) else None
+        db = torch.empty(n, dtype=torch.float32, device=x.device) if (need_b and ctx.has_bias) else None
+        work = None
+        if dw is not None:
+            wb = int(N.lib().bcnf_linear_work_bytes(rows, k, n))
+            work = torch.empty(max(wb // 4, 1), dtype=torch.float32, device=x.device)
+        N.check(N.lib().bcnf_linear_gelu_backward(N.ptr(x), N.ptr(weight), N.ptr(da), N.ptr(g), rows, k, n, N.ptr(dx),
+                                                  N.ptr(dw), N.ptr(db), N.ptr(work), N.stream_handle(x.device)),
+                "bcnf_linear_gelu_backward")
+        return dx, (dw if need_w else None), db, None, None, None, None
 
 
 class HIPLinear(nn.Linear):
@@ -108,7 +151,48 @@ class FullyConnectedFeatureNetwork(FeatureNetwork):
         self.nn.append(HIPLinear(sizes[-2], sizes[-1]))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return self.nn(x.view(x.size(0), -1))
+        return self.run(x.view(x.size(0), -1))
+
+    # Philox stream of the fused dropout: the owning CondRealNVP_v2's coupling (seed, offset) state when one is
+    # attached (weakly: a deep copy of this module keeps it as is), so one device offset -- advanced once per training
+    # step on the device, replay-safe in HIP graphs -- serves the feature and the coupling dropout, and
+    # `model.fused.set_seed` / TrainStep's snapshot cover both; else this module's own state.
+    _rng_owner = None
+    _own_rng = None
+
+    def rng_state(self, device) -> torch.Tensor:
+        owner = self._rng_owner() if self._rng_owner is not None else None
+        fused = getattr(owner, "_fused", None) if owner is not None else None
+        if fused is not None and hasattr(fused, "rng_state") and getattr(fused, "flat", None) is not None \
+                and fused.flat.device == device:
+            return fused.rng_state()
+        if self._own_rng is None or self._own_rng.device != device:
+            seed = (torch.cuda.initial_seed() * 0x9E3779B97F4A7C15 + 0xFEA7) & ((1 << 62) - 1)
+            self._own_rng = torch.tensor([seed, 0], dtype=torch.int64, device=device)
+        return self._own_rng
+
+    def run(self, x: torch.Tensor, upto: int | None = None) -> torch.Tensor:
+        """Modules [0, upto) of the MLP on the flattened input. Each Linear -> GELU(exact) [-> Dropout] group of fp32
+        CUDA tensors runs as ONE fused launch (bcnf_linear_gelu_forward, salt = its module index); the rest as the
+        modules themselves (BatchNorm, other activations, CPU)."""
+        mods = list(self.nn)[:upto]
+        i = 0
+        while i < len(mods):
+            m = mods[i]
+            act = mods[i + 1] if i + 1 < len(mods) else None
+            if isinstance(m, nn.Linear) and isinstance(act, nn.GELU) and act.approximate == "none" \
+                    and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and m.weight.dtype == torch.float32:
+                drop = mods[i + 2] if i + 2 < len(mods) and isinstance(mods[i + 2], nn.Dropout) else None
+                p = drop.p if (drop is not None and drop.training) else 0.0
+                rng = self.rng_state(x.device) if p > 0.0 else None
+                need_g = torch.is_grad_enabled() and (x.requires_grad or m.weight.requires_grad or
+                                                      (m.bias is not None and m.bias.requires_grad))
+                x = _LinearGeluFn.apply(x.contiguous(), m.weight, m.bias, p, rng, i, need_g)
+                i += 3 if drop is not None else 2
+                continue
+            x = m(x)
+            i += 1
+        return x
 
 
 class LSTMFeatureNetwork(FeatureNetwork):
@@ -125,9 +209,19 @@ class LSTMFeatureNetwork(FeatureNetwork):
         self.pooling = pooling
         self.pool_dim = pool_dim
 
+    # The LSTM itself stays on PyTorch-ROCm (north star): MIOpen's fused RNN kernels by default; False runs torch's
+    # native per-step GEMM + pointwise kernels instead (BCNF_LSTM_MIOPEN=0; tools/gpu_r04.sh lstmab measures both).
+    use_miopen = os.environ.get("BCNF_LSTM_MIOPEN", "1") != "0"
+
+    def lstm_out(self, x: torch.Tensor) -> torch.Tensor:
+        """The LSTM's output sequence (B, T, hidden * directions)."""
+        if self.use_miopen or not x.is_cuda:
+            return self.lstm(x)[0]
+        with torch.backends.cudnn.flags(enabled=False):
+            return self.lstm(x)[0]
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x, _ = self.lstm(x)
-        x = self.linear(x)
+        x = self.linear(self.lstm_out(x))
         if self.pooling == "mean":
             return x.mean(dim=self.pool_dim)
         return x.max(dim=self.pool_dim).values

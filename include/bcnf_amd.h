@@ -137,7 +137,9 @@ int bcnf_backward_tail(const BcnfStackDesc* desc, const void* packed, const void
 /* ---- Folded linear feature network (training fast path; no reference counterpart as a function: it
  * computes the same sums as feature_network.py:114-145's single nn.Linear [X -> C] feeding cnf.py:74-107's
  * condition input, reassociated). With Wf (C x X, row-major) and bf (C, nullable) of that Linear:
- *   Wc = W1h Wf, bc = b1 + W1h bf  (bcnf_pack_params_fold, alongside the regular pack, one launch)
+ *   Wc = W1h Wf, bc = b1 + W1h bf  (bcnf_pack_params_fold, alongside the training sections of the regular pack
+ *                                   -- forward / backward records, W1hR, log-det constant; NOT the inverse records,
+ *                                   so its `packed` serves the folded training pass only -- one launch)
  *   HP = x Wc^T + bc               (bcnf_fold_nll_forward: bcnf_nll_forward with x (B x X) in place of h)
  *   dW1h, dWf, dbf from Gx = D1^T [x | 1]  (bcnf_fold_backward_tail, after bcnf_nll_backward(dh = dparams
  *   = NULL) wrote `slab` sized by bcnf_fold_slab_bytes). h and dL/dh are never formed. X + 1 <= 256.
@@ -314,6 +316,19 @@ int64_t bcnf_linear_work_bytes(int64_t rows, int32_t in_features, int32_t out_fe
  * (fixed-order split-K reduction through `work`). dweight may be NULL only when dbias is NULL too. */
 int bcnf_linear_backward(const float* x, const float* weight, const float* dy, int64_t rows, int32_t in_features,
                          int32_t out_features, float* dx, float* dweight, float* dbias, void* work, void* stream);
+/* One hidden layer of a FullyConnectedFeatureNetwork, nn.Linear -> nn.GELU() -> nn.Dropout(p) (feature_network.py:
+ * 128-134, the reference runs them as three ATen ops), in ONE launch: a = mask GELU(x W^T + b) with the exact-erf
+ * GELU, and g (nullable) = mask GELU'(x W^T + b) for the backward. mask = 1 / (1 - p) or 0 from an in-kernel
+ * Philox4x32-10 stream when rng (device uint64 [seed, offset], read only) is given and p > 0, else 1; salt separates
+ * the layers of one network. Same element-wise distribution as torch's dropout, not its bits. */
+int bcnf_linear_gelu_forward(const float* x, const float* weight, const float* bias, int64_t rows, int32_t in_features,
+                             int32_t out_features, float p, const uint64_t* rng, int32_t salt, float* a, float* g,
+                             void* stream);
+/* Backward of bcnf_linear_gelu_forward from dL/da and its g: dL/dpre = da * g is formed as the operands are loaded
+ * (never stored), then as bcnf_linear_backward (same work bytes). */
+int bcnf_linear_gelu_backward(const float* x, const float* weight, const float* da, const float* g, int64_t rows,
+                              int32_t in_features, int32_t out_features, float* dx, float* dweight, float* dbias,
+                              void* work, void* stream);
 
 /* ---- Wide-MLP family (trajectory_FC_large / trajectory_LSTM_large class: nested_sizes = [H] * NH with H too
  * wide for the register-resident kernels above, e.g. [526] * 5, C = 1360, 26 blocks) ----------------------------

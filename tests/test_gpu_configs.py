@@ -253,3 +253,112 @@ def test_lstm_large_pool_dim1_folded_nll_equals_unfolded():
     for name in gf:
         ok, err = close(gf[name], gu[name], rtol=1e-4, floor=1e-4)
         assert ok, (name, err)
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+# The wide training step at the BENCH batch sizes (FC_large B = 2048 per GPU, LSTM_large B = 1024), so the GEMM cost
+# model's large-M tilings (tiling W on 96 x 48 / 48 x 48, K slices, XCD-contiguous grids; engaged only at M >= 1024)
+# run through the fused ACT / GRAD / LINGRAD epilogues and the fold's condition GEMMs, not only the plain-store hook.
+# nb = 2 blocks keep the fp64 oracle at a few seconds of host time; every per-block kernel is the full-width one.
+def _bench_shape(cfg, pool_dim=None, n_blocks=2):
+    cfg = copy.deepcopy(cfg)
+    cfg["model"]["kwargs"]["n_blocks"] = n_blocks
+    cfg["model"]["kwargs"].pop("random_state", None)
+    if pool_dim is not None:
+        cfg["feature_networks"][1]["kwargs"]["pool_dim"] = pool_dim
+    return cfg
+
+
+def _bench_inputs(B, lstm, seed=31):
+    g = torch.Generator().manual_seed(seed)
+    y = torch.randn(B, 19, generator=g)
+    traj = torch.randn(B, 30, 3, generator=g)
+    return y, traj
+
+
+def _fp64_step(m, sd, cfg, y, traj, lstm):
+    """Loss, z, ldj and every gradient of the eval NLL step in float64 on the host: the oracle's flow, the oracle's
+    FC feature MLP (FC_large) or torch's own LSTM + Linear in double (LSTM_large, pool over time)."""
+    kw = cfg["model"]["kwargs"]
+    sdg = {k: torch.from_numpy(np.ascontiguousarray(v)).double().requires_grad_(not k.endswith("orthonormal_matrix"))
+           for k, v in sd.items()}
+    if lstm:
+        spec = O.StackSpec(size=19, nested_sizes=kw["nested_sizes"], n_blocks=kw["n_blocks"],
+                           n_conditions=kw["n_conditions"], dropout=kw["dropout"], act_norm=True)
+        fref = copy.deepcopy(m.feature_network_stack).double().eval()
+        h64 = fref(traj.double())
+        named = {"feature_network_stack." + n: p for n, p in fref.named_parameters()}
+    else:
+        fk = cfg["feature_networks"][1]["kwargs"]
+        spec = O.StackSpec(size=19, nested_sizes=kw["nested_sizes"], n_blocks=kw["n_blocks"],
+                           n_conditions=kw["n_conditions"], dropout=kw["dropout"], act_norm=True,
+                           feature_sizes=fk["sizes"], feature_dropout=fk["dropout"])
+        h64 = O.feature_forward(sdg, spec, traj.double())
+        named = {}
+    zo, lo = O.model_forward({k: v for k, v in sdg.items() if k.startswith("layers.")} if lstm else sdg, spec,
+                             y.double(), h64)
+    loss = O.inn_nll_loss(zo, lo)
+    loss.backward()
+    grads = {k: v.grad for k, v in sdg.items() if v.grad is not None}
+    grads.update({k: p.grad for k, p in named.items() if p.grad is not None})
+    return loss.detach(), zo.detach(), lo.detach(), grads
+
+
+@pytest.mark.parametrize("which,B", [("fc_large", 2048), ("lstm_large", 1024)])
+def test_wide_bench_batch_step_vs_fp64(which, B):
+    """configs[2] / [3] shapes at the bench's per-GPU batch: z, ldj (1e-5 gate), the folded NLL loss and every
+    gradient -- coupling, fold, feature MLP / LSTM -- against float64 (1e-4), on the cost model's own tilings."""
+    lstm = which == "lstm_large"
+    cfg = _bench_shape(LSTM_LARGE_CFG if lstm else FC_LARGE_CFG, pool_dim=1 if lstm else None)
+    m, sd = _build(cfg, SEED + 41, SEED + 42)
+    y, traj = _bench_inputs(B, lstm)
+    loss64, z64, l64, g64 = _fp64_step(m, sd, cfg, y, traj, lstm)
+    m.to(DEV).eval()
+    yd, td = y.to(DEV), traj.to(DEV)
+    with torch.no_grad():
+        z = m.forward(yd, td, log_det_J=True)
+        ldj = m.log_det_J.clone()
+    for name, got, ref in (("z", z, z64), ("ldj", ldj, l64)):
+        ok, err = close(got.cpu(), ref)
+        assert ok, (name, err)
+    m.zero_grad(set_to_none=True)
+    with torch.backends.cudnn.flags(enabled=False):      # MIOpen's RNN backward refuses eval mode
+        vals = m.nll_loss(yd, td)
+        vals[0].backward()
+        with torch.no_grad():
+            assert m._wide_fold(yd, (td,)) is not None   # the folded training path ran
+    ok, err = close(vals[:1].detach().cpu(), loss64.reshape(1))
+    assert ok, ("loss", err)
+    n = 0
+    for name, p in m.named_parameters():
+        if p.grad is None:
+            continue
+        ok, err = close(p.grad.cpu(), g64[name], rtol=1e-4, floor=1e-4)
+        assert ok, (name, err)
+        n += 1
+    assert n == len(g64) == sum(1 for k in sd if not k.endswith("orthonormal_matrix"))
+
+
+@pytest.mark.parametrize("which,B", [("fc_large", 2048), ("lstm_large", 1024)])
+def test_wide_bench_batch_training_fused_equals_unfolded(which, B):
+    """Training mode at the bench batch (feature dropout, coupling dropout 0.407): the fused (folded) step and the
+    unfolded launches draw the same masks from the same torch / Philox states and agree on the loss and every
+    gradient."""
+    lstm = which == "lstm_large"
+    cfg = _bench_shape(LSTM_LARGE_CFG if lstm else FC_LARGE_CFG, pool_dim=1 if lstm else None)
+    m, _ = _build(cfg, SEED + 43, SEED + 44)
+    y, traj = _bench_inputs(B, lstm, seed=37)
+    m.to(DEV).train()
+    yd, td = y.to(DEV), traj.to(DEV)
+    st = m.fused.rng_state().clone()
+    torch.manual_seed(5)
+    vf, gf = _nll_and_grads(m, yd, td, True)
+    m.fused.rng_state().copy_(st)
+    torch.manual_seed(5)
+    vu, gu = _nll_and_grads(m, yd, td, False)
+    ok, err = close(vf, vu, rtol=1e-5, floor=1e-5)
+    assert ok, ("vals", err)
+    assert set(gf) == set(gu)
+    for name in gf:
+        ok, err = close(gf[name], gu[name], rtol=1e-4, floor=1e-4)
+        assert ok, (name, err)

@@ -160,5 +160,39 @@ def gelu_fit(deg=6, zmax=7.0, n=8000):
     print("  p / sqrt2 =", f"{ps:.9e}", " Q / 2 (highest first):", ", ".join(f"{v:.9e}" for v in C))
 
 
+def tanh_check():
+    """r04 bcnf_device.h tanh_bf: 1 - 2 / (exp(2a) + 1) in emulated fp32 against float64 tanh."""
+    a = np.linspace(-12, 12, 2000001).astype(f32)
+    e = f32(np.exp2(np.float64(f32(a * f32(2 * np.log2(np.e))))))
+    r = f32(1.0 / np.float64(f32(e + f32(1))))
+    got = fma(f32(-2), r, f32(1))
+    print(f"tanh_check: max abs err {np.abs(got - np.tanh(a.astype(np.float64))).max():.3e}")
+
+
+def gelu_r04_check():
+    """r04 bcnf_device.h gelu_tq / gelu_f / gelu_fg: Q scaled by sqrt(2 pi), phi = exp2(x^2 k + log2(1/sqrt(2 pi))),
+    Phi(x) = 1/2 + sign(x) (1/2 - h), GELU = max(x, 0) - |x| h."""
+    from scipy.special import ndtr
+    C = [f32(v) for v in (-1.828701629e-01, 5.613370996e-01, -2.561027660e-01, 4.147041470e-01, 1.844545274e-01,
+                          2.707437625e-01, 2.610471003e-01)]
+    x = np.linspace(-12, 12, 2000001).astype(f32)
+    t = f32(1) / fma(f32(2.616295218e-01), np.abs(x), f32(1))
+    q = np.full_like(x, C[0])
+    for cc in C[1:]:
+        q = fma(q, t, cc)
+    phi = f32(np.exp2(np.float64(fma(f32(x * x), f32(-0.72134752044448170368), f32(-1.32574806473615920)))))
+    tq = f32(t * q)
+    hm = fma(-tq, phi, f32(0.5))
+    cdf = f32(f32(0.5) + f32(np.copysign(hm, x)))
+    g, dg = f32(x * cdf), fma(x, phi, cdf)
+    g2 = fma(-np.abs(x), f32(tq * phi), np.maximum(x, f32(0)))
+    xd = x.astype(np.float64)
+    P = ndtr(xd)
+    print(f"gelu_r04_check: |GELU err| fg {np.abs(g - xd * P).max():.2e}, f {np.abs(g2 - xd * P).max():.2e}; "
+          f"|GELU' err| {np.abs(dg - (P + xd * np.exp(-xd * xd / 2) / np.sqrt(2 * np.pi))).max():.2e}")
+
+
 if __name__ == "__main__":
     gelu_fit()
+    tanh_check()
+    gelu_r04_check()

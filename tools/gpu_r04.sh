@@ -25,11 +25,27 @@ for s in $STEPS; do
     abk)
       for i in 1 2; do
         timeout -k 10 120 python tools/abk.py
-        BCNF_AMD_LIB=build_exp/libhead.so timeout -k 10 120 python tools/abk.py
+        for lib in ${AB_LIBS:-build_exp/libhead.so}; do BCNF_AMD_LIB=$lib timeout -k 10 120 python tools/abk.py; done
       done 2>&1 | grep -v amdgpu.ids | tee gpurun_out/${T}_ab_kernels.txt ;;
+    absample)
+      bash tools/ab_sample.sh ${AB_LIBS:-build_exp/libhead.so} 2>&1 | tee gpurun_out/${T}_ab_sample.txt ;;
+    pmc)
+      bash tools/pmc_insts.sh $T > gpurun_out/${T}_pmc.log 2>&1 || { tail -20 gpurun_out/${T}_pmc.log; exit 1; }
+      python tools/summarize_pmc.py $T | tail -30 ;;
+    proflstm|proffcl)
+      wl=$([ $s = proflstm ] && echo lstm_large || echo fc_large)
+      cd /tmp && export TMPDIR=/tmp
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/${T}_$s -o run -- python3 $GRAFT_REPO_ROOT/bench.py --workload $wl --no-cpu-baseline --steps 10 --warmup 3 --kernel-iters 3 > $GRAFT_REPO_ROOT/gpurun_out/${T}_$s.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/${T}_$s.log; exit 1; }
+      cd $GRAFT_REPO_ROOT
+      python tools/show_stats.py gpurun_out/${T}_$s 40 ;;
+    lstmab)
+      for i in 1 2; do for mi in 1 0; do
+        BCNF_LSTM_MIOPEN=$mi timeout -k 10 200 python bench.py --workload lstm_large --no-cpu-baseline --steps 10 --warmup 3 > gpurun_out/${T}_lstmab.json 2>/dev/null
+        python -c "import json; d=json.loads(open('gpurun_out/${T}_lstmab.json').read().strip().splitlines()[-1]); print('miopen=$mi', d['ms_per_step'], round(d['value']), d['kernels_us'])"
+      done; done 2>&1 | tee gpurun_out/${T}_lstmab.txt ;;
     prof)
       cd /tmp && export TMPDIR=/tmp
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/${T}_prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --no-secondary --no-cpu-baseline --steps 40 > $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.log; exit 1; }
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/${T}_prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --no-secondary --no-cpu-baseline --steps 40 > $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.log; exit 1; }
       cd $GRAFT_REPO_ROOT ;;
   esac
 done
