@@ -1897,6 +1897,125 @@ int gemm_splitk(const GemmArgs& g, int np, float* part, long long part_floats, h
   return bcnf_rt::launched();
 }
 
+// Skinny split-K Linear-gradient partials: part[g1][s][m][n] = sum_{k in split s} A[k][m] B[k][n] with one operand
+// "wide" (W = 526 / 527 columns: the activation rows A_{NH-1} of the last Linear's gradient, or dZ_0 of Linear 1's
+// input columns) and the other narrow (Q <= 36: the last Linear's 2 nout outputs, or Linear 1's nin + 1 inputs).
+// HBM-bound: the wide operand is 111 MB per call at FC_large B = 2048, streamed once. Each thread owns 4 wide columns
+// (float4 loads, 8 rows in flight), the split's narrow rows sit in LDS (broadcast b128 reads), every (q, column)
+// accumulates in registers on packed FMAs; the four waves take quarters of the split's rows and meet in LDS in a fixed
+// order (deterministic). The 64 x 64 register-staged tile this replaces kept ~1.5 TB/s (r03: 59-258 us per call).
+typedef float f32x2w __attribute__((ext_vector_type(2)));
+constexpr int SK_COLS = 4 * 64;      // wide columns per workgroup
+constexpr int SK_ROWS = 8;           // rows in flight per thread
+
+template <int QT, bool WIDE_A>
+__global__ __launch_bounds__(WWG) void k_skinny(const GemmArgs g, int np, float* __restrict__ part, long long ldp) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int g1 = blockIdx.z, sp = blockIdx.y;
+  const int W = WIDE_A ? g.M : g.N, Q = WIDE_A ? g.N : g.M;
+  const float* __restrict__ wb = WIDE_A ? g.A + g1 * g.sA1 : g.B + g1 * g.sB1;
+  const float* __restrict__ nb = WIDE_A ? g.B + g1 * g.sB1 : g.A + g1 * g.sA1;
+  const long long ldw = WIDE_A ? g.lda : g.ldb, ldn = WIDE_A ? g.ldb : g.lda;
+  const int KS = g.K / np;                       // rows of this split (the dispatch checks KS % (4 SK_ROWS) == 0)
+  const long long k0 = (long long)sp * KS;
+  for (int i = threadIdx.x; i < KS * QT; i += WWG) {   // the split's narrow rows, zero beyond Q
+    const int r = i / QT, q = i - r * QT;
+    sm[i] = q < Q ? nb[(k0 + r) * ldn + q] : 0.f;
+  }
+  __syncthreads();
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int c0 = blockIdx.x * SK_COLS + 4 * l;
+  const int cl = c0 < W ? c0 : 0;                // columns past W read column 0 (inside the row), never stored
+  const int rq = KS / 4, r0 = wv * rq;
+  f32x2w acc[QT][2];
+#pragma unroll
+  for (int q = 0; q < QT; ++q) acc[q][0] = acc[q][1] = f32x2w{0.f, 0.f};
+  const float* wrow = wb + (k0 + r0) * ldw + cl;
+  for (int r = 0; r < rq; r += SK_ROWS) {
+    floatx4 v[SK_ROWS];
+#pragma unroll
+    for (int t = 0; t < SK_ROWS; ++t) v[t] = ld4(wrow + (long long)(r + t) * ldw);
+#pragma unroll
+    for (int t = 0; t < SK_ROWS; ++t) {
+      const float* nr = sm + (r0 + r + t) * QT;
+      const f32x2w lo = {v[t][0], v[t][1]}, hi = {v[t][2], v[t][3]};
+#pragma unroll
+      for (int q4 = 0; q4 < QT / 4; ++q4) {
+        const floatx4 n4 = *reinterpret_cast<const floatx4*>(nr + 4 * q4);   // same address in every lane
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const f32x2w nn = {n4[u], n4[u]};
+          acc[4 * q4 + u][0] = __builtin_elementwise_fma(lo, nn, acc[4 * q4 + u][0]);
+          acc[4 * q4 + u][1] = __builtin_elementwise_fma(hi, nn, acc[4 * q4 + u][1]);
+        }
+      }
+    }
+  }
+  __syncthreads();                               // narrow rows consumed: the LDS now holds waves 1..3's partials
+  floatx4* red = reinterpret_cast<floatx4*>(sm);   // [3][QT][64 lanes]
+  if (wv > 0) {
+#pragma unroll
+    for (int q = 0; q < QT; ++q)
+      red[((wv - 1) * QT + q) * 64 + l] = floatx4{acc[q][0][0], acc[q][0][1], acc[q][1][0], acc[q][1][1]};
+  }
+  __syncthreads();
+  if (wv != 0 || c0 >= W) return;
+  float* out = part + ((long long)g1 * np + sp) * ((long long)g.M * ldp);
+#pragma unroll
+  for (int q = 0; q < QT; ++q) {
+    floatx4 t = floatx4{acc[q][0][0], acc[q][0][1], acc[q][1][0], acc[q][1][1]};
+#pragma unroll
+    for (int w = 0; w < 3; ++w) t += red[(w * QT + q) * 64 + l];      // wave order 0, 1, 2, 3
+    if (q >= Q) continue;
+    if (!WIDE_A) {
+      *reinterpret_cast<floatx4*>(out + (long long)q * ldp + c0) = t;   // row q, columns c0..c0+3 (< ldp)
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (c0 + u < W) out[(long long)(c0 + u) * ldp + q] = t[u];
+    }
+  }
+}
+
+template <int QT, bool WIDE_A>
+int launch_skinny(const GemmArgs& g, int groups, int np, float* part, long long ldp, hipStream_t st) {
+  const int W = WIDE_A ? g.M : g.N;
+  const size_t rows = (size_t)(g.K / np);
+  const size_t bytes = 4 * std::max(rows * QT, (size_t)3 * QT * 64 * 4);
+  static bool attr = false;
+  if (!attr) {
+    if (const int rc = bcnf_rt::hip_status(hipFuncSetAttribute((const void*)k_skinny<QT, WIDE_A>,
+                                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)))
+      return rc;
+    attr = true;
+  }
+  if (bytes > 160 * 1024) return BCNF_ERR_UNSUPPORTED;
+  const dim3 grid((unsigned)((W + SK_COLS - 1) / SK_COLS), (unsigned)np, (unsigned)groups);
+  hipLaunchKernelGGL((k_skinny<QT, WIDE_A>), grid, dim3(WWG), bytes, st, g, np, part, ldp);
+  return bcnf_rt::launched();
+}
+
+// The skinny kernel when it applies (cost-model dispatch only; a forced tiling keeps the tiled GEMM): -1 otherwise.
+int try_skinny(const GemmArgs& g, int groups, int np, float* part, long long ldp, hipStream_t st) {
+  if (g.tiling != 0 || np < 1 || g.K % np != 0 || (g.K / np) % (4 * SK_ROWS) != 0) return -1;
+  const bool wide_a = g.N <= 36 && g.M >= 64, wide_b = g.M <= 36 && g.N >= 64;
+  if (!wide_a && !wide_b) return -1;
+  const long long ldw = wide_a ? g.lda : g.ldb, sw = wide_a ? g.sA1 : g.sB1;
+  const int W = wide_a ? g.M : g.N;
+  if ((ldw & 3) || (sw & 3) || ldw < ((W + 3) & ~3) || !aligned16(wide_a ? g.A : g.B) || (!wide_a && (ldp & 3)))
+    return -1;
+  if ((long long)(g.K / np) * 36 * 4 > 160 * 1024) return -1;
+  const int Q = wide_a ? g.N : g.M;
+  if (wide_a) {
+    if (Q <= 12) return launch_skinny<12, true>(g, groups, np, part, ldp, st);
+    if (Q <= 20) return launch_skinny<20, true>(g, groups, np, part, ldp, st);
+    return launch_skinny<36, true>(g, groups, np, part, ldp, st);
+  }
+  if (Q <= 12) return launch_skinny<12, false>(g, groups, np, part, ldp, st);
+  if (Q <= 20) return launch_skinny<20, false>(g, groups, np, part, ldp, st);
+  return launch_skinny<36, false>(g, groups, np, part, ldp, st);
+}
+
 // Grouped strided x strided EPI_LINGRAD GEMM with K (= the batch) split into np parts: partials in `part`, then a
 // fixed-order sum through the LINGRAD mapping. The last-Linear and Linear-1 input-column gradients have M or N <= 36,
 // so unsplit their grid is ~one 64 x 64 workgroup per block and column tile, each streaming the whole batch
@@ -1916,7 +2035,8 @@ int lingrad_splitk(const GemmArgs& g, int groups, float* part, long long part_fl
   p.sC0 = (long long)g.M * ldp;
   p.sC1 = (long long)np * p.sC0;
   p.use_cb = 0;
-  const int rc = gemm<false, false, EPI_STORE>(p, groups * np, st);
+  int rc = try_skinny(g, groups, np, part, ldp, st);       // the HBM-streaming kernel for the skinny shapes
+  if (rc < 0) rc = gemm<false, false, EPI_STORE>(p, groups * np, st);
   if (rc) return rc;
   hipLaunchKernelGGL(k_wsum_lingrad, dim3((unsigned)(((long long)g.M * g.N + WWG - 1) / WWG), groups), dim3(WWG), 0, st,
                      g, part, np, ldp);

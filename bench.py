@@ -310,6 +310,35 @@ def log_prob_errors_more(device):
     return {f"{k}_{n}": v[i] for k, v in out.items() for i, n in enumerate(("max_abs", "max_rel"))}
 
 
+def wide_fixture_error(workload, device):
+    """log_prob max-abs / max-rel error of the wide workload's model at FULL depth (26 blocks) against the reference's
+    own outputs: g11 (trajectory_FC_large, FC[90, 310 x 7, 1360]) or g10's pool-over-time outputs (trajectory_LSTM_large
+    with pool_dim=1, the reference's own LSTM / Linear modules), both on PCG64 weights
+    (tests/golden/make_golden.py: the same seeds rebuild the same model here), eval mode."""
+    from bcnf_amd import CondRealNVP_v2
+    lstm = workload == "lstm_large"
+    path = os.path.join(ROOT, "tests", "golden", "g10_lstm_large.npz" if lstm else "g11_fc_large.npz")
+    if not os.path.exists(path):
+        return None
+    d = np.load(path)
+    cfg = json.loads(json.dumps(WORKLOADS[workload][0]))
+    torch.manual_seed(2024_03_25 + (12 if lstm else 15))
+    m = CondRealNVP_v2.from_config(cfg)
+    sd = _proxy_sd(m, 2024_03_25 + (13 if lstm else 16))
+    for k in sd:
+        if k.endswith("orthonormal_matrix"):      # the reference's own Q bytes (host LAPACK rounding aside)
+            sd[k] = d["q"] if lstm else d["q/" + k]
+    m.load_state_dict({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in sd.items()})
+    m.to(device).eval()
+    y, traj, z, ldj = (d["y1"], d["traj1"], d["z1"], d["ldj1"]) if lstm else (d["y"], d["traj"], d["z"], d["ldj"])
+    with torch.no_grad():
+        lp = m.log_prob(torch.from_numpy(y).to(device), torch.from_numpy(traj).to(device))
+    mx, rel = _lp_err(lp, z, ldj)
+    del m
+    return {"fixture": os.path.basename(path), "rows": int(y.shape[0]), "log_prob_max_abs_err": mx,
+            "log_prob_max_rel_err": rel}
+
+
 def cpu_baseline(args):
     """The CPU oracle (PyTorch-eager restatement of the reference, pinned to its outputs) timed on this host's
     cores: same FC_small step at the same batch, bounded sample."""
@@ -746,6 +775,11 @@ def run_wide(workload, batch, steps, warmup, world, rank, device, graph=True, ke
         "kernels_us": {k: round(v, 2) for k, v in kern.items()},
     }
     del step, model, data
+    torch.cuda.empty_cache()
+    try:
+        line["parity"] = wide_fixture_error(workload, device)
+    except Exception as e:                   # parity evidence never takes the throughput line down
+        line["parity"] = {"error": f"{type(e).__name__}: {e}"}
     torch.cuda.empty_cache()
     if cpu and world == 1:
         line["cpu_baseline"] = cpu_baseline_wide(workload, cfg, batch=cpu_batch, steps=cpu_steps)
