@@ -1908,6 +1908,17 @@ typedef float f32x2w __attribute__((ext_vector_type(2)));
 constexpr int SK_COLS = 4 * 64;      // wide columns per workgroup
 constexpr int SK_ROWS = 8;           // rows in flight per thread
 
+// acc + a * (w[H], w[H]): one v_pk_fma_f32 reading one half of the w pair for both lanes (op_sel), so the column value
+// needs no broadcast copy
+template <int H>
+__device__ __forceinline__ f32x2w pk_fma_bc(f32x2w a, f32x2w w, f32x2w acc) {
+  if (H == 0)
+    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(acc) : "v"(a), "v"(w));
+  else
+    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(a), "v"(w));
+  return acc;
+}
+
 template <int QT, bool WIDE_A>
 __global__ __launch_bounds__(WWG) void k_skinny(const GemmArgs g, int np, float* __restrict__ part, long long ldp) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -1916,7 +1927,7 @@ __global__ __launch_bounds__(WWG) void k_skinny(const GemmArgs g, int np, float*
   const float* __restrict__ wb = WIDE_A ? g.A + g1 * g.sA1 : g.B + g1 * g.sB1;
   const float* __restrict__ nb = WIDE_A ? g.B + g1 * g.sB1 : g.A + g1 * g.sA1;
   const long long ldw = WIDE_A ? g.lda : g.ldb, ldn = WIDE_A ? g.ldb : g.lda;
-  const int KS = g.K / np;                       // rows of this split (the dispatch checks KS % (4 SK_ROWS) == 0)
+  const int KS = g.K / np;                       // rows of this split (the dispatch checks KS % (8 SK_ROWS) == 0)
   const long long k0 = (long long)sp * KS;
   for (int i = threadIdx.x; i < KS * QT; i += WWG) {   // the split's narrow rows, zero beyond Q
     const int r = i / QT, q = i - r * QT;
@@ -1927,43 +1938,63 @@ __global__ __launch_bounds__(WWG) void k_skinny(const GemmArgs g, int np, float*
   const int c0 = blockIdx.x * SK_COLS + 4 * l;
   const int cl = c0 < W ? c0 : 0;                // columns past W read column 0 (inside the row), never stored
   const int rq = KS / 4, r0 = wv * rq;
-  f32x2w acc[QT][2];
+  f32x2w acc[QT / 2][4];                         // acc[p][c] = (out[2p][c], out[2p + 1][c]) of column c0 + c
 #pragma unroll
-  for (int q = 0; q < QT; ++q) acc[q][0] = acc[q][1] = f32x2w{0.f, 0.f};
+  for (int p = 0; p < QT / 2; ++p)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[p][c] = f32x2w{0.f, 0.f};
   const float* wrow = wb + (k0 + r0) * ldw + cl;
-  for (int r = 0; r < rq; r += SK_ROWS) {
-    floatx4 v[SK_ROWS];
+  // two register sets of SK_ROWS rows, the next set's loads issued before the current set is consumed; the empty
+  // asm statements with a memory clobber keep hipcc from sinking each load to its first use (one round trip per row)
+  auto load = [&](floatx4 (&v)[SK_ROWS], int r) {       // rows past the wave's range re-read its last row
 #pragma unroll
-    for (int t = 0; t < SK_ROWS; ++t) v[t] = ld4(wrow + (long long)(r + t) * ldw);
+    for (int t = 0; t < SK_ROWS; ++t) v[t] = ld4(wrow + (long long)(r + t < rq ? r + t : rq - 1) * ldw);
+    asm volatile("" ::: "memory");
+  };
+  auto consume = [&](const floatx4 (&v)[SK_ROWS], int r) {
 #pragma unroll
     for (int t = 0; t < SK_ROWS; ++t) {
       const float* nr = sm + (r0 + r + t) * QT;
-      const f32x2w lo = {v[t][0], v[t][1]}, hi = {v[t][2], v[t][3]};
 #pragma unroll
       for (int q4 = 0; q4 < QT / 4; ++q4) {
         const floatx4 n4 = *reinterpret_cast<const floatx4*>(nr + 4 * q4);   // same address in every lane
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const f32x2w nn = {n4[u], n4[u]};
-          acc[4 * q4 + u][0] = __builtin_elementwise_fma(lo, nn, acc[4 * q4 + u][0]);
-          acc[4 * q4 + u][1] = __builtin_elementwise_fma(hi, nn, acc[4 * q4 + u][1]);
-        }
+        const f32x2w n01 = __builtin_shufflevector(n4, n4, 0, 1), n23 = __builtin_shufflevector(n4, n4, 2, 3);
+        const f32x2w w01 = __builtin_shufflevector(v[t], v[t], 0, 1), w23 = __builtin_shufflevector(v[t], v[t], 2, 3);
+        acc[2 * q4][0] = pk_fma_bc<0>(n01, w01, acc[2 * q4][0]);
+        acc[2 * q4 + 1][0] = pk_fma_bc<0>(n23, w01, acc[2 * q4 + 1][0]);
+        acc[2 * q4][1] = pk_fma_bc<1>(n01, w01, acc[2 * q4][1]);
+        acc[2 * q4 + 1][1] = pk_fma_bc<1>(n23, w01, acc[2 * q4 + 1][1]);
+        acc[2 * q4][2] = pk_fma_bc<0>(n01, w23, acc[2 * q4][2]);
+        acc[2 * q4 + 1][2] = pk_fma_bc<0>(n23, w23, acc[2 * q4 + 1][2]);
+        acc[2 * q4][3] = pk_fma_bc<1>(n01, w23, acc[2 * q4][3]);
+        acc[2 * q4 + 1][3] = pk_fma_bc<1>(n23, w23, acc[2 * q4 + 1][3]);
       }
     }
+  };
+  floatx4 va[SK_ROWS], vb[SK_ROWS];
+  load(va, 0);
+  for (int r = 0; r < rq; r += 2 * SK_ROWS) {    // rq % (2 SK_ROWS) == 0 (try_skinny)
+    load(vb, r + SK_ROWS);
+    consume(va, r);
+    load(va, r + 2 * SK_ROWS);                   // unconditional (clamped): static wait counts
+    consume(vb, r + SK_ROWS);
   }
   __syncthreads();                               // narrow rows consumed: the LDS now holds waves 1..3's partials
-  floatx4* red = reinterpret_cast<floatx4*>(sm);   // [3][QT][64 lanes]
+  floatx4* red = reinterpret_cast<floatx4*>(sm);   // [3][QT][64 lanes]: (q, columns c0..c0+3)
+  auto row_q = [&](int q) {
+    const int p = q >> 1, h = q & 1;
+    return floatx4{acc[p][0][h], acc[p][1][h], acc[p][2][h], acc[p][3][h]};
+  };
   if (wv > 0) {
 #pragma unroll
-    for (int q = 0; q < QT; ++q)
-      red[((wv - 1) * QT + q) * 64 + l] = floatx4{acc[q][0][0], acc[q][0][1], acc[q][1][0], acc[q][1][1]};
+    for (int q = 0; q < QT; ++q) red[((wv - 1) * QT + q) * 64 + l] = row_q(q);
   }
   __syncthreads();
   if (wv != 0 || c0 >= W) return;
   float* out = part + ((long long)g1 * np + sp) * ((long long)g.M * ldp);
 #pragma unroll
   for (int q = 0; q < QT; ++q) {
-    floatx4 t = floatx4{acc[q][0][0], acc[q][0][1], acc[q][1][0], acc[q][1][1]};
+    floatx4 t = row_q(q);
 #pragma unroll
     for (int w = 0; w < 3; ++w) t += red[(w * QT + q) * 64 + l];      // wave order 0, 1, 2, 3
     if (q >= Q) continue;
@@ -1997,7 +2028,7 @@ int launch_skinny(const GemmArgs& g, int groups, int np, float* part, long long 
 
 // The skinny kernel when it applies (cost-model dispatch only; a forced tiling keeps the tiled GEMM): -1 otherwise.
 int try_skinny(const GemmArgs& g, int groups, int np, float* part, long long ldp, hipStream_t st) {
-  if (g.tiling != 0 || np < 1 || g.K % np != 0 || (g.K / np) % (4 * SK_ROWS) != 0) return -1;
+  if (g.tiling != 0 || np < 1 || g.K % np != 0 || (g.K / np) % (8 * SK_ROWS) != 0) return -1;
   const bool wide_a = g.N <= 36 && g.M >= 64, wide_b = g.M <= 36 && g.N >= 64;
   if (!wide_a && !wide_b) return -1;
   const long long ldw = wide_a ? g.lda : g.ldb, sw = wide_a ? g.sA1 : g.sB1;
