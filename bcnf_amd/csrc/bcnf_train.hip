@@ -63,6 +63,10 @@ struct AdamBook {
   int* done;                    // workgroups finished; 0 between launches (the last one resets it); NULL: off
 };
 
+// G groups of EPT elements per thread (G = 4 for the wide family's ~49M parameters: a quarter of the workgroups, so a
+// quarter of the per-workgroup reductions and launch ramps, and 4x the bytes in flight per thread; G = 1 for small
+// sets, where more workgroups cover the chip). Group q of workgroup b starts at b * G * CHUNK + q * CHUNK.
+template <int G>
 __global__ __launch_bounds__(BCNF_WG) void k_adam(TList T, const float* __restrict__ step, double lr, double b1d,
                                                   double b2d, double epsd, double wdd, float* __restrict__ part,
                                                   const int32_t* __restrict__ guard, AdamBook bk) {
@@ -71,42 +75,46 @@ __global__ __launch_bounds__(BCNF_WG) void k_adam(TList T, const float* __restri
   // every operand load is issued first: none depends on the guard, the step count or the bias corrections,
   // so their round trip overlaps the scalar loads and thread 0's double pow
   const long long total = T.start[T.n];
-  // thread x owns the EPT = 4 consecutive elements i0..i0+3: one 16-B load / store per array when they lie in one
-  // tensor at a 16-B aligned offset (the whole flat coupling buffer), element-wise at tensor seams
-  const long long i0 = (long long)blockIdx.x * CHUNK + EPT * threadIdx.x;
-  const int t0 = find_tensor(T, i0 < total ? i0 : total - 1);
-  const long long o0 = i0 - T.start[t0];
-  const bool vec = i0 + EPT <= T.start[t0 + 1] &&
-                   ((((uintptr_t)(T.p[t0] + o0)) | ((uintptr_t)(T.g[t0] + o0)) | ((uintptr_t)(T.m[t0] + o0)) |
-                     ((uintptr_t)(T.v[t0] + o0))) & 15) == 0;
-  float g[EPT], p[EPT], m[EPT], v[EPT];
-  int t[EPT];
-  long long o[EPT];
-  if (vec) {
-    const floatx4 g4 = *reinterpret_cast<const floatx4*>(T.g[t0] + o0);
-    const floatx4 p4 = *reinterpret_cast<const floatx4*>(T.p[t0] + o0);
-    const floatx4 m4 = *reinterpret_cast<const floatx4*>(T.m[t0] + o0);
-    const floatx4 v4 = *reinterpret_cast<const floatx4*>(T.v[t0] + o0);
+  // thread x owns the EPT = 4 consecutive elements i0..i0+3 of each group: one 16-B load / store per array when they
+  // lie in one tensor at a 16-B aligned offset (the whole flat coupling buffer), element-wise at tensor seams
+  float g[G][EPT], p[G][EPT], m[G][EPT], v[G][EPT];
+  int t[G][EPT];
+  long long o[G][EPT], i0[G];
+  bool vec[G];
 #pragma unroll
-    for (int e = 0; e < EPT; ++e) {
-      g[e] = g4[e];
-      p[e] = p4[e];
-      m[e] = m4[e];
-      v[e] = v4[e];
-      t[e] = t0;
-      o[e] = o0 + e;
-    }
-  } else {
+  for (int q = 0; q < G; ++q) {
+    i0[q] = (long long)blockIdx.x * G * CHUNK + q * CHUNK + EPT * threadIdx.x;
+    const int t0 = find_tensor(T, i0[q] < total ? i0[q] : total - 1);
+    const long long o0 = i0[q] - T.start[t0];
+    vec[q] = i0[q] + EPT <= T.start[t0 + 1] &&
+             ((((uintptr_t)(T.p[t0] + o0)) | ((uintptr_t)(T.g[t0] + o0)) | ((uintptr_t)(T.m[t0] + o0)) |
+               ((uintptr_t)(T.v[t0] + o0))) & 15) == 0;
+    if (vec[q]) {
+      const floatx4 g4 = *reinterpret_cast<const floatx4*>(T.g[t0] + o0);
+      const floatx4 p4 = *reinterpret_cast<const floatx4*>(T.p[t0] + o0);
+      const floatx4 m4 = *reinterpret_cast<const floatx4*>(T.m[t0] + o0);
+      const floatx4 v4 = *reinterpret_cast<const floatx4*>(T.v[t0] + o0);
 #pragma unroll
-    for (int e = 0; e < EPT; ++e) {
-      long long i = i0 + e;
-      i = i < total ? i : total - 1;
-      t[e] = find_tensor(T, i);
-      o[e] = i - T.start[t[e]];
-      g[e] = T.g[t[e]][o[e]];
-      p[e] = T.p[t[e]][o[e]];
-      m[e] = T.m[t[e]][o[e]];
-      v[e] = T.v[t[e]][o[e]];
+      for (int e = 0; e < EPT; ++e) {
+        g[q][e] = g4[e];
+        p[q][e] = p4[e];
+        m[q][e] = m4[e];
+        v[q][e] = v4[e];
+        t[q][e] = t0;
+        o[q][e] = o0 + e;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) {
+        long long i = i0[q] + e;
+        i = i < total ? i : total - 1;
+        t[q][e] = find_tensor(T, i);
+        o[q][e] = i - T.start[t[q][e]];
+        g[q][e] = T.g[t[q][e]][o[q][e]];
+        p[q][e] = T.p[t[q][e]][o[q][e]];
+        m[q][e] = T.m[t[q][e]][o[q][e]];
+        v[q][e] = T.v[t[q][e]][o[q][e]];
+      }
     }
   }
   if (guard && guard[BCNF_GUARD_HALTED]) return;   // a halted step (see nll_finalize) leaves all state
@@ -116,24 +124,29 @@ __global__ __launch_bounds__(BCNF_WG) void k_adam(TList T, const float* __restri
   const AdamScalars as = adam_scalars(step[0] + 1.0f, lr, b1d, b2d, epsd, wdd, sc);
   float ss = 0.f;
 #pragma unroll
-  for (int e = 0; e < EPT; ++e) {
-    if (i0 + e < total) {
-      ss = fmaf(g[e], g[e], ss);
-      adam_elem(p[e], g[e], m[e], v[e], as);
-    }
-  }
-  if (vec) {
-    *reinterpret_cast<floatx4*>(T.m[t0] + o0) = floatx4{m[0], m[1], m[2], m[3]};
-    *reinterpret_cast<floatx4*>(T.v[t0] + o0) = floatx4{v[0], v[1], v[2], v[3]};
-    *reinterpret_cast<floatx4*>(T.p[t0] + o0) = floatx4{p[0], p[1], p[2], p[3]};
-  } else {
+  for (int q = 0; q < G; ++q) {
 #pragma unroll
-    for (int e = 0; e < EPT; ++e)
-      if (i0 + e < total) {
-        T.m[t[e]][o[e]] = m[e];
-        T.v[t[e]][o[e]] = v[e];
-        T.p[t[e]][o[e]] = p[e];
+    for (int e = 0; e < EPT; ++e) {
+      if (i0[q] + e < total) {
+        ss = fmaf(g[q][e], g[q][e], ss);
+        adam_elem(p[q][e], g[q][e], m[q][e], v[q][e], as);
       }
+    }
+    if (vec[q]) {
+      const int t0 = t[q][0];
+      const long long o0 = o[q][0];
+      *reinterpret_cast<floatx4*>(T.m[t0] + o0) = floatx4{m[q][0], m[q][1], m[q][2], m[q][3]};
+      *reinterpret_cast<floatx4*>(T.v[t0] + o0) = floatx4{v[q][0], v[q][1], v[q][2], v[q][3]};
+      *reinterpret_cast<floatx4*>(T.p[t0] + o0) = floatx4{p[q][0], p[q][1], p[q][2], p[q][3]};
+    } else {
+#pragma unroll
+      for (int e = 0; e < EPT; ++e)
+        if (i0[q] + e < total) {
+          T.m[t[q][e]][o[q][e]] = m[q][e];
+          T.v[t[q][e]][o[q][e]] = v[q][e];
+          T.p[t[q][e]][o[q][e]] = p[q][e];
+        }
+    }
   }
   const float s = wg_sum(ss, red);
   if (threadIdx.x == 0 && part) part[blockIdx.x] = s;
@@ -154,19 +167,23 @@ __global__ void k_advance(float* step, long long* cursor, long long n_batches, c
   if (threadIdx.x == 0) advance_counters(step, cursor, n_batches);
 }
 
+template <int G>
 __global__ __launch_bounds__(BCNF_WG) void k_sumsq(TList T, float* __restrict__ part) {
   __shared__ float red[BCNF_WG];
   const long long total = T.start[T.n];
-  // the same element order and fmaf chain as k_adam's partials (clip norms bit-identical either way)
-  const long long i0 = (long long)blockIdx.x * CHUNK + EPT * threadIdx.x;
+  // the same element order and fmaf chain as k_adam<G>'s partials (clip norms bit-identical either way)
   float ss = 0.f;
 #pragma unroll
-  for (int e = 0; e < EPT; ++e) {
-    const long long i = i0 + e;
-    if (i < total) {
-      const int t = find_tensor(T, i);
-      const float g = T.g[t][i - T.start[t]];
-      ss = fmaf(g, g, ss);
+  for (int q = 0; q < G; ++q) {
+    const long long i0 = (long long)blockIdx.x * G * CHUNK + q * CHUNK + EPT * threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      const long long i = i0 + e;
+      if (i < total) {
+        const int t = find_tensor(T, i);
+        const float g = T.g[t][i - T.start[t]];
+        ss = fmaf(g, g, ss);
+      }
     }
   }
   const float s = wg_sum(ss, red);
@@ -174,6 +191,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_sumsq(TList T, float* __restrict__ 
 }
 
 // torch.nn.utils.clip_grad_norm_: coef = min(max_norm / (||g||_2 + 1e-6), 1); g *= coef.
+template <int G>
 __global__ __launch_bounds__(BCNF_WG) void k_clip(TList T, const float* __restrict__ part, int nparts, float max_norm,
                                                   float* __restrict__ norm_out, float* step, long long* cursor,
                                                   long long n_batches, const float* __restrict__ log_values,
@@ -181,12 +199,13 @@ __global__ __launch_bounds__(BCNF_WG) void k_clip(TList T, const float* __restri
   __shared__ float red[BCNF_WG];
   // the gradient loads go out first, beside the partials' (the scaling needs the total norm, not the loads)
   const long long total = T.start[T.n];
-  float g[EPT];
-  int t[EPT];
-  long long o[EPT];
+  constexpr int NE = G * EPT;                    // elements per thread: this workgroup's G * CHUNK
+  float g[NE];
+  int t[NE];
+  long long o[NE];
 #pragma unroll
-  for (int e = 0; e < EPT; ++e) {
-    long long i = (long long)blockIdx.x * CHUNK + e * BCNF_WG + threadIdx.x;
+  for (int e = 0; e < NE; ++e) {
+    long long i = (long long)blockIdx.x * G * CHUNK + e * BCNF_WG + threadIdx.x;
     i = i < total ? i : total - 1;
     t[e] = find_tensor(T, i);
     o[e] = i - T.start[t[e]];
@@ -198,8 +217,8 @@ __global__ __launch_bounds__(BCNF_WG) void k_clip(TList T, const float* __restri
   const float tot = sqrtf(wg_sum(acc, red));
   const float coef = fminf(max_norm / (tot + 1e-6f), 1.0f);
 #pragma unroll
-  for (int e = 0; e < EPT; ++e) {
-    const long long i = (long long)blockIdx.x * CHUNK + e * BCNF_WG + threadIdx.x;
+  for (int e = 0; e < NE; ++e) {
+    const long long i = (long long)blockIdx.x * G * CHUNK + e * BCNF_WG + threadIdx.x;
     if (i < total) T.g[t[e]][o[e]] = g[e] * coef;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -424,7 +443,12 @@ int split_rows(long long M) {        // rows per split-K chunk of the weight gra
   return (int)((r + 31) & ~31LL);
 }
 
-inline int64_t n_partials(int64_t total_numel) { return total_numel <= 0 ? 1 : (total_numel + CHUNK - 1) / CHUNK; }
+// Element groups per thread of k_adam / k_sumsq / k_clip: 4 for large parameter sets (>= 4M), else 1.
+inline int adam_groups(int64_t total_numel) { return total_numel >= (1 << 22) ? 4 : 1; }
+inline int64_t n_partials(int64_t total_numel) {
+  const int64_t per = (int64_t)CHUNK * adam_groups(total_numel);
+  return total_numel <= 0 ? 1 : (total_numel + per - 1) / per;
+}
 
 // Sum of many partials by one workgroup (fixed order), so that every clip workgroup then reads one value
 // instead of re-reducing all partials (quadratic in the parameter count otherwise).
@@ -458,8 +482,12 @@ int bcnf_adam_step(int32_t n_tensors, float* const* params, float* const* grads,
     if (!T.p[i] || !T.m[i] || !T.v[i]) return BCNF_ERR_ARG;
   const long long total = T.start[T.n];
   const unsigned nwg = (unsigned)n_partials(total);
-  hipLaunchKernelGGL(k_adam, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, step, lr, beta1, beta2, eps,
-                     weight_decay, grad_partials, guard, AdamBook{});
+  if (adam_groups(total) == 4)
+    hipLaunchKernelGGL(k_adam<4>, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, step, lr, beta1, beta2, eps,
+                       weight_decay, grad_partials, guard, AdamBook{});
+  else
+    hipLaunchKernelGGL(k_adam<1>, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, step, lr, beta1, beta2, eps,
+                       weight_decay, grad_partials, guard, AdamBook{});
   if ((rc = launched()) || !advance_step) return rc;
   hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, (hipStream_t)stream, step, (long long*)nullptr, 0LL, guard);
   return launched();
@@ -481,8 +509,12 @@ int bcnf_adam_step_bookkeep(int32_t n_tensors, float* const* params, float* cons
   const unsigned nwg = (unsigned)n_partials(total);
   const AdamBook bk{step, (long long*)advance_cursor, (long long)cursor_modulo, log_values, log_history,
                     (int*)done_counter};
-  hipLaunchKernelGGL(k_adam, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, step, lr, beta1, beta2, eps,
-                     weight_decay, (float*)nullptr, guard, bk);
+  if (adam_groups(total) == 4)
+    hipLaunchKernelGGL(k_adam<4>, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, step, lr, beta1, beta2, eps,
+                       weight_decay, (float*)nullptr, guard, bk);
+  else
+    hipLaunchKernelGGL(k_adam<1>, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, step, lr, beta1, beta2, eps,
+                       weight_decay, (float*)nullptr, guard, bk);
   return launched();
 }
 
@@ -492,7 +524,10 @@ int bcnf_grad_sumsq(int32_t n_tensors, float* const* grads, const int64_t* numel
   if (rc) return rc;
   if (!grad_partials) return BCNF_ERR_ARG;
   const unsigned nwg = (unsigned)n_partials(T.start[T.n]);
-  hipLaunchKernelGGL(k_sumsq, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, grad_partials);
+  if (adam_groups(T.start[T.n]) == 4)
+    hipLaunchKernelGGL(k_sumsq<4>, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, grad_partials);
+  else
+    hipLaunchKernelGGL(k_sumsq<1>, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, grad_partials);
   return launched();
 }
 
@@ -514,9 +549,14 @@ int bcnf_clip_grad_norm(int32_t n_tensors, float* const* grads, const int64_t* n
     part = grad_partials + np;
     nread = 1;
   }
-  hipLaunchKernelGGL(k_clip, dim3((unsigned)np), dim3(BCNF_WG), 0, (hipStream_t)stream, T, part, nread,
-                     max_norm, total_norm, advance_step, (long long*)advance_cursor, (long long)cursor_modulo,
-                     log_values, log_history, guard);
+  if (adam_groups(T.start[T.n]) == 4)
+    hipLaunchKernelGGL(k_clip<4>, dim3((unsigned)np), dim3(BCNF_WG), 0, (hipStream_t)stream, T, part, nread,
+                       max_norm, total_norm, advance_step, (long long*)advance_cursor, (long long)cursor_modulo,
+                       log_values, log_history, guard);
+  else
+    hipLaunchKernelGGL(k_clip<1>, dim3((unsigned)np), dim3(BCNF_WG), 0, (hipStream_t)stream, T, part, nread,
+                       max_norm, total_norm, advance_step, (long long*)advance_cursor, (long long)cursor_modulo,
+                       log_values, log_history, guard);
   return launched();
 }
 
