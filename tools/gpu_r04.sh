@@ -43,6 +43,12 @@ for s in $STEPS; do
         BCNF_LSTM_MIOPEN=$mi timeout -k 10 200 python bench.py --workload lstm_large --no-cpu-baseline --steps 10 --warmup 3 > gpurun_out/${T}_lstmab.json 2>/dev/null
         python -c "import json; d=json.loads(open('gpurun_out/${T}_lstmab.json').read().strip().splitlines()[-1]); print('miopen=$mi', d['ms_per_step'], round(d['value']), d['kernels_us'])"
       done; done 2>&1 | tee gpurun_out/${T}_lstmab.txt ;;
+    abbench)
+      for i in 1 2; do for lib in default ${AB_LIBS:-build_exp/libhead.so}; do
+        if [ $lib = default ]; then timeout -k 10 200 python bench.py --no-secondary --no-cpu-baseline > gpurun_out/${T}_abb.json 2>/dev/null
+        else BCNF_AMD_LIB=$lib timeout -k 10 200 python bench.py --no-secondary --no-cpu-baseline > gpurun_out/${T}_abb.json 2>/dev/null; fi
+        python -c "import json; d=json.loads(open('gpurun_out/${T}_abb.json').read().strip().splitlines()[-1]); print('$lib', d['ms_per_step'], round(d['value']), d['kernels_us'])"
+      done; done 2>&1 | tee gpurun_out/${T}_abbench.txt ;;
     prof)
       cd /tmp && export TMPDIR=/tmp
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/${T}_prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --no-secondary --no-cpu-baseline --steps 40 > $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.log; exit 1; }
