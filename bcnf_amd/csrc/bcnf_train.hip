@@ -317,6 +317,157 @@ __global__ __launch_bounds__(BCNF_WG) void k_gemm(const float* __restrict__ A, i
   }
 }
 
+// Feature-MLP GEMMs (nn.Linear forward and dL/dx, e.g. FC_large's 2048 x 310 x 310 layers): C[M][Nc] =
+// sum_r A[m][r] Bop[r][n] + bias with the reduction index r contiguous in A's rows (x, or dL/dy), Bop[r][n] =
+// TB ? Bm[n][r] (forward: W) : Bm[r][n] (dL/dx: W). A workgroup owns 64 rows x LN_NT * 16 columns: its slab of Bop
+// (R x LN_NT * 16 floats, coalesced loads) is staged in LDS once; each wave takes 16 rows, its A operand for 16
+// reductions is ONE float4 (lane (q, r) contracts r' = 16 g + 4 q + i at MFMA step i), 4 groups in flight,
+// LN_NT output tiles per A load. SA / ACT: as k_gemm. The tile-per-wave k_gemm above re-read every operand from L2
+// one scalar per MFMA step (33 us for FC_large's 310 x 310 layer at B = 2048).
+constexpr int LN_NT = 2;                 // 16-column MFMA tiles per wave
+constexpr int LN_G = 8;                  // 16-reduction groups in flight per wave
+constexpr int LN_RMAX = 1024;            // largest reduction staged in LDS (larger: k_gemm)
+
+template <bool TB, bool SA, bool ACT>
+__global__ __launch_bounds__(BCNF_WG) void k_lin(const float* __restrict__ A, int lda, const float* __restrict__ Bm,
+                                                 int ldb, const float* __restrict__ bias, float* __restrict__ C, int ldc,
+                                                 long long M, int Nc, int R, const float* __restrict__ sa, ActArgs act) {
+  constexpr int NC = LN_NT * 16, BP = NC + 1;          // slab row pitch (odd: conflict-free column reads)
+  extern __shared__ float bs[];                          // [R][BP]
+  const int col0 = blockIdx.y * NC;
+  // stage Bop[r][col0 .. col0 + NC) -> bs[r][c] (zero past Nc)
+  constexpr int SU = 20;                                 // staging loads in flight per thread
+  const int tot = R * NC;
+  for (int i0 = threadIdx.x; i0 < tot; i0 += SU * BCNF_WG) {
+    float v[SU];
+    int dst[SU];
+    bool live[SU];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const int i = i0 + u * BCNF_WG;
+      const int ic = i < tot ? i : tot - 1;
+      int r, c;
+      if (TB) { c = ic / R; r = ic - c * R; }            // W rows: consecutive threads walk r (contiguous)
+      else { r = ic / NC; c = ic - r * NC; }             // W rows: consecutive threads walk columns
+      const int n = col0 + c < Nc ? col0 + c : Nc - 1;
+      v[u] = TB ? Bm[(long long)n * ldb + r] : Bm[(long long)r * ldb + n];
+      dst[u] = r * BP + c;
+      live[u] = col0 + c < Nc;                            // columns past Nc stage zeros
+    }
+    asm volatile("" ::: "memory");                        // all SU loads issued before the first store
+#pragma unroll
+    for (int u = 0; u < SU; ++u)
+      if (i0 + u * BCNF_WG < tot) bs[dst[u]] = live[u] ? v[u] : 0.f;
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lq = l >> 4;
+  const long long row0 = ((long long)blockIdx.x * 4 + wave) * 16;
+  if (row0 >= M) return;
+  const long long ar = row0 + lr < M ? row0 + lr : M - 1;     // clamped rows: loaded, never stored
+  const float* a = A + ar * lda;
+  const float* as = SA ? sa + ar * lda : nullptr;
+  floatx4 acc[LN_NT];
+#pragma unroll
+  for (int t = 0; t < LN_NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int ng = R / 16;                                  // whole 16-reduction groups
+  auto ld4u = [](const float* p) {                         // 4 floats at a 4-byte aligned address
+    floatx4 v;
+    __builtin_memcpy(&v, p, 16);
+    return v;
+  };
+  auto group = [&](const floatx4& av, const floatx4& sv, int g) {   // reductions 16 g .. 16 g + 15
+    const float* b = bs + (16 * g + 4 * lq) * BP + lr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float x = SA ? av[i] * sv[i] : av[i];
+#pragma unroll
+      for (int t = 0; t < LN_NT; ++t) acc[t] = mfma4(x, b[i * BP + 16 * t], acc[t]);
+    }
+  };
+  for (int g0 = 0; g0 < ng; g0 += LN_G) {
+    floatx4 av[LN_G], sv[LN_G];
+#pragma unroll
+    for (int u = 0; u < LN_G; ++u) {                      // every load of the step first (clamped: static waits)
+      const int g = g0 + u < ng ? g0 + u : ng - 1;
+      av[u] = ld4u(a + 16 * g + 4 * lq);
+      if (SA) sv[u] = ld4u(as + 16 * g + 4 * lq);
+    }
+    asm volatile("" ::: "memory");                        // hipcc may not sink them to their first use
+#pragma unroll
+    for (int u = 0; u < LN_G; ++u)
+      if (g0 + u < ng) group(av[u], sv[u], g0 + u);       // uniform
+  }
+  for (int r0 = 16 * ng; r0 < R; r0 += 4) {               // reduction tail (R % 16)
+    const int r = r0 + lq;
+    const int rc = r < R ? r : R - 1;
+    float x = a[rc];
+    if (SA) x *= as[rc];
+    x = r < R ? x : 0.f;
+#pragma unroll
+    for (int t = 0; t < LN_NT; ++t) acc[t] = mfma4(x, r < R ? bs[rc * BP + lr + 16 * t] : 0.f, acc[t]);
+  }
+#pragma unroll
+  for (int t = 0; t < LN_NT; ++t) {
+    const int col = col0 + 16 * t + lr;
+    if (col >= Nc) continue;
+    const float bb = bias ? bias[col] : 0.f;
+    if (ACT) {
+      float m[4] = {1.f, 1.f, 1.f, 1.f};
+      if (act.rng) {
+        const uint64_t seed = act.rng[0], off = act.rng[1];
+        const uint4 rn = philox4x32_10(make_uint4((uint32_t)col, (uint32_t)((row0 >> 2) + lq), (uint32_t)off,
+                                                  (uint32_t)(off >> 32)),
+                                       make_uint2((uint32_t)seed ^ act.salt, (uint32_t)(seed >> 32)));
+        m[0] = rn.x >= act.thresh ? act.keep : 0.f;
+        m[1] = rn.y >= act.thresh ? act.keep : 0.f;
+        m[2] = rn.z >= act.thresh ? act.keep : 0.f;
+        m[3] = rn.w >= act.thresh ? act.keep : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long long rr = row0 + 4 * lq + i;
+        float g, dg;
+        gelu_fg(acc[t][i] + bb, g, dg);
+        if (rr < M) {
+          C[rr * ldc + col] = g * m[i];
+          if (act.G) act.G[rr * ldc + col] = dg * m[i];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long long rr = row0 + 4 * lq + i;
+        if (rr < M) C[rr * ldc + col] = acc[t][i] + bb;
+      }
+    }
+  }
+}
+
+// One feature-MLP GEMM: the LDS-slab kernel when the reduction fits, else the tile-per-wave one.
+template <bool TB, bool SA, bool ACT>
+int launch_lin(const float* A, int lda, const float* Bm, int ldb, const float* bias, float* C, int ldc, long long M,
+               int Nc, int R, const float* sa, const ActArgs& act, hipStream_t st) {
+  if (R <= LN_RMAX) {
+    constexpr size_t kmax = sizeof(float) * LN_RMAX * (LN_NT * 16 + 1);
+    static bool attr = false;                            // first (eager) call, before any capture
+    if (!attr) {
+      if (const int rc = bcnf_rt::hip_status(hipFuncSetAttribute((const void*)k_lin<TB, SA, ACT>,
+                                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kmax)))
+        return rc;
+      attr = true;
+    }
+    const size_t lds = sizeof(float) * (size_t)R * (LN_NT * 16 + 1);
+    const dim3 grid((unsigned)((M + 63) / 64), (unsigned)((Nc + LN_NT * 16 - 1) / (LN_NT * 16)));
+    hipLaunchKernelGGL((k_lin<TB, SA, ACT>), grid, dim3(BCNF_WG), lds, st, A, lda, Bm, ldb, bias, C, ldc, M, Nc, R, sa,
+                       act);
+  } else {
+    const dim3 grid((unsigned)((M + 63) / 64), (unsigned)((Nc + 15) / 16));
+    hipLaunchKernelGGL((k_gemm<TB, SA, ACT>), grid, dim3(BCNF_WG), 0, st, A, lda, Bm, ldb, bias, C, ldc, M, Nc, R, sa,
+                       act);
+  }
+  return bcnf_rt::launched();
+}
+
 // Split-K weight gradient: work[s][n][k] = sum_{m in split s} dY[m][n] X[m][k],
 // bwork[s][n] = sum_{m in split s} dY[m][n]. grid = (tiles_n * tiles_k / 4 rounded up, splits).
 template <bool SA>
@@ -611,11 +762,8 @@ int bcnf_linear_forward(const float* x, const float* weight, const float* bias, 
   if (rows < 0 || in_features < 1 || out_features < 1) return BCNF_ERR_ARG;
   if (rows == 0) return BCNF_OK;
   if (!x || !weight || !y) return BCNF_ERR_ARG;
-  const dim3 grid((unsigned)((rows + 63) / 64), (unsigned)((out_features + 15) / 16));
-  hipLaunchKernelGGL((k_gemm<true, false, false>), grid, dim3(BCNF_WG), 0, (hipStream_t)stream, x, in_features, weight,
-                     in_features, bias, y, out_features, (long long)rows, out_features, in_features,
-                     (const float*)nullptr, ActArgs{});
-  return launched();
+  return launch_lin<true, false, false>(x, in_features, weight, in_features, bias, y, out_features, rows, out_features,
+                                        in_features, nullptr, ActArgs{}, (hipStream_t)stream);
 }
 
 int bcnf_linear_gelu_forward(const float* x, const float* weight, const float* bias, int64_t rows, int32_t in_features,
@@ -629,11 +777,8 @@ int bcnf_linear_gelu_forward(const float* x, const float* weight, const float* b
     act.thresh = (uint32_t)fmin(4294967295.0, floor((double)p * 4294967296.0 + 0.5));   // keep iff u >= thresh
     act.keep = (float)(1.0 / (1.0 - (double)p));
   }
-  const dim3 grid((unsigned)((rows + 63) / 64), (unsigned)((out_features + 15) / 16));
-  hipLaunchKernelGGL((k_gemm<true, false, true>), grid, dim3(BCNF_WG), 0, (hipStream_t)stream, x, in_features, weight,
-                     in_features, bias, a, out_features, (long long)rows, out_features, in_features,
-                     (const float*)nullptr, act);
-  return launched();
+  return launch_lin<true, false, true>(x, in_features, weight, in_features, bias, a, out_features, rows, out_features,
+                                       in_features, nullptr, act, (hipStream_t)stream);
 }
 
 int64_t bcnf_linear_work_bytes(int64_t rows, int32_t in_features, int32_t out_features) {
@@ -659,14 +804,8 @@ int linear_backward(const float* x, const float* weight, const float* dy, const 
   if (!dy) return BCNF_ERR_ARG;
   if (dx) {   // dX[m][k] = sum_n dY[m][n] W[n][k]
     if (!weight) return BCNF_ERR_ARG;
-    const dim3 grid((unsigned)((rows + 63) / 64), (unsigned)((K + 15) / 16));
-    if (sg)
-      hipLaunchKernelGGL((k_gemm<false, true, false>), grid, dim3(BCNF_WG), 0, st, dy, N, weight, K,
-                         (const float*)nullptr, dx, K, (long long)rows, K, N, sg, ActArgs{});
-    else
-      hipLaunchKernelGGL((k_gemm<false, false, false>), grid, dim3(BCNF_WG), 0, st, dy, N, weight, K,
-                         (const float*)nullptr, dx, K, (long long)rows, K, N, (const float*)nullptr, ActArgs{});
-    int rc = launched();
+    int rc = sg ? launch_lin<false, true, false>(dy, N, weight, K, nullptr, dx, K, rows, K, N, sg, ActArgs{}, st)
+                : launch_lin<false, false, false>(dy, N, weight, K, nullptr, dx, K, rows, K, N, nullptr, ActArgs{}, st);
     if (rc) return rc;
   }
   if (dweight || dbias) {
