@@ -18,7 +18,16 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
+#include <utility>
+#include <vector>
+
+// Experiment switches of the pack-free forward (timing probes only, results wrong): 1 no side outputs, 2 no h GEMM,
+// 4 no record gathers, 8 no ldc sum, 16 no x loads, 32 no Wf / bf loads
+#ifndef BCNF_RAW_EXP
+#define BCNF_RAW_EXP 0
+#endif
 
 // Phase stamps (s_memtime per phase of workgroup 0's first compute and helper waves) exist only in a diagnostic
 // build with -DBCNF_PHASE_STAMPS (tools/exp_variants.sh); the shipped library has no stamp code, no debug globals
@@ -139,8 +148,9 @@ int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
 size_t fwd_lds_bytes(const BcnfLayout& L) {   // forward / inverse record ring (2 blocks)
   return sizeof(float) * (size_t)(2 * RING);
 }
-size_t fwd2_lds_bytes(const BcnfLayout& L) {  // k_forward: record ring, projection partials, dropout masks (3 slots)
-  return sizeof(float) * (size_t)(3 * RING + 3 * 4 * 256 + 3 * 8 * 256);
+size_t fwd2_lds_bytes(const BcnfLayout& L, bool raw = false) {  // k_forward: record ring, projection partials,
+  return sizeof(float) * (size_t)(3 * RING + 3 * 4 * 256 + 3 * 8 * 256 +   // dropout masks (3 slots)
+                                  (raw ? 4 + 16 * (128 + 4) : 0));         // RAW: log-det partials, h tile
 }
 size_t bwd_lds_bytes(const BcnfLayout& L) {   // backward record ring, delta tiles (2), activation tiles (3), derivative slots (2)
   return sizeof(float) * (size_t)(2 * RING + 2 * (L.NH + 6) * TILE + 3 * (L.NH + 1) * TILE + 2 * 3 * 4 * 256);
@@ -287,6 +297,140 @@ __device__ float rec_pm(const BcnfLayout& L, const float* P, const float* Q, int
   e -= 32;                                                                 // ActNorm inverse [1/sa ba 1/sb bb]
   const int q = e >> 4, r = (e >> 2) & 3, i = e & 3;
   return rec_f(L, P, Q, k, feat(q, r), i, true);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Pack-free training forward (bcnf_fold_train_forward, round 4): the forward's helper waves build each block's
+// forward record straight from the canonical parameters instead of reading a packed copy, so the folded training
+// step needs no pack launch. The record entries of a block k < nb - 1 that are not structurally zero are each one
+// parameter at a block-independent offset from k * blk_stride (ActNorm, coupling Linears) or from k * D * D
+// (the orthonormal mix); RawTable lists them once per layout, split into P-sourced and Q-sourced slots of RAW_NP /
+// RAW_NQ entries per helper thread (padding entries copy parameter 0 into an unused word of the ring slot), so a
+// helper thread gathers its entries with block-uniform base pointers and never branches. The zero entries stay zero
+// in the LDS ring (zeroed once); the last block (no ActNorm, identity mix) goes through rec_f itself.
+// ------------------------------------------------------------------------------------------------
+constexpr int RAW_NP = 10, RAW_NQ = 2, RAW_NZ = 6;   // slots per helper thread (FC_small: 2152 P-sourced, 361
+                                                     // Q-sourced and 1071 zero entries)
+constexpr int RAW_NS = RAW_NP + RAW_NQ + RAW_NZ;
+constexpr int RAW_DUMMY = RING - 1;       // an unused float of a ring slot (16 RF <= RING - 1)
+constexpr int RAW_SRC_MAX = 1 << 20;
+
+// A table entry: destination float of the ring slot (j * RF + e, < 4096) | source offset << 12.
+__host__ __device__ constexpr uint32_t raw_entry(int dst, int src) { return (uint32_t)dst | ((uint32_t)src << 12); }
+
+// Source of forward-record entry e of lane j for a block k < nb - 1: kind 0 = structurally zero, 1 = params at
+// k * blk_stride + off, 2 = qmats at k * D * D + off; -1 = a constant the table cannot express (no ActNorm: 1.0).
+// Mirrors rec_f (inverse = false) entry by entry.
+int rec_f_source(const BcnfLayout& L, int j, int e, int* off) {
+  const int Da = L.Da, Db = L.Db, D = L.D, NH = L.NH, an = L.an_size;
+  auto lin_w = [&](int l, int row, int col) { return an + L.lin_w[l] + row * L.lin_in[l] + col; };
+  *off = 0;
+  if (e < 4) {
+    if (!L.act_norm) return ((e == 0 && j < Da) || (e == 2 && j < Db)) ? -1 : 0;
+    switch (e) {
+      case 0: return j < Da ? (*off = j, 1) : 0;
+      case 1: return j < Da ? (*off = D + j, 1) : 0;
+      case 2: return j < Db ? (*off = Da + j, 1) : 0;
+      default: return j < Db ? (*off = D + Da + j, 1) : 0;
+    }
+  }
+  if (e == L.rf_b1) return j < L.H[1] ? (*off = an + L.lin_b[1] + j, 1) : 0;
+  if (e >= L.rf_w1 && e < L.rf_w1 + 16) {
+    const int src = (j - (e - L.rf_w1)) & 15;
+    return (j < L.H[1] && src < Da) ? (*off = lin_w(1, j, src), 1) : 0;
+  }
+  if (e >= L.rf_hid && e < L.rf_t) {
+    const int l = 2 + (e - L.rf_hid) / 17, r = (e - L.rf_hid) % 17;
+    if (r == 16) return j < L.H[l] ? (*off = an + L.lin_b[l] + j, 1) : 0;
+    const int src = (j - r) & 15;
+    return (j < L.H[l] && src < L.H[l - 1]) ? (*off = lin_w(l, j, src), 1) : 0;
+  }
+  if (e >= L.rf_t && e < L.rf_t + 34) {
+    const int half = (e - L.rf_t) / 17, r = (e - L.rf_t) % 17;
+    if (r == 16) return j < Db ? (*off = an + L.lin_b[NH + 1] + half * Db + j, 1) : 0;
+    const int src = (j - r) & 15;
+    return (j < Db && src < L.H[NH]) ? (*off = lin_w(NH + 1, half * Db + j, src), 1) : 0;
+  }
+  if (e >= L.rf_q && e < L.rf_q + 64) {
+    const int qi = (e - L.rf_q) / 16, r = (e - L.rf_q) % 16, src = (j - r) & 15;
+    switch (qi) {
+      case 0: return (j < Da && src < Da) ? (*off = src * D + j, 2) : 0;
+      case 1: return (j < Da && src < Db) ? (*off = (Da + src) * D + j, 2) : 0;
+      case 2: return (j < Db && src < Da) ? (*off = src * D + Da + j, 2) : 0;
+      default: return (j < Db && src < Db) ? (*off = (Da + src) * D + Da + j, 2) : 0;
+    }
+  }
+  return 0;
+}
+
+// Source of backward-record entry e of lane j for a block k < nb - 1 (mirrors rec_b): kinds as rec_f_source.
+int rec_b_source(const BcnfLayout& L, int j, int e, int* off) {
+  const int NH = L.NH, Da = L.Da, Db = L.Db, D = L.D, an = L.an_size;
+  auto lin_w = [&](int l, int row, int col) { return an + L.lin_w[l] + row * L.lin_in[l] + col; };
+  *off = 0;
+  if (e >= L.rb_w1t && e < L.rb_w1t + 16) {
+    const int src = (j - (e - L.rb_w1t)) & 15;
+    return (j < Da && src < L.H[1]) ? (*off = lin_w(1, src, j), 1) : 0;
+  }
+  if (e >= L.rb_hid && e < L.rb_w1t) {
+    const int l = NH - (e - L.rb_hid) / 16, r = (e - L.rb_hid) % 16, src = (j - r) & 15;
+    return (j < L.H[l - 1] && src < L.H[l]) ? (*off = lin_w(l, src, j), 1) : 0;
+  }
+  if (e >= L.rb_tt && e < L.rb_tt + 32) {
+    const int half = (e - L.rb_tt) / 16, r = (e - L.rb_tt) % 16, src = (j - r) & 15;
+    return (j < L.H[NH] && src < Db) ? (*off = lin_w(NH + 1, half * Db + src, j), 1) : 0;
+  }
+  if (e >= L.rb_qt && e < L.rb_qt + 64) {                 // rec_f(inverse = true) of the mix: Q^T
+    const int qi = (e - L.rb_qt) / 16, r = (e - L.rb_qt) % 16, src = (j - r) & 15;
+    switch (qi) {
+      case 0: return (j < Da && src < Da) ? (*off = j * D + src, 2) : 0;
+      case 1: return (j < Da && src < Db) ? (*off = j * D + Da + src, 2) : 0;
+      case 2: return (j < Db && src < Da) ? (*off = (Da + j) * D + src, 2) : 0;
+      default: return (j < Db && src < Db) ? (*off = (Da + j) * D + Da + src, 2) : 0;
+    }
+  }
+  if (e >= L.rb_an && e < L.rb_an + 4) return rec_f_source(L, j, e - L.rb_an, off);
+  return 0;
+}
+
+// Floats of the pack-free forward's table: the forward slots [RAW_NS][256], then one block's backward record
+// [16 RB] as (source << 2 | kind) with kind 0 params, 1 qmats, 2 zero.
+long long raw_table_words(const BcnfLayout& L) { return (long long)RAW_NS * BCNF_WG + 16LL * L.RB; }
+
+// The table [RAW_NS][BCNF_WG] (P slots, then Q slots, then zero slots) for layout L: every float of a ring slot's
+// 16 RF record floats belongs to exactly one (thread, slot), so a helper thread writes its own words and no two
+// threads race. Within a kind the entries go in SOURCE order, entry n to slot n / 256, thread n % 256: a wave's
+// gather then reads 64 consecutive parameters (the P entries are exactly a block's parameters minus the W1
+// condition columns, the Q entries all of Q_k) -- a few cache lines per load instead of one per lane -- and the
+// scattered side is the LDS write. Padding entries name RAW_DUMMY. False if the raw path does not apply (no
+// ActNorm: constant entries; or more entries of a kind than slots).
+bool build_raw_table(const BcnfLayout& L, uint32_t* out) {
+  if (L.nb < 2 || 16 * L.RF > RAW_DUMMY || L.blk_stride >= RAW_SRC_MAX) return false;
+  std::vector<std::pair<int, int>> ent[3];                  // (src, dst) per kind: P, Q, zero
+  for (int j = 0; j < 16; ++j)
+    for (int e = 0; e < L.RF; ++e) {
+      int off;
+      const int kind = rec_f_source(L, j, e, &off);
+      if (kind < 0) return false;
+      ent[kind == 1 ? 0 : kind == 2 ? 1 : 2].emplace_back(off, j * L.RF + e);
+    }
+  const int cap[3] = {RAW_NP, RAW_NQ, RAW_NZ}, first[3] = {0, RAW_NP, RAW_NP + RAW_NQ};
+  for (int i = 0; i < RAW_NS * BCNF_WG; ++i) out[i] = raw_entry(RAW_DUMMY, 0);
+  for (int g = 0; g < 3; ++g) {
+    if ((int)ent[g].size() > cap[g] * BCNF_WG) return false;
+    std::sort(ent[g].begin(), ent[g].end());
+    for (int n = 0; n < (int)ent[g].size(); ++n)
+      out[(first[g] + n / BCNF_WG) * BCNF_WG + n % BCNF_WG] = raw_entry(ent[g][n].second, ent[g][n].first);
+  }
+  uint32_t* pb = out + (long long)RAW_NS * BCNF_WG;
+  for (int j = 0; j < 16; ++j)
+    for (int e = 0; e < L.RB; ++e) {
+      int off;
+      const int kind = rec_b_source(L, j, e, &off);
+      if (kind < 0 || off >= (1 << 29)) return false;
+      pb[j * L.RB + e] = ((uint32_t)off << 2) | (uint32_t)(kind == 1 ? 0 : kind == 2 ? 1 : 2);
+    }
+  return true;
 }
 
 // Grid: 1 workgroup that computes the ActNorm log|det| constant  sum_k sum_i log|scale_k,i|  (cnf.py:350) in a
@@ -1146,6 +1290,42 @@ struct ProjArgs {
   long long ldh;
   int C, Cp, NKp;
 };
+// RAW (bcnf_fold_train_forward): the pack-free folded training forward, so the folded training step needs no pack
+// launch. Differences from the packed forward, all in the prologue and the helper waves:
+//  * records: each helper thread owns RAW_NS words of a ring slot (build_raw_table) and gathers block k's record
+//    straight from the parameters -- RAW_NP loads at k * blk_stride + src, RAW_NQ at k * D * D + src, zero words
+//    written once; the last block (no ActNorm, identity mix) through rec_f on the same words;
+//  * projection: helper wave hw computes h^T = Wf x^T + bf for its 16-column tiles ct = hw, hw + 4, .. of the
+//    workgroup's 16 samples on fp32 MFMA (once), and that output layout IS the projection's A operand with the K
+//    order (ct, r) -> column 16 ct + 4 lq + r, so no LDS round trip: per block the B operand is W1_k[j][Da + that
+//    column] read from the parameters. The sums are the unfolded ones (h first), not the folded Wc;
+//  * batch rows: with idx the rows come from the pools (the captured step's batch gather), and the forward writes
+//    the gathered y and x rows for the backward;
+//  * side outputs for the backward kernels, spread over the grid in the helpers' first interval: the backward
+//    records PB and W1hR into `pk`; the compute waves sum the ActNorm log-det constant themselves.
+struct RawArgs {
+  const float* P;          // canonical flat parameters
+  const float* Q;          // orthonormal matrices [nb - 1][D][D]
+  const uint32_t* table;   // [RAW_NS][256] (build_raw_table)
+  const float* wf;         // feature Linear weight [C][X]
+  const float* bf;         // its bias [C] (nullable)
+  const float* ypool;      // y rows [*][D]
+  float* ydst;             // gathered y rows [B][D] (nullable: no copy)
+  const float* xpool;      // x rows [*][ldx]
+  float* xdst;             // gathered x rows [B][ldx] (nullable: no copy)
+  const int64_t* idx;      // batch row b -> pool row idx[(cursor ? cursor[0] * B : 0) + b]; NULL: row b
+  const long long* cursor;
+  float* pk;               // packed buffer: PB and W1hR are written here
+  int X, ldx;
+};
+constexpr int RAW_XS = 24;             // K-steps of the h GEMM: X <= 96
+constexpr int RAW_TPW = 2;             // h column tiles per helper wave: C <= 128
+constexpr int RAW_SIDE_Q = 4;          // side units per workgroup done in the idle interval
+__host__ __device__ constexpr int raw_hs_pitch(int C) { return 16 * ((C + 15) / 16) + 4; }
+__device__ __forceinline__ long long raw_row(const RawArgs& R, long long B, long long b) {
+  return R.idx ? (long long)R.idx[(R.cursor ? R.cursor[0] * B : 0) + b] : b;
+}
+
 constexpr int FWD_WG = 2 * BCNF_WG;
 constexpr int HP_SMAX = 16;            // K-steps of 4 per helper wave: Cp / 16 <= 16 (Cp <= 256)
 constexpr int FWD_SLOTS = 3;           // ring depth: the helpers prepare block k + 2 while block k runs
@@ -1166,17 +1346,20 @@ constexpr int FWD_HEAD = 24;           // record floats the compute waves prefet
 // waited for 27 record reads of all four compute waves.
 // The projection needs no separate GEMM launch and no HBM round trip, and the compute waves' loop issues no global
 // loads (the record stores of SAVE are its only VMEM traffic).
-template <int NH, bool DROP, bool SAVE>
+template <int NH, bool DROP, bool SAVE, bool RAW = false>
 __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const float* __restrict__ pk,
                                                     const float* __restrict__ y, ProjArgs P,
                                                     long long B, float* __restrict__ z, float* __restrict__ ldj_out,
                                                     float* __restrict__ logp, const uint64_t* rng,
-                                                    float* __restrict__ arec, float* __restrict__ nll_part) {
+                                                    float* __restrict__ arec, float* __restrict__ nll_part,
+                                                    RawArgs R) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int RFL = 16 * L.RF;
   float* rec = smem;                          // [3][16*RF]
   float* hpb = rec + FWD_SLOTS * RING;        // [3][4][16][16]
   floatx4* mkb = reinterpret_cast<floatx4*>(hpb + FWD_HP);   // [3][2][256] dropout multipliers of layers 1..8
+  float* lps = hpb + FWD_HP + FWD_SLOTS * 8 * 256;            // RAW: the helpers' log-det constant partials [4]
+  float* hs = lps + 4;                                        // RAW: h of the 16 rows [16][raw_hs_pitch(C)]
   using AR = ActRec<NH>;
   static_assert(NH <= 8, "two float4 of dropout multipliers");
   const int nb = L.nb;
@@ -1190,6 +1373,10 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
   if (DROP) { seed = rng[0]; off = rng[1]; }
   // diagnostic build: per-phase cycles of workgroup 0's wave 0 (compute) and wave 4 (helper) -> g_phase[8..]
   unsigned long long ph_t = BCNF_STAMPS ? __builtin_amdgcn_s_memtime() : 0ULL, ph_acc[3] = {0, 0, 0};
+  const unsigned long long ph_t0 = ph_t;
+  unsigned long long ph_b[2] = {0, 0};   // RAW prologue: cycles from the start to barrier #0 / #1 arrival
+#define PHB(i)                                                 \
+  if (BCNF_STAMPS) ph_b[i] = __builtin_amdgcn_s_memtime() - ph_t0;
 #define PHF(i)                                                                                   \
   if (BCNF_STAMPS) {                                                                             \
     const unsigned long long _t = __builtin_amdgcn_s_memtime();                                  \
@@ -1200,6 +1387,219 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
   if (helper) {
     const int hw = __builtin_amdgcn_readfirstlane(t8 >> 6);
     const int l64 = t8 & 63, lr = l64 & 15, lq = l64 >> 4;
+    if constexpr (RAW) {
+      const int Da = L.Da, C = L.C, X = R.X, H1 = L.H[1], D = L.D, an = L.an_size;
+      const int nt = (C + 15) >> 4;                               // 16-column tiles of h (<= 4 RAW_TPW)
+      const long long row = (long long)blockIdx.x * 16 + lr;
+      const float* xrow = R.xpool + raw_row(R, B, row < B ? row : B - 1) * R.ldx;
+      // ---- prologue loads, all issued before any of them is consumed ----
+      uint32_t srcb[RAW_NP + RAW_NQ], dstb[RAW_NP + RAW_NQ];      // byte offsets: source, word of the ring slot
+#pragma unroll
+      for (int i = 0; i < RAW_NP + RAW_NQ; ++i) {
+        const uint32_t t = R.table[i * BCNF_WG + t8];
+        srcb[i] = (t >> 12) * 4u;
+        dstb[i] = (t & 4095u) * 4u;
+      }
+      uint32_t zw[RAW_NZ];
+#pragma unroll
+      for (int i = 0; i < RAW_NZ; ++i) zw[i] = R.table[(RAW_NP + RAW_NQ + i) * BCNF_WG + t8] & 4095u;
+      // side units of this workgroup (RawSide): backward-record chunks u < nb * ch, then W1hR rows
+      const int rb16 = 16 * L.RB, ch = (rb16 + BCNF_WG - 1) / BCNF_WG, n_units = nb * ch + L.NKp;
+      const uint32_t* tpb = R.table + RAW_NS * BCNF_WG;
+      uint32_t pbe[RAW_SIDE_Q];                                   // (the unit checks happen at the use)
+#pragma unroll
+      for (int q = 0; q < RAW_SIDE_Q; ++q) {
+        const int u = blockIdx.x + q * gridDim.x, n = (u % ch) * BCNF_WG + t8;
+        pbe[q] = tpb[n < rb16 ? n : 0];
+      }
+      // projection B operand of block k: W1_k[lr][Da + 16 ct + 4 lq + r], r = 0..3 one (dword-aligned) 16-byte load
+      // per tile (at most 3 floats past the row end: still inside the block's parameters), zero past C or H[1]
+      int wo[RAW_TPW];
+      uint32_t wok = 0;
+#pragma unroll
+      for (int i = 0; i < RAW_TPW; ++i) {
+        const int c0 = 16 * (hw + 4 * i) + 4 * lq;
+        wo[i] = (c0 < C && lr < H1) ? L.lin_w[1] + lr * L.lin_in[1] + Da + c0 : 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wok |= (c0 + r < C && lr < H1) ? 1u << (4 * i + r) : 0u;
+      }
+      const bool bias_lane = hw == 0 && lr < H1;
+      struct Pre {                                                // one block's loaded operands
+        float v[RAW_NP + RAW_NQ];
+        floatx4 w4[RAW_TPW];
+        float bias;
+      };
+      // buffer loads: the block base goes in the scalar offset, the table's byte offset in the vector offset (no
+      // per-lane 64-bit address arithmetic, which otherwise stays live across the loop)
+      const __amdgpu_buffer_rsrc_t rP = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(R.P), (short)0,
+                                                                         (int)(L.n_trainable * 4), 0x00020000);
+      const __amdgpu_buffer_rsrc_t rQ = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(R.Q), (short)0,
+                                                                         (nb - 1) * D * D * 4, 0x00020000);
+      auto load = [&](int k, Pre& g) {
+        const int cb = coupling_base(L, k);
+        if (k < nb - 1) {
+          const int sp = k * L.blk_stride * 4, sq = k * D * D * 4;
+#pragma unroll
+          for (int i = 0; i < RAW_NP; ++i)
+            g.v[i] = (BCNF_RAW_EXP & 4) ? 0.f : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rP, srcb[i], sp, 0));
+#pragma unroll
+          for (int i = RAW_NP; i < RAW_NP + RAW_NQ; ++i)
+            g.v[i] = (BCNF_RAW_EXP & 4) ? 0.f : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rQ, srcb[i], sq, 0));
+        } else {
+          // the last block (rec_f with k = nb - 1): its coupling sits an_size floats earlier in its block (no
+          // ActNorm), whose entries become scale 1 / bias 0; the mix is the identity (Q entry at i (D + 1))
+          const int sp = (k * L.blk_stride - an) * 4;
+#pragma unroll
+          for (int i = 0; i < RAW_NP; ++i) {
+            const uint32_t src = srcb[i] >> 2;
+            const float x = __uint_as_float(
+                __builtin_amdgcn_raw_buffer_load_b32(rP, (int)src < an ? 4u * an : srcb[i], sp, 0));
+            g.v[i] = (int)src < an ? ((int)src < D ? 1.f : 0.f) : x;
+          }
+#pragma unroll
+          for (int i = RAW_NP; i < RAW_NP + RAW_NQ; ++i)
+            g.v[i] = ((srcb[i] >> 2) % (uint32_t)(D + 1)) == 0 ? 1.f : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < RAW_TPW; ++i) {
+          if (hw + 4 * i < nt) {
+            const auto w = __builtin_amdgcn_raw_buffer_load_b128(rP, wo[i] * 4, cb * 4, 0);
+            g.w4[i] = floatx4{__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]), __uint_as_float(w[3])};
+          } else {
+            g.w4[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+          }
+        }
+        // raw: the select waits for the load, so it happens at the use (finish_proj), not here
+        g.bias = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rP, (L.lin_b[1] + lr) * 4, cb * 4, 0));
+      };
+      float xa[RAW_TPW][4];                                       // h[row lr][16 (hw + 4 i) + 4 lq + r]
+      // block k -> slot sl (a constant after unrolling): dropout multipliers and record (no h needed), then the
+      // projection partial
+      auto finish_rec = [&](int k, int sl, const Pre& g) {
+        if (DROP) {
+          const uint32_t bits = dropout_bits(L, seed, off, bc, k, j, 0u);
+          float m[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) m[i] = ((bits >> i) & 1u) ? L.keep_scale : 0.f;
+          mkb[(2 * sl) * BCNF_WG + t8] = floatx4{m[0], m[1], m[2], m[3]};
+          mkb[(2 * sl + 1) * BCNF_WG + t8] = floatx4{m[4], m[5], m[6], m[7]};
+        }
+        char* slot = reinterpret_cast<char*>(rec + sl * RING);
+#pragma unroll
+        for (int i = 0; i < RAW_NP + RAW_NQ; ++i) *reinterpret_cast<float*>(slot + dstb[i]) = g.v[i];
+      };
+      auto finish_proj = [&](int sl, const Pre& g) {
+        const float bias = bias_lane ? g.bias : 0.f;
+        floatx4 acc = {bias, bias, bias, bias};
+#pragma unroll
+        for (int i = 0; i < RAW_TPW; ++i)
+          if (hw + 4 * i < nt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              acc = mfma4(xa[i][r], ((wok >> (4 * i + r)) & 1u) ? g.w4[i][r] : 0.f, acc);
+        float* hd = hpb + sl * 1024 + hw * 256 + 64 * lq + lr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hd[16 * r] = acc[r];
+      };
+      auto finish = [&](int k, int sl, const Pre& g) {
+        finish_rec(k, sl, g);
+        finish_proj(sl, g);
+      };
+      Pre g0, g1, gn;
+      load(0, g0);
+      load(1, g1);                                                // nb >= 2 (build_raw_table)
+      if (nb > 2) load(2, gn);                                    // software pipeline: see interval()
+#pragma unroll
+      for (int i = 0; i < RAW_NZ; ++i)                            // this thread's zero words, in all three slots
+#pragma unroll
+        for (int sl = 0; sl < FWD_SLOTS; ++sl) rec[sl * RING + zw[i]] = 0.f;
+      finish_rec(0, 0, g0);
+      finish_rec(1, 1, g1);
+      PHB(0)
+      __syncthreads();                                            // the compute waves' h tile is in hs
+#pragma unroll
+      for (int i = 0; i < RAW_TPW; ++i) {
+        const floatx4 v = *reinterpret_cast<const floatx4*>(hs + lr * raw_hs_pitch(C) + 16 * (hw + 4 * i) + 4 * lq);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xa[i][r] = v[r];
+      }
+      finish_proj(0, g0);
+      finish_proj(1, g1);
+      // ---- side work: the backward kernels' inputs, one unit per workgroup and q (coalesced rows) ----
+      auto side_unit = [&](int u, uint32_t e) {
+        if (u < nb * ch) {
+          const int k = u / ch, n = (u - k * ch) * BCNF_WG + t8;
+          if (n >= rb16) return;
+          const uint32_t kind = e & 3u, src = e >> 2;
+          float v = 0.f;
+          if (k < nb - 1) {
+            if (kind == 0) v = R.P[(long long)k * L.blk_stride + src];
+            else if (kind == 1) v = R.Q[(long long)k * D * D + src];
+          } else if (kind == 0) {
+            v = (int)src < an ? ((int)src < D ? 1.f : 0.f) : R.P[(long long)k * L.blk_stride - an + src];
+          } else if (kind == 1) {
+            v = (src % (uint32_t)(D + 1)) == 0 ? 1.f : 0.f;
+          }
+          R.pk[L.pb_off + (long long)k * rb16 + n] = v;
+        } else if (u < n_units) {
+          const int kj = u - nb * ch, k = kj >> 4, jj = kj & 15;
+          const bool live = k < nb && jj < H1;
+          const float* w = live ? R.P + coupling_base(L, k) + L.lin_w[1] + jj * L.lin_in[1] + Da : R.P;
+          for (int c = t8; c < L.Cp; c += BCNF_WG) R.pk[L.w1r_off + (long long)kj * L.Cp + c] = (live && c < C) ? w[c] : 0.f;
+        }
+      };
+      // intervals k < nb - 2 prepare block k + 2 into slot (k + 2) % 3 (unrolled by 3: constant LDS offsets); the
+      // last two intervals have no block to prepare and take the side work: this workgroup's units (k = nb - 2) and
+      // the log-det constant into lps for the compute epilogue (k = nb - 1)
+      // software-pipelined: block k + 3's operands are loaded in interval k and consumed in interval k + 1, so an
+      // interval never waits for its own loads
+      PHB(1)
+      auto interval = [&](int k, int sl) {
+        const Pre g = gn;
+        if (k + 3 < nb) load(k + 3, gn);
+        finish(k + 2, sl, g);
+        PHF(1)
+        // LDS writes complete, then a bare barrier: __syncthreads' release fence would also wait for the loads of
+        // block k + 3 still in flight (vmcnt counts them too)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        PHF(2)
+      };
+      __syncthreads();
+      PHF(0)
+      for (int k = 0; k < nb - 2; k += FWD_SLOTS) {
+        interval(k, 2);
+        if (k + 1 < nb - 2) interval(k + 1, 0);
+        if (k + 2 < nb - 2) interval(k + 2, 1);
+      }
+      if (!(BCNF_RAW_EXP & 1)) {
+#pragma unroll
+        for (int q = 0; q < RAW_SIDE_Q; ++q) side_unit(blockIdx.x + q * gridDim.x, pbe[q]);
+      }
+      {  // the ActNorm log-det constant  sum_k sum_i log|scale_k,i|  (cnf.py:350): strided partials (loads issued
+         // together), a fixed-order butterfly per wave, lps[hw] for the compute epilogue after the last barrier
+        constexpr int LU = 4;
+        float acc = 0.f;
+        const int n = (BCNF_RAW_EXP & 8) ? 0 : (nb - 1) * D;
+        for (int i0 = t8; i0 < n; i0 += LU * BCNF_WG) {
+          float v[LU];
+#pragma unroll
+          for (int u = 0; u < LU; ++u) {
+            const int i = i0 + u * BCNF_WG, ii = i < n ? i : 0, kb = ii / D;
+            v[u] = R.P[(long long)kb * L.blk_stride + (ii - kb * D)];
+          }
+#pragma unroll
+          for (int u = 0; u < LU; ++u)
+            if (i0 + u * BCNF_WG < n) acc += logf(fabsf(v[u]));
+        }
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) acc += __shfl_xor(acc, m);
+        if (l64 == 0) lps[hw] = acc;
+      }
+      __syncthreads();                                            // interval nb - 2
+      __syncthreads();                                            // interval nb - 1
+      for (int u = blockIdx.x + RAW_SIDE_Q * gridDim.x; u < n_units; u += gridDim.x)   // small grids only
+        side_unit(u, u < nb * ch ? tpb[(u % ch) * BCNF_WG + t8 < rb16 ? (u % ch) * BCNF_WG + t8 : 0] : 0u);
+    } else {
     const int S = P.Cp >> 4;                                     // K-steps per helper wave
     const long long row = (long long)blockIdx.x * 16 + lr;
     const float* hrow = P.h + (row < B ? row : B - 1) * P.ldh;
@@ -1247,15 +1647,97 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
       __syncthreads();
       PHF(2)
     }
+    }
   } else {
     const int tid = t8;
 #ifdef BCNF_PRIO_F
     __builtin_amdgcn_s_setprio(BCNF_PRIO_F);
 #endif
     const int D = L.D, Da = L.Da, Db = L.Db;
-    float ya = (j < Da) ? y[bc * D + j] : 0.f;
-    float yb = (j < Db) ? y[bc * D + Da + j] : 0.f;
-    const float ldc = pk[L.ldc_off];
+    float ya, yb, ldc = 0.f;
+    if constexpr (RAW) {
+      // every load of the prologue is issued before the first use of any (one round trip after the row index):
+      // y, x, Wf and bf, then an empty asm with a memory clobber so none of them sinks into a consumer's branch
+      const long long src = raw_row(R, B, bc);
+      ya = (j < Da) ? R.ypool[src * D + j] : 0.f;
+      yb = (j < Db) ? R.ypool[src * D + Da + j] : 0.f;
+      // h^T = Wf x^T + bf of the workgroup's 16 rows on the matrix cores, compute wave cw taking the column tiles
+      // ct = cw + 4 i, which helper wave cw reads back in the MFMA output layout (h[row lr][16 ct + 4 lq + r] at
+      // lane (lr, lq)) as its projection A operand. ldc: the helpers' wave sums of the ActNorm log-det constant
+      // (lps), read after the last barrier.
+      const int cw = __builtin_amdgcn_readfirstlane(tid >> 6), l64 = tid & 63, lr = l64 & 15, lq = l64 >> 4;
+      const int C = L.C, X = R.X;
+      const long long row = (long long)blockIdx.x * 16 + lr;
+      const float* xrow = R.xpool + raw_row(R, B, row < B ? row : B - 1) * R.ldx;
+      float xb[RAW_XS];                                           // B operand: x[row lr][4 u + lq]
+#pragma unroll
+      for (int u = 0; u < RAW_XS; ++u) {
+        const int kx = 4 * u + lq;
+        xb[u] = (BCNF_RAW_EXP & 16) ? 1.f : xrow[kx < X ? kx : 0];
+      }
+      float wa[RAW_TPW][RAW_XS];                                  // A operand: Wf[16 ct + lr][4 u + lq]
+      float hb[RAW_TPW][4];                                       // bf of the columns this lane ends with
+      const float* bfp = R.bf ? R.bf : R.wf;
+#pragma unroll
+      for (int i = 0; i < RAW_TPW; ++i) {
+        const int c = 16 * (cw + 4 * i) + lr;
+        const float* wrow = R.wf + (long long)(c < C ? c : 0) * X;
+#pragma unroll
+        for (int u = 0; u < RAW_XS; ++u) {
+          const int kx = 4 * u + lq;
+          wa[i][u] = (BCNF_RAW_EXP & 32) ? 1.f : wrow[kx < X ? kx : 0];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int cc = 16 * (cw + 4 * i) + 4 * lq + r;
+          hb[i][r] = (BCNF_RAW_EXP & 32) ? 1.f : bfp[cc < C ? cc : 0];
+        }
+      }
+      asm volatile("" ::: "memory");
+      // independent accumulation chains (tile i, parity of u), summed in a fixed order
+      floatx4 acc[RAW_TPW][2];
+#pragma unroll
+      for (int i = 0; i < RAW_TPW; ++i) acc[i][0] = acc[i][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < RAW_XS; ++u) {
+        const float xv = (4 * u + lq < X) ? xb[u] : 0.f;
+#pragma unroll
+        for (int i = 0; i < RAW_TPW; ++i)
+          if (!(BCNF_RAW_EXP & 2) && 16 * (cw + 4 * i) < C && 4 * u < X)
+            acc[i][u & 1] = mfma4(wa[i][u], xv, acc[i][u & 1]);
+      }
+#pragma unroll
+      for (int i = 0; i < RAW_TPW; ++i) {
+        const int ct = cw + 4 * i;
+        if (16 * ct < C) {                                        // uniform
+          floatx4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int cc = 16 * ct + 4 * lq + r;
+            o[r] = cc < C ? (acc[i][0][r] + acc[i][1][r]) + (R.bf ? hb[i][r] : 0.f) : 0.f;
+          }
+          *reinterpret_cast<floatx4*>(hs + lr * raw_hs_pitch(C) + 16 * ct + 4 * lq) = o;
+        }
+      }
+      PHB(0)
+      __syncthreads();                                            // hs complete
+      PHB(1)
+      // the gathered rows for the backward: y by every compute lane, x by wave 0 from the B operand it holds
+      // (columns < X; the padding columns past X are never read)
+      if (R.ydst && b < B) {
+        if (j < Da) R.ydst[b * D + j] = ya;
+        if (j < Db) R.ydst[b * D + Da + j] = yb;
+      }
+      if (R.xdst && cw == 0 && row < B) {
+#pragma unroll
+        for (int u = 0; u < RAW_XS; ++u)
+          if (4 * u + lq < X) R.xdst[row * R.ldx + 4 * u + lq] = xb[u];
+      }
+    } else {
+      ya = (j < Da) ? y[bc * D + j] : 0.f;
+      yb = (j < Db) ? y[bc * D + Da + j] : 0.f;
+      ldc = pk[L.ldc_off];
+    }
     __syncthreads();
     // block k + 1's head: record floats [0, FWD_HEAD), the four projection partials, the dropout multipliers
     float hd[FWD_HEAD], hq4[4];
@@ -1312,6 +1794,7 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
       asm volatile("s_barrier" ::: "memory");
       PHF(2)
     }
+    if constexpr (RAW) ldc = ((lps[0] + lps[1]) + lps[2]) + lps[3];
     const float ltot = row_sum16(ldj) + ldc;
     const float q2 = row_sum16(ya * ya + yb * yb);
     if (j < Da) z[bc * D + j] = ya;
@@ -1322,9 +1805,13 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
   }
 #if BCNF_STAMPS
   if (SAVE && blockIdx.x == 0 && (threadIdx.x == 0 || threadIdx.x == BCNF_WG))
+  {
     for (int i = 0; i < 3; ++i) g_phase[8 + (helper ? 4 : 0) + i] = ph_acc[i];
+    g_phase[helper ? 15 : 11] = (ph_b[1] << 32) | (ph_b[0] & 0xffffffffULL);   // slots 3 / 7 belong to the backward
+  }
 #endif
 #undef PHF
+#undef PHB
   if (nll_part) {   // per-workgroup partial of inn_nll_loss (utils.py:40-46); reduced by nll_finalize
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2185,22 +2672,26 @@ int launch_hp(const BcnfLayout& L, const float* pk, const float* h, long long R,
 template <int NH>
 int fwd_dispatch(const BcnfLayout& L, const float* pk, const float* y, const ProjArgs& P, long long B, float* z,
                  float* ldj, float* logp, bool drop, const uint64_t* rng, float* arec, const NllOut& no,
-                 hipStream_t st) {
+                 hipStream_t st, const RawArgs* raw = nullptr) {
   if (!layout_matches<NH>(L)) return BCNF_ERR_ARG;
   if (P.Cp % 16 != 0 || P.Cp / 16 > HP_SMAX || P.C > P.Cp) return BCNF_ERR_UNSUPPORTED;
   const dim3 grid((unsigned)((B + 15) / 16));
-  size_t lds = fwd2_lds_bytes(L);
+  size_t lds = fwd2_lds_bytes(L, raw != nullptr);
   const bool save = arec != nullptr;
+  const RawArgs R = raw ? *raw : RawArgs{};
   int rc;
-#define BCNF_FWD(DR, SV)                                                                                    \
-  rc = launch_lds(k_forward<NH, DR, SV>, lds);                                                              \
-  if (rc) return rc;                                                                                        \
-  hipLaunchKernelGGL((k_forward<NH, DR, SV>), grid, dim3(2 * BCNF_WG), lds, st, L, pk, y, P, B, z, ldj, logp, \
-                     rng, arec, no.part);
-  if (drop) {
-    if (save) { BCNF_FWD(true, true) } else { BCNF_FWD(true, false) }
+#define BCNF_FWD(DR, SV, RW)                                                                                   \
+  rc = launch_lds(k_forward<NH, DR, SV, RW>, lds);                                                             \
+  if (rc) return rc;                                                                                           \
+  hipLaunchKernelGGL((k_forward<NH, DR, SV, RW>), grid, dim3(2 * BCNF_WG), lds, st, L, pk, y, P, B, z, ldj, logp, \
+                     rng, arec, no.part, R);
+  if (raw) {
+    if (!save) return BCNF_ERR_ARG;
+    if (drop) { BCNF_FWD(true, true, true) } else { BCNF_FWD(false, true, true) }
+  } else if (drop) {
+    if (save) { BCNF_FWD(true, true, false) } else { BCNF_FWD(true, false, false) }
   } else {
-    if (save) { BCNF_FWD(false, true) } else { BCNF_FWD(false, false) }
+    if (save) { BCNF_FWD(false, true, false) } else { BCNF_FWD(false, false, false) }
   }
 #undef BCNF_FWD
   return check_launch();
@@ -2274,7 +2765,7 @@ long long ws_floats(const BcnfLayout& L, long long B, bool drop) {
 int forward_impl(const BcnfStackDesc* desc, const void* packed, const float* y, const float* h, int64_t batch,
                  float* z, float* ldj, float* log_prob, int32_t training, const uint64_t* rng_state, void* workspace,
                  bool save, bool nll, bool finalize, float* loss_out, int32_t* guard, void* stream,
-                 const float* fold = nullptr, int X = 0, int ldx = 0) {
+                 const float* fold = nullptr, int X = 0, int ldx = 0, const RawArgs* raw = nullptr) {
   BcnfLayout L;
   int rc = make_layout(desc, &L);
   if (rc) return rc;
@@ -2297,7 +2788,7 @@ int forward_impl(const BcnfStackDesc* desc, const void* packed, const float* y, 
   const float* pbase = fold ? fold : pk;
   const ProjArgs P{h, pbase + Lp.w1c_off, pbase + Lp.b1c_off, (long long)Lp.ldh, Lp.C, Lp.Cp, Lp.NKp};
   switch (L.NH) {
-#define BCNF_CASE(N) case N: rc = fwd_dispatch<N>(L, pk, y, P, batch, z, ldj, log_prob, drop, rng_state, arec, no, st); break;
+#define BCNF_CASE(N) case N: rc = fwd_dispatch<N>(L, pk, y, P, batch, z, ldj, log_prob, drop, rng_state, arec, no, st, raw); break;
     BCNF_CASE(1) BCNF_CASE(2) BCNF_CASE(3) BCNF_CASE(4) BCNF_CASE(5) BCNF_CASE(6) BCNF_CASE(7) BCNF_CASE(8)
 #undef BCNF_CASE
     default: return BCNF_ERR_UNSUPPORTED;
@@ -2466,6 +2957,10 @@ int fold_setup(const BcnfStackDesc* desc, int32_t X, BcnfLayout* L) {
   return BCNF_OK;
 }
 long long fold_floats(const BcnfLayout& L, int X) { return (long long)(fold_xp(X) + 1) * L.NKp; }
+// The pack-free forward's shape limits (its table must also build: build_raw_table).
+bool raw_applicable(const BcnfLayout& L, int X) {
+  return X <= 4 * RAW_XS && L.C <= 64 * RAW_TPW && L.nb >= 2 && L.act_norm;
+}
 }  // namespace
 
 int bcnf_fold_bytes(const BcnfStackDesc* desc, int32_t in_features, int64_t* bytes) {
@@ -2522,6 +3017,67 @@ int bcnf_fold_nll_forward(const BcnfStackDesc* desc, const void* packed, const f
   if (!fold || ldx < in_features) return BCNF_ERR_ARG;
   return forward_impl(desc, packed, y, x, batch, z, ldj, nullptr, training, rng_state, workspace, true, true,
                       finalize != 0, loss_out, guard, stream, fold, in_features, ldx);
+}
+
+int bcnf_fold_raw_table_bytes(const BcnfStackDesc* desc, int32_t in_features, int64_t* bytes) {
+  BcnfLayout L;
+  const int rc = fold_setup(desc, in_features, &L);
+  if (rc) return rc;
+  if (!bytes) return BCNF_ERR_ARG;
+  if (!raw_applicable(L, in_features)) return BCNF_ERR_UNSUPPORTED;
+  std::vector<uint32_t> t((size_t)raw_table_words(L));
+  if (!build_raw_table(L, t.data())) return BCNF_ERR_UNSUPPORTED;
+  *bytes = (int64_t)t.size() * (int64_t)sizeof(uint32_t);
+  return BCNF_OK;
+}
+
+int bcnf_fold_raw_table(const BcnfStackDesc* desc, int32_t in_features, void* host_table) {
+  BcnfLayout L;
+  const int rc = fold_setup(desc, in_features, &L);
+  if (rc) return rc;
+  if (!host_table) return BCNF_ERR_ARG;
+  if (!raw_applicable(L, in_features)) return BCNF_ERR_UNSUPPORTED;
+  return build_raw_table(L, (uint32_t*)host_table) ? BCNF_OK : BCNF_ERR_UNSUPPORTED;
+}
+
+int bcnf_fold_train_forward(const BcnfStackDesc* desc, const float* params, const float* qmats, const void* table,
+                            const float* feat_weight, const float* feat_bias, int32_t in_features,
+                            const BcnfGather2* gather, const float* y, const float* x, int32_t ldx, int64_t batch,
+                            void* packed, float* z, float* ldj, int32_t training, uint64_t* rng_state,
+                            void* workspace, int32_t finalize, float* loss_out, int32_t* guard, void* stream) {
+  BcnfLayout L;
+  const int rc = fold_setup(desc, in_features, &L);
+  if (rc) return rc;
+  if (!raw_applicable(L, in_features)) return BCNF_ERR_UNSUPPORTED;
+  if (!params || !qmats || !table || !feat_weight || !packed || batch < 1) return BCNF_ERR_ARG;
+  RawArgs R = {};
+  R.P = params;
+  R.Q = qmats;
+  R.table = (const uint32_t*)table;
+  R.wf = feat_weight;
+  R.bf = feat_bias;
+  R.pk = (float*)packed;
+  R.X = in_features;
+  if (gather) {
+    const BcnfGather2& g = *gather;
+    if (g.n != batch || g.cols0 != L.D || g.cols1 < in_features || !g.idx || !g.src0 || !g.src1 || !g.dst0 ||
+        !g.dst1)
+      return BCNF_ERR_ARG;
+    R.idx = g.idx;
+    R.cursor = (const long long*)g.cursor;
+    R.ypool = g.src0;
+    R.ydst = g.dst0;
+    R.xpool = g.src1;
+    R.xdst = g.dst1;
+    R.ldx = g.cols1;
+  } else {
+    if (!y || !x || ldx < in_features) return BCNF_ERR_ARG;
+    R.ypool = y;
+    R.xpool = x;
+    R.ldx = ldx;
+  }
+  return forward_impl(desc, packed, R.ypool, R.xpool, batch, z, ldj, nullptr, training, rng_state, workspace, true,
+                      true, finalize != 0, loss_out, guard, stream, nullptr, 0, 0, &R);
 }
 
 int bcnf_fold_backward_tail(const BcnfStackDesc* desc, const void* packed, const void* slab, const float* x,

@@ -16,6 +16,7 @@ per-layer `.grad` tensors as views of that flat gradient.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import torch
@@ -106,6 +107,7 @@ class FusedStack:
             off += p.numel()
         self._packed = None
         self._rng_state = None
+        self._raw_tables = {}
 
     def _on_flat_grad(self, fp):
         if self.grad_mode != "per_param" or fp.grad is None:
@@ -334,10 +336,37 @@ class FusedStack:
         out = ctypes.c_int64(0)
         return N.lib().bcnf_fold_bytes(self._pdesc, ctypes.c_int32(int(in_features)), ctypes.byref(out)) == N.OK
 
+    # bcnf_fold_train_forward (the pack-free folded forward, one launch) where its table applies; False: always the
+    # two-launch form (pack + fold, then the forward) -- BCNF_FOLD_RAW=0 in the environment, for A/B runs
+    use_raw_forward = os.environ.get("BCNF_FOLD_RAW", "1") != "0"
+
+    def raw_table(self, X: int):
+        """The device copy of bcnf_fold_raw_table for in_features X (built once per device), or None where the
+        pack-free forward does not apply (or the library predates it)."""
+        if not self.use_raw_forward or not hasattr(N.lib(), "bcnf_fold_train_forward"):
+            return None
+        dev = self.flat.device
+        key = (X, str(dev))
+        if key not in self._raw_tables:
+            if torch.cuda.is_current_stream_capturing():
+                return None                     # no host -> device copy inside a graph capture
+            L = N.lib()
+            nb = ctypes.c_int64(0)
+            if L.bcnf_fold_raw_table_bytes(self._pdesc, ctypes.c_int32(X), ctypes.byref(nb)) != N.OK:
+                self._raw_tables[key] = None
+            else:
+                host = torch.empty(nb.value // 4, dtype=torch.int32)
+                N.check(L.bcnf_fold_raw_table(self._pdesc, ctypes.c_int32(X), ctypes.c_void_p(host.data_ptr())),
+                        "bcnf_fold_raw_table")
+                self._raw_tables[key] = host.to(dev)
+        return self._raw_tables[key]
+
     def launch_fold_nll_forward(self, y, x, wf, bf, training: bool, finalize: bool = True, gather=None):
-        """launch_nll_forward with h = x Wf^T + bf never formed: the pack launch also folds the Linear into
-        the projection weights (Wc = W1h Wf, bc = b1 + W1h bf) and the projection runs on x. gather (an
-        N.BcnfGather2 that fills y and x): the batch gather runs inside the pack launch."""
+        """launch_nll_forward with h = x Wf^T + bf never formed as a tensor. Pack-free form (raw_table applies):
+        ONE launch, bcnf_fold_train_forward, builds its records from the parameters and computes h of its rows
+        on the fly. Otherwise the pack launch also folds the Linear into the projection weights (Wc = W1h Wf,
+        bc = b1 + W1h bf) and the projection runs on x. gather (an N.BcnfGather2 that fills y and x): the batch
+        gather runs inside the first launch."""
         self._check_device(y, x, wf, bf)
         B, X = x.shape
         if y.dim() != 2 or y.shape != (B, self.cfg.size):
@@ -348,6 +377,23 @@ class FusedStack:
         dev = y.device
         stream = N.stream_handle(dev)
         pk = torch.empty(N.query_i64(L.bcnf_packed_bytes, self._pdesc) // 4, dtype=torch.float32, device=dev)
+        table = self.raw_table(X)
+        if table is not None:
+            z = torch.empty_like(y)
+            ldj = torch.empty(B, dtype=torch.float32, device=dev)
+            vals = torch.empty(3, dtype=torch.float32, device=dev)
+            rng = self.rng_state() if (training and self.cfg.dropout > 0.0) else None
+            wb, _ = self.workspace_bytes(B, training)
+            ws = torch.empty(max(wb // 4, 1), dtype=torch.float32, device=dev)
+            rc = L.bcnf_fold_train_forward(self._pdesc, N.ptr(self.flat), N.ptr(self.qflat), N.ptr(table), N.ptr(wf),
+                                           N.ptr(bf), ctypes.c_int32(X),
+                                           None if gather is None else ctypes.byref(gather), N.ptr(y), N.ptr(x),
+                                           ctypes.c_int32(x.stride(0)), ctypes.c_int64(B), N.ptr(pk), N.ptr(z),
+                                           N.ptr(ldj), ctypes.c_int32(int(training)), N.ptr(rng), N.ptr(ws),
+                                           ctypes.c_int32(int(finalize)), N.ptr(vals),
+                                           N.ptr(self.guard if finalize else None), stream)
+            N.check(rc, "bcnf_fold_train_forward")
+            return z, ldj, vals, (ws, pk)
         fold = torch.empty(N.query_i64(L.bcnf_fold_bytes, self._pdesc, ctypes.c_int32(X)) // 4, dtype=torch.float32,
                            device=dev)
         N.check(L.bcnf_pack_params_fold(self._pdesc, N.ptr(self.flat), N.ptr(self.qflat), N.ptr(wf), N.ptr(bf),
@@ -476,6 +522,7 @@ class FusedStack:
         dwf, dbf = torch.empty_like(wf), (torch.empty_like(bf) if bf is not None else None)
         ldj = torch.empty(B, dtype=torch.float32, device=dev)
         rng = self.rng_state() if (training and self.cfg.dropout > 0.0) else None
+        table = self.raw_table(X)
         calls = {
             "k_pack_fold": lambda: L.bcnf_pack_params_fold(self._pdesc, N.ptr(self.flat), N.ptr(self.qflat), N.ptr(wf),
                                                     N.ptr(bf), ctypes.c_int32(X), N.ptr(pk), N.ptr(fold), None, stream),
@@ -491,6 +538,12 @@ class FusedStack:
                                                       ctypes.c_int64(B), ctypes.c_int32(int(training)),
                                                       N.ptr(dparams), N.ptr(dwf), N.ptr(dbf), None, stream),
         }
+        if table is not None:           # the pack-free forward: no pack launch
+            del calls["k_pack_fold"]
+            calls["k_forward"] = lambda: L.bcnf_fold_train_forward(
+                self._pdesc, N.ptr(self.flat), N.ptr(self.qflat), N.ptr(table), N.ptr(wf), N.ptr(bf), ctypes.c_int32(X),
+                None, N.ptr(y), N.ptr(x), ldx, ctypes.c_int64(B), N.ptr(pk), N.ptr(z), N.ptr(ldj),
+                ctypes.c_int32(int(training)), N.ptr(rng), N.ptr(ws), ctypes.c_int32(0), N.ptr(vals), None, stream)
         return self._event_times(calls, iters)
 
     def launch_inverse(self, z, h, cond_index=None, training: bool = False):

@@ -168,6 +168,24 @@ int bcnf_fold_nll_forward(const BcnfStackDesc* desc, const void* packed, const f
                           int32_t training,
                           uint64_t* rng_state, void* workspace, int32_t finalize, float* loss_out, int32_t* guard,
                           void* stream);
+/* Pack-free folded training forward: bcnf_pack_params_fold + bcnf_fold_nll_forward in ONE launch. The
+ * forward builds its records from `params` / `qmats` through a per-layout table (bcnf_fold_raw_table, built once on
+ * the host and copied to the device by the caller), computes h = x Wf^T + bf of its rows on the matrix cores and the
+ * condition projection from h (the unfolded sums, so the loss rounds like bcnf_nll_forward on h rather than like the
+ * folded Wc), and writes into `packed` exactly what bcnf_nll_backward + bcnf_fold_backward_tail read (backward
+ * records, W1hR) -- `packed` serves that training pass only. gather (nullable): the rows come from the pools
+ * (src0 [*][D], src1 [*][cols1]; n == batch), y / x are then unused and the forward writes the gathered rows into
+ * dst0 / dst1 (ldx = cols1), as bcnf_pack_params_fold's gather did. BCNF_ERR_UNSUPPORTED where the table does not
+ * apply (no ActNorm, one block, X > 128) -- use the two-launch form there. bcnf_fold_raw_table_bytes: the table's
+ * size in bytes; bcnf_fold_raw_table fills `host_table` (host memory) with it. */
+int bcnf_fold_raw_table_bytes(const BcnfStackDesc* desc, int32_t in_features, int64_t* bytes);
+int bcnf_fold_raw_table(const BcnfStackDesc* desc, int32_t in_features, void* host_table);
+int bcnf_fold_train_forward(const BcnfStackDesc* desc, const float* params, const float* qmats, const void* table,
+                            const float* feat_weight, const float* feat_bias, int32_t in_features,
+                            const BcnfGather2* gather /* nullable */, const float* y, const float* x, int32_t ldx,
+                            int64_t batch, void* packed, float* z, float* ldj, int32_t training,
+                            uint64_t* rng_state, void* workspace, int32_t finalize, float* loss_out, int32_t* guard,
+                            void* stream);
 /* Adam fused into bcnf_fold_backward_tail (nullable argument): every gradient the tail produces -- the flat coupling
  * parameters (slot 0), the feature Linear's weight (1) and bias (2, NULL without bias) -- also takes its
  * torch.optim.Adam update where it is produced, with the end-of-step bookkeeping of bcnf_adam_step_bookkeep

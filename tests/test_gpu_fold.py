@@ -1,5 +1,5 @@
-"""GPU tests of the folded linear feature network (bcnf_pack_params_fold / bcnf_fold_nll_forward /
-bcnf_fold_backward_tail): model.nll_loss folds a single-Linear feature stack (trajectory_FC_small) into the
+"""GPU tests of the folded linear feature network (bcnf_fold_train_forward, or bcnf_pack_params_fold +
+bcnf_fold_nll_forward where its table does not apply, then bcnf_fold_backward_tail): model.nll_loss folds a single-Linear feature stack (trajectory_FC_small) into the
 condition projection. Oracle: the same model with the fold switched off (fold_features = False: feature
 Linear GEMM -> h -> projection -> dL/dh -> feature dW), itself pinned to the reference's golden fixture in
 test_gpu_train.py. The fold computes the same sums reassociated, so the gate is fp32 rounding: loss within
@@ -177,10 +177,12 @@ def test_trainstep_pads_fold_pool(g1):
     assert st2._cond_shape is None and st2._pool[1].shape == (64, 30, 3)
 
 
+@pytest.mark.parametrize("raw", [False, True])
 @pytest.mark.parametrize("epoch", [False, True])
-def test_gather_inside_pack_launch_is_exact(g1, epoch):
-    """The captured step's batch gather run inside the pack launch (BcnfGather2) == the separate gather launch:
-    logged values, parameters and gradients bit for bit (index buffer and epoch-cursor forms)."""
+def test_gather_inside_pack_launch_is_exact(g1, epoch, raw):
+    """The captured step's batch gather run inside the first launch (BcnfGather2: the pack launch, or the pack-free
+    forward, which reads the pool rows itself and writes the gathered rows for the backward) == the separate
+    gather launch: logged values, parameters and gradients bit for bit (index buffer and epoch-cursor forms)."""
     from bcnf_amd.train import TrainStep
     gen = torch.Generator().manual_seed(31)
     py = torch.randn(600, 19, generator=gen).to(DEV)
@@ -190,6 +192,7 @@ def test_gather_inside_pack_launch_is_exact(g1, epoch):
     for fuse in (False, True):
         m = _model(FC_SMALL_CFG, golden_sd(g1), train=True)
         m.fused.set_seed(3)
+        m.fused.use_raw_forward = raw
         st = TrainStep(m, lr=2e-4)
         st.fuse_gather = fuse
         st.epoch_unroll = 2
@@ -228,5 +231,55 @@ def test_fold_without_feature_bias(g1, train):
     (v1, g1_, w1), (v0, g0, w0) = out
     assert abs(v1[0].item() - v0[0].item()) <= 2e-6 * abs(v0[0].item()) + 1e-6
     for a, b, what in ((g1_, g0, "stack"), (w1, w0, "feature W")):
+        ok, err = close(a.cpu(), b.cpu(), rtol=1e-4, floor=1e-5)
+        assert ok, (what, err)
+
+
+def test_raw_forward_is_taken_for_fc_small(g1):
+    m = _model(FC_SMALL_CFG, golden_sd(g1))
+    assert m.fused.raw_table(90) is not None
+    assert m.fused.raw_table(200) is None                   # X > 128: the two-launch form
+    m.fused.use_raw_forward = False
+    assert m.fused.raw_table(90) is None
+
+
+@pytest.mark.parametrize("train", [False, True])
+@pytest.mark.parametrize("B", [1, 37, 4096])
+def test_raw_forward_equals_pack_forward(g1, B, train):
+    """The pack-free forward (records from the parameters, h of the workgroup's rows on the matrix cores) against the
+    two-launch form (pack + fold, projection on x with Wc): the same sums in a different association -- loss within
+    2e-6 relative, gradients within rtol 1e-4 -- and the same dropout stream."""
+    gen = torch.Generator().manual_seed(B + 1)
+    y = torch.randn(B, 19, generator=gen).to(DEV)
+    traj = torch.randn(B, 30, 3, generator=gen).to(DEV)
+    m = _model(FC_SMALL_CFG, golden_sd(g1), train=train)
+    res = []
+    for raw in (True, False):
+        m.fused.use_raw_forward = raw
+        res.append(_grads(m, y, traj, True, 4321))
+    (v1, g1_, w1, b1, r1), (v0, g0, w0, b0, r0) = res
+    assert r1 == r0
+    assert abs(v1[0].item() - v0[0].item()) <= 2e-6 * abs(v0[0].item()) + 1e-6
+    for a, b, what in ((g1_, g0, "stack"), (w1, w0, "feature W"), (b1, b0, "feature b")):
+        ok, err = close(a.cpu(), b.cpu(), rtol=1e-4, floor=1e-5)
+        assert ok, (what, err)
+
+
+@pytest.mark.parametrize("nb", [2, 3])
+def test_raw_forward_few_blocks(nb):
+    """nb = 2 (both records prepared before the first barrier; the last block's record through rec_f) and 3."""
+    cfg = _cfg((30, 3), 80, nb)
+    m = _model(cfg, train=True, seed=5)
+    assert m.fused.raw_table(90) is not None
+    gen = torch.Generator().manual_seed(3)
+    y = torch.randn(100, 19, generator=gen).to(DEV)
+    traj = torch.randn(100, 30, 3, generator=gen).to(DEV)
+    res = []
+    for raw in (True, False):
+        m.fused.use_raw_forward = raw
+        res.append(_grads(m, y, traj, True, 77))
+    (v1, g1_, w1, b1, _), (v0, g0, w0, b0, _) = res
+    assert abs(v1[0].item() - v0[0].item()) <= 2e-6 * abs(v0[0].item()) + 1e-6
+    for a, b, what in ((g1_, g0, "stack"), (w1, w0, "feature W"), (b1, b0, "feature b")):
         ok, err = close(a.cpu(), b.cpu(), rtol=1e-4, floor=1e-5)
         assert ok, (what, err)

@@ -220,3 +220,46 @@ def test_fold_adam_spec_host_logic():
     assert opt.fold_adam_spec((flat, w, None), counter=counter) is None       # b would not be updated
     other = torch.nn.Parameter(torch.zeros(2))
     assert opt.fold_adam_spec((flat, w, other), counter=counter) is None
+
+
+def test_fold_raw_table_partitions_the_record():
+    """bcnf_fold_raw_table (host): every float of a forward record's 16 lanes belongs to exactly one (thread, slot)
+    of the pack-free forward's table -- no two helper threads write the same LDS word -- with P-sourced offsets
+    inside one block's parameters (sorted: a wave reads consecutive parameters) and Q-sourced ones inside one D x D
+    matrix; the backward-record appendix holds one (source, kind) per word; shapes it cannot express are refused."""
+    import numpy as np
+    from bcnf_amd import _native as N
+    L = N.lib()
+    for nested, C, X in (([16] * 7, 80, 90), ([16, 8, 12], 13, 21), ([4], 40, 96)):
+        d = N.make_desc(19, nested, 32, C, 0.1, True)
+        nb = ctypes.c_int64(0)
+        assert L.bcnf_fold_raw_table_bytes(ctypes.byref(d), X, ctypes.byref(nb)) == N.OK
+        raw = np.zeros(nb.value // 4, dtype=np.uint32)
+        assert L.bcnf_fold_raw_table(ctypes.byref(d), X, ctypes.c_void_p(raw.ctypes.data)) == N.OK
+        t, pb = raw[:18 * 256].reshape(-1, 256), raw[18 * 256:]
+        dst, src = t & 4095, t >> 12
+        live = dst != 4095
+        words = dst[live]
+        assert len(np.unique(words)) == words.size                  # each word once
+        assert words.max() + 1 == words.size                        # ... and all of 0 .. 16 RF - 1
+        assert words.size % 16 == 0
+        n_tr = ctypes.c_int64(0)
+        assert L.bcnf_param_count(ctypes.byref(d), ctypes.byref(n_tr), None) == N.OK
+        p_src = src[:10][live[:10]]
+        assert p_src.max() < n_tr.value // 31                       # within one block's parameters
+        assert (np.diff(src[:10].reshape(-1)[live[:10].reshape(-1)].astype(np.int64)) > 0).all()   # sorted, distinct
+        assert src[10:12][live[10:12]].max() < 19 * 19
+        assert (src[12:][live[12:]] == 0).all()                     # zero words carry no source
+        kind = pb & 3
+        assert pb.size % 16 == 0 and set(np.unique(kind)) <= {0, 1, 2}
+        assert (pb[kind == 0] >> 2).max() < n_tr.value // 31
+        assert (pb[kind == 1] >> 2).max() < 19 * 19
+    nb = ctypes.c_int64(0)
+    no_an = N.make_desc(19, [16] * 7, 32, 80, 0.1, False)
+    assert L.bcnf_fold_raw_table_bytes(ctypes.byref(no_an), 90, ctypes.byref(nb)) == N.ERR_UNSUPPORTED
+    one = N.make_desc(19, [16] * 7, 1, 80, 0.1, True)
+    assert L.bcnf_fold_raw_table_bytes(ctypes.byref(one), 90, ctypes.byref(nb)) == N.ERR_UNSUPPORTED
+    fc = N.make_desc(19, [16] * 7, 32, 80, 0.1, True)
+    assert L.bcnf_fold_raw_table_bytes(ctypes.byref(fc), 97, ctypes.byref(nb)) == N.ERR_UNSUPPORTED
+    wide_c = N.make_desc(19, [16] * 7, 32, 129, 0.1, True)
+    assert L.bcnf_fold_raw_table_bytes(ctypes.byref(wide_c), 90, ctypes.byref(nb)) == N.ERR_UNSUPPORTED

@@ -1,7 +1,7 @@
 # GPU box, one call (round 4): STEPS selects what runs, in this order, each under its own limit, the chain stopping at
 # the first failure:  tests = the full GPU suite; bench = the default bench line; bench2 = `bench.py --gpus 2` (two
 # ranks sharing the card over gloo: a plumbing rehearsal, not a scaling number); abk = same-box A/B of the FC_small
-# kernels against build_exp/libhead.so; prof = rocprofv3 kernel stats of the default bench.
+# kernels against build_exp/libhead.so; abraw = the pack-free folded forward on / off (BCNF_FOLD_RAW); prof = rocprofv3 kernel stats of the default bench.
 #   bash tools/gpu_r04.sh <tag> "tests bench bench2"
 set -e
 cd $GRAFT_REPO_ROOT
@@ -49,6 +49,11 @@ for s in $STEPS; do
         else BCNF_AMD_LIB=$lib timeout -k 10 200 python bench.py --no-secondary --no-cpu-baseline > gpurun_out/${T}_abb.json 2>/dev/null; fi
         python -c "import json; d=json.loads(open('gpurun_out/${T}_abb.json').read().strip().splitlines()[-1]); print('$lib', d['ms_per_step'], round(d['value']), d['kernels_us'])"
       done; done 2>&1 | tee gpurun_out/${T}_abbench.txt ;;
+    abraw)
+      for i in 1 2 3; do for raw in 1 0; do
+        BCNF_FOLD_RAW=$raw timeout -k 10 200 python bench.py --no-secondary --no-cpu-baseline > gpurun_out/${T}_abr.json 2>/dev/null
+        python -c "import json; d=json.loads(open('gpurun_out/${T}_abr.json').read().strip().splitlines()[-1]); print('raw=$raw', d['ms_per_step'], round(d['value']), d['kernels_us'])"
+      done; done 2>&1 | tee gpurun_out/${T}_abraw.txt ;;
     prof)
       cd /tmp && export TMPDIR=/tmp
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/${T}_prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --no-secondary --no-cpu-baseline --steps 40 > $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.log; exit 1; }

@@ -1,0 +1,37 @@
+"""Device times of the folded training pass's launches (FusedStack.time_kernels with fold) for the library named by
+BCNF_AMD_LIB, plus the forward's phase stamps when that build has them: python tools/raw_probe.py"""
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    from bcnf_amd import CondRealNVP_v2
+    from bcnf_amd import _native as N
+    from bench import FC_SMALL
+    torch.manual_seed(0)
+    m = CondRealNVP_v2.from_config(FC_SMALL).cuda().train()
+    m.flat_parameters()
+    B = 4096
+    y = torch.randn(B, 19, device="cuda")
+    x = torch.randn(B, 90, device="cuda")
+    lin = m.feature_network_stack.feature_networks[1].nn[0]
+    t = m.fused.time_kernels(y, None, training=True, iters=50, fold=(x, lin.weight.detach(), lin.bias.detach()))
+    print(os.environ.get("BCNF_AMD_LIB", "default"), os.environ.get("BCNF_FOLD_RAW", "1"),
+          {k: round(v, 2) for k, v in t.items()})
+    L = N.lib()
+    if hasattr(L, "bcnf_debug_phases"):
+        buf = (ctypes.c_ulonglong * 16)()
+        L.bcnf_debug_phases(buf)
+        print("  fwd compute prologue/chain/wait", buf[8], buf[9], buf[10], " helper prologue/work/wait", buf[12],
+              buf[13], buf[14])
+        print("  prologue: compute at barrier0 / past it", buf[11] & 0xffffffff, buf[11] >> 32,
+              " helper at barrier0 / barrier1", buf[15] & 0xffffffff, buf[15] >> 32)
+
+
+if __name__ == "__main__":
+    main()
