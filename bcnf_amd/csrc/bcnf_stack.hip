@@ -416,6 +416,7 @@ bool build_raw_table(const BcnfLayout& L, uint32_t* out) {
     }
   const int cap[3] = {RAW_NP, RAW_NQ, RAW_NZ}, first[3] = {0, RAW_NP, RAW_NP + RAW_NQ};
   for (int i = 0; i < RAW_NS * BCNF_WG; ++i) out[i] = raw_entry(RAW_DUMMY, 0);
+  if (L.an_size > BCNF_WG) return false;                     // the ActNorm words (smallest sources) in P slot 0
   for (int g = 0; g < 3; ++g) {
     if ((int)ent[g].size() > cap[g] * BCNF_WG) return false;
     std::sort(ent[g].begin(), ent[g].end());
@@ -1435,39 +1436,29 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
                                                                          (int)(L.n_trainable * 4), 0x00020000);
       const __amdgpu_buffer_rsrc_t rQ = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(R.Q), (short)0,
                                                                          (nb - 1) * D * D * 4, 0x00020000);
+      // The last block (rec_f with k = nb - 1) goes through the same branch-free loads: its coupling sits an_size
+      // floats earlier in its block (no ActNorm), so the P base shifts by -an_size and only the ActNorm words --
+      // the an_size smallest sources, slot 0 of threads < an_size -- take constants (scale 1, bias 0); its Q base
+      // lies past the end of qmats, where the buffer range check returns 0, and the diagonal words take 1
+      // (identity mix). Those fix-ups happen at the use (finish_rec), so no load is waited for early.
+      const bool an_word = (int)(srcb[0] >> 2) < an;
+      const float an_val = (int)(srcb[0] >> 2) < D ? 1.f : 0.f;
+      bool q_diag[RAW_NQ];
+#pragma unroll
+      for (int i = 0; i < RAW_NQ; ++i) q_diag[i] = ((srcb[RAW_NP + i] >> 2) % (uint32_t)(D + 1)) == 0;
       auto load = [&](int k, Pre& g) {
         const int cb = coupling_base(L, k);
-        if (k < nb - 1) {
-          const int sp = k * L.blk_stride * 4, sq = k * D * D * 4;
+        const int sp = (k < nb - 1 ? k * L.blk_stride : k * L.blk_stride - an) * 4, sq = k * D * D * 4;
 #pragma unroll
-          for (int i = 0; i < RAW_NP; ++i)
-            g.v[i] = (BCNF_RAW_EXP & 4) ? 0.f : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rP, srcb[i], sp, 0));
+        for (int i = 0; i < RAW_NP; ++i)
+          g.v[i] = (BCNF_RAW_EXP & 4) ? 0.f : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rP, srcb[i], sp, 0));
 #pragma unroll
-          for (int i = RAW_NP; i < RAW_NP + RAW_NQ; ++i)
-            g.v[i] = (BCNF_RAW_EXP & 4) ? 0.f : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rQ, srcb[i], sq, 0));
-        } else {
-          // the last block (rec_f with k = nb - 1): its coupling sits an_size floats earlier in its block (no
-          // ActNorm), whose entries become scale 1 / bias 0; the mix is the identity (Q entry at i (D + 1))
-          const int sp = (k * L.blk_stride - an) * 4;
+        for (int i = RAW_NP; i < RAW_NP + RAW_NQ; ++i)
+          g.v[i] = (BCNF_RAW_EXP & 4) ? 0.f : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rQ, srcb[i], sq, 0));
 #pragma unroll
-          for (int i = 0; i < RAW_NP; ++i) {
-            const uint32_t src = srcb[i] >> 2;
-            const float x = __uint_as_float(
-                __builtin_amdgcn_raw_buffer_load_b32(rP, (int)src < an ? 4u * an : srcb[i], sp, 0));
-            g.v[i] = (int)src < an ? ((int)src < D ? 1.f : 0.f) : x;
-          }
-#pragma unroll
-          for (int i = RAW_NP; i < RAW_NP + RAW_NQ; ++i)
-            g.v[i] = ((srcb[i] >> 2) % (uint32_t)(D + 1)) == 0 ? 1.f : 0.f;
-        }
-#pragma unroll
-        for (int i = 0; i < RAW_TPW; ++i) {
-          if (hw + 4 * i < nt) {
-            const auto w = __builtin_amdgcn_raw_buffer_load_b128(rP, wo[i] * 4, cb * 4, 0);
-            g.w4[i] = floatx4{__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]), __uint_as_float(w[3])};
-          } else {
-            g.w4[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-          }
+        for (int i = 0; i < RAW_TPW; ++i) {   // unconditional (wo = 0 for an absent tile, whose MFMAs are skipped)
+          const auto w = __builtin_amdgcn_raw_buffer_load_b128(rP, wo[i] * 4, cb * 4, 0);
+          g.w4[i] = floatx4{__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]), __uint_as_float(w[3])};
         }
         // raw: the select waits for the load, so it happens at the use (finish_proj), not here
         g.bias = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rP, (L.lin_b[1] + lr) * 4, cb * 4, 0));
@@ -1485,8 +1476,19 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
           mkb[(2 * sl + 1) * BCNF_WG + t8] = floatx4{m[4], m[5], m[6], m[7]};
         }
         char* slot = reinterpret_cast<char*>(rec + sl * RING);
+        float v0 = g.v[0], vq[RAW_NQ];
 #pragma unroll
-        for (int i = 0; i < RAW_NP + RAW_NQ; ++i) *reinterpret_cast<float*>(slot + dstb[i]) = g.v[i];
+        for (int i = 0; i < RAW_NQ; ++i) vq[i] = g.v[RAW_NP + i];
+        if (k == nb - 1) {                                        // uniform
+          v0 = an_word ? an_val : v0;
+#pragma unroll
+          for (int i = 0; i < RAW_NQ; ++i) vq[i] = q_diag[i] ? 1.f : vq[i];
+        }
+        *reinterpret_cast<float*>(slot + dstb[0]) = v0;
+#pragma unroll
+        for (int i = 1; i < RAW_NP; ++i) *reinterpret_cast<float*>(slot + dstb[i]) = g.v[i];
+#pragma unroll
+        for (int i = 0; i < RAW_NQ; ++i) *reinterpret_cast<float*>(slot + dstb[RAW_NP + i]) = vq[i];
       };
       auto finish_proj = [&](int sl, const Pre& g) {
         const float bias = bias_lane ? g.bias : 0.f;
@@ -1505,16 +1507,17 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
         finish_rec(k, sl, g);
         finish_proj(sl, g);
       };
-      Pre g0, g1, gn;
-      load(0, g0);
-      load(1, g1);                                                // nb >= 2 (build_raw_table)
-      if (nb > 2) load(2, gn);                                    // software pipeline: see interval()
+      Pre gb[FWD_SLOTS];                                          // block b's operands in gb[b % 3] (interval())
+      load(0, gb[0]);
+      load(1, gb[1]);                                             // nb >= 2 (build_raw_table)
+      load(nb > 2 ? 2 : 1, gb[2]);
+      asm volatile("" ::: "memory");                              // all three blocks' loads issued here, not sunk
 #pragma unroll
       for (int i = 0; i < RAW_NZ; ++i)                            // this thread's zero words, in all three slots
 #pragma unroll
         for (int sl = 0; sl < FWD_SLOTS; ++sl) rec[sl * RING + zw[i]] = 0.f;
-      finish_rec(0, 0, g0);
-      finish_rec(1, 1, g1);
+      finish_rec(0, 0, gb[0]);
+      finish_rec(1, 1, gb[1]);
       PHB(0)
       __syncthreads();                                            // the compute waves' h tile is in hs
 #pragma unroll
@@ -1523,8 +1526,8 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
 #pragma unroll
         for (int r = 0; r < 4; ++r) xa[i][r] = v[r];
       }
-      finish_proj(0, g0);
-      finish_proj(1, g1);
+      finish_proj(0, gb[0]);
+      finish_proj(1, gb[1]);
       // ---- side work: the backward kernels' inputs, one unit per workgroup and q (coalesced rows) ----
       auto side_unit = [&](int u, uint32_t e) {
         if (u < nb * ch) {
@@ -1552,12 +1555,14 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
       // last two intervals have no block to prepare and take the side work: this workgroup's units (k = nb - 2) and
       // the log-det constant into lps for the compute epilogue (k = nb - 1)
       // software-pipelined: block k + 3's operands are loaded in interval k and consumed in interval k + 1, so an
-      // interval never waits for its own loads
+      // interval never waits for its own loads; with the loop unrolled by 3 every buffer index is a constant
       PHB(1)
       auto interval = [&](int k, int sl) {
-        const Pre g = gn;
-        if (k + 3 < nb) load(k + 3, gn);
-        finish(k + 2, sl, g);
+        // unconditional (block nb - 1 again past the end, unused): a load on one path only would make the wait
+        // counts conservative -- the consumers would wait for this interval's loads too
+        load(k + 3 < nb ? k + 3 : nb - 1, gb[sl == FWD_SLOTS - 1 ? 0 : sl + 1]);
+        asm volatile("" ::: "memory");                            // issued here, consumed next interval
+        finish(k + 2, sl, gb[sl]);
         PHF(1)
         // LDS writes complete, then a bare barrier: __syncthreads' release fence would also wait for the loads of
         // block k + 3 still in flight (vmcnt counts them too)
@@ -1977,8 +1982,25 @@ __device__ __forceinline__ f32x2 gelu_f2(f32x2 x) {
   const f32x2 h = (t * q) * ez;
   return f32x2{fmaf(-fabsf(x.x), h.x, relu_f(x.x, den.x)), fmaf(-fabsf(x.y), h.y, relu_f(x.y, den.y))};
 }
+// GELU for the forward-only kernels (sampling): x Phi(x) = max(x, 0) - |x| h(|x|) with log2 h fitted as ONE degree-6
+// polynomial in a = min(|x|, 6.5) (the -x^2/2 of erfc's decay is quadratic in a, so it is inside the fit): one exp2
+// and no reciprocal per element, 14 instructions per pair against gelu_f2's 20 (two of them transcendental instead
+// of four). fp32 error <= 1 ulp of the result above 0, <= 1e-7 below (tools/fit_erf.py: fit_log2h); past |x| = 6.5
+// |x| h < 3e-10.
+__device__ __forceinline__ f32x2 gelu_p2(f32x2 x) {
+  const f32x2 a = {fminf(fabsf(x.x), 6.5f), fminf(fabsf(x.y), 6.5f)};   // one VOP3 v_min each (|x| modifier)
+  f32x2 p = {3.3094816899392754e-05f, 3.3094816899392754e-05f};
+  p = __builtin_elementwise_fma(p, a, f32x2{-7.692371727898717e-04f, -7.692371727898717e-04f});
+  p = __builtin_elementwise_fma(p, a, f32x2{8.080773986876011e-03f, 8.080773986876011e-03f});
+  p = __builtin_elementwise_fma(p, a, f32x2{-5.3412191569805145e-02f, -5.3412191569805145e-02f});
+  p = __builtin_elementwise_fma(p, a, f32x2{-4.5877090096473694e-01f, -4.5877090096473694e-01f});
+  p = __builtin_elementwise_fma(p, a, f32x2{-1.1512017250061035e+00f, -1.1512017250061035e+00f});
+  p = __builtin_elementwise_fma(p, a, f32x2{-9.99993085861206e-01f, -9.99993085861206e-01f});
+  const f32x2 h = {__builtin_amdgcn_exp2f(p.x), __builtin_amdgcn_exp2f(p.y)};
+  return f32x2{fmaf(-fabsf(x.x), h.x, relu_f(x.x, a.x)), fmaf(-fabsf(x.y), h.y, relu_f(x.y, a.y))};
+}
 __device__ __forceinline__ void gelu4(floatx4& a) {
-  const f32x2 lo = gelu_f2(f32x2{a[0], a[1]}), hi = gelu_f2(f32x2{a[2], a[3]});
+  const f32x2 lo = gelu_p2(f32x2{a[0], a[1]}), hi = gelu_p2(f32x2{a[2], a[3]});
   a[0] = lo.x;
   a[1] = lo.y;
   a[2] = hi.x;
