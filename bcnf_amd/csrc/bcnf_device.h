@@ -290,9 +290,22 @@ __device__ __forceinline__ float gelu_tq(float x, float& phi) {   // t Q(t); phi
   phi = __builtin_amdgcn_exp2f(fmaf(x * x, -0.72134752044448170368f, -1.32574806473615920f));
   return t * q;
 }
+// Forward-only GELU (no derivative needed): x Phi(x) = max(x, 0) - |x| h, h = Phi(-|x|) = exp2(P6(min(|x|, 6.5))) --
+// erfc's e^{-x^2/2} decay is quadratic in |x|, so log2 h is ONE polynomial (tools/fit_erf.py fit_log2h: fp32 GELU error
+// 2.8e-7 = the result's rounding; 8.7e-8 for x < 0): one exp2 and no reciprocal.
+__device__ __forceinline__ float gelu_h(float x) {
+  const float a = fminf(fabsf(x), 6.5f);
+  float p = 3.309481690e-05f;
+  p = fmaf(p, a, -7.692371728e-04f);
+  p = fmaf(p, a, 8.080773987e-03f);
+  p = fmaf(p, a, -5.341219157e-02f);
+  p = fmaf(p, a, -4.587709010e-01f);
+  p = fmaf(p, a, -1.151201725e+00f);
+  p = fmaf(p, a, -9.999930859e-01f);
+  return __builtin_amdgcn_exp2f(p);
+}
 __device__ __forceinline__ float gelu_f(float x) {          // x Phi(x) = max(x, 0) - |x| Phi(-|x|)
-  float phi;
-  const float h = gelu_tq(x, phi) * phi;
+  const float h = gelu_h(x);
   // max(x, 0) as ONE v_max_f32 (fmaxf under IEEE mode canonicalises an operand that comes out of inline asm); it reads
   // x after h, whose computation from x carries any wait states an MFMA-produced x needs
   float r;

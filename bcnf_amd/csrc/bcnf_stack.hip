@@ -312,6 +312,7 @@ __device__ float rec_pm(const BcnfLayout& L, const float* P, const float* Q, int
 constexpr int RAW_NP = 10, RAW_NQ = 2, RAW_NZ = 6;   // slots per helper thread (FC_small: 2152 P-sourced, 361
                                                      // Q-sourced and 1071 zero entries)
 constexpr int RAW_NS = RAW_NP + RAW_NQ + RAW_NZ;
+constexpr int RAW_NSP = (RAW_NS + 3) & ~3;   // a thread's entries, contiguous: RAW_NSP / 4 16-byte loads
 constexpr int RAW_DUMMY = RING - 1;       // an unused float of a ring slot (16 RF <= RING - 1)
 constexpr int RAW_SRC_MAX = 1 << 20;
 
@@ -393,9 +394,10 @@ int rec_b_source(const BcnfLayout& L, int j, int e, int* off) {
   return 0;
 }
 
-// Floats of the pack-free forward's table: the forward slots [RAW_NS][256], then one block's backward record
-// [16 RB] as (source << 2 | kind) with kind 0 params, 1 qmats, 2 zero.
-long long raw_table_words(const BcnfLayout& L) { return (long long)RAW_NS * BCNF_WG + 16LL * L.RB; }
+// Words of the pack-free forward's table: the forward slots [256 threads][RAW_NSP] (a thread's slots contiguous, so
+// it loads them with RAW_NSP / 4 16-byte loads), then one block's backward record [16 RB] as (source << 2 | kind)
+// with kind 0 params, 1 qmats, 2 zero.
+long long raw_table_words(const BcnfLayout& L) { return (long long)RAW_NSP * BCNF_WG + 16LL * L.RB; }
 
 // The table [RAW_NS][BCNF_WG] (P slots, then Q slots, then zero slots) for layout L: every float of a ring slot's
 // 16 RF record floats belongs to exactly one (thread, slot), so a helper thread writes its own words and no two
@@ -415,15 +417,15 @@ bool build_raw_table(const BcnfLayout& L, uint32_t* out) {
       ent[kind == 1 ? 0 : kind == 2 ? 1 : 2].emplace_back(off, j * L.RF + e);
     }
   const int cap[3] = {RAW_NP, RAW_NQ, RAW_NZ}, first[3] = {0, RAW_NP, RAW_NP + RAW_NQ};
-  for (int i = 0; i < RAW_NS * BCNF_WG; ++i) out[i] = raw_entry(RAW_DUMMY, 0);
+  for (int i = 0; i < RAW_NSP * BCNF_WG; ++i) out[i] = raw_entry(RAW_DUMMY, 0);
   if (L.an_size > BCNF_WG) return false;                     // the ActNorm words (smallest sources) in P slot 0
   for (int g = 0; g < 3; ++g) {
     if ((int)ent[g].size() > cap[g] * BCNF_WG) return false;
     std::sort(ent[g].begin(), ent[g].end());
     for (int n = 0; n < (int)ent[g].size(); ++n)
-      out[(first[g] + n / BCNF_WG) * BCNF_WG + n % BCNF_WG] = raw_entry(ent[g][n].second, ent[g][n].first);
+      out[(n % BCNF_WG) * RAW_NSP + first[g] + n / BCNF_WG] = raw_entry(ent[g][n].second, ent[g][n].first);
   }
-  uint32_t* pb = out + (long long)RAW_NS * BCNF_WG;
+  uint32_t* pb = out + (long long)RAW_NSP * BCNF_WG;
   for (int j = 0; j < 16; ++j)
     for (int e = 0; e < L.RB; ++e) {
       int off;
@@ -1278,7 +1280,7 @@ __device__ __forceinline__ void mix(const float* __restrict__ rq, float a, float
 // Forward
 // ------------------------------------------------------------------------------------------------
 #if BCNF_STAMPS
-__device__ unsigned long long g_phase[16];   // phase stamps (bcnf_debug_phases), diagnostic build only
+__device__ unsigned long long g_phase[24];   // phase stamps (bcnf_debug_phases), diagnostic build only
 #endif
 
 // Condition projection operands of the forward (the y-independent part of Linear 1, cnf.py:98-107 with the
@@ -1378,6 +1380,12 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
   unsigned long long ph_b[2] = {0, 0};   // RAW prologue: cycles from the start to barrier #0 / #1 arrival
 #define PHB(i)                                                 \
   if (BCNF_STAMPS) ph_b[i] = __builtin_amdgcn_s_memtime() - ph_t0;
+  unsigned long long ph_p[4] = {0, 0, 0, 0};   // RAW prologue points (each after an explicit wait: stamped build only)
+#define PHP(i)                                                                           \
+  if (BCNF_STAMPS) {                                                                     \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                          \
+    ph_p[i] = __builtin_amdgcn_s_memtime() - ph_t0;                                      \
+  }
 #define PHF(i)                                                                                   \
   if (BCNF_STAMPS) {                                                                             \
     const unsigned long long _t = __builtin_amdgcn_s_memtime();                                  \
@@ -1394,25 +1402,37 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
       const long long row = (long long)blockIdx.x * 16 + lr;
       const float* xrow = R.xpool + raw_row(R, B, row < B ? row : B - 1) * R.ldx;
       // ---- prologue loads, all issued before any of them is consumed ----
-      uint32_t srcb[RAW_NP + RAW_NQ], dstb[RAW_NP + RAW_NQ];      // byte offsets: source, word of the ring slot
+      // this thread's table slots: RAW_NSP / 4 16-byte loads, all issued before any is used (decoded one at a time,
+      // the compiler waited for each load before issuing the next)
+      uint32_t tw[RAW_NSP];
 #pragma unroll
-      for (int i = 0; i < RAW_NP + RAW_NQ; ++i) {
-        const uint32_t t = R.table[i * BCNF_WG + t8];
-        srcb[i] = (t >> 12) * 4u;
-        dstb[i] = (t & 4095u) * 4u;
+      for (int i = 0; i < RAW_NSP / 4; ++i) {
+        const uint4 v = reinterpret_cast<const uint4*>(R.table + t8 * RAW_NSP)[i];
+        tw[4 * i] = v.x;
+        tw[4 * i + 1] = v.y;
+        tw[4 * i + 2] = v.z;
+        tw[4 * i + 3] = v.w;
       }
-      uint32_t zw[RAW_NZ];
-#pragma unroll
-      for (int i = 0; i < RAW_NZ; ++i) zw[i] = R.table[(RAW_NP + RAW_NQ + i) * BCNF_WG + t8] & 4095u;
       // side units of this workgroup (RawSide): backward-record chunks u < nb * ch, then W1hR rows
       const int rb16 = 16 * L.RB, ch = (rb16 + BCNF_WG - 1) / BCNF_WG, n_units = nb * ch + L.NKp;
-      const uint32_t* tpb = R.table + RAW_NS * BCNF_WG;
+      const uint32_t* tpb = R.table + RAW_NSP * BCNF_WG;
       uint32_t pbe[RAW_SIDE_Q];                                   // (the unit checks happen at the use)
 #pragma unroll
       for (int q = 0; q < RAW_SIDE_Q; ++q) {
         const int u = blockIdx.x + q * gridDim.x, n = (u % ch) * BCNF_WG + t8;
         pbe[q] = tpb[n < rb16 ? n : 0];
       }
+      asm volatile("" ::: "memory");                              // the table loads above are all in flight
+      uint32_t srcb[RAW_NP + RAW_NQ], dstb[RAW_NP + RAW_NQ];      // byte offsets: source, word of the ring slot
+#pragma unroll
+      for (int i = 0; i < RAW_NP + RAW_NQ; ++i) {
+        srcb[i] = (tw[i] >> 12) * 4u;
+        dstb[i] = (tw[i] & 4095u) * 4u;
+      }
+      uint32_t zw[RAW_NZ];
+#pragma unroll
+      for (int i = 0; i < RAW_NZ; ++i) zw[i] = tw[RAW_NP + RAW_NQ + i] & 4095u;
+      PHP(0)
       // projection B operand of block k: W1_k[lr][Da + 16 ct + 4 lq + r], r = 0..3 one (dword-aligned) 16-byte load
       // per tile (at most 3 floats past the row end: still inside the block's parameters), zero past C or H[1]
       int wo[RAW_TPW];
@@ -1512,12 +1532,14 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
       load(1, gb[1]);                                             // nb >= 2 (build_raw_table)
       load(nb > 2 ? 2 : 1, gb[2]);
       asm volatile("" ::: "memory");                              // all three blocks' loads issued here, not sunk
+      PHP(1)
 #pragma unroll
       for (int i = 0; i < RAW_NZ; ++i)                            // this thread's zero words, in all three slots
 #pragma unroll
         for (int sl = 0; sl < FWD_SLOTS; ++sl) rec[sl * RING + zw[i]] = 0.f;
       finish_rec(0, 0, gb[0]);
       finish_rec(1, 1, gb[1]);
+      PHP(2)
       PHB(0)
       __syncthreads();                                            // the compute waves' h tile is in hs
 #pragma unroll
@@ -1699,6 +1721,7 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
         }
       }
       asm volatile("" ::: "memory");
+      PHP(0)
       // independent accumulation chains (tile i, parity of u), summed in a fixed order
       floatx4 acc[RAW_TPW][2];
 #pragma unroll
@@ -1813,10 +1836,12 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
   {
     for (int i = 0; i < 3; ++i) g_phase[8 + (helper ? 4 : 0) + i] = ph_acc[i];
     g_phase[helper ? 15 : 11] = (ph_b[1] << 32) | (ph_b[0] & 0xffffffffULL);   // slots 3 / 7 belong to the backward
+    for (int i = 0; i < 4; ++i) g_phase[16 + (helper ? 4 : 0) + i] = ph_p[i];
   }
 #endif
 #undef PHF
 #undef PHB
+#undef PHP
   if (nll_part) {   // per-workgroup partial of inn_nll_loss (utils.py:40-46); reduced by nll_finalize
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1985,8 +2010,8 @@ __device__ __forceinline__ f32x2 gelu_f2(f32x2 x) {
 // GELU for the forward-only kernels (sampling): x Phi(x) = max(x, 0) - |x| h(|x|) with log2 h fitted as ONE degree-6
 // polynomial in a = min(|x|, 6.5) (the -x^2/2 of erfc's decay is quadratic in a, so it is inside the fit): one exp2
 // and no reciprocal per element, 14 instructions per pair against gelu_f2's 20 (two of them transcendental instead
-// of four). fp32 error <= 1 ulp of the result above 0, <= 1e-7 below (tools/fit_erf.py: fit_log2h); past |x| = 6.5
-// |x| h < 3e-10.
+// of four). The pair form of bcnf_device.h gelu_h / gelu_f (same coefficients): fp32 error <= 1 ulp of the result
+// above 0, <= 1e-7 below (tools/fit_erf.py: fit_log2h); past |x| = 6.5, |x| h < 3e-10.
 __device__ __forceinline__ f32x2 gelu_p2(f32x2 x) {
   const f32x2 a = {fminf(fabsf(x.x), 6.5f), fminf(fabsf(x.y), 6.5f)};   // one VOP3 v_min each (|x| modifier)
   f32x2 p = {3.3094816899392754e-05f, 3.3094816899392754e-05f};

@@ -236,7 +236,7 @@ def test_fold_raw_table_partitions_the_record():
         assert L.bcnf_fold_raw_table_bytes(ctypes.byref(d), X, ctypes.byref(nb)) == N.OK
         raw = np.zeros(nb.value // 4, dtype=np.uint32)
         assert L.bcnf_fold_raw_table(ctypes.byref(d), X, ctypes.c_void_p(raw.ctypes.data)) == N.OK
-        t, pb = raw[:18 * 256].reshape(-1, 256), raw[18 * 256:]
+        t, pb = raw[:20 * 256].reshape(256, 20)[:, :18].T, raw[20 * 256:]   # [thread][20 slots] -> [slot][thread]
         dst, src = t & 4095, t >> 12
         live = dst != 4095
         words = dst[live]

@@ -192,7 +192,35 @@ def gelu_r04_check():
           f"|GELU' err| {np.abs(dg - (P + xd * np.exp(-xd * xd / 2) / np.sqrt(2 * np.pi))).max():.2e}")
 
 
+def fit_log2h(deg=6, amax=6.5, iters=200):
+    """r04 gelu_p2 / gelu_pf (forward-only GELU): log2 h(a), h = erfc(a / sqrt 2) / 2, as ONE polynomial in
+    a = min(|x|, amax) (erfc's e^{-a^2/2} decay is quadratic in a, so it sits inside the fit), reweighted toward the
+    minimax of the GELU error |a (h_fit - h)|; then the emulated-fp32 GELU error of the rounded coefficients."""
+    from scipy.special import erfc
+    a = np.linspace(0, amax, 400001)
+    h = erfc(a / np.sqrt(2)) / 2
+    V = np.vander(a, deg + 1)
+    w = np.ones_like(a)
+    for _ in range(iters):
+        c, *_ = np.linalg.lstsq(V * w[:, None], np.log2(h) * w, rcond=None)
+        err = np.abs(a * (np.exp2(V @ c) - h))
+        w = w * (1 + 0.5 * err / err.max())
+    c32 = c.astype(f32)
+    x = np.linspace(-12, 12, 2000001).astype(f32)
+    aa = np.minimum(np.abs(x), f32(amax))
+    p = np.full_like(x, c32[0])
+    for cc in c32[1:]:
+        p = fma(p, aa, cc)
+    g = fma(-np.abs(x), f32(np.exp2(np.float64(p))), np.maximum(x, f32(0)))
+    from scipy.special import ndtr
+    xd = x.astype(np.float64)
+    print(f"fit_log2h(deg={deg}): exact-arith max |a dh| {err.max():.2e}; fp32 |GELU err| "
+          f"{np.abs(g - xd * ndtr(xd)).max():.2e} (x < 0: {np.abs(g - xd * ndtr(xd))[x < 0].max():.2e})")
+    print("  coefficients (highest first):", ", ".join(f"{float(v):.9e}" for v in c32))
+
+
 if __name__ == "__main__":
     gelu_fit()
     tanh_check()
     gelu_r04_check()
+    fit_log2h()

@@ -25,12 +25,14 @@ def main():
           {k: round(v, 2) for k, v in t.items()})
     L = N.lib()
     if hasattr(L, "bcnf_debug_phases"):
-        buf = (ctypes.c_ulonglong * 16)()
+        buf = (ctypes.c_ulonglong * 24)()
         L.bcnf_debug_phases(buf)
         print("  fwd compute prologue/chain/wait", buf[8], buf[9], buf[10], " helper prologue/work/wait", buf[12],
               buf[13], buf[14])
         print("  prologue: compute at barrier0 / past it", buf[11] & 0xffffffff, buf[11] >> 32,
               " helper at barrier0 / barrier1", buf[15] & 0xffffffff, buf[15] >> 32)
+        print("  compute: x/Wf landed", buf[16], " helper: table landed", buf[20], "gathers landed", buf[21],
+              "records written", buf[22])
 
 
 if __name__ == "__main__":
