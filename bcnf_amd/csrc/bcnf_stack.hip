@@ -56,6 +56,7 @@ __host__ __device__ constexpr int tile_ix(int s, int r) { return 4 * tile_slot(r
 __host__ __device__ constexpr int sample_of(int t8) { return (t8 >> 6) + 4 * ((t8 >> 4) & 3); }
 constexpr int STAGE_REC = 4;   // 16 * RF (RB) floats  <= 4 float4 per thread (RF, RB <= 256)
 constexpr int RING = STAGE_REC * BCNF_WG * 4;    // floats per record-ring slot: a Stage stores all of it
+constexpr int RAW_KP = 100;   // pack-free forward: LDS row pitch of the staged Wf / x rows (X <= 96), = 4 mod 32
 // floats per lane of a block's activation record (ActRec); the AR1 single floats follow all the float4 parts
 __host__ __device__ constexpr int act_rec_floats(int NH) { return 2 * NH + 3; }
 __host__ __device__ constexpr long long ar1_off(int nb, long long nwg, int ar4) { return (long long)nb * nwg * ar4 * 4 * 256; }
@@ -150,7 +151,8 @@ size_t fwd_lds_bytes(const BcnfLayout& L) {   // forward / inverse record ring (
 }
 size_t fwd2_lds_bytes(const BcnfLayout& L, bool raw = false) {  // k_forward: record ring, projection partials,
   return sizeof(float) * (size_t)(3 * RING + 3 * 4 * 256 + 3 * 8 * 256 +   // dropout masks (3 slots)
-                                  (raw ? 4 + 16 * (128 + 4) : 0));         // RAW: log-det partials, h tile
+                                  (raw ? 4 + 16 * (128 + 4) + (L.C + 16) * RAW_KP : 0));   // RAW: log-det
+                                                                           // partials, h tile, staged Wf / x
 }
 size_t bwd_lds_bytes(const BcnfLayout& L) {   // backward record ring, delta tiles (2), activation tiles (3), derivative slots (2)
   return sizeof(float) * (size_t)(2 * RING + 2 * (L.NH + 6) * TILE + 3 * (L.NH + 1) * TILE + 2 * 3 * 4 * 256);
@@ -1321,7 +1323,7 @@ struct RawArgs {
   float* pk;               // packed buffer: PB and W1hR are written here
   int X, ldx;
 };
-constexpr int RAW_XS = 24;             // K-steps of the h GEMM: X <= 96
+constexpr int RAW_WQ = 8;              // Wf quads per thread in flight while staging (C * ceil(X / 4) <= 2048 in one go)
 constexpr int RAW_TPW = 2;             // h column tiles per helper wave: C <= 128
 constexpr int RAW_SIDE_Q = 4;          // side units per workgroup done in the idle interval
 __host__ __device__ constexpr int raw_hs_pitch(int C) { return 16 * ((C + 15) / 16) + 4; }
@@ -1540,8 +1542,9 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
       finish_rec(0, 0, gb[0]);
       finish_rec(1, 1, gb[1]);
       PHP(2)
+      __syncthreads();                                            // barrier A (the compute waves' operand staging)
       PHB(0)
-      __syncthreads();                                            // the compute waves' h tile is in hs
+      __syncthreads();                                            // barrier B: the compute waves' h tile is in hs
 #pragma unroll
       for (int i = 0; i < RAW_TPW; ++i) {
         const floatx4 v = *reinterpret_cast<const floatx4*>(hs + lr * raw_hs_pitch(C) + 16 * (hw + 4 * i) + 4 * lq);
@@ -1683,56 +1686,120 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
     const int D = L.D, Da = L.Da, Db = L.Db;
     float ya, yb, ldc = 0.f;
     if constexpr (RAW) {
-      // every load of the prologue is issued before the first use of any (one round trip after the row index):
-      // y, x, Wf and bf, then an empty asm with a memory clobber so none of them sinks into a consumer's branch
+      // h^T = Wf x^T + bf of the workgroup's 16 rows on the matrix cores. Wf (C x X) and the 16 x rows are staged
+      // into LDS by coalesced 16-byte loads of all four compute waves (per-lane strided operand loads made ~1.2M
+      // cache-line requests per launch and queued everyone's first loads behind them), then compute wave
+      // cw takes the column tiles ct = cw + 4 i. K order: MFMA step (u, r) of lane (lr, lq) is column
+      // 16 u + 4 lq + r, so each operand quad is one conflict-free ds_read_b128 (row pitch RAW_KP = 4 mod 32), and
+      // the output layout (h[row lr][16 ct + 4 lq + r] at lane (lr, lq)) is helper wave cw's projection A operand.
+      // ldc: the helpers' wave sums of the ActNorm log-det constant (lps), read after the last barrier.
       const long long src = raw_row(R, B, bc);
       ya = (j < Da) ? R.ypool[src * D + j] : 0.f;
       yb = (j < Db) ? R.ypool[src * D + Da + j] : 0.f;
-      // h^T = Wf x^T + bf of the workgroup's 16 rows on the matrix cores, compute wave cw taking the column tiles
-      // ct = cw + 4 i, which helper wave cw reads back in the MFMA output layout (h[row lr][16 ct + 4 lq + r] at
-      // lane (lr, lq)) as its projection A operand. ldc: the helpers' wave sums of the ActNorm log-det constant
-      // (lps), read after the last barrier.
+      const int C = L.C, X = R.X, XQ = (X + 3) >> 2;              // float4 quads per row (<= RAW_KP / 4 - 1)
+      float* ws = hs + 16 * raw_hs_pitch(C);                      // Wf [C][RAW_KP]
+      float* xs = ws + C * RAW_KP;                                // x rows [16][RAW_KP]
       const int cw = __builtin_amdgcn_readfirstlane(tid >> 6), l64 = tid & 63, lr = l64 & 15, lq = l64 >> 4;
-      const int C = L.C, X = R.X;
-      const long long row = (long long)blockIdx.x * 16 + lr;
-      const float* xrow = R.xpool + raw_row(R, B, row < B ? row : B - 1) * R.ldx;
-      float xb[RAW_XS];                                           // B operand: x[row lr][4 u + lq]
-#pragma unroll
-      for (int u = 0; u < RAW_XS; ++u) {
-        const int kx = 4 * u + lq;
-        xb[u] = (BCNF_RAW_EXP & 16) ? 1.f : xrow[kx < X ? kx : 0];
-      }
-      float wa[RAW_TPW][RAW_XS];                                  // A operand: Wf[16 ct + lr][4 u + lq]
-      float hb[RAW_TPW][4];                                       // bf of the columns this lane ends with
       const float* bfp = R.bf ? R.bf : R.wf;
+      float hb[RAW_TPW][4];                                       // bf of the columns this lane ends with
 #pragma unroll
-      for (int i = 0; i < RAW_TPW; ++i) {
-        const int c = 16 * (cw + 4 * i) + lr;
-        const float* wrow = R.wf + (long long)(c < C ? c : 0) * X;
-#pragma unroll
-        for (int u = 0; u < RAW_XS; ++u) {
-          const int kx = 4 * u + lq;
-          wa[i][u] = (BCNF_RAW_EXP & 32) ? 1.f : wrow[kx < X ? kx : 0];
-        }
+      for (int i = 0; i < RAW_TPW; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int cc = 16 * (cw + 4 * i) + 4 * lq + r;
-          hb[i][r] = (BCNF_RAW_EXP & 32) ? 1.f : bfp[cc < C ? cc : 0];
+          hb[i][r] = bfp[cc < C ? cc : 0];
+        }
+      {
+        // every staging load in flight at once (one round trip): Wf quad (c, q) = columns 4q .. 4q + 3 of row c,
+        // read past the row end into the next row (zeroed below) and past the tensor's end through a range-checked
+        // buffer load (0); the x quads of the 16 rows (gathered through idx when given), the row's last partial
+        // quad element by element
+        const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(R.wf), (short)0,
+                                                                           C * X * 4, 0x00020000);
+        const int nq = C * XQ;
+        uint32_t v[RAW_WQ][4];
+#pragma unroll
+        for (int u = 0; u < RAW_WQ; ++u) {
+          const int i = tid + u * BCNF_WG, ii = i < nq ? i : 0, c = ii / XQ, q = ii - c * XQ;
+          const auto w = __builtin_amdgcn_raw_buffer_load_b128(rW, (c * X + 4 * q) * 4, 0, 0);
+          v[u][0] = w[0]; v[u][1] = w[1]; v[u][2] = w[2]; v[u][3] = w[3];
+        }
+        constexpr int NXQ = (16 * (RAW_KP / 4) + BCNF_WG - 1) / BCNF_WG;
+        floatx4 xo[NXQ];
+#pragma unroll
+        for (int u = 0; u < NXQ; ++u) {
+          const int i = tid + u * BCNF_WG, ii = i < 16 * (RAW_KP / 4) ? i : 0;
+          const int rr = ii / (RAW_KP / 4), q = ii - rr * (RAW_KP / 4);
+          const long long bb = (long long)blockIdx.x * 16 + rr;
+          const float* xr = R.xpool + raw_row(R, B, bb < B ? bb : B - 1) * R.ldx + 4 * q;
+          xo[u] = floatx4{0.f, 0.f, 0.f, 0.f};
+          if (4 * q + 3 < X) {
+            __builtin_memcpy(&xo[u], xr, sizeof(floatx4));
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (4 * q + r < X) xo[u][r] = xr[r];
+          }
+        }
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < RAW_WQ; ++u) {
+          const int i = tid + u * BCNF_WG, c = i / XQ, q = i - c * XQ;
+          if (i < nq) {
+            floatx4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = 4 * q + r < X ? __uint_as_float(v[u][r]) : 0.f;
+            *reinterpret_cast<floatx4*>(ws + c * RAW_KP + 4 * q) = o;
+          }
+        }
+        for (int i = nq > RAW_WQ * BCNF_WG ? tid + RAW_WQ * BCNF_WG : nq; i < nq; i += BCNF_WG) {   // C X > 7680
+          const int c = i / XQ, q = i - c * XQ;
+          const auto w = __builtin_amdgcn_raw_buffer_load_b128(rW, (c * X + 4 * q) * 4, 0, 0);
+          floatx4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = 4 * q + r < X ? __uint_as_float(w[r]) : 0.f;
+          *reinterpret_cast<floatx4*>(ws + c * RAW_KP + 4 * q) = o;
+        }
+#pragma unroll
+        for (int u = 0; u < NXQ; ++u) {
+          const int i = tid + u * BCNF_WG;
+          if (i < 16 * (RAW_KP / 4)) {
+            const int rr = i / (RAW_KP / 4), q = i - rr * (RAW_KP / 4);
+            *reinterpret_cast<floatx4*>(xs + rr * RAW_KP + 4 * q) = xo[u];
+            const long long bb = (long long)blockIdx.x * 16 + rr;
+            if (R.xdst && bb < B && 4 * q < X) {                  // the backward tail's x rows
+              float* xd = R.xdst + bb * R.ldx + 4 * q;
+              if (4 * q + 3 < X) {
+                __builtin_memcpy(xd, &xo[u], sizeof(floatx4));
+              } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                  if (4 * q + r < X) xd[r] = xo[u][r];
+              }
+            }
+          }
         }
       }
-      asm volatile("" ::: "memory");
       PHP(0)
-      // independent accumulation chains (tile i, parity of u), summed in a fixed order
+      __syncthreads();                                            // ws / xs complete (barrier A)
+      // independent accumulation chains (tile i, parity of r), summed in a fixed order
       floatx4 acc[RAW_TPW][2];
 #pragma unroll
       for (int i = 0; i < RAW_TPW; ++i) acc[i][0] = acc[i][1] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int u = 0; u < RAW_XS; ++u) {
-        const float xv = (4 * u + lq < X) ? xb[u] : 0.f;
+      for (int u = 0; u < RAW_KP / 16; ++u) {
+        if (16 * u >= X) break;                                   // uniform
+        const floatx4 xv = *reinterpret_cast<const floatx4*>(xs + lr * RAW_KP + 16 * u + 4 * lq);
 #pragma unroll
-        for (int i = 0; i < RAW_TPW; ++i)
-          if (!(BCNF_RAW_EXP & 2) && 16 * (cw + 4 * i) < C && 4 * u < X)
-            acc[i][u & 1] = mfma4(wa[i][u], xv, acc[i][u & 1]);
+        for (int i = 0; i < RAW_TPW; ++i) {
+          const int ct = cw + 4 * i;
+          if (!(BCNF_RAW_EXP & 2) && 16 * ct < C) {
+            const int c = 16 * ct + lr;
+            const floatx4 wv = *reinterpret_cast<const floatx4*>(ws + (c < C ? c : 0) * RAW_KP + 16 * u + 4 * lq);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[i][r & 1] = mfma4(wv[r], xv[r], acc[i][r & 1]);
+          }
+        }
       }
 #pragma unroll
       for (int i = 0; i < RAW_TPW; ++i) {
@@ -1748,18 +1815,11 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
         }
       }
       PHB(0)
-      __syncthreads();                                            // hs complete
+      __syncthreads();                                            // hs complete (barrier B)
       PHB(1)
-      // the gathered rows for the backward: y by every compute lane, x by wave 0 from the B operand it holds
-      // (columns < X; the padding columns past X are never read)
-      if (R.ydst && b < B) {
+      if (R.ydst && b < B) {                                      // the gathered y rows for the backward
         if (j < Da) R.ydst[b * D + j] = ya;
         if (j < Db) R.ydst[b * D + Da + j] = yb;
-      }
-      if (R.xdst && cw == 0 && row < B) {
-#pragma unroll
-        for (int u = 0; u < RAW_XS; ++u)
-          if (4 * u + lq < X) R.xdst[row * R.ldx + 4 * u + lq] = xb[u];
       }
     } else {
       ya = (j < Da) ? y[bc * D + j] : 0.f;
@@ -3006,7 +3066,7 @@ int fold_setup(const BcnfStackDesc* desc, int32_t X, BcnfLayout* L) {
 long long fold_floats(const BcnfLayout& L, int X) { return (long long)(fold_xp(X) + 1) * L.NKp; }
 // The pack-free forward's shape limits (its table must also build: build_raw_table).
 bool raw_applicable(const BcnfLayout& L, int X) {
-  return X <= 4 * RAW_XS && L.C <= 64 * RAW_TPW && L.nb >= 2 && L.act_norm;
+  return X <= RAW_KP - 4 && L.C <= 64 * RAW_TPW && L.nb >= 2 && L.act_norm;
 }
 }  // namespace
 
