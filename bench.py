@@ -47,6 +47,8 @@ FC_SMALL = {
 #                   k_backward's own share excludes the W1 condition columns (dW1h and dL/dh: 2 * 32 * 16 * 80 =
 #                   81,920 MAC, done by the tail's split-K): 138,167 MAC
 FWD_FLOP_PER_SAMPLE = 2 * 115_639
+# the pack-free forward (bcnf_fold_train_forward) also computes the feature Linear h = x Wf^T + bf of its rows
+FEAT_FLOP_PER_SAMPLE = 2 * 90 * 80
 BWD_FLOP_PER_SAMPLE = 2 * 220_087
 KBWD_FLOP_PER_SAMPLE = 2 * (220_087 - 81_920)
 # SURVEY §8d minimal HBM bytes per sample of per-block kernels (recompute in backward), nb = 32, D = 19, C = 80:
@@ -574,9 +576,13 @@ def fc_small_rooflines(kern, B):
     FLOPs per launch (reference count) / its HIP-event duration; algorithmic_bytes = SURVEY §8d's per-block
     minimum x B; traffic = PMC FETCH (x2, gfx950) + WRITE bytes per launch of the same build (profiles/pmc_traffic.json,
     tools/profile_round.sh), traffic_ratio = traffic / algorithmic_bytes (> 1: bytes beyond the per-block minimum)."""
-    spec = {"k_forward": (FWD_FLOP_PER_SAMPLE, FWD_ALG_BYTES_PER_SAMPLE,
+    raw = "k_pack_fold" not in kern            # the pack-free forward: no pack launch, the feature Linear inside
+    spec = {"k_forward": (FWD_FLOP_PER_SAMPLE + (FEAT_FLOP_PER_SAMPLE if raw else 0), FWD_ALG_BYTES_PER_SAMPLE,
                           "whole-stack forward: ActNorm, nested MLP (DPP-rotation VALU), coupling, log-det, mix; "
-                          "condition projection on fp32 MFMA helper waves; saves the activation records"),
+                          "condition projection on fp32 MFMA helper waves; saves the activation records" +
+                          ("; pack-free (bcnf_fold_train_forward): records gathered from the parameters, the feature "
+                           "Linear h = x Wf^T + bf on the compute waves' matrix cores (its FLOPs counted)" if raw
+                           else "")),
               "k_backward": (KBWD_FLOP_PER_SAMPLE, BWD_ALG_BYTES_PER_SAMPLE,
                              "whole-stack backward from the saved records: dX chain (DPP VALU) + dW tiles (fp32 "
                              "MFMA); the W1 condition-column gradients run in the tail (excluded from its FLOPs)")}
