@@ -294,7 +294,7 @@ __device__ __forceinline__ float gelu_tq(float x, float& phi) {   // t Q(t); phi
 // erfc's e^{-x^2/2} decay is quadratic in |x|, so log2 h is ONE polynomial (tools/fit_erf.py fit_log2h: fp32 GELU error
 // 2.8e-7 = the result's rounding; 8.7e-8 for x < 0): one exp2 and no reciprocal.
 __device__ __forceinline__ float gelu_h(float x) {
-  const float a = fminf(fabsf(x), 6.5f);
+  const float a = __builtin_amdgcn_fmed3f(fabsf(x), 0.f, 6.5f);   // one v_med3 (fminf adds a canonicalising v_max)
   float p = 3.309481690e-05f;
   p = fmaf(p, a, -7.692371728e-04f);
   p = fmaf(p, a, 8.080773987e-03f);

@@ -2073,7 +2073,9 @@ __device__ __forceinline__ f32x2 gelu_f2(f32x2 x) {
 // of four). The pair form of bcnf_device.h gelu_h / gelu_f (same coefficients): fp32 error <= 1 ulp of the result
 // above 0, <= 1e-7 below (tools/fit_erf.py: fit_log2h); past |x| = 6.5, |x| h < 3e-10.
 __device__ __forceinline__ f32x2 gelu_p2(f32x2 x) {
-  const f32x2 a = {fminf(fabsf(x.x), 6.5f), fminf(fabsf(x.y), 6.5f)};   // one VOP3 v_min each (|x| modifier)
+  // med3(|x|, 0, 6.5): ONE v_med3_f32 with the |x| source modifier (fminf under IEEE mode adds a canonicalising
+  // v_max first)
+  const f32x2 a = {__builtin_amdgcn_fmed3f(fabsf(x.x), 0.f, 6.5f), __builtin_amdgcn_fmed3f(fabsf(x.y), 0.f, 6.5f)};
   f32x2 p = {3.3094816899392754e-05f, 3.3094816899392754e-05f};
   p = __builtin_elementwise_fma(p, a, f32x2{-7.692371727898717e-04f, -7.692371727898717e-04f});
   p = __builtin_elementwise_fma(p, a, f32x2{8.080773986876011e-03f, 8.080773986876011e-03f});
