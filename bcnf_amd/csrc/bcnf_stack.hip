@@ -2027,7 +2027,10 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse(BcnfLayout L, const float* 
 // as the accumulator), hidden layers and the T / S heads run on the matrix pipe; the VALU keeps GELU, tanh, exp
 // and the coupling / ActNorm inverse (row-layout k_inverse: ~380 VALU instructions per block per 4 samples, 95% of
 // VALU issue in profiles/r02y_k_inverse_pmc_insts.csv). Same sums as k_inverse in a different association order.
-constexpr int INV_M_SPW = 16;                       // samples per wave
+// G independent 16-sample groups per wave interleaving their MFMA chains and GELUs (G = 2 measured neutral, DESIGN 3e;
+// again with the r04 GELU: 1.304 against 1.295 ms per 512k draws, profiles/r04zc_ab_sample.txt).
+constexpr int INV_M_G = 1;
+constexpr int INV_M_SPW = 16 * INV_M_G;              // samples per wave
 constexpr int INV_M_WG = 512;                       // 8 waves share one record ring (2 x 16 KB): 4 workgroups per CU
 constexpr int INV_M_SPB = INV_M_SPW * (INV_M_WG / 64);
 template <int NH>
@@ -2103,8 +2106,6 @@ __device__ __forceinline__ floatx4 inv_mv(floatx4 acc, const float* __restrict__
 }
 constexpr int INV_M_OCC = 6;   // min waves per SIMD (80 VGPRs, no spills; 5 and 8 measured slower)
 
-// G independent 16-sample groups per wave interleaving their MFMA chains and GELUs (G = 2 measured neutral).
-constexpr int INV_M_G = 1;
 
 // One dense layer on the matrix cores: the lane's A operands of the KS K-steps are ONE float4 of the operand-ordered
 // record (rec_pm: matrix mat, lane l), conflict-free ds_read_b128.
