@@ -704,6 +704,22 @@ def cpu_baseline_wide(workload, cfg, batch=256, steps=4):
                       f"steps after 1 warmup, {threads} threads, {med * 1e3:.0f} ms/step"}
 
 
+def wide_mfma_busy(workload):
+    """Matrix-pipe busy fractions of a wide workload's kernels from the committed SQ counters of a short run of the
+    same build (profiles/pmc_wide.json, tools/pmc_wide.sh + tools/pmc_wide.py): SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x
+    kernel-trace duration x 2.4 GHz) for the chain GEMMs (k_wbr: ACT / GRAD) and over all library kernels, with their
+    VALU-per-MFMA instruction ratio (f32 MFMA and VALU do not co-issue on a SIMD)."""
+    path = os.path.join(ROOT, "profiles", "pmc_wide.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f).get(workload)
+    if not d:
+        return None
+    return {"chain_gemms": d.get("chain"), "all_library_kernels": d.get("library_kernels_mfma_busy_frac"),
+            "source": "profiles/pmc_wide.json"}
+
+
 def run_wide(workload, batch, steps, warmup, world, rank, device, graph=True, kernel_iters=20, cpu=True,
              cpu_batch=256, cpu_steps=4, overlap_ranges=0):
     """NLL-training samples/s of a wide workload (trajectory_FC_large = configs[2], trajectory_LSTM_large =
@@ -780,6 +796,9 @@ def run_wide(workload, batch, steps, warmup, world, rank, device, graph=True, ke
                              "of the last feature Linear executes fewer condition-GEMM FLOPs than it counts"},
         "kernels_us": {k: round(v, 2) for k, v in kern.items()},
     }
+    mb = wide_mfma_busy(workload)
+    if mb:
+        line["roofline"]["mfma_busy"] = mb
     del step, model, data
     torch.cuda.empty_cache()
     try:
