@@ -38,7 +38,7 @@ EXPORTS = (
     "bcnf_wide_supported", "bcnf_wide_param_count", "bcnf_wide_packed_bytes", "bcnf_wide_workspace_bytes", "bcnf_wide_inverse_scratch_bytes",
     "bcnf_wide_pack", "bcnf_wide_forward", "bcnf_wide_nll_finalize", "bcnf_wide_backward", "bcnf_wide_inverse",
     "bcnf_wide_fold_prepare", "bcnf_wide_fold_forward", "bcnf_wide_fold_backward", "bcnf_wide_proj_rows",
-    "bcnf_wide_fold_backward_range", "bcnf_wide_block_offset",
+    "bcnf_wide_fold_backward_range", "bcnf_wide_fold_backward_phase", "bcnf_wide_block_offset",
     "bcnf_wide_gemm_test", "bcnf_rank_count", "bcnf_resimulate",
     "bcnf_guard_check_global", "bcnf_abi_version",
 )
@@ -183,6 +183,8 @@ def _bind(lib):
                                            _vp, _vp]),
         "bcnf_wide_fold_backward_range": (_i32, [_pdesc, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                                  _vp, _vp, _i32, _i32, _vp]),
+        "bcnf_wide_fold_backward_phase": (_i32, [_pdesc, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                                 _vp, _vp, _i32, _vp]),
         "bcnf_wide_block_offset": (_i32, [_pdesc, _i32, _pi64]),
         "bcnf_wide_proj_rows": (_i32, [_pdesc, _pi64]),
         "bcnf_wide_nll_finalize": (_i32, [_pdesc, _vp, _i64, _i32, _vp, _vp, _vp, _vp]),

@@ -2297,14 +2297,28 @@ int wide_forward(const WideLayout& L, const float* prm, const float* pk, const f
 // and starts v - 1 (head-B, then its hidden-layer chain), so a range runs v = (vhi == nv ? nv : vhi - 1) .. vlo.
 // Per-element results do not depend on the split: every GEMM keeps its K order, the split-K partials of the small
 // Linear gradients go to the finished range's G slots (dead once its chain has run).
+// phase (whole range only): bit 1 = what the caller's next layers wait for (the chain, then Gx, dL/dx, [dWf | dbf] /
+// dL/dh), bit 2 = the coupling parameter gradients. Bit 2 reads only the workspace, Gx and the operands and puts its
+// split-K partials at the head of the G region, bit 1's at its tail, so a caller may run bit 2 on a second stream
+// (after bit 1's chain in stream order) while its own backward continues on the first.
 int wide_backward(const WideLayout& L, const float* prm, const float* pk, const float* h, const float* zn,
                   const float* dz, const float* dldj, const float* dvals, int nll, long long B, float* ws, float* dy,
-                  float* dh, float* dprm, hipStream_t st, const WideFold* fold = nullptr, int blo = 0, int bhi = -1) {
+                  float* dh, float* dprm, hipStream_t st, const WideFold* fold = nullptr, int blo = 0, int bhi = -1,
+                  int phase = 3) {
   if (B == 0) return BCNF_OK;
   if (bhi < 0) bhi = L.nb;
   if (blo < 0 || bhi > L.nb || blo >= bhi) return BCNF_ERR_ARG;
   ensure_lds_attrs();
   const WideWs w = carve(L, B, true, ws);
+  // the last range's dL/dx and [dWf | dbf] put their split-K partials at the END of the G region, the parameter
+  // gradients at its head, so phase 1 and phase 2 may run on two streams
+  const long long gfl_all = (long long)L.nv * L.NH * B * L.HP;
+  // (a need larger than the whole region reserves nothing: that GEMM runs unsplit, as it always did)
+  long long dx_need = (fold && fold->dx && blo == 0) ? (long long)L.nv * B * ((fold->Xp + 3) & ~3) : 0;
+  long long dwfb_need = (fold && fold->dwfb && blo == 0) ? (long long)L.nv * L.C * ((fold->Xp + 3) & ~3) : 0;
+  if (dx_need > gfl_all) dx_need = 0;
+  if (dwfb_need > gfl_all) dwfb_need = 0;
+  const long long tail = std::max(dx_need, dwfb_need);
   const long long slab = B * L.HP;
   const long long ld0 = (long long)L.nv * L.HP;
   const int vlo = blo * L.S, vhi = bhi * L.S, nvr = vhi - vlo;
@@ -2318,6 +2332,7 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
     *ld = L.HP;
     return w.dZ + ((long long)v * (L.NH - 1) + (l - 1)) * slab;
   };
+  if (phase & 1) {
   for (int v = vhi == L.nv ? L.nv : vhi - 1; v >= vlo; --v) {
     // link: tail-B(v) (v < nv), head-B(v-1)
     LinkBArgs a;
@@ -2362,16 +2377,32 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
       WCHK((gemm<true, true, EPI_GRAD>(g, 1, st)));
     }
   }
-  int rc = BCNF_OK;
-  const float* hp = fold ? nullptr : padded_h(L, h, B, w.Hp, st, &rc);
-  WCHK(rc);
-  float* const gsc = Gptr(vlo, 0);                  // the range's G slots: split-K scratch once its chain has run
-  const long long gsc_floats = (long long)nvr * L.NH * slab;
-  if (fold) {   // Gx rows of the range = dZ0_all[:, range]^T x1 (the condition-side gradients below go through it)
+  if (fold) {   // Gx rows of the range = dZ0_all[:, range]^T x1 (the condition-side gradients go through it)
     GemmArgs g = gemm_args(L.tiling, nvr * L.HP, fold->Xp, (int)B, w.dZ0 + (long long)vlo * L.HP, ld0, fold->x1,
                            fold->Xp, fold->gx + (long long)vlo * L.HP * fold->Xp, fold->Xp);
     WCHK((gemm<false, false, EPI_STORE>(g, 1, st)));
   }
+  // what needs every block (the last range): the feature side's gradients, split K = nv * HP per virtual block,
+  // partials in the tail of the G region (dead once the chain has run)
+  if (fold && fold->dx && blo == 0) {     // dL/dx = dZ0_all Wcb
+    GemmArgs g = gemm_args(L.tiling, (int)B, fold->Xp, L.nv * L.HP, w.dZ0, ld0, fold->wcb, fold->Xp, fold->dx, fold->Xp);
+    WCHK((gemm_splitk<true, false>(g, L.nv, w.G + gfl_all - tail, tail, st)));
+  }
+  if (fold && fold->dwfb && blo == 0) {   // [dWf | dbf] = W0h_all^T Gx
+    GemmArgs g = gemm_args(L.tiling, L.C, fold->Xp, L.nv * L.HP, pk + L.pk_w0h, L.Cp, fold->gx, fold->Xp, fold->dwfb, fold->Xp);
+    WCHK((gemm_splitk<false, false>(g, L.nv, w.G + gfl_all - tail, tail, st)));
+  }
+  if (!fold && dh && blo == 0) {   // dh = dZ0_all W0h_all
+    GemmArgs g = gemm_args(L.tiling, (int)B, L.C, L.nv * L.HP, w.dZ0, ld0, pk + L.pk_w0h, L.Cp, dh, L.C);
+    WCHK((gemm<true, false, EPI_STORE>(g, 1, st)));
+  }
+  }
+  if (!(phase & 2)) return BCNF_OK;
+  int rc = BCNF_OK;
+  const float* hp = fold ? nullptr : padded_h(L, h, B, w.Hp, st, &rc);
+  WCHK(rc);
+  float* const gsc = Gptr(vlo, 0);                  // the range's G slots: split-K scratch once its chain has run
+  const long long gsc_floats = std::min((long long)nvr * L.NH * slab, gfl_all - tail);
   // ---- parameter gradients of the range (canonical flat, every element written exactly once) ----
   if (dprm) {
     auto flat_groups = [&](GemmArgs& g) {   // group g1 = virtual block (or real block with S = 1 semantics)
@@ -2453,22 +2484,6 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
                          dprm, blo);
       WCHK(bcnf_rt::launched());
     }
-  }
-  if (blo > 0) return BCNF_OK;
-  if (fold) {
-    // split K = nv * HP per virtual block; partials in the G region (dead once the chain has run)
-    const long long gfl = (long long)L.nv * L.NH * slab;
-    if (fold->dwfb) {   // [dWf | dbf] = W0h_all^T Gx
-      GemmArgs g = gemm_args(L.tiling, L.C, fold->Xp, L.nv * L.HP, pk + L.pk_w0h, L.Cp, fold->gx, fold->Xp, fold->dwfb, fold->Xp);
-      WCHK((gemm_splitk<false, false>(g, L.nv, w.G, gfl, st)));
-    }
-    if (fold->dx) {     // dL/dx = dZ0_all Wcb
-      GemmArgs g = gemm_args(L.tiling, (int)B, fold->Xp, L.nv * L.HP, w.dZ0, ld0, fold->wcb, fold->Xp, fold->dx, fold->Xp);
-      WCHK((gemm_splitk<true, false>(g, L.nv, w.G, gfl, st)));
-    }
-  } else if (dh) {   // dh = dZ0_all W0h_all
-    GemmArgs g = gemm_args(L.tiling, (int)B, L.C, L.nv * L.HP, w.dZ0, ld0, pk + L.pk_w0h, L.Cp, dh, L.C);
-    WCHK((gemm<true, false, EPI_STORE>(g, 1, st)));
   }
   return BCNF_OK;
 }
@@ -2669,6 +2684,21 @@ int bcnf_wide_fold_backward(const BcnfStackDesc* desc, const float* params, cons
   WideFold f = {x1, wfb, wcb, gx_scratch, dwfb, dx, (int)xp};
   return wide_backward(L, params, (const float*)packed, nullptr, z, nullptr, nullptr, dloss, 1, batch,
                        (float*)workspace, nullptr, nullptr, dparams, (hipStream_t)stream, &f);
+}
+
+int bcnf_wide_fold_backward_phase(const BcnfStackDesc* desc, const float* params, const void* packed, const float* x1,
+                                  int32_t xp, const float* wfb, const float* wcb, const float* z, const float* dloss,
+                                  int64_t batch, void* workspace, float* gx_scratch, float* dparams, float* dwfb,
+                                  float* dx, int32_t phase, void* stream) {
+  WideLayout L;
+  WCHK(wide_layout(desc, &L));
+  if (batch < 1 || !params || !packed || !x1 || !wfb || !wcb || !z || !workspace || !gx_scratch || !dparams ||
+      xp < 4 || (xp & 3) || !aligned16(x1) || !aligned16(wfb) || !aligned16(wcb) || !aligned16(gx_scratch) ||
+      (dwfb && !aligned16(dwfb)) || (dx && !aligned16(dx)) || phase < 1 || phase > 3)
+    return BCNF_ERR_ARG;
+  WideFold f = {x1, wfb, wcb, gx_scratch, dwfb, dx, (int)xp};
+  return wide_backward(L, params, (const float*)packed, nullptr, z, nullptr, nullptr, dloss, 1, batch,
+                       (float*)workspace, nullptr, nullptr, dparams, (hipStream_t)stream, &f, 0, -1, phase);
 }
 
 int bcnf_wide_fold_backward_range(const BcnfStackDesc* desc, const float* params, const void* packed, const float* x1,

@@ -39,6 +39,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -96,6 +97,13 @@ class TrainStep:
             self.overlap_ranges = min(int(overlap_ranges), model.fused.cfg.n_blocks)
             self.capture = False
         dev = self.params[0].device
+        # wide family, ranges off, BCNF_WIDE_SIDE=1: the parameter-gradient phase of the folded backward overlaps the
+        # feature network's backward on a side stream. Off by default: measured same-box it gains 0.3%
+        # on FC_large and costs 5.6% on LSTM_large (the MIOpen RNN backward's serial kernels lose CUs to it)
+        self._side = None
+        if dev.type == "cuda" and self.overlap_ranges == 0 and isinstance(getattr(model, "fused", None), WideStack) \
+                and os.environ.get("BCNF_WIDE_SIDE", "0") != "0":
+            self._side = torch.cuda.Stream(device=dev)
         self._guard = None
         self._hist = None
         if dev.type == "cuda":
@@ -105,8 +113,24 @@ class TrainStep:
 
     # ------------------------------------------------------------------ step pieces
     def _forward_backward(self, y, traj, gather=None, adam=None):
-        with self._stack_hooks():
+        with self._stack_hooks(), self._side_overlap():
             return self._forward_backward_body(y, traj, gather, adam)
+
+    @contextlib.contextmanager
+    def _side_overlap(self):
+        """Wide family: the coupling parameter gradients on a second stream, overlapping the feature network's
+        backward (WideStack.side_stream); joined before anything reads the gradients (bucket pack, all-reduce, Adam).
+        Eager or captured alike (the fork and join are stream-event edges of the graph)."""
+        if self._side is None:
+            yield
+            return
+        st = self.model.fused
+        st.side_stream = self._side
+        try:
+            yield
+        finally:
+            st.side_stream = None
+            st.join_side(st.flat_param)
 
     def _forward_backward_body(self, y, traj, gather=None, adam=None):
         self.opt.zero_grad(set_to_none=True)

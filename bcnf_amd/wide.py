@@ -200,6 +200,22 @@ class WideStack(FusedStack):
     grad_bucket = None
     range_blocks = None
     on_range = None
+    # TrainStep: with side_stream set, the coupling parameter gradients (bcnf_wide_fold_backward_phase 2) run on it
+    # while the rest of the backward (the feature network's, fed by dL/dx from phase 1) continues on the launch
+    # stream; join_side() makes the launch stream wait for them (before the gradients are read).
+    side_stream = None
+    _side_pending = None
+
+    def join_side(self, param=None):
+        """The launch stream waits for the side-stream parameter gradients of the last backward (no-op if none)."""
+        pend, self._side_pending = self._side_pending, None
+        if pend is None:
+            return
+        ev, stream, ptr, _keep = pend
+        stream.wait_event(ev)
+        if param is not None and param.requires_grad and (param.grad is None or param.grad.data_ptr() != ptr):
+            # autograd copied the gradient (a clone on the launch stream) instead of adopting the side-stream buffer
+            raise RuntimeError("bcnf_amd: the side-stream coupling gradient was not adopted as .grad")
 
     def block_offset(self, block: int) -> int:
         """Canonical flat offset of real block `block` (block = nb: the parameter count)."""
@@ -229,6 +245,21 @@ class WideStack(FusedStack):
                 N.check(L.bcnf_wide_fold_backward_range(*args, ctypes.c_int32(lo), ctypes.c_int32(hi), stream),
                         "bcnf_wide_fold_backward_range")
                 self.on_range(off + self.block_offset(lo), off + self.block_offset(hi))
+        elif self.side_stream is not None:
+            if self._side_pending is not None:
+                raise RuntimeError("bcnf_amd: a side-stream backward is still pending (join_side() not called)")
+            cur = torch.cuda.current_stream(dev)
+            rc = self._timed("k_backward", lambda: L.bcnf_wide_fold_backward_phase(*args, ctypes.c_int32(1), stream))
+            N.check(rc, "bcnf_wide_fold_backward_phase")
+            side = self.side_stream
+            side.wait_stream(cur)
+            N.check(L.bcnf_wide_fold_backward_phase(*args, ctypes.c_int32(2), ctypes.c_void_p(side.cuda_stream)),
+                    "bcnf_wide_fold_backward_phase")
+            ev = torch.cuda.Event()
+            ev.record(side)
+            # everything phase 2 reads stays alive until the join (freed afterwards on the launch stream, so a reuse
+            # is ordered after the side stream's work); dparams itself must be adopted as .grad, not copied
+            self._side_pending = (ev, cur, dparams.data_ptr(), (ws, pk, x1, wfb, wcb, z, dvals, gx, self.flat))
         else:
             rc = self._timed("k_backward", lambda: L.bcnf_wide_fold_backward(*args, stream))
             N.check(rc, "bcnf_wide_fold_backward")

@@ -411,6 +411,15 @@ int bcnf_wide_fold_backward_range(const BcnfStackDesc* desc, const float* params
                                   int32_t xp, const float* wfb, const float* wcb, const float* z, const float* dloss,
                                   int64_t batch, void* workspace, float* gx_scratch, float* dparams, float* dwfb,
                                   float* dx, int32_t block_lo, int32_t block_hi, void* stream);
+/* bcnf_wide_fold_backward in two phases, for a caller that overlaps the coupling parameter gradients with the rest of
+ * its own backward (the feature network's, trainer.py:244-277 runs both in one loss.backward()): phase 1 writes dx and
+ * dwfb (and gx_scratch), phase 2 writes dparams; phase 2 must follow phase 1 in stream order (a second stream waiting
+ * on an event recorded after phase 1 is the intended use) and both must finish before the next call on the same
+ * workspace. phase 3 = both, one stream. Results equal one bcnf_wide_fold_backward call bit for bit. */
+int bcnf_wide_fold_backward_phase(const BcnfStackDesc* desc, const float* params, const void* packed, const float* x1,
+                                  int32_t xp, const float* wfb, const float* wcb, const float* z, const float* dloss,
+                                  int64_t batch, void* workspace, float* gx_scratch, float* dparams, float* dwfb,
+                                  float* dx, int32_t phase, void* stream);
 /* Canonical flat offset of real block `block`'s first trainable parameter (its ActNorm, cnf.py:296-335 module order);
  * block = nb gives the parameter count. Host-only. */
 int bcnf_wide_block_offset(const BcnfStackDesc* desc, int32_t block, int64_t* offset);

@@ -67,3 +67,74 @@ def test_range_backward_equals_one_call(two_way, ranges):
     assert seen[0][1] == 5 + st.flat.numel() and seen[-1][0] == 5        # the slices tile the coupling gradient
     assert all(seen[i][0] == seen[i + 1][1] for i in range(len(seen) - 1))
     assert torch.equal(bucket[5:5 + st.flat.numel()], ref[0])
+
+
+def _cfg_deep(two_way):
+    c = _cfg(two_way)
+    c["feature_networks"][1]["kwargs"]["sizes"] = [90, 64, 80]     # a layer below the folded Linear: its backward
+    return c                                                       # runs on the launch stream during phase 2
+
+
+def _side_grads(m, y, traj, side):
+    st = m.fused
+    m.zero_grad(set_to_none=True)
+    st.flat_param.grad = None
+    st.set_seed(7)
+    st.side_stream = side
+    try:
+        vals = m.nll_loss(y, traj)
+        torch.autograd.backward(vals, torch.tensor([1.0, 0.0, 0.0], device=DEV))
+    finally:
+        st.side_stream = None
+        st.join_side(st.flat_param)
+    return [st.flat_param.grad.clone(), vals.detach().clone()] + \
+        [p.grad.clone() for p in m.feature_network_stack.parameters()]
+
+
+@pytest.mark.parametrize("two_way", [False, True], ids=["one_way", "two_way"])
+@pytest.mark.parametrize("B", [77, 1024])
+def test_side_stream_backward_equals_one_call(two_way, B):
+    """bcnf_wide_fold_backward_phase: phase 1 (chain, dL/dx, Gx, [dWf | dbf]) on the launch stream, phase 2 (the
+    coupling parameter gradients) on a side stream while the feature layer below the fold runs its backward: equal
+    to the one-call backward bit for bit, and the side buffer is what autograd adopted as .grad."""
+    from bcnf_amd import CondRealNVP_v2
+    from bcnf_amd.wide import WideStack
+    torch.manual_seed(3)
+    m = CondRealNVP_v2.from_config(_cfg_deep(two_way)).to(DEV).train()
+    m.flat_parameters()
+    assert isinstance(m.fused, WideStack)
+    g = torch.Generator().manual_seed(4)
+    y = torch.randn(B, 19, generator=g).to(DEV)
+    traj = torch.randn(B, 30, 3, generator=g).to(DEV)
+    ref = _side_grads(m, y, traj, None)
+    side = torch.cuda.Stream()
+    for _ in range(2):
+        got = _side_grads(m, y, traj, side)
+        torch.cuda.synchronize()
+        assert len(got) == len(ref)
+        for a, b in zip(ref, got):
+            assert torch.equal(a, b)
+
+
+def test_side_stream_trainstep_equals_single_stream(monkeypatch):
+    """TrainStep (captured) with the side-stream parameter gradients (BCNF_WIDE_SIDE=1) vs without: identical parameters after
+    three steps (the join precedes Adam in the graph)."""
+    from bcnf_amd import CondRealNVP_v2
+    from bcnf_amd.train import TrainStep
+    g = torch.Generator().manual_seed(5)
+    y = torch.randn(256, 19, generator=g).to(DEV)
+    traj = torch.randn(256, 30, 3, generator=g).to(DEV)
+    out = []
+    for side in ("1", "0"):
+        monkeypatch.setenv("BCNF_WIDE_SIDE", side)
+        torch.manual_seed(3)
+        m = CondRealNVP_v2.from_config(_cfg_deep(True)).to(DEV).train()
+        ts = TrainStep(m, capture=True)
+        assert (ts._side is not None) == (side == "1")
+        m.fused.set_seed(11)
+        vals = [ts.step(y, traj) for _ in range(3)]
+        torch.cuda.synchronize()
+        out.append((vals, [p.detach().clone() for p in m.parameters()]))
+    assert out[0][0] == out[1][0]
+    for a, b in zip(out[0][1], out[1][1]):
+        assert torch.equal(a, b)
