@@ -49,6 +49,11 @@ for s in $STEPS; do
         else BCNF_AMD_LIB=$lib timeout -k 10 200 python bench.py --no-secondary --no-cpu-baseline > gpurun_out/${T}_abb.json 2>/dev/null; fi
         python -c "import json; d=json.loads(open('gpurun_out/${T}_abb.json').read().strip().splitlines()[-1]); print('$lib', d['ms_per_step'], round(d['value']), d['kernels_us'])"
       done; done 2>&1 | tee gpurun_out/${T}_abbench.txt ;;
+    abwl)
+      for i in 1 2; do for wl in ${WLS:-fc_large}; do for lib in ${AB_LIBS:-build_exp/libprev.so}; do
+        BCNF_AMD_LIB=$lib timeout -k 10 200 python bench.py --workload $wl --no-secondary --no-cpu-baseline --steps 20 --warmup 5 > gpurun_out/${T}_abw.json 2>/dev/null
+        python -c "import json; d=json.loads(open('gpurun_out/${T}_abw.json').read().strip().splitlines()[-1]); print('$wl $lib', d['ms_per_step'], round(d['value']), d.get('kernels_us'))"
+      done; done; done 2>&1 | tee gpurun_out/${T}_abwl.txt ;;
     abside)
       for i in 1 2; do for wl in fc_large lstm_large; do for sd in 1 0; do
         BCNF_WIDE_SIDE=$sd timeout -k 10 200 python bench.py --workload $wl --no-cpu-baseline --steps 20 --warmup 5 > gpurun_out/${T}_abs.json 2>/dev/null
