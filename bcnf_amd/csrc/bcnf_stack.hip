@@ -1696,7 +1696,10 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
       const long long src = raw_row(R, B, bc);
       ya = (j < Da) ? R.ypool[src * D + j] : 0.f;
       yb = (j < Db) ? R.ypool[src * D + Da + j] : 0.f;
-      const int C = L.C, X = R.X, XQ = (X + 3) >> 2;              // float4 quads per row (<= RAW_KP / 4 - 1)
+      // float4 quads staged per Wf row: whole 16-column K steps of the h GEMM (<= RAW_KP / 4 - 1), the quads past
+      // column X as zeros -- the K loop reads them, and LDS holds whatever the previous kernel left there (a 0 x NaN
+      // residue made the loss NaN when only the ceil(X / 4) quads holding columns were staged)
+      const int C = L.C, X = R.X, XQP = ((X + 15) >> 4) * 4;
       float* ws = hs + 16 * raw_hs_pitch(C);                      // Wf [C][RAW_KP]
       float* xs = ws + C * RAW_KP;                                // x rows [16][RAW_KP]
       const int cw = __builtin_amdgcn_readfirstlane(tid >> 6), l64 = tid & 63, lr = l64 & 15, lq = l64 >> 4;
@@ -1716,11 +1719,11 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
         // quad element by element
         const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(R.wf), (short)0,
                                                                            C * X * 4, 0x00020000);
-        const int nq = C * XQ;
+        const int nq = C * XQP;
         uint32_t v[RAW_WQ][4];
 #pragma unroll
         for (int u = 0; u < RAW_WQ; ++u) {
-          const int i = tid + u * BCNF_WG, ii = i < nq ? i : 0, c = ii / XQ, q = ii - c * XQ;
+          const int i = tid + u * BCNF_WG, ii = i < nq ? i : 0, c = ii / XQP, q = ii - c * XQP;
           const auto w = __builtin_amdgcn_raw_buffer_load_b128(rW, (c * X + 4 * q) * 4, 0, 0);
           v[u][0] = w[0]; v[u][1] = w[1]; v[u][2] = w[2]; v[u][3] = w[3];
         }
@@ -1744,7 +1747,7 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int u = 0; u < RAW_WQ; ++u) {
-          const int i = tid + u * BCNF_WG, c = i / XQ, q = i - c * XQ;
+          const int i = tid + u * BCNF_WG, c = i / XQP, q = i - c * XQP;
           if (i < nq) {
             floatx4 o;
 #pragma unroll
@@ -1752,8 +1755,8 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
             *reinterpret_cast<floatx4*>(ws + c * RAW_KP + 4 * q) = o;
           }
         }
-        for (int i = nq > RAW_WQ * BCNF_WG ? tid + RAW_WQ * BCNF_WG : nq; i < nq; i += BCNF_WG) {   // C X > 7680
-          const int c = i / XQ, q = i - c * XQ;
+        for (int i = nq > RAW_WQ * BCNF_WG ? tid + RAW_WQ * BCNF_WG : nq; i < nq; i += BCNF_WG) {   // C XQP > 2048
+          const int c = i / XQP, q = i - c * XQP;
           const auto w = __builtin_amdgcn_raw_buffer_load_b128(rW, (c * X + 4 * q) * 4, 0, 0);
           floatx4 o;
 #pragma unroll

@@ -6,6 +6,7 @@ test_gpu_train.py. The fold computes the same sums reassociated, so the gate is 
 2e-6 relative, gradients within rtol 1e-4 / atol 1e-5 of the unfolded path (their own tolerance vs the fp64
 oracle is 1e-4 as well)."""
 import copy
+import math
 
 import numpy as np
 import pytest
@@ -263,6 +264,32 @@ def test_raw_forward_equals_pack_forward(g1, B, train):
     for a, b, what in ((g1_, g0, "stack"), (w1, w0, "feature W"), (b1, b0, "feature b")):
         ok, err = close(a.cpu(), b.cpu(), rtol=1e-4, floor=1e-5)
         assert ok, (what, err)
+
+
+@pytest.mark.parametrize("train", [False, True])
+@pytest.mark.parametrize("B", [64, 4096])
+def test_raw_forward_after_unfused_forward(B, train):
+    """The smoke's sequence (random init, an unfused training forward, then the fused NLL): the unfused launches leave
+    non-finite values in LDS, and the pack-free forward's h GEMM reads Wf's K padding (columns 90 .. 95 of FC_small)
+    from LDS -- staged as zeros, so the loss stays finite and equals the two-launch form (parity unpinned beyond
+    that: random init, no reference fixture)."""
+    from bcnf_amd import CondRealNVP_v2
+    cfg = copy.deepcopy(FC_SMALL_CFG)
+    del cfg["feature_networks"][1]["kwargs"]["dropout"]
+    gen = torch.Generator().manual_seed(1)
+    y = torch.randn(B, 19, generator=gen).to(DEV)
+    traj = torch.randn(B, 30, 3, generator=gen).to(DEV)
+    res = []
+    for raw in (True, False):
+        torch.manual_seed(2024_03_25)
+        m = CondRealNVP_v2.from_config(cfg).to(DEV).train()
+        m.fused.set_seed(3)
+        with torch.no_grad():
+            m(y, traj, log_det_J=True)
+        m.fused.use_raw_forward = raw
+        m.train(train)
+        res.append(m.nll_loss(y, traj)[0].item())
+    assert math.isfinite(res[0]) and abs(res[0] - res[1]) <= 2e-6 * abs(res[1]) + 1e-6, res
 
 
 @pytest.mark.parametrize("nb", [2, 3])
