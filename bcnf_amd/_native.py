@@ -34,7 +34,7 @@ EXPORTS = (
     "bcnf_inverse_scratch_bytes", "bcnf_stack_dh", "bcnf_backward_tail", "bcnf_gather_rows2",
     "bcnf_gather_batch", "bcnf_advance_counters", "bcnf_fold_bytes", "bcnf_fold_slab_bytes",
     "bcnf_pack_params_fold", "bcnf_fold_nll_forward", "bcnf_fold_backward_tail",
-    "bcnf_fold_raw_table_bytes", "bcnf_fold_raw_table", "bcnf_fold_train_forward",
+    "bcnf_fold_raw_table_bytes", "bcnf_fold_raw_table", "bcnf_fold_train_forward", "bcnf_lds_fill",
     "bcnf_wide_supported", "bcnf_wide_param_count", "bcnf_wide_packed_bytes", "bcnf_wide_workspace_bytes", "bcnf_wide_inverse_scratch_bytes",
     "bcnf_wide_pack", "bcnf_wide_forward", "bcnf_wide_nll_finalize", "bcnf_wide_backward", "bcnf_wide_inverse",
     "bcnf_wide_fold_prepare", "bcnf_wide_fold_forward", "bcnf_wide_fold_backward", "bcnf_wide_proj_rows",
@@ -150,6 +150,7 @@ def _bind(lib):
         "bcnf_fold_nll_forward": (_i32, [_pdesc, _vp, _vp, _i32, _vp, _vp, _i32, _i64, _vp, _vp, _i32, _vp, _vp,
                                          _i32, _vp, _vp, _vp]),
         "bcnf_fold_raw_table_bytes": (_i32, [_pdesc, _i32, _pi64]),
+        "bcnf_lds_fill": (_i32, [ctypes.c_float, _vp]),
         "bcnf_fold_raw_table": (_i32, [_pdesc, _i32, _vp]),
         "bcnf_fold_train_forward": (_i32, [_pdesc, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _i64, _vp,
                                            _vp, _vp, _i32, _vp, _vp, _i32, _vp, _vp, _vp]),

@@ -24,7 +24,7 @@
 #include <vector>
 
 // Experiment switches of the pack-free forward (timing probes only, results wrong): 1 no side outputs, 2 no h GEMM,
-// 4 no record gathers, 8 no ldc sum, 16 no x loads, 32 no Wf / bf loads
+// 4 no record gathers, 8 no ldc sum, 16 no x loads, 32 no Wf / bf loads, 64 no zeroed K padding (the NaN regression)
 #ifndef BCNF_RAW_EXP
 #define BCNF_RAW_EXP 0
 #endif
@@ -1696,10 +1696,10 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
       const long long src = raw_row(R, B, bc);
       ya = (j < Da) ? R.ypool[src * D + j] : 0.f;
       yb = (j < Db) ? R.ypool[src * D + Da + j] : 0.f;
-      // float4 quads staged per Wf row: whole 16-column K steps of the h GEMM (<= RAW_KP / 4 - 1), the quads past
-      // column X as zeros -- the K loop reads them, and LDS holds whatever the previous kernel left there (a 0 x NaN
-      // residue made the loss NaN when only the ceil(X / 4) quads holding columns were staged)
-      const int C = L.C, X = R.X, XQP = ((X + 15) >> 4) * 4;
+      // float4 quads per row (<= RAW_KP / 4 - 1): XQ hold columns; the h GEMM's K steps run to XQP, so Wf's quads
+      // XQ .. XQP - 1 are stored as zeros -- LDS holds whatever the previous kernel left there, and a 0 x NaN residue
+      // made the loss NaN
+      const int C = L.C, X = R.X, XQ = (X + 3) >> 2, XQP = ((X + 15) >> 4) * 4;
       float* ws = hs + 16 * raw_hs_pitch(C);                      // Wf [C][RAW_KP]
       float* xs = ws + C * RAW_KP;                                // x rows [16][RAW_KP]
       const int cw = __builtin_amdgcn_readfirstlane(tid >> 6), l64 = tid & 63, lr = l64 & 15, lq = l64 >> 4;
@@ -1719,11 +1719,16 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
         // quad element by element
         const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(R.wf), (short)0,
                                                                            C * X * 4, 0x00020000);
-        const int nq = C * XQP;
+        // the K padding quads first: their stores need no load and go out before the staging round trip
+        for (int i = (BCNF_RAW_EXP & 64) ? C * (XQP - XQ) : tid; i < C * (XQP - XQ); i += BCNF_WG) {
+          const int c = i / (XQP - XQ), q = XQ + (i - c * (XQP - XQ));
+          *reinterpret_cast<floatx4*>(ws + c * RAW_KP + 4 * q) = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+        const int nq = C * XQ;
         uint32_t v[RAW_WQ][4];
 #pragma unroll
         for (int u = 0; u < RAW_WQ; ++u) {
-          const int i = tid + u * BCNF_WG, ii = i < nq ? i : 0, c = ii / XQP, q = ii - c * XQP;
+          const int i = tid + u * BCNF_WG, ii = i < nq ? i : 0, c = ii / XQ, q = ii - c * XQ;
           const auto w = __builtin_amdgcn_raw_buffer_load_b128(rW, (c * X + 4 * q) * 4, 0, 0);
           v[u][0] = w[0]; v[u][1] = w[1]; v[u][2] = w[2]; v[u][3] = w[3];
         }
@@ -1747,7 +1752,7 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int u = 0; u < RAW_WQ; ++u) {
-          const int i = tid + u * BCNF_WG, c = i / XQP, q = i - c * XQP;
+          const int i = tid + u * BCNF_WG, c = i / XQ, q = i - c * XQ;
           if (i < nq) {
             floatx4 o;
 #pragma unroll
@@ -1755,8 +1760,8 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
             *reinterpret_cast<floatx4*>(ws + c * RAW_KP + 4 * q) = o;
           }
         }
-        for (int i = nq > RAW_WQ * BCNF_WG ? tid + RAW_WQ * BCNF_WG : nq; i < nq; i += BCNF_WG) {   // C XQP > 2048
-          const int c = i / XQP, q = i - c * XQP;
+        for (int i = nq > RAW_WQ * BCNF_WG ? tid + RAW_WQ * BCNF_WG : nq; i < nq; i += BCNF_WG) {   // C X > 7680
+          const int c = i / XQ, q = i - c * XQ;
           const auto w = __builtin_amdgcn_raw_buffer_load_b128(rW, (c * X + 4 * q) * 4, 0, 0);
           floatx4 o;
 #pragma unroll
@@ -2706,6 +2711,14 @@ __global__ __launch_bounds__(BCNF_WG) void k_red_gx(BcnfLayout L, long long tota
   reduce_body(L, slab, stride, nwg, dparams, bx - n_gx, smem);
 }
 
+// Test hook: the whole dynamic LDS of the workgroup set to `value` (bcnf_lds_fill).
+__global__ __launch_bounds__(BCNF_WG) void k_fill_lds(float value) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  for (int i = threadIdx.x; i < (int)(LDS_MAX / 16); i += BCNF_WG)
+    reinterpret_cast<floatx4*>(smem)[i] = floatx4{value, value, value, value};
+  __syncthreads();
+}
+
 // ------------------------------------------------------------------------------------------------
 // Launch helpers
 // ------------------------------------------------------------------------------------------------
@@ -3130,6 +3143,14 @@ int bcnf_fold_nll_forward(const BcnfStackDesc* desc, const void* packed, const f
   if (!fold || ldx < in_features) return BCNF_ERR_ARG;
   return forward_impl(desc, packed, y, x, batch, z, ldj, nullptr, training, rng_state, workspace, true, true,
                       finalize != 0, loss_out, guard, stream, fold, in_features, ldx);
+}
+
+int bcnf_lds_fill(float value, void* stream) {
+  size_t lds = LDS_MAX;
+  const int rc = launch_lds(k_fill_lds, lds);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_fill_lds, dim3(4 * 256), dim3(BCNF_WG), LDS_MAX, (hipStream_t)stream, value);
+  return check_launch();
 }
 
 int bcnf_fold_raw_table_bytes(const BcnfStackDesc* desc, int32_t in_features, int64_t* bytes) {

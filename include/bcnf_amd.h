@@ -186,6 +186,10 @@ int bcnf_fold_train_forward(const BcnfStackDesc* desc, const float* params, cons
                             int64_t batch, void* packed, float* z, float* ldj, int32_t training,
                             uint64_t* rng_state, void* workspace, int32_t finalize, float* loss_out, int32_t* guard,
                             void* stream);
+/* Test hook (no reference counterpart): fill every CU's LDS with `value` (one full-LDS workgroup per CU, several
+ * rounds), so a test can check that a following launch never reads LDS it did not write (the pack-free forward's
+ * K padding, tests/test_gpu_fold.py). */
+int bcnf_lds_fill(float value, void* stream);
 /* Adam fused into bcnf_fold_backward_tail (nullable argument): every gradient the tail produces -- the flat coupling
  * parameters (slot 0), the feature Linear's weight (1) and bias (2, NULL without bias) -- also takes its
  * torch.optim.Adam update where it is produced, with the end-of-step bookkeeping of bcnf_adam_step_bookkeep

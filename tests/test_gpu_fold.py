@@ -6,6 +6,7 @@ test_gpu_train.py. The fold computes the same sums reassociated, so the gate is 
 2e-6 relative, gradients within rtol 1e-4 / atol 1e-5 of the unfolded path (their own tolerance vs the fp64
 oracle is 1e-4 as well)."""
 import copy
+import ctypes
 import math
 
 import numpy as np
@@ -288,6 +289,9 @@ def test_raw_forward_after_unfused_forward(B, train):
             m(y, traj, log_det_J=True)
         m.fused.use_raw_forward = raw
         m.train(train)
+        from bcnf_amd import _native as N
+        N.check(N.lib().bcnf_lds_fill(ctypes.c_float(float("nan")), N.stream_handle(y.device)),
+                "bcnf_lds_fill")                 # the residue the smoke met, made certain
         res.append(m.nll_loss(y, traj)[0].item())
     assert math.isfinite(res[0]) and abs(res[0] - res[1]) <= 2e-6 * abs(res[1]) + 1e-6, res
 
