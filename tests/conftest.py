@@ -95,3 +95,19 @@ def large_proxy_sd(model, seed):
             a = rng.uniform(-0.05, 0.05, size=shape)
         sd[k] = a.astype(np.float32)
     return sd
+
+
+@pytest.fixture(autouse=True)
+def _lds_poison(request):
+    """BCNF_LDS_POISON=1: every GPU test starts with every CU's LDS filled with NaN (bcnf_lds_fill), so a kernel that
+    reads LDS it did not write shows up as a non-finite result instead of depending on what ran before."""
+    import os
+    if os.environ.get("BCNF_LDS_POISON") != "1" or request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    import ctypes
+    import torch
+    from bcnf_amd import _native as N
+    dev = torch.device("cuda", torch.cuda.current_device())
+    N.check(N.lib().bcnf_lds_fill(ctypes.c_float(float("nan")), N.stream_handle(dev)), "bcnf_lds_fill")
+    yield
