@@ -621,10 +621,10 @@ def secondary_figures(step, args, device, n_loop=50, n_trainer=12):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(n_loop):
-        step.step_epoch()
+        last = step.step_epoch()
     dt = time.perf_counter() - t0
     out["trainer_loop_shape"] = {"value": round(B * n_loop / dt, 1), "unit": "samples/s",
-                                 "ms_per_step": round(dt / n_loop * 1e3, 4), "steps": n_loop,
+                                 "ms_per_step": round(dt / n_loop * 1e3, 4), "steps": n_loop, "last_loss": last[0],
                                  "what": "captured step + host sync + 3 logged values read per step"}
     from torch.utils.data import DataLoader, TensorDataset
     from bcnf_amd.data import simulate
@@ -657,7 +657,7 @@ def secondary_figures(step, args, device, n_loop=50, n_trainer=12):
         t_prev = time.perf_counter()
         for data in loader:                      # the DataLoader's fetch + collate is inside the timing
             yb, *conds = data
-            train_batch(yb, *conds)
+            last = train_batch(yb, *conds)
             now = time.perf_counter()
             times.append(now - t_prev)
             t_prev = now
@@ -666,7 +666,7 @@ def secondary_figures(step, args, device, n_loop=50, n_trainer=12):
                 break
     med = statistics.median(times[3:])
     out["unchanged_trainer"] = {"value": round(B / med, 1), "unit": "samples/s", "ms_per_step": round(med * 1e3, 3),
-                                "steps": n_trainer,
+                                "steps": n_trainer, "last_loss": last[0],
                                 "what": "Trainer._train_batch restated + host DataLoader (num_workers=0), torch Adam"}
     return out
 
