@@ -54,7 +54,7 @@ for s in $STEPS; do
         BCNF_AMD_LIB=$lib timeout -k 10 200 python bench.py --workload $wl --no-secondary --no-cpu-baseline --steps 20 --warmup 5 > gpurun_out/${T}_abw.json 2>/dev/null
         python -c "import json; d=json.loads(open('gpurun_out/${T}_abw.json').read().strip().splitlines()[-1]); print('$wl $lib', d['ms_per_step'], round(d['value']), d.get('kernels_us'))"
       done; done; done 2>&1 | tee gpurun_out/${T}_abwl.txt ;;
-    abunroll)
+    abunroll)   # r04zj only: the BCNF_EPOCH_UNROLL / BCNF_REMAINDER_GRAPH switches were a temporary build of train.py
       for i in 1 2; do for K in 20 50; do for cfg in "8 0" "8 1" "16 1"; do set -- $cfg
         BCNF_EPOCH_UNROLL=$1 BCNF_REMAINDER_GRAPH=$2 timeout -k 10 200 python bench.py --no-secondary --no-cpu-baseline --steps $K > gpurun_out/${T}_abu.json 2>/dev/null
         python -c "import json; d=json.loads(open('gpurun_out/${T}_abu.json').read().strip().splitlines()[-1]); print('K=$K unroll=$1 rem=$2', d['ms_per_step'], round(d['value']))"
