@@ -16,7 +16,6 @@ There is no CPU path for the coupling stack: CPU tensors raise.
 from __future__ import annotations
 
 import math
-import weakref
 from abc import abstractmethod
 from typing import Any
 
@@ -27,7 +26,7 @@ import torch.nn as nn
 
 from bcnf_amd.factories import FeatureNetworkFactory, LayerFactory
 from bcnf_amd.feature_network import (ConcatenateCondition, FeatureNetwork, FeatureNetworkStack,
-                                      FullyConnectedFeatureNetwork, HIPLinear, LSTMFeatureNetwork)
+                                      FullyConnectedFeatureNetwork, HIPLinear, LSTMFeatureNetwork, bind_rng_owner)
 from bcnf_amd.fft_stack import FFTWideStack
 from bcnf_amd.fused import FusedStack, StackConfig, stack_forward, stack_inverse, stack_nll, stack_nll_fold
 from bcnf_amd.layers import AnyGLU, LinearFFTEnriched
@@ -337,10 +336,43 @@ class CondRealNVP_v2(ConditionalInvertibleLayer):
         self.layers.append(ConditionalAffineCouplingLayer(self.size, self.nested_sizes, self.n_conditions,
                                                           **coupling_kwargs))
         self._build_fused()
-        if n_conditions > 0:       # the fused feature dropout draws from the coupling's device Philox state
-            for fn in self.feature_network_stack.feature_networks:
+        self._bind_feature_rng()
+
+    def _bind_feature_rng(self):
+        """The fused feature dropout draws from this model's coupling device Philox state (bind_rng_owner)."""
+        fns = getattr(self, "feature_network_stack", None)
+        if self.n_conditions > 0 and fns is not None:
+            for fn in fns.feature_networks:
                 if isinstance(fn, FullyConnectedFeatureNetwork):
-                    fn._rng_owner = weakref.ref(self)
+                    bind_rng_owner(fn, self)
+
+    # copy.deepcopy / pickle: the fused stack (ctypes descriptor, flat buffers whose views ARE the parameters, a grad
+    # hook bound to this model's stack) is not copied; the copy rebuilds its own over its copied parameters and carries
+    # the stack's gradient mode and dropout Philox state (seed, device offset), and its feature networks follow the
+    # copy's state
+    def __getstate__(self):
+        state = self.__dict__.copy()
+        fused = state.pop("_fused", None)
+        if fused is not None:
+            rng = getattr(fused, "_rng_state", None)
+            state["_fused_carry"] = (getattr(fused, "grad_mode", None), getattr(fused, "seed", None),
+                                     rng.detach().clone() if rng is not None else None)
+        return state
+
+    def __setstate__(self, state):
+        carry = state.pop("_fused_carry", None)
+        super().__setstate__(state)
+        if carry is not None:
+            self._build_fused()
+            fused = self._fused
+            grad_mode, seed, rng = carry
+            if grad_mode is not None and hasattr(fused, "grad_mode"):
+                fused.grad_mode = grad_mode
+            if hasattr(fused, "seed"):
+                fused.seed = seed
+            if rng is not None and getattr(fused, "flat", None) is not None:
+                fused._rng_state = rng.to(fused.flat.device)
+        self._bind_feature_rng()
 
     # ------------------------------------------------------------------ fused stack plumbing
     def _canonical(self):

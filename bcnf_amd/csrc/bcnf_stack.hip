@@ -1192,10 +1192,26 @@ struct RecB {   // consumption order (make_layout): ActNorm, Q^T, T / S heads, h
 // Activation record a training forward saves per (block, sample, lane) for the backward, so the backward never
 // recomputes the MLP: masked activations, masked GELU derivatives, tanh(s) and the block input, 2 NH + 3 floats
 // stored as AR4 float4 [k][workgroup][AR4][256 threads] plus AR1 floats [k][workgroup][AR1][256] (no padding).
+// Order (r05): (activation, derivative) of hidden layer 1, 2, ..., then y_a, y_b, tanh(s) -- a float4 is complete
+// every two layers and the forward stores it there (ready_layer), spread over the block. Measured: the
+// record writes cost k_forward ~7 us (an ablation without them: 57 -> 50 us), the same whether the stores go out in
+// one burst after the coupling, spread like this, or from the helper waves through LDS -- the cost is the 132 MB of
+// writes in the memory system, not the issuing wave.
 template <int NH>
 struct ActRec {
-  static constexpr int ACT = 0, GD = NH, S = 2 * NH, YA = 2 * NH + 1, YB = 2 * NH + 2;
+  static constexpr int YA = 2 * NH, YB = 2 * NH + 1, S = 2 * NH + 2;
   static constexpr int AR = 2 * NH + 3, AR4 = AR / 4, AR1 = AR - 4 * AR4;
+  __host__ __device__ static constexpr int act(int l) { return 2 * l; }   // hidden layer l + 1
+  __host__ __device__ static constexpr int gd(int l) { return 2 * l + 1; }
+  // the hidden layer (1-based) after which float4 q is complete; NH + 1: only after tanh(s)
+  __host__ __device__ static constexpr int ready_layer(int q) {
+    int r = 0;
+    for (int i = 4 * q; i < 4 * q + 4; ++i) {
+      const int li = i < 2 * NH ? i / 2 + 1 : (i == S ? NH + 1 : 0);
+      r = li > r ? li : r;
+    }
+    return r;
+  }
 };
 
 // Burst-load floats [lo, hi) of this lane's LDS record into registers (compile-time indices, so the
@@ -1267,6 +1283,74 @@ __device__ __forceinline__ void mlp_forward_m(const float* __restrict__ rr, floa
   T = rr[F::T + 16];
   Sp = rr[F::S + 16];
   rot16x2(a, rr + F::T, T, a, rr + F::S, Sp);
+}
+
+// Streamed form for k_forward's compute waves (r05). The record is read in consumption order: before stage l (hidden
+// layer l = 1..NH, then NH + 1 = the T / S heads, NH + 2 = the mix) the wave issues the quads stage l + FWD_AHEAD
+// ends in, behind a scheduling barrier, so each lgkmcnt wait covers reads issued two layers earlier. (r04's
+// burst form ld_rec<FWD_HEAD, USED> let hipcc issue 17 reads after layer 1 and wait for all of them at once, then
+// 4 and 8 more each with a wait one GELU later: five exposed LDS round trips per block under four waves' load.)
+constexpr int FWD_AHEAD = 2;
+template <int NH>
+__host__ __device__ constexpr int rf_stage_end(int l) {   // exclusive end (floats) of what stage l reads
+  return l <= NH ? 24 + 17 * (l - 1) : (l == NH + 1 ? RecF<NH>::S + 17 : RecF<NH>::USED);
+}
+template <int NH>
+__host__ __device__ constexpr int rf_stage_q(int l) {     // quads issued once stage l's reads are out
+  // at most 8 new quads per stage (lgkmcnt tracks 15 outstanding: a 16-read burst at the last layer made hipcc wait
+  // for its oldest reads at once); whatever the cap defers goes out with the next stage, all of it by the mix
+  int q = 6;
+  for (int i = 1; i <= l; ++i) {
+    const int want = (rf_stage_end<NH>(i + FWD_AHEAD < NH + 2 ? i + FWD_AHEAD : NH + 2) + 3) / 4;
+    q = i >= NH + 2 ? want : (want < q + 8 ? want : q + 8);
+  }
+  return q;
+}
+template <int NH>
+__device__ __forceinline__ void rf_issue(float* __restrict__ rr, const float* __restrict__ R, int l) {
+  const floatx4* R4 = reinterpret_cast<const floatx4*>(R);
+#pragma unroll
+  for (int q = rf_stage_q<NH>(l - 1); q < rf_stage_q<NH>(l); ++q) {
+    const floatx4 v = R4[q];
+    rr[4 * q] = v.x;
+    rr[4 * q + 1] = v.y;
+    rr[4 * q + 2] = v.z;
+    rr[4 * q + 3] = v.w;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+// KEEP: the activation record goes to ar (ActRec order), and emit(q) is called right after float4 q is complete.
+template <int NH, bool KEEP, bool DROP, typename Emit>
+__device__ __forceinline__ void mlp_forward_s(float* __restrict__ rr, const float* __restrict__ R, float x, float hp,
+                                              const float* __restrict__ msk, float& T, float& Sp, float* ar,
+                                              Emit&& emit) {
+  static_assert(RecF<NH>::HID == 24, "stage 1 reads only the prefetched head (FWD_HEAD = 24)");
+  using F = RecF<NH>;
+  using AR = ActRec<NH>;
+  float a = x;
+#pragma unroll
+  for (int l = 1; l <= NH; ++l) {
+    rf_issue<NH>(rr, R, l);
+    const float* w = (l == 1) ? rr + F::W1 : rr + F::HID + 17 * (l - 2);
+    const float pre = rot16(a, w, (l == 1) ? hp : w[16]);
+    if (KEEP) {
+      float g, dg;
+      gelu_fg(pre, g, dg);
+      a = DROP ? g * msk[l - 1] : g;
+      ar[AR::act(l - 1)] = a;
+      ar[AR::gd(l - 1)] = DROP ? dg * msk[l - 1] : dg;
+#pragma unroll
+      for (int q = 0; q < AR::AR4; ++q)
+        if (AR::ready_layer(q) == l) emit(q);
+    } else {
+      a = DROP ? gelu_f(pre) * msk[l - 1] : gelu_f(pre);
+    }
+  }
+  rf_issue<NH>(rr, R, NH + 1);
+  T = rr[F::T + 16];
+  Sp = rr[F::S + 16];
+  rot16x2(a, rr + F::T, T, a, rr + F::S, Sp);
+  rf_issue<NH>(rr, R, NH + 2);   // (empty: the mix's quads went out with stage NH)
 }
 
 // Row-layout orthonormal mix: (na, nb) = (a, b) @ M with the four pre-rotated quadrants at rq
@@ -1851,33 +1935,44 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
     fetch_head(0);
     float ldj = 0.f;
     int cur = 0;
+    // activation-record destinations, advanced per block: nothing in the loop reads the grid size (hipcc reloaded
+    // it from the kernarg segment after every barrier's memory clobber, and that scalar load in flight turned the
+    // next LDS wait into lgkmcnt(0))
+    int gdim = gridDim.x;
+    asm volatile("" : "+s"(gdim));
+    floatx4* d4 = reinterpret_cast<floatx4*>(arec) + (long long)blockIdx.x * AR::AR4 * BCNF_WG + tid;
+    float* d1p = arec + ar1_off(nb, gdim, AR::AR4) + (long long)blockIdx.x * AR::AR1 * BCNF_WG + tid;
+    const long long d4s = (long long)gdim * AR::AR4 * BCNF_WG, d1s = (long long)gdim * AR::AR1 * BCNF_WG;
     for (int k = 0; k < nb; ++k) {
       const int nxt = cur == FWD_SLOTS - 1 ? 0 : cur + 1;
       float rr[RecF<NH>::USED];
 #pragma unroll
       for (int i = 0; i < FWD_HEAD; ++i) rr[i] = hd[i];
-      ld_rec<FWD_HEAD, RecF<NH>::USED>(rr, rec + cur * RING + j * L.RF);   // the rest streams in behind layer 1
       const float hpk = ((hq4[0] + hq4[1]) + hq4[2]) + hq4[3];
       const float msk[8] = {mk0[0], mk0[1], mk0[2], mk0[3], mk1[0], mk1[1], mk1[2], mk1[3]};
       const float xa = fmaf(rr[0], ya, rr[1]);          // ActNorm (cnf.py:349)
       const float xb = fmaf(rr[2], yb, rr[3]);
       float T, Sp;
       float ar[AR::AR];                                   // activation record of this block (SAVE)
-      mlp_forward_m<NH, SAVE, DROP>(rr, xa, hpk, msk, T, Sp, ar + AR::ACT, ar + AR::GD);
+      ar[AR::YA] = ya;
+      ar[AR::YB] = yb;
+      // each float4 of the record is stored as soon as it is complete (coalesced across the wave)
+      auto emit = [&](int q) {
+        if (SAVE) d4[q * BCNF_WG] = floatx4{ar[4 * q], ar[4 * q + 1], ar[4 * q + 2], ar[4 * q + 3]};
+      };
+      mlp_forward_s<NH, SAVE, DROP>(rr, rec + cur * RING + j * L.RF, xa, hpk, msk, T, Sp, ar, emit);
       const float Sv = tanh_bf(Sp);                      // cnf.py:107
       const float zb = fmaf(exp_fast(Sv), xb, T);        // cnf.py:179
       ldj += Sv;                                         // cnf.py:190
-      if (SAVE) {                                         // coalesced across the wave
+      if (SAVE) {
         ar[AR::S] = Sv;
-        ar[AR::YA] = ya;
-        ar[AR::YB] = yb;
-        const long long rb0 = (long long)k * gridDim.x + blockIdx.x;
-        floatx4* d4 = reinterpret_cast<floatx4*>(arec) + rb0 * AR::AR4 * BCNF_WG + tid;
 #pragma unroll
-        for (int i = 0; i < AR::AR4; ++i) d4[i * BCNF_WG] = floatx4{ar[4 * i], ar[4 * i + 1], ar[4 * i + 2], ar[4 * i + 3]};
-        float* d1p = arec + ar1_off(nb, gridDim.x, AR::AR4) + rb0 * AR::AR1 * BCNF_WG + tid;
+        for (int q = 0; q < AR::AR4; ++q)
+          if (AR::ready_layer(q) == NH + 1) emit(q);
 #pragma unroll
         for (int i = 0; i < AR::AR1; ++i) d1p[i * BCNF_WG] = ar[4 * AR::AR4 + i];
+        d4 += d4s;
+        d1p += d1s;
       }
       fetch_head(nxt);     // slot nxt is complete since the previous barrier (after the last block: unused, no
                            // branch); the reads land while the mix runs
@@ -2424,11 +2519,11 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
       for (int i = 0; i < AR::AR1; ++i) ar[4 * AR::AR4 + i] = P.rec1[i];
       float* ta = aT + (k % 3) * J::NA * TILE + tix;
 #pragma unroll
-      for (int l = 1; l <= NH; ++l) ta[l * TILE] = ar[AR::ACT + l - 1];
+      for (int l = 1; l <= NH; ++l) ta[l * TILE] = ar[AR::act(l - 1)];
       ta[0] = fmaf(P.sa, ar[AR::YA], P.ba);                // A_0: ActNorm output of the y-part (cnf.py:349)
       float gs[4 * BWD_G4];
 #pragma unroll
-      for (int l = 0; l < NH; ++l) gs[l] = ar[AR::GD + l];
+      for (int l = 0; l < NH; ++l) gs[l] = ar[AR::gd(l)];
       gs[NH] = ar[AR::S];
       gs[NH + 1] = ar[AR::YA];
       gs[NH + 2] = ar[AR::YB];

@@ -236,8 +236,11 @@ __global__ __launch_bounds__(BCNF_WG) void k_clip(TList T, const float* __restri
 // GELU + dropout layer, dL/dpre = dL/da * g, never stored.
 // ACT (feature MLP layer, feature_network.py:128-134: Linear -> GELU -> Dropout): the epilogue stores
 // a = mask GELU(pre) and, when G is given, g = mask GELU'(pre), mask = keep_scale or 0 from Philox4x32-10
-// (key = rng seed ^ salt, counter = (column, row / 4, rng offset)) when rng is given, else 1.
+// (key = (rng seed ^ salt, (seed >> 32) ^ BCNF_FEATURE_KEY), counter = (column, row / 4, rng offset)) when rng is given,
+// else 1. BCNF_FEATURE_KEY keeps every feature layer's key apart from the coupling dropout's (seed, (seed >> 32) ^
+// (offset >> 32)), which otherwise coincided with the salt-0 layer's for offsets below 2^32.
 // ------------------------------------------------------------------------------------------------
+constexpr uint32_t BCNF_FEATURE_KEY = 0x80000000u;
 struct ActArgs {
   float* G;
   const uint64_t* rng;
@@ -291,7 +294,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_gemm(const float* __restrict__ A, i
         const uint64_t seed = act.rng[0], off = act.rng[1];
         const uint4 r = philox4x32_10(make_uint4((uint32_t)col, (uint32_t)((row0 >> 2) + lq), (uint32_t)off,
                                                  (uint32_t)(off >> 32)),
-                                      make_uint2((uint32_t)seed ^ act.salt, (uint32_t)(seed >> 32)));
+                                      make_uint2((uint32_t)seed ^ act.salt, (uint32_t)(seed >> 32) ^ BCNF_FEATURE_KEY));
         m[0] = r.x >= act.thresh ? act.keep : 0.f;
         m[1] = r.y >= act.thresh ? act.keep : 0.f;
         m[2] = r.z >= act.thresh ? act.keep : 0.f;
@@ -417,7 +420,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_lin(const float* __restrict__ A, in
         const uint64_t seed = act.rng[0], off = act.rng[1];
         const uint4 rn = philox4x32_10(make_uint4((uint32_t)col, (uint32_t)((row0 >> 2) + lq), (uint32_t)off,
                                                   (uint32_t)(off >> 32)),
-                                       make_uint2((uint32_t)seed ^ act.salt, (uint32_t)(seed >> 32)));
+                                       make_uint2((uint32_t)seed ^ act.salt, (uint32_t)(seed >> 32) ^ BCNF_FEATURE_KEY));
         m[0] = rn.x >= act.thresh ? act.keep : 0.f;
         m[1] = rn.y >= act.thresh ? act.keep : 0.f;
         m[2] = rn.z >= act.thresh ? act.keep : 0.f;

@@ -13,6 +13,7 @@ Restated from the reference's behaviour (src/bcnf/models/feature_network.py); th
 from __future__ import annotations
 
 import os
+import weakref
 from typing import Any, Type
 
 import torch
@@ -107,6 +108,14 @@ class HIPLinear(nn.Linear):
         return super().forward(x)
 
 
+# feature network -> weakref to the CondRealNVP_v2 whose coupling Philox state its fused dropout shares
+_RNG_OWNERS: "weakref.WeakKeyDictionary[nn.Module, weakref.ref]" = weakref.WeakKeyDictionary()
+
+
+def bind_rng_owner(fn: nn.Module, owner: nn.Module) -> None:
+    _RNG_OWNERS[fn] = weakref.ref(owner)
+
+
 class FeatureNetwork(nn.Module):
     input_size: int
     output_size: int
@@ -153,23 +162,32 @@ class FullyConnectedFeatureNetwork(FeatureNetwork):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return self.run(x.view(x.size(0), -1))
 
-    # Philox stream of the fused dropout: the owning CondRealNVP_v2's coupling (seed, offset) state when one is
-    # attached (weakly: a deep copy of this module keeps it as is), so one device offset -- advanced once per training
-    # step on the device, replay-safe in HIP graphs -- serves the feature and the coupling dropout, and
-    # `model.fused.set_seed` / TrainStep's snapshot cover both; else this module's own state.
-    _rng_owner = None
+    # Philox stream of the fused dropout: the owning CondRealNVP_v2's coupling (seed, offset) state when one is bound
+    # (bind_rng_owner; a registry outside the module, so deepcopy / pickle of this module never carry a reference to
+    # another model -- CondRealNVP_v2 re-binds its copies), so one device offset serves the feature and the coupling
+    # dropout and `model.fused.set_seed` / TrainStep's snapshot cover both; else this module's own state.
+    # Advancing: the owner's coupling launch bumps the shared offset once per training step when the coupling itself
+    # drops out; otherwise (coupling dropout 0, the owner in eval mode or elsewhere, no owner) run() bumps it after
+    # the network's last fused dropout layer -- a device-side add, replay-safe in HIP graphs -- so every training
+    # step draws fresh feature masks.
     _own_rng = None
 
     def rng_state(self, device) -> torch.Tensor:
-        owner = self._rng_owner() if self._rng_owner is not None else None
-        fused = getattr(owner, "_fused", None) if owner is not None else None
+        return self._rng(device)[0]
+
+    def _rng(self, device) -> tuple[torch.Tensor, bool]:
+        """(device (seed, offset) state, whether the owner's coupling launch advances it this step)."""
+        ref = _RNG_OWNERS.get(self)
+        owner = ref() if ref is not None else None
+        fused = owner.__dict__.get("_fused") if owner is not None else None
         if fused is not None and hasattr(fused, "rng_state") and getattr(fused, "flat", None) is not None \
                 and fused.flat.device == device:
-            return fused.rng_state()
+            cfg = getattr(fused, "cfg", None)
+            return fused.rng_state(), bool(owner.training and cfg is not None and cfg.dropout > 0.0)
         if self._own_rng is None or self._own_rng.device != device:
             seed = (torch.cuda.initial_seed() * 0x9E3779B97F4A7C15 + 0xFEA7) & ((1 << 62) - 1)
             self._own_rng = torch.tensor([seed, 0], dtype=torch.int64, device=device)
-        return self._own_rng
+        return self._own_rng, False
 
     def run(self, x: torch.Tensor, upto: int | None = None) -> torch.Tensor:
         """Modules [0, upto) of the MLP on the flattened input. Each Linear -> GELU(exact) [-> Dropout] group of fp32
@@ -177,6 +195,7 @@ class FullyConnectedFeatureNetwork(FeatureNetwork):
         modules themselves (BatchNorm, other activations, CPU)."""
         mods = list(self.nn)[:upto]
         i = 0
+        bump = None                       # the state to advance after the last fused dropout layer, if run() must
         while i < len(mods):
             m = mods[i]
             act = mods[i + 1] if i + 1 < len(mods) else None
@@ -184,7 +203,10 @@ class FullyConnectedFeatureNetwork(FeatureNetwork):
                     and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and m.weight.dtype == torch.float32:
                 drop = mods[i + 2] if i + 2 < len(mods) and isinstance(mods[i + 2], nn.Dropout) else None
                 p = drop.p if (drop is not None and drop.training) else 0.0
-                rng = self.rng_state(x.device) if p > 0.0 else None
+                rng = None
+                if p > 0.0:
+                    rng, owner_bumps = self._rng(x.device)
+                    bump = None if owner_bumps else rng
                 need_g = torch.is_grad_enabled() and (x.requires_grad or m.weight.requires_grad or
                                                       (m.bias is not None and m.bias.requires_grad))
                 x = _LinearGeluFn.apply(x.contiguous(), m.weight, m.bias, p, rng, i, need_g)
@@ -192,6 +214,8 @@ class FullyConnectedFeatureNetwork(FeatureNetwork):
                 continue
             x = m(x)
             i += 1
+        if bump is not None:
+            bump[1:2].add_(1)
         return x
 
 

@@ -128,9 +128,14 @@ class TrainStep:
         st.side_stream = self._side
         try:
             yield
-        finally:
+        except BaseException:
+            # the body raised (e.g. a divergence or launch error, possibly before autograd adopted the side buffer):
+            # join the stream but skip the adoption check, so the original error is the one reported
             st.side_stream = None
-            st.join_side(st.flat_param)
+            st.join_side(None)
+            raise
+        st.side_stream = None
+        st.join_side(st.flat_param)
 
     def _forward_backward_body(self, y, traj, gather=None, adam=None):
         self.opt.zero_grad(set_to_none=True)

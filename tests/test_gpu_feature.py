@@ -110,3 +110,64 @@ def test_model_feature_dropout_follows_coupling_state():
     assert torch.equal(v1, v2)
     v3 = m.nll_loss(y, traj).detach().clone()               # the finalize advanced the offset
     assert not torch.equal(v1, v3)
+
+
+@pytest.mark.parametrize("owner", ["coupling_dropout_0", "standalone", "owner_eval"])
+def test_feature_dropout_advances_without_coupling_dropout(owner):
+    """with coupling dropout 0 (the coupling launches never bump the shared offset), a standalone
+    feature network, or an owner not in training mode, the feature network advances the Philox offset itself after its
+    last fused dropout layer, so consecutive training steps draw fresh feature masks."""
+    from bcnf_amd import CondRealNVP_v2
+    x = torch.randn(256, 30, 3, device=DEV)
+    if owner == "standalone":
+        fn = _net().to(DEV).train()
+        run = lambda: fn(x)                                         # noqa: E731
+    else:
+        cfg = copy.deepcopy(FC_LARGE_CFG)
+        cfg["model"]["kwargs"].update(n_blocks=2, dropout=0.0 if owner == "coupling_dropout_0" else 0.407)
+        torch.manual_seed(4)
+        m = CondRealNVP_v2.from_config(cfg).to(DEV).train()
+        fn = m.feature_network_stack.feature_networks[1]
+        fn.train()
+        if owner == "owner_eval":
+            m.eval()
+            fn.train()                                              # the feature dropout alone stays on
+        y = torch.randn(256, 19, device=DEV)
+        run = lambda: m.nll_loss(y, x) if owner == "coupling_dropout_0" else fn(x)   # noqa: E731
+    # the feature activations of two consecutive steps
+    acts = []
+    for _ in range(2):
+        off0 = int(fn.rng_state(x.device)[1].item())
+        run()
+        torch.cuda.synchronize()
+        acts.append(fn.run(x.view(x.shape[0], -1), upto=3).detach().clone())
+        # run() above advanced the offset too (one bump per run), so the step itself advanced it exactly once
+        assert int(fn.rng_state(x.device)[1].item()) == off0 + 2
+    assert not torch.equal(acts[0], acts[1])
+
+
+def test_deepcopy_feature_dropout_follows_the_copy():
+    """a deep-copied model's feature dropout draws from the COPY's coupling Philox state, so
+    copy.fused.set_seed / a state restore on the copy cover its feature masks, and the original is untouched."""
+    from bcnf_amd import CondRealNVP_v2
+    cfg = copy.deepcopy(FC_LARGE_CFG)
+    cfg["model"]["kwargs"]["n_blocks"] = 2
+    torch.manual_seed(5)
+    m = CondRealNVP_v2.from_config(cfg).to(DEV).train()
+    c = copy.deepcopy(m)
+    fm = m.feature_network_stack.feature_networks[1]
+    fc = c.feature_network_stack.feature_networks[1]
+    x = torch.randn(64, 90, device=DEV)
+    assert fc.rng_state(x.device) is c.fused.rng_state()
+    assert fm.rng_state(x.device) is m.fused.rng_state()
+    assert fc.rng_state(x.device) is not fm.rng_state(x.device)
+    c.fused.set_seed(1234)
+    st = c.fused.rng_state().clone()
+    a1 = fc.run(x, upto=3)
+    m_state = m.fused.rng_state().clone()
+    c.fused.rng_state().copy_(st)
+    a2 = fc.run(x, upto=3)
+    assert torch.equal(a1, a2)
+    assert torch.equal(m.fused.rng_state(), m_state)              # the original's offset never moved
+    import pickle
+    pickle.loads(pickle.dumps(fc))                                  # no weakref inside the module's state

@@ -61,7 +61,7 @@ def test_layout_queries_match_module_tree():
     assert m.fused.supported
     d = m.fused.desc
     ws = N.query_i64(N.lib().bcnf_workspace_bytes, ctypes.byref(d), ctypes.c_int64(4096), ctypes.c_int32(1))
-    # activation records (7 masked activations, 7 masked GELU derivatives, tanh(s), y_a, y_b -> 20 floats
+    # activation records ((masked activation, masked GELU derivative) x 7, y_a, y_b, tanh(s) -> 17 floats
     # per lane and block), loss partials, condition projection HP, Linear-1 deltas D1 (+ a dummy row)
     assert ws == 32 * 4096 * 16 * 17 * 4 + 256 * 4 + 2 * 32 * 4096 * 16 * 4 + 16 * 4   # 17-float records, + D1 dummy row
     sb = N.query_i64(N.lib().bcnf_slab_bytes, ctypes.byref(d), ctypes.c_int64(4096))
