@@ -23,11 +23,6 @@
 #include <utility>
 #include <vector>
 
-// Experiment switches of the pack-free forward (timing probes only, results wrong): 1 no side outputs, 2 no h GEMM,
-// 4 no record gathers, 8 no ldc sum, 16 no x loads, 32 no Wf / bf loads, 64 no zeroed K padding (the NaN regression)
-#ifndef BCNF_RAW_EXP
-#define BCNF_RAW_EXP 0
-#endif
 
 // Phase stamps (s_memtime per phase of workgroup 0's first compute and helper waves) exist only in a diagnostic
 // build with -DBCNF_PHASE_STAMPS (tools/exp_variants.sh); the shipped library has no stamp code, no debug globals
@@ -1557,10 +1552,10 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
         const int sp = (k < nb - 1 ? k * L.blk_stride : k * L.blk_stride - an) * 4, sq = k * D * D * 4;
 #pragma unroll
         for (int i = 0; i < RAW_NP; ++i)
-          g.v[i] = (BCNF_RAW_EXP & 4) ? 0.f : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rP, srcb[i], sp, 0));
+          g.v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rP, srcb[i], sp, 0));
 #pragma unroll
         for (int i = RAW_NP; i < RAW_NP + RAW_NQ; ++i)
-          g.v[i] = (BCNF_RAW_EXP & 4) ? 0.f : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rQ, srcb[i], sq, 0));
+          g.v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rQ, srcb[i], sq, 0));
 #pragma unroll
         for (int i = 0; i < RAW_TPW; ++i) {   // unconditional (wo = 0 for an absent tile, whose MFMAs are skipped)
           const auto w = __builtin_amdgcn_raw_buffer_load_b128(rP, wo[i] * 4, cb * 4, 0);
@@ -1685,15 +1680,13 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
         if (k + 1 < nb - 2) interval(k + 1, 0);
         if (k + 2 < nb - 2) interval(k + 2, 1);
       }
-      if (!(BCNF_RAW_EXP & 1)) {
 #pragma unroll
-        for (int q = 0; q < RAW_SIDE_Q; ++q) side_unit(blockIdx.x + q * gridDim.x, pbe[q]);
-      }
+      for (int q = 0; q < RAW_SIDE_Q; ++q) side_unit(blockIdx.x + q * gridDim.x, pbe[q]);
       {  // the ActNorm log-det constant  sum_k sum_i log|scale_k,i|  (cnf.py:350): strided partials (loads issued
          // together), a fixed-order butterfly per wave, lps[hw] for the compute epilogue after the last barrier
         constexpr int LU = 4;
         float acc = 0.f;
-        const int n = (BCNF_RAW_EXP & 8) ? 0 : (nb - 1) * D;
+        const int n = (nb - 1) * D;
         for (int i0 = t8; i0 < n; i0 += LU * BCNF_WG) {
           float v[LU];
 #pragma unroll
@@ -1764,9 +1757,6 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
     }
   } else {
     const int tid = t8;
-#ifdef BCNF_PRIO_F
-    __builtin_amdgcn_s_setprio(BCNF_PRIO_F);
-#endif
     const int D = L.D, Da = L.Da, Db = L.Db;
     float ya, yb, ldc = 0.f;
     if constexpr (RAW) {
@@ -1804,7 +1794,7 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
         const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(R.wf), (short)0,
                                                                            C * X * 4, 0x00020000);
         // the K padding quads first: their stores need no load and go out before the staging round trip
-        for (int i = (BCNF_RAW_EXP & 64) ? C * (XQP - XQ) : tid; i < C * (XQP - XQ); i += BCNF_WG) {
+        for (int i = tid; i < C * (XQP - XQ); i += BCNF_WG) {
           const int c = i / (XQP - XQ), q = XQ + (i - c * (XQP - XQ));
           *reinterpret_cast<floatx4*>(ws + c * RAW_KP + 4 * q) = floatx4{0.f, 0.f, 0.f, 0.f};
         }
@@ -1885,7 +1875,7 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
 #pragma unroll
         for (int i = 0; i < RAW_TPW; ++i) {
           const int ct = cw + 4 * i;
-          if (!(BCNF_RAW_EXP & 2) && 16 * ct < C) {
+          if (16 * ct < C) {
             const int c = 16 * ct + lr;
             const floatx4 wv = *reinterpret_cast<const floatx4*>(ws + (c < C ? c : 0) * RAW_KP + 16 * u + 4 * lq);
 #pragma unroll
@@ -2473,9 +2463,6 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
   }
 
   if (helper) {
-#ifdef BCNF_PRIO_B
-    __builtin_amdgcn_s_setprio(BCNF_PRIO_B);
-#endif
     const int hw = __builtin_amdgcn_readfirstlane(t8 >> 6);
     float* slab = slab_all + (long long)blockIdx.x * slab_stride;
     // activation records [k][workgroup][AR/4][256 threads] float4 (k_forward)
@@ -2828,20 +2815,8 @@ const void* g_attr_fn[256];
 size_t g_attr_lds[256];
 int g_attr_n = 0;
 
-// Optional occupancy shaping (env BCNF_LDS_MIN_KB): pad the dynamic LDS request so at most
-// floor(160 / pad) workgroups share a CU. Read once.
-size_t lds_floor_bytes() {
-  static size_t v = [] {
-    const char* e = getenv("BCNF_LDS_MIN_KB");
-    return e ? (size_t)atoi(e) * 1024 : (size_t)0;
-  }();
-  return v;
-}
-
-
 template <typename K>
 int launch_lds(K kernel, size_t& lds) {
-  if (lds < lds_floor_bytes()) lds = lds_floor_bytes();
   if (lds > LDS_MAX) return BCNF_ERR_UNSUPPORTED;
   const void* fn = reinterpret_cast<const void*>(kernel);
   std::lock_guard<std::mutex> lk(g_attr_mu);

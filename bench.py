@@ -903,11 +903,41 @@ def run_sample(n_cond, steps, warmup, world, rank, device, n_draws=500, cpu=True
                              "repeated per draw); flop_executed: projection once per condition (k_hp) + "
                              "k_inverse_mfma (fp32 MFMA dense layers, VALU GELU / tanh / coupling)"},
     }
+    if cpu and world == 1:
+        # the oracle as the checker, outside the timed region (world 1, with the cpu_baseline leg): 8 conditions'
+        # rows of the full 500 x 1024 launch vs the oracle's tiled inverse on the same z
+        line["parity"] = sample_parity(model, traj, n_draws)
     del model
     torch.cuda.empty_cache()
     if cpu and world == 1:
         line["cpu_baseline"] = cpu_baseline_sample(n_draws, cpu_conds)
     return line
+
+
+def sample_parity(model, traj, n_draws, n_check=8):
+    """Max error of the configs[4] launch shape against the oracle: z for all n_draws x N rows, ONE draw over all N
+    conditions (the benchmarked launch), then n_check conditions spread over [0, N) checked against the CPU oracle's
+    inverse of the tiled features (cnf.py:577-582) on the same z rows, at the north star's 1e-5 gate."""
+    from oracle import cnf_oracle as O
+    from bcnf_amd.sampling import draw
+    n = traj.shape[0]
+    g = torch.Generator(device=traj.device).manual_seed(31)
+    z = torch.randn(n_draws * n, 19, device=traj.device, generator=g)
+    with torch.no_grad():
+        got = draw(model, n_draws, traj, z=z)
+    cols = torch.linspace(0, n - 1, n_check).round().long()
+    got = got[:, cols.to(got.device)].cpu()
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    with torch.no_grad():
+        h = O.feature_forward(sd, O.FC_SMALL_SPEC, traj[cols.to(traj.device)].cpu())
+        zs = z.view(n_draws, n, 19)[:, cols.to(z.device)].reshape(-1, 19).cpu()
+        ref = O.model_inverse(sd, O.FC_SMALL_SPEC, zs, h.repeat(n_draws, 1)).view(n_draws, n_check, 19)
+    err = (got.double() - ref.double()).abs()
+    tol = 1e-5 * ref.double().abs() + 1e-5 * max(1.0, ref.abs().max().item())
+    return {"checker": "oracle/cnf_oracle.model_inverse (tiled features)", "conditions": cols.tolist(),
+            "rows": n_draws * n_check, "of_launch": [n_draws, n], "max_abs_err": float(err.max()),
+            "max_rel_err": float((err / ref.double().abs().clamp(min=1e-6)).max()),
+            "tol_ratio": float((err / tol).max()), "within_1e-5_gate": bool((err <= tol).all())}
 
 
 def main_sample(args, n_draws=500):

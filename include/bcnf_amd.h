@@ -186,10 +186,6 @@ int bcnf_fold_train_forward(const BcnfStackDesc* desc, const float* params, cons
                             int64_t batch, void* packed, float* z, float* ldj, int32_t training,
                             uint64_t* rng_state, void* workspace, int32_t finalize, float* loss_out, int32_t* guard,
                             void* stream);
-/* Test hook (no reference counterpart): fill every CU's LDS with `value` (one full-LDS workgroup per CU, several
- * rounds), so a test can check that a following launch never reads LDS it did not write (the pack-free forward's
- * K padding, tests/test_gpu_fold.py). */
-int bcnf_lds_fill(float value, void* stream);
 /* Adam fused into bcnf_fold_backward_tail (nullable argument): every gradient the tail produces -- the flat coupling
  * parameters (slot 0), the feature Linear's weight (1) and bias (2, NULL without bias) -- also takes its
  * torch.optim.Adam update where it is produced, with the end-of-step bookkeeping of bcnf_adam_step_bookkeep
@@ -459,6 +455,17 @@ int bcnf_resimulate(const void* y_hat, int32_t y_hat_f64, int64_t n_draws, int64
                     int32_t break_on_impact, double rtol, double atol, int32_t max_attempts, double* x,
                     int32_t* attempts, int32_t* status, void* stream);
 
+
+const char* bcnf_status_string(int status);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * TEST-ONLY entry points. Not part of the drop-in boundary (no reference interface maps to them; INTEGRATION.md
+ * binds none of them): exported so the GPU tests can poison LDS and exercise single GEMM tilings through ctypes.
+ * ------------------------------------------------------------------------------------------------------------- */
+/* Test hook (no reference counterpart): fill every CU's LDS with `value` (one full-LDS workgroup per CU, several
+ * rounds), so a test can check that a following launch never reads LDS it did not write (the pack-free forward's
+ * K padding, tests/test_gpu_fold.py). */
+int bcnf_lds_fill(float value, void* stream);
 /* Test hook for the GEMM tiles: C (M x N) = A B with (layout & 15) 0 = A[m][k] B[n][k], 1 = A[m][k] B[k][n],
  * 2 = A[k][m] B[k][n], 3 = A[k][m] B[n][k]; layout >> 4 forces a tiling as BcnfStackDesc.gemm_tiling (0 = the
  * dispatcher's choice, t + 1 = tiling t: 0 = 128x128 and 1 = 64x64 on v_mfma_f32_32x32x2_f32, 2 = 128x48, 3 = 128x48
@@ -470,8 +477,6 @@ int bcnf_resimulate(const void* y_hat, int32_t y_hat_f64, int64_t n_draws, int64
  * floats for them (a tight (K - 1) * ld + M buffer is read out of bounds). */
 int bcnf_wide_gemm_test(int32_t layout, int32_t M, int32_t N, int32_t K, const float* A, int64_t lda, const float* B,
                         int64_t ldb, float* C, int64_t ldc, void* stream);
-
-const char* bcnf_status_string(int status);
 
 #ifdef __cplusplus
 }

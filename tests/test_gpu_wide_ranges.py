@@ -138,3 +138,63 @@ def test_side_stream_trainstep_equals_single_stream(monkeypatch):
     assert out[0][0] == out[1][0]
     for a, b in zip(out[0][1], out[1][1]):
         assert torch.equal(a, b)
+
+
+def _guarded_workspace(monkeypatch, st, guards):
+    """WideStack workspaces with NaN canaries of 64K floats before and after (16-B aligned views): any write of the
+    library outside the workspace it was given shows up as a changed canary."""
+    orig = type(st)._workspace
+
+    def ws(self, batch, save, dev):
+        inner = orig(self, batch, save, dev)
+        n, g = inner.numel(), 1 << 16
+        buf = torch.full((n + 2 * g,), float("nan"), device=dev)
+        guards.append(buf)
+        return buf[g:g + n]
+
+    monkeypatch.setattr(type(st), "_workspace", ws)
+
+
+@pytest.mark.parametrize("B", [24, 33, 34, 35, 36, 38, 48, 77])
+def test_fold_backward_g_region_boundaries(monkeypatch, B):
+    """VERDICT r04 item 4 (the r04ze illegal address): the folded wide backward puts the feature side's split-K
+    partials (dL/dx, [dWf | dbf]; need nv * B * Xp and nv * C * Xp floats) at the END of the G region (nv * NH * B * HP
+    floats, dead once the chain has run) and the coupling parameter gradients' partials at its head. At this shape
+    (nv 5, NH 3, HP 52, C 80, Xp 68: region 780 B floats, [dWf | dbf] needs 27,200) the need crosses the region's size
+    between B = 34 and 35 (B = 35 leaves the head 100 floats; FC_large at B = 48 leaves it 40K of 3.29M), so these batches
+    cover a tail that exceeds the region (must reserve nothing and run unsplit: a reservation of more than the region
+    pointed BEFORE it, into the activation region the parameter gradients read), a tail that fills it exactly or
+    nearly (the head partials get a region of ~0 floats) and the usual case. Checks: no write outside the workspace
+    (NaN canaries), phase 1 + phase 2 on two streams == one call bit for bit, folded == unfolded (rtol 1e-4)."""
+    from bcnf_amd import CondRealNVP_v2
+    from bcnf_amd.wide import WideStack
+    torch.manual_seed(3)
+    m = CondRealNVP_v2.from_config(_cfg_deep(False)).to(DEV).train()
+    m.flat_parameters()
+    st = m.fused
+    assert isinstance(st, WideStack)
+    guards = []
+    _guarded_workspace(monkeypatch, st, guards)
+    g = torch.Generator().manual_seed(B)
+    y = torch.randn(B, 19, generator=g).to(DEV)
+    traj = torch.randn(B, 30, 3, generator=g).to(DEV)
+    one = _side_grads(m, y, traj, None)
+    two = _side_grads(m, y, traj, torch.cuda.Stream())
+    torch.cuda.synchronize()
+    for a, b in zip(one, two):
+        assert torch.equal(a, b)
+    for buf in guards:
+        gsz = 1 << 16
+        assert torch.isnan(buf[:gsz]).all() and torch.isnan(buf[-gsz:]).all(), "write outside the workspace"
+    # folded vs unfolded (no fold split-K at all) on the same dropout streams
+    m.fold_features = False
+    try:
+        assert m._wide_fold(y, (traj,)) is None
+        ref = _side_grads(m, y, traj, None)
+    finally:
+        del m.fold_features
+    assert torch.allclose(one[1], ref[1], rtol=2e-6, atol=1e-5)                  # the loss values
+    scale = max(1.0, ref[0].abs().max().item())
+    assert (one[0] - ref[0]).abs().max().item() <= 1e-4 * scale, "coupling gradient"
+    for a, b in zip(one[2:], ref[2:]):
+        assert (a - b).abs().max().item() <= 1e-4 * max(1.0, b.abs().max().item()), "feature gradient"

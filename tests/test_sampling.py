@@ -95,3 +95,31 @@ def test_draw_matches_oracle_tiled_inverse(g1):
     g = torch.Generator(device="cuda").manual_seed(5)
     b = draw(m, 4, cond.cuda(), generator=g)
     assert a.shape == (4, 37, 19) and torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_config4_launch_rows_match_small_launch_and_oracle(g1):
+    """configs[4] at its launch shape: ONE draw over all 1024 conditions x 500 draws; the rows of 8 conditions are
+    bit-identical to a small launch over just those conditions (the row -> condition map and the 16-row MFMA tiles
+    mix no rows), and match the oracle's tiled inverse at the 1e-5 gate."""
+    from bcnf_amd import CondRealNVP_v2
+    from bcnf_amd.sampling import draw
+    torch.manual_seed(0)
+    m = CondRealNVP_v2.from_config(FC_SMALL_CFG)
+    m.load_state_dict(golden_sd(g1))
+    m.to("cuda").eval()
+    sd = golden_sd(g1)
+    gen = torch.Generator().manual_seed(41)
+    n, N = 500, 1024
+    cond = torch.randn(N, 30, 3, generator=gen)
+    z = torch.randn(n * N, 19, generator=gen)
+    full = draw(m, n, cond.cuda(), z=z.cuda()).cpu()
+    assert full.shape == (n, N, 19)
+    cols = torch.tensor([0, 1, 146, 511, 512, 877, 1022, 1023])
+    zs = z.view(n, N, 19)[:, cols].reshape(-1, 19)
+    small = draw(m, n, cond[cols].cuda(), z=zs.cuda()).cpu()
+    assert torch.equal(full[:, cols], small)
+    h = O.feature_forward(sd, O.FC_SMALL_SPEC, cond[cols])
+    ref = O.model_inverse(sd, O.FC_SMALL_SPEC, zs, h.repeat(n, 1)).view(n, len(cols), 19)
+    ok, err = close(full[:, cols], ref)
+    assert ok, err
