@@ -1361,7 +1361,7 @@ __device__ __forceinline__ void mix(const float* __restrict__ rq, float a, float
 // Forward
 // ------------------------------------------------------------------------------------------------
 #if BCNF_STAMPS
-__device__ unsigned long long g_phase[24];   // phase stamps (bcnf_debug_phases), diagnostic build only
+__device__ unsigned long long g_phase[32];   // phase stamps (bcnf_debug_phases), diagnostic build only
 #endif
 
 // Condition projection operands of the forward (the y-independent part of Linear 1, cnf.py:98-107 with the
@@ -1425,9 +1425,9 @@ constexpr int FWD_HEAD = 24;           // record floats the compute waves prefet
 //    the compute lanes add the four partials in a fixed order), and draw its dropout multipliers (Philox -> floats).
 // With the ring one block deeper, the compute waves read block k + 1's record head, projection partials and
 // multipliers at the end of block k (its slot is complete since the previous barrier), so a block starts without
-// an LDS round trip: a lone wave per SIMD is issue-bound (tools/probe_issue.py: ~8 s_memtime ticks per VALU
-// instruction against ~5.5 per wave with two waves per SIMD, profiles/r03b_probe.txt), and the old block start
-// waited for 27 record reads of all four compute waves.
+// an LDS round trip: a lone wave per SIMD is issue-bound on its own stream (tools/probe_issue.py, recalibrated in
+// r05: ~5 cycles per plain VALU, 6-8 per DPP FMA), and the old block start waited for 27 record reads of
+// all four compute waves. The rest of the record streams in two stages ahead (mlp_forward_s).
 // The projection needs no separate GEMM launch and no HBM round trip, and the compute waves' loop issues no global
 // loads (the record stores of SAVE are its only VMEM traffic).
 template <int NH, bool DROP, bool SAVE, bool RAW = false>
@@ -1458,6 +1458,7 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
   // diagnostic build: per-phase cycles of workgroup 0's wave 0 (compute) and wave 4 (helper) -> g_phase[8..]
   unsigned long long ph_t = BCNF_STAMPS ? __builtin_amdgcn_s_memtime() : 0ULL, ph_acc[3] = {0, 0, 0};
   const unsigned long long ph_t0 = ph_t;
+  const unsigned long long ph_r0 = BCNF_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0ULL;   // 100 MHz
   unsigned long long ph_b[2] = {0, 0};   // RAW prologue: cycles from the start to barrier #0 / #1 arrival
 #define PHB(i)                                                 \
   if (BCNF_STAMPS) ph_b[i] = __builtin_amdgcn_s_memtime() - ph_t0;
@@ -1990,6 +1991,9 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
     for (int i = 0; i < 3; ++i) g_phase[8 + (helper ? 4 : 0) + i] = ph_acc[i];
     g_phase[helper ? 15 : 11] = (ph_b[1] << 32) | (ph_b[0] & 0xffffffffULL);   // slots 3 / 7 belong to the backward
     for (int i = 0; i < 4; ++i) g_phase[16 + (helper ? 4 : 0) + i] = ph_p[i];
+    // the wave's whole life in shader cycles and in 100 MHz ticks: the clock it ran at (MI355X_MICROARCH note 6)
+    g_phase[24 + (helper ? 2 : 0)] = __builtin_amdgcn_s_memtime() - ph_t0;
+    g_phase[25 + (helper ? 2 : 0)] = __builtin_amdgcn_s_memrealtime() - ph_r0;
   }
 #endif
 #undef PHF

@@ -66,7 +66,7 @@ def phases():
     L = N.lib()
     if not hasattr(L, "bcnf_debug_phases"):
         return
-    buf = (ctypes.c_ulonglong * 24)()
+    buf = (ctypes.c_ulonglong * 32)()
     L.bcnf_debug_phases(buf)
     names = ["bwd compute: prologue", "bwd compute: chain", "bwd compute: barrier wait", "-",
              "bwd helper: loop top/barrier", "bwd helper: prep_load issue", "bwd helper: grad jobs",

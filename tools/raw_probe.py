@@ -25,7 +25,7 @@ def main():
           {k: round(v, 2) for k, v in t.items()})
     L = N.lib()
     if hasattr(L, "bcnf_debug_phases"):
-        buf = (ctypes.c_ulonglong * 24)()
+        buf = (ctypes.c_ulonglong * 32)()
         L.bcnf_debug_phases(buf)
         print("  fwd compute prologue/chain/wait", buf[8], buf[9], buf[10], " helper prologue/work/wait", buf[12],
               buf[13], buf[14])
@@ -33,6 +33,9 @@ def main():
               " helper at barrier0 / barrier1", buf[15] & 0xffffffff, buf[15] >> 32)
         print("  compute: x/Wf landed", buf[16], " helper: table landed", buf[20], "gathers landed", buf[21],
               "records written", buf[22])
+        if buf[25]:
+            print(f"  compute wave: {buf[24]} cycles in {buf[25] * 10 / 1e3:.2f} us -> {buf[24] / buf[25] / 10:.3f} GHz;"
+                  f" helper wave: {buf[26]} cycles in {buf[27] * 10 / 1e3:.2f} us")
 
 
 if __name__ == "__main__":
