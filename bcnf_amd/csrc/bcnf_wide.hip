@@ -448,6 +448,15 @@ struct EpiCtx {
 };
 
 template <int EPI>
+__device__ __forceinline__ void epi_rng(const GemmArgs& g, EpiCtx& e) {   // the dropout state (EPI_ACT)
+  if (EPI == EPI_ACT && g.rng) {
+    e.seed = g.rng[0];
+    e.offs = g.rng[1];
+  }
+}
+
+// RNG = false: seed / offs stay 0 here and epi_rng loads them later (just before the epilogue)
+template <int EPI, bool RNG = true>
 __device__ __forceinline__ EpiCtx epi_ctx(const GemmArgs& g, int g1, int g0) {
   EpiCtx e;
   e.C = g.C;
@@ -461,10 +470,7 @@ __device__ __forceinline__ EpiCtx epi_ctx(const GemmArgs& g, int g1, int g0) {
   e.X = (EPI == EPI_ACT || EPI == EPI_GRAD) && g.aux ? g.aux + g1 * g.saux1 + g0 * g.saux0 : nullptr;
   e.seed = 0;
   e.offs = 0;
-  if (EPI == EPI_ACT && g.rng) {
-    e.seed = g.rng[0];
-    e.offs = g.rng[1];
-  }
+  if (RNG) epi_rng<EPI>(g, e);
   e.tag = g.tag + (uint32_t)g1 * g.tag_s1;
   return e;
 }
@@ -931,10 +937,25 @@ struct WbCfg {
   }
 };
 
+// Phase stamps of tiling W (diagnostic build only, -DBCNF_PHASE_STAMPS): wave 0 of each of the first 256 tiles of the
+// latest launch -> g_wbr_st[tile][8] = cycles to (A + band issued, band landed, K loop done, KS merge done, epilogue
+// done), 100 MHz ticks over the whole wave, its total cycles, the dispatch order (bcnf_wide_debug_wbr).
+#ifdef BCNF_PHASE_STAMPS
+__device__ unsigned long long g_wbr_st[256 * 8];
+#define WBR_ST(i) do { if (threadIdx.x == 0) wst_[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define WBR_ST(i) do {} while (0)
+#endif
+
 // KT: K has a partial last chunk (K % CK != 0). Without one (the chain GEMMs: K = 528) the A loads are a pointer plus
 // a chunk offset and nothing is zeroed: no per-chunk index selects or masks on the VALU.
 template <int WGM, int KS, int P, int KQ, int TI, int EPI, bool KT = true>
 __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const GemmArgs g) {
+#ifdef BCNF_PHASE_STAMPS
+  unsigned long long wst_[6] = {0, 0, 0, 0, 0, 0};
+  const unsigned long long wrt0_ = __builtin_amdgcn_s_memrealtime();
+  WBR_ST(0);
+#endif
   using T = WbCfg<WGM, KS, P, KQ, TI>;
   constexpr int CK = T::CK;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -947,21 +968,17 @@ __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const
   const float* __restrict__ A = g.A + g1 * g.sA1 + g0 * g.sA0;
   const float* __restrict__ B = g.B + g1 * g.sB1 + g0 * g.sB0;
   const int am0 = tl.y * T::BM + wm * 16 * TI, n0 = tl.x * T::BN;
-  const EpiCtx e = epi_ctx<EPI>(g, g1, g0);
   const int K = g.K, S = T::stride(K);
-  // 1. A: this wave's 16 rows, its contiguous share of the chunks, the first P chunks issued now. A float4 wholly
-  //    past K (K % 4 == 0) reads the row start instead and is zeroed before use.
+  // 1. A: this wave's 16 rows, its contiguous share of the chunks, the first P chunks issued now -- before anything
+  //    else, from the first batch of kernel arguments (r05: behind the epilogue's context they waited for four
+  //    dependent scalar-load round trips, ~2k cycles). A float4 wholly past K (K % 4 == 0) reads the row start
+  //    instead and is zeroed before use.
   const float* pa[TI];
 #pragma unroll
   for (int i = 0; i < TI; ++i) pa[i] = A + (long long)min(am0 + 16 * i + c16, g.M - 1) * g.lda + 4 * KQ * qq;
   const int nchunk = (K + CK - 1) / CK;
   const int c_lo = kh * nchunk / KS, n = (kh + 1) * nchunk / KS - c_lo;
   const int clast = min(c_lo + (n > 0 ? n - 1 : 0), nchunk - 1);
-  auto mine = [&](int f) { return KS == 1 || f % KS == kh; };     // accumulator tile f = i * TJ + j
-  float pre[T::NF][4];
-#pragma unroll
-  for (int f = 0; f < T::NF; ++f)
-    if (mine(f)) epi_pre<EPI>(g, e.X, am0 + 16 * (f / T::TJ) + 4 * qq, n0 + 16 * (f % T::TJ) + c16, pre[f]);
   floatx4 buf[P][TI][KQ];
   auto load = [&](int u, int c) {
 #pragma unroll
@@ -972,13 +989,31 @@ __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const
   };
 #pragma unroll
   for (int u = 0; u < P; ++u) load(u, min(c_lo + u, clast));
+  // the epilogue's context and operands (bias / G), its dropout state only at the epilogue (a pointer round trip)
+  EpiCtx e = epi_ctx<EPI, false>(g, g1, g0);
+  auto mine = [&](int f) { return KS == 1 || f % KS == kh; };     // accumulator tile f = i * TJ + j
+  float pre[T::NF][4];
+#pragma unroll
+  for (int f = 0; f < T::NF; ++f)
+    if (mine(f)) epi_pre<EPI>(g, e.X, am0 + 16 * (f / T::TJ) + 4 * qq, n0 + 16 * (f % T::TJ) + c16, pre[f]);
   // 2. the B band: piece p (1 KB) = LDS floats [256 p, 256 p + 256); lane l's float4 is column f / S, k = f % S
-  //    (k >= K: padding, any valid source)
+  //    (k >= K: padding, any valid source). (col, k) advance by a constant step per piece: one division per lane,
+  //    not one per piece (r05)
   {
     const int np = T::band_floats(K) / 256;
+    constexpr int STEP = 256 * T::NW;              // floats between a wave's consecutive pieces
+    const int f0 = 256 * wave + 4 * lane;
+    int col = f0 / S, k = f0 - col * S;
+    const int dcol = STEP / S, dk = STEP - dcol * S, nlast = g.N - 1;
+    const unsigned ldb = (unsigned)g.ldb;
     for (int p = wave; p < np; p += T::NW) {     // wave-uniform trip count
-      const int f = 256 * p + 4 * lane, col = f / S, k = f - col * S;
-      const float* src = B + (long long)min(n0 + col, g.N - 1) * g.ldb + (k < K ? k : 0);
+      const float* src = B + ((unsigned long long)(unsigned)min(n0 + col, nlast) * ldb + (unsigned)(k < K ? k : 0));
+      k += dk;
+      col += dcol;
+      if (k >= S) {
+        k -= S;
+        ++col;
+      }
       // the DMA as inline asm: hipcc's wait pass, seeing an LDS-DMA builtin before the K loop, puts a vmcnt(0) at
       // the loop head (it cannot bound the DMA against the band reads there), draining the A ring every iteration;
       // the explicit vmcnt(0) below retires these copies before anything reads the band
@@ -991,9 +1026,11 @@ __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const
   floatx4 acc[T::NF];
 #pragma unroll
   for (int f = 0; f < T::NF; ++f) acc[f] = floatx4{0.f, 0.f, 0.f, 0.f};
+  WBR_ST(1);
   // everything landed (every other wave's pieces too after the barrier)
   __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0)
   raw_barrier();
+  WBR_ST(2);
   const float* bs = lds + c16 * S + 4 * KQ * qq;  // column 16 j + c16 at k = CK c + 4 KQ q: bs + 16 j S + CK c
   // B fragments one chunk ahead (bq): a chunk's MFMAs never wait for their own ds_reads
   static_assert(KQ == 1, "the B prefetch holds one float4 per fragment and chunk");
@@ -1031,6 +1068,7 @@ __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const
       load(u, min(c_lo + c + u + P, clast));
     }
   }
+  WBR_ST(3);
   if constexpr (KS > 1) {    // the band is dead once every wave has finished its MFMAs: partials reuse its LDS
     raw_barrier();
     float* part = lds + (wm * T::NF) * KS * 256 + lane * 4;      // [wave tile][f][slice][64 lanes][4]
@@ -1050,6 +1088,8 @@ __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const
         acc[f] = s;
       }
   }
+  WBR_ST(4);
+  epi_rng<EPI>(g, e);
 #pragma unroll
   for (int f = 0; f < T::NF; ++f)
     if (mine(f)) {
@@ -1057,6 +1097,18 @@ __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const
       const int rb = am0 + 16 * (f / T::TJ) + 4 * qq, col = n0 + 16 * (f % T::TJ) + c16;
       epi4<EPI>(g, e.C, e.X, rb, col, v, epi_rnd<EPI>(g, e, rb, col), pre[f]);
     }
+#ifdef BCNF_PHASE_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  WBR_ST(5);
+  const int tix_ = tl.x + gridDim.x * (tl.y + gridDim.y * tl.z);
+  if (threadIdx.x == 0 && tix_ < 256) {
+    unsigned long long* o = g_wbr_st + 8 * tix_;
+    for (int i = 1; i < 6; ++i) o[i - 1] = wst_[i] - wst_[0];
+    o[5] = __builtin_amdgcn_s_memrealtime() - wrt0_;
+    o[6] = wst_[5] - wst_[0];
+    o[7] = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);   // dispatch order
+  }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2758,6 +2810,9 @@ int bcnf_wide_inverse(const BcnfStackDesc* desc, const float* params, const void
 int bcnf_wide_debug_phases(unsigned long long* dbg) {
   g_link_dbg = dbg;
   return BCNF_OK;
+}
+int bcnf_wide_debug_wbr(unsigned long long* out) {   // g_wbr_st of the latest tiling-W launch -> host [256][8]
+  return bcnf_rt::hip_status(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wbr_st), sizeof(g_wbr_st)));
 }
 #endif
 
