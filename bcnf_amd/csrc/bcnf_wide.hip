@@ -150,15 +150,38 @@ int wide_layout(const BcnfStackDesc* d, WideLayout* L) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Packing: padded, GEMM-friendly copies of the weights (k_wpack_rows + k_wpack + k_wtranspose + ldc / b0 per
-// parameter update).
+// Packing: padded, GEMM-friendly copies of the weights, ONE launch per parameter update (k_wpack_all). The
+// workgroups of the launch take, in blockIdx order:
+//   * the small regions (W0y^T, last Linear, Q, Linear-1 biases, the ActNorm log-det constants);
+//   * 64 x 64 tiles of every hidden W_l (l = 1..NH-1): the tile is read once from the flat parameters and written
+//     twice, row-major into pk_hid and, through an LDS transpose, into pk_hidT (both sides coalesced);
+//   * WP_ROWS rows of W0h_all per workgroup, one per wave.
+// Round 5 replaced five launches (209 us alone at FC_large: a row kernel that left most of its threads idle on the
+// 528-wide rows, a transpose that re-read pk_hid, three small ones) with this one: 104 us, 4.8 TB/s of written +
+// read bytes against 5.4 TB/s for a device copy of the same byte count (tools/pack_bench.py).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(WWG) void k_wpack(const WideLayout L, const float* __restrict__ prm,
-                                               const float* __restrict__ q, float* __restrict__ pk) {
-  const long long stride = (long long)gridDim.x * WWG;
-  for (long long e = L.pk_w0y + (long long)blockIdx.x * WWG + threadIdx.x; e < L.pk_ldc; e += stride) {
+constexpr int WP_T = 64;                // hidden-W tile edge (32: 3% slower)
+constexpr int WP_ROWS = WWG / 64;       // W0h_all rows per workgroup (one per wave)
+constexpr int WP_SMALL = 256;   // workgroups of the small regions
+
+struct WpackGrid {
+  int t;                        // tiles per hidden-W edge
+  long long n_tiles, n_rows, n_small;
+};
+inline WpackGrid wpack_grid(const WideLayout& L) {
+  WpackGrid g;
+  g.t = (L.HP + WP_T - 1) / WP_T;
+  g.n_tiles = L.NH > 1 ? (long long)L.nv * (L.NH - 1) * g.t * g.t : 0;
+  g.n_rows = ((long long)L.nv * L.HP + WP_ROWS - 1) / WP_ROWS;
+  g.n_small = WP_SMALL;
+  return g;
+}
+
+__device__ void wpack_small(const WideLayout& L, const float* __restrict__ prm, const float* __restrict__ q,
+                            float* __restrict__ pk, int wg, int nwg) {
+  const long long stride = (long long)nwg * WWG;
+  for (long long e = L.pk_w0y + (long long)wg * WWG + threadIdx.x; e < L.pk_ldc; e += stride) {
     float v = 0.f;
-    // W0h_all and the hidden W (and W^T) are written by k_wpack_rows / k_wtranspose; this loop starts at pk_w0y
     if (e < L.pk_wl) {
       const long long i = e - L.pk_w0y;
       const long long per = (long long)L.WY * L.HP;
@@ -185,61 +208,92 @@ __global__ __launch_bounds__(WWG) void k_wpack(const WideLayout L, const float* 
     }
     pk[e] = v;
   }
-}
-
-// The two big packed regions (W0h_all: nv*HP x Cp, hidden W: nv*(NH-1)*HP x HP; 96% of the packed floats) by
-// row: blockIdx.y walks rows, each thread 4 consecutive columns (one float4 store, 4 coalesced parameter loads) --
-// no per-element 64-bit division, which bounds k_wpack's element loop (247 us at FC_large).
-__global__ __launch_bounds__(WWG) void k_wpack_rows(const WideLayout L, const float* __restrict__ prm,
-                                                    float* __restrict__ pk) {
-  const long long rows_w0h = (long long)L.nv * L.HP;
-  const long long rows_hid = (long long)L.nv * (L.NH - 1) * L.HP;
-  for (long long r = blockIdx.y; r < rows_w0h + rows_hid; r += gridDim.y) {
-    const bool w0h = r < rows_w0h;
-    const int cols = w0h ? L.Cp : L.HP;
-    const int c = 4 * (blockIdx.x * WWG + threadIdx.x);
-    if (c >= cols) continue;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    long long dst;
-    if (w0h) {
-      const int vb = (int)(r / L.HP), n = (int)(r - (long long)vb * L.HP);
-      dst = L.pk_w0h + r * L.Cp + c;
-      if (n < L.H) {
-        const int sd = vb % L.S;
-        const float* src = prm + vbase(L, vb) + L.lin_w[sd][0] + (long long)n * L.in0[sd] + L.nin[sd];
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (c + e < L.C) v[e] = src[c + e];
-      }
-    } else {
-      const long long rh = r - rows_w0h;
-      const long long kl = rh / L.HP;
-      const int n = (int)(rh - kl * L.HP);
-      dst = L.pk_hid + rh * L.HP + c;
-      if (n < L.H) {
-        const int vb = (int)(kl / (L.NH - 1)), l = (int)(kl % (L.NH - 1)) + 1;
-        const float* src = prm + vbase(L, vb) + L.lin_w[vb % L.S][l] + (long long)n * L.H;
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (c + e < L.H) v[e] = src[c + e];
-      }
-    }
-    *reinterpret_cast<floatx4*>(pk + dst) = floatx4{v[0], v[1], v[2], v[3]};
+  // Linear-1 biases (zero beyond H) and the ActNorm log|det J| constant per block (ActNorm.forward,
+  // cnf.py:348-351: torch.sum(log|scale|))
+  for (long long e = (long long)wg * WWG + threadIdx.x; e < (long long)L.nv * L.HP; e += stride) {
+    const int vb = (int)(e / L.HP), n = (int)(e - (long long)vb * L.HP);
+    pk[L.pk_b0 + e] = n < L.H ? prm[vbase(L, vb) + L.lin_b[vb % L.S][0] + n] : 0.f;
+  }
+  for (long long k = (long long)wg * WWG + threadIdx.x; k < L.nb; k += stride) {
+    float s = 0.f;
+    if (L.an && k < L.nb - 1)
+      for (int i = 0; i < L.D; ++i) s += logf(fabsf(prm[k * L.blk_stride + i]));
+    pk[L.pk_ldc + k] = s;
   }
 }
 
-// pk_hidT[kl] = pk_hid[kl]^T (HP x HP each), 32 x 32 tiles through LDS (coalesced on both sides).
-__global__ __launch_bounds__(256) void k_wtranspose(const WideLayout L, float* __restrict__ pk) {
-  __shared__ float t[32][33];
-  const long long off = (long long)blockIdx.z * L.HP * L.HP;
-  const float* __restrict__ src = pk + L.pk_hid + off;
-  float* __restrict__ dst = pk + L.pk_hidT + off;
-  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  for (int r = ty; r < 32; r += 8)
-    if (r0 + r < L.HP && c0 + tx < L.HP) t[r][tx] = src[(long long)(r0 + r) * L.HP + c0 + tx];
-  __syncthreads();
-  for (int r = ty; r < 32; r += 8)
-    if (c0 + r < L.HP && r0 + tx < L.HP) dst[(long long)(c0 + r) * L.HP + r0 + tx] = t[tx][r];
+__global__ __launch_bounds__(WWG) void k_wpack_all(const WideLayout L, const WpackGrid G,
+                                                   const float* __restrict__ prm, const float* __restrict__ q,
+                                                   float* __restrict__ pk) {
+  __shared__ float tile[WP_T][WP_T + 1];
+  long long b = blockIdx.x;
+  if (b < G.n_small) {          // first in the grid: their grid-stride loops overlap the bulk instead of trailing it
+    wpack_small(L, prm, q, pk, (int)b, (int)G.n_small);
+    return;
+  }
+  b -= G.n_small;
+  if (b < G.n_tiles) {
+    const int tt = G.t * G.t;
+    const long long kl = b / tt;                              // hidden matrix index vb * (NH - 1) + (l - 1)
+    const int r = (int)(b - kl * tt), n0 = (r / G.t) * WP_T, k0 = (r % G.t) * WP_T;
+    const int vb = (int)(kl / (L.NH - 1)), l = (int)(kl % (L.NH - 1)) + 1;
+    const float* __restrict__ src = prm + vbase(L, vb) + L.lin_w[vb % L.S][l];    // W_l[n][k] = src[n H + k]
+    float* __restrict__ dst = pk + L.pk_hid + kl * L.HP * L.HP;
+    float* __restrict__ dstT = pk + L.pk_hidT + kl * L.HP * L.HP;
+    const int c = threadIdx.x % WP_T, r0 = threadIdx.x / WP_T;
+    const int k = k0 + c;
+    constexpr int RPT = WP_T / (WWG / WP_T);                  // rows per thread: every load issued before a store
+    float v[RPT];
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      const int n = n0 + r0 + j * (WWG / WP_T);
+      v[j] = (n < L.H && k < L.H) ? src[(long long)n * L.H + k] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      const int i = r0 + j * (WWG / WP_T), n = n0 + i;
+      tile[i][c] = v[j];
+      if (n < L.HP && k < L.HP) dst[(long long)n * L.HP + k] = v[j];
+    }
+    __syncthreads();
+    // W^T[k][n] = W[n][k]: row k0 + i of the transposed copy, consecutive lanes on consecutive n
+#pragma unroll 4
+    for (int i = r0; i < WP_T; i += WWG / WP_T) {
+      const int kk = k0 + i, n = n0 + c;
+      if (kk < L.HP && n < L.HP) dstT[(long long)kk * L.HP + n] = tile[c][i];
+    }
+    return;
+  }
+  b -= G.n_tiles;
+  if (b < G.n_rows) {
+    // W0h_all row rr = vb * HP + n: W0_vb[n][nin + c], zero beyond H / C. One row per wave, so the row's block,
+    // side and source offset are wave-uniform (scalar); batches of WP_EB columns per lane, every load of a batch
+    // issued before its stores.
+    constexpr int WP_EB = 24;         // 1536 columns: one batch at C = 1360
+    const int rows = L.nv * L.HP;
+    const int rr = (int)b * WP_ROWS + (int)(threadIdx.x / 64), lane = threadIdx.x % 64;
+    if (rr < rows) {
+      const int vb = __builtin_amdgcn_readfirstlane(rr / L.HP);
+      const int n = __builtin_amdgcn_readfirstlane(rr - vb * L.HP);
+      const int sd = vb % L.S;
+      const float* __restrict__ src = prm + vbase(L, vb) + L.lin_w[sd][0] + (long long)n * L.in0[sd] + L.nin[sd];
+      float* __restrict__ dst = pk + L.pk_w0h + (long long)rr * L.Cp;
+      const int cv = n < L.H ? L.C : 0;
+      for (int c0 = 0; c0 < L.Cp; c0 += WP_EB * 64) {
+        float v[WP_EB];
+#pragma unroll
+        for (int j = 0; j < WP_EB; ++j) {
+          const int c = c0 + j * 64 + lane;
+          v[j] = c < cv ? src[c] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < WP_EB; ++j) {
+          const int c = c0 + j * 64 + lane;
+          if (c < L.Cp) dst[c] = v[j];
+        }
+      }
+    }
+  }
 }
 
 // out[m][n] = sum_p part[p][m][n] in p order (split-K partials; deterministic)
@@ -255,22 +309,6 @@ __global__ __launch_bounds__(WWG) void k_wsum_parts(const float* __restrict__ pa
     }
     *reinterpret_cast<floatx4*>(out + (long long)m * ldo + c) = a;
   }
-}
-
-// ActNorm log|det J| constant per block (ActNorm.forward, cnf.py:348-351: torch.sum(log|scale|)).
-__global__ void k_wpack_ldc(const WideLayout L, const float* __restrict__ prm, float* __restrict__ pk) {
-  const int k = threadIdx.x;
-  if (k >= L.nb) return;
-  float s = 0.f;
-  if (L.an && k < L.nb - 1)
-    for (int i = 0; i < L.D; ++i) s += logf(fabsf(prm[(long long)k * L.blk_stride + i]));
-  pk[L.pk_ldc + k] = s;
-}
-
-__global__ __launch_bounds__(WWG) void k_wpack_b0(const WideLayout L, const float* __restrict__ prm, float* __restrict__ pk) {
-  const int vb = blockIdx.x;
-  for (int n = threadIdx.x; n < L.HP; n += WWG)
-    pk[L.pk_b0 + (long long)vb * L.HP + n] = n < L.H ? prm[vbase(L, vb) + L.lin_b[vb % L.S][0] + n] : 0.f;
 }
 
 // rows of C floats -> rows of Cp floats (zero tail), for condition widths that are not a multiple of 4
@@ -2640,26 +2678,11 @@ int bcnf_wide_pack(const BcnfStackDesc* desc, const float* params, const float* 
   WideLayout L;
   WCHK(wide_layout(desc, &L));
   if (!params || !packed || (L.nb > 1 && !qmats) || !aligned16(packed)) return BCNF_ERR_ARG;
-  hipStream_t st = (hipStream_t)stream;
-  const long long n = L.pk_ldc - L.pk_w0y;
-  const int grid = (int)std::min<long long>((n + WWG - 1) / WWG, 4096);
-  {
-    const int cx = (std::max(L.Cp, L.HP) / 4 + WWG - 1) / WWG;
-    const long long rows = (long long)L.nv * L.HP * L.NH;   // W0h_all rows + hidden rows
-    hipLaunchKernelGGL(k_wpack_rows, dim3(cx, (unsigned)std::min<long long>(rows, 8192)), dim3(WWG), 0, st, L, params,
-                       (float*)packed);
-    WCHK(bcnf_rt::launched());
-  }
-  hipLaunchKernelGGL(k_wpack, dim3(grid), dim3(WWG), 0, st, L, params, qmats, (float*)packed);
-  WCHK(bcnf_rt::launched());
-  if (L.NH > 1) {
-    const int t = (L.HP + 31) / 32;
-    hipLaunchKernelGGL(k_wtranspose, dim3(t, t, L.nv * (L.NH - 1)), dim3(256), 0, st, L, (float*)packed);
-    WCHK(bcnf_rt::launched());
-  }
-  hipLaunchKernelGGL(k_wpack_ldc, dim3(1), dim3(((L.nb + 63) / 64) * 64), 0, st, L, params, (float*)packed);
-  WCHK(bcnf_rt::launched());
-  hipLaunchKernelGGL(k_wpack_b0, dim3(L.nv), dim3(WWG), 0, st, L, params, (float*)packed);
+  const WpackGrid g = wpack_grid(L);
+  const long long nwg = g.n_tiles + g.n_rows + g.n_small;
+  if (nwg > 0x7fffffffLL) return BCNF_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(k_wpack_all, dim3((unsigned)nwg), dim3(WWG), 0, (hipStream_t)stream, L, g, params, qmats,
+                     (float*)packed);
   return bcnf_rt::launched();
 }
 
