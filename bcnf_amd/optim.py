@@ -208,10 +208,23 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0):
     grads = [p.grad for p in parameters if p.grad is not None]
     if not grads:
         return torch.zeros(())
-    if len(grads) > N.MAX_TENSORS:
-        raise NotImplementedError(f"bcnf_amd clip_grad_norm_: at most {N.MAX_TENSORS} tensors per call")
     L = N.lib()
     dev = grads[0].device
+    if len(grads) > N.MAX_TENSORS:
+        # more tensors than one launch takes (a layerwise AnyGLU stack's per-layer parameters): the squared sums per
+        # group on the HIP kernel, the total and the scaling as torch.nn.utils.clip_grad_norm_ does them
+        sq = []
+        for chunk in _groups(grads):
+            numel = N.i64_array([g.numel() for g in chunk])
+            part = torch.empty(int(L.bcnf_grad_partials(sum(g.numel() for g in chunk))), dtype=torch.float32,
+                               device=dev)
+            N.check(L.bcnf_grad_sumsq(len(chunk), N.ptr_array(chunk), numel, N.ptr(part), N.stream_handle(dev)),
+                    "bcnf_grad_sumsq")
+            sq.append(part[:-1].sum())              # the last slot is the clip's pre-reduce scratch
+        norm = torch.stack(sq).sum().sqrt()
+        coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
+        torch._foreach_mul_(grads, coef)
+        return norm
     numel = N.i64_array([g.numel() for g in grads])
     total = sum(g.numel() for g in grads)
     part = torch.empty(int(L.bcnf_grad_partials(total)), dtype=torch.float32, device=dev)

@@ -54,15 +54,17 @@ GUARD_CHECK, GUARD_DIVERGED, GUARD_HALTED, GUARD_CHECK_GLOBAL, GUARD_WORDS = 0, 
 class TrainStep:
     def __init__(self, model, lr: float = 2e-4, hybrid_weight: float = 0.0, capture: bool = True,
                  max_norm: float = 1.0, process_group=None, overlap_ranges: int = 0):
-        if getattr(model, "_path", "fused") != "fused":
-            raise NotImplementedError(
-                f"bcnf_amd.TrainStep drives the fused Linear + GELU coupling kernels; a layer={model._fam[0]!r} model "
-                "trains through the reference's Trainer loop (torch.optim on model.parameters())")
+        # An AnyGLU coupling stack (layer="AnyGLU", reference layers.py:9-31, dev configs) has no fused kernel family:
+        # it runs layer by layer (its Linear layers on the library's MFMA GEMMs, autograd), so its step is the same
+        # Trainer step run eagerly over model.parameters() -- FusedAdam, the clip after the step, the bucket
+        # all-reduce -- without graph capture or the device divergence guard (the loss is checked on the host).
+        self.layerwise = getattr(model, "_path", "fused") == "layerwise"
         self.model = model
-        self.params = model.flat_parameters()
+        self.params = [p for p in model.parameters() if p.requires_grad] if self.layerwise \
+            else model.flat_parameters()
         self.hybrid_weight = float(hybrid_weight)
         self.max_norm = max_norm
-        self.capture = capture
+        self.capture = capture and not self.layerwise
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
         self.opt = FusedAdam(self.params, lr=lr)
@@ -202,7 +204,7 @@ class TrainStep:
             return
         self._alloc_bucket(self.params[0].device)
         lin = self.model._fold_linear() if hasattr(self.model, "_fold_linear") else None
-        if lin is None or not self.fused_loss:
+        if lin is None or not self.fused_loss or self.layerwise:
             return
         offs, off = {}, 0
         for p in self.params:
@@ -326,6 +328,12 @@ class TrainStep:
                 self._book = torch.zeros(1, dtype=torch.int32, device=self.params[0].device)
             self.opt.step(guard=self._guard, bookkeep=(cursor, log, self._book))
             return
+        if self.layerwise:
+            # eager only: the values go back to the caller directly (no history row); no device guard, and the
+            # parameter list may span several Adam launches (the generic clip of FusedAdam)
+            self.opt.step(defer_step_count=True)
+            self.opt.clip_grad_norm_after_step(self.max_norm, cursor=cursor)
+            return
         self.opt.step(defer_step_count=True, guard=self._guard)
         self.opt.clip_grad_norm_after_step(self.max_norm, cursor=cursor, log=log, guard=self._guard)
 
@@ -334,7 +342,8 @@ class TrainStep:
         if self.world == 1:
             return
         with torch.no_grad():
-            for p in list(self.model.parameters()) + [self.model.fused.qflat]:
+            frozen = [] if self.layerwise else [self.model.fused.qflat]   # layerwise: Q are model parameters
+            for p in list(self.model.parameters()) + frozen:
                 dist.broadcast(p.data, src=src, group=self.pg)
 
     # ------------------------------------------------------------------ eager / graph
@@ -360,7 +369,7 @@ class TrainStep:
         t = torch.empty((n,) + tuple(pt.shape[1:]), dtype=pt.dtype, device=pt.device)
         cy = py[0].numel()
         ct = pt[0].numel()
-        if defer and self.fused_loss and self.fuse_gather and \
+        if defer and self.fused_loss and self.fuse_gather and not self.layerwise and \
                 self.model._foldable_linear(y, (self._unpad(t),)) is not None:
             epoch = self._epoch is not None
             spec = N.BcnfGather2(idx=(self._epoch[0] if epoch else self._static[2]).data_ptr(),

@@ -357,3 +357,21 @@ def test_step_indexed_rejects_out_of_range_indices(g1):
         st.step_indexed(torch.tensor([0, 5, 64], device=DEV))
     with pytest.raises(IndexError):
         st.set_epoch(torch.tensor([0, -1], device=DEV), 2)
+
+
+def test_clip_grad_norm_over_more_tensors_than_one_launch_matches_torch():
+    """bcnf_amd.optim.clip_grad_norm_ over 120 tensors (> BCNF_MAX_TENSORS = 48: the layerwise AnyGLU TrainStep's
+    case) == torch.nn.utils.clip_grad_norm_ (norm and scaled gradients within 1e-6 relative)."""
+    from bcnf_amd.optim import clip_grad_norm_
+    g = torch.Generator().manual_seed(3)
+    sizes = [37, 5000, 1] * 40
+    ours = [torch.nn.Parameter(torch.zeros(n, device="cuda")) for n in sizes]
+    ref = [torch.nn.Parameter(torch.zeros(n, device="cuda")) for n in sizes]
+    for a, b, n in zip(ours, ref, sizes):
+        gr = torch.randn(n, generator=g).to("cuda")
+        a.grad, b.grad = gr.clone(), gr.clone()
+    n_ours = clip_grad_norm_(ours, 1.0)
+    n_ref = torch.nn.utils.clip_grad_norm_(ref, 1.0)
+    assert abs(n_ours.item() - n_ref.item()) <= 1e-6 * n_ref.item()
+    for a, b in zip(ours, ref):
+        assert torch.allclose(a.grad, b.grad, rtol=1e-6, atol=1e-9)
