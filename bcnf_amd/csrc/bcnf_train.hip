@@ -63,9 +63,9 @@ struct AdamBook {
   int* done;                    // workgroups finished; 0 between launches (the last one resets it); NULL: off
 };
 
-// G groups of EPT elements per thread (G = 4 for the wide family's ~49M parameters: a quarter of the workgroups, so a
-// quarter of the per-workgroup reductions and launch ramps, and 4x the bytes in flight per thread; G = 1 for small
-// sets, where more workgroups cover the chip). Group q of workgroup b starts at b * G * CHUNK + q * CHUNK.
+// G groups of EPT elements per thread (G = BIG_G = 2 for the wide family's ~49M parameters: half the workgroups, so
+// half the per-workgroup reductions and launch ramps, and 2x the bytes in flight per thread; G = 1 for small sets,
+// where more workgroups cover the chip). Group q of workgroup b starts at b * G * CHUNK + q * CHUNK.
 template <int G>
 __global__ __launch_bounds__(BCNF_WG) void k_adam(TList T, const float* __restrict__ step, double lr, double b1d,
                                                   double b2d, double epsd, double wdd, float* __restrict__ part,
@@ -197,19 +197,39 @@ __global__ __launch_bounds__(BCNF_WG) void k_clip(TList T, const float* __restri
                                                   long long n_batches, const float* __restrict__ log_values,
                                                   float* log_history, const int32_t* __restrict__ guard) {
   __shared__ float red[BCNF_WG];
-  // the gradient loads go out first, beside the partials' (the scaling needs the total norm, not the loads)
+  // the gradient loads go out first, beside the partials' (the scaling needs the total norm, not the loads). The
+  // element layout is k_adam<G>'s: thread x owns EPT = 4 consecutive elements of each group, one 16-B load / store
+  // when they lie in one tensor at a 16-B aligned offset (r05: per-element loads and tensor lookups ran FC_large's
+  // 49M-gradient clip at 2.3 TB/s)
   const long long total = T.start[T.n];
-  constexpr int NE = G * EPT;                    // elements per thread: this workgroup's G * CHUNK
-  float g[NE];
-  int t[NE];
-  long long o[NE];
+  float g[G][EPT];
+  int t[G][EPT];
+  long long o[G][EPT], i0[G];
+  bool vec[G];
 #pragma unroll
-  for (int e = 0; e < NE; ++e) {
-    long long i = (long long)blockIdx.x * G * CHUNK + e * BCNF_WG + threadIdx.x;
-    i = i < total ? i : total - 1;
-    t[e] = find_tensor(T, i);
-    o[e] = i - T.start[t[e]];
-    g[e] = T.g[t[e]][o[e]];
+  for (int q = 0; q < G; ++q) {
+    i0[q] = (long long)blockIdx.x * G * CHUNK + q * CHUNK + EPT * threadIdx.x;
+    const int t0 = find_tensor(T, i0[q] < total ? i0[q] : total - 1);
+    const long long o0 = i0[q] - T.start[t0];
+    vec[q] = i0[q] + EPT <= T.start[t0 + 1] && (((uintptr_t)(T.g[t0] + o0)) & 15) == 0;
+    if (vec[q]) {
+      const floatx4 g4 = *reinterpret_cast<const floatx4*>(T.g[t0] + o0);
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) {
+        g[q][e] = g4[e];
+        t[q][e] = t0;
+        o[q][e] = o0 + e;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) {
+        long long i = i0[q] + e;
+        i = i < total ? i : total - 1;
+        t[q][e] = find_tensor(T, i);
+        o[q][e] = i - T.start[t[q][e]];
+        g[q][e] = T.g[t[q][e]][o[q][e]];
+      }
+    }
   }
   if (guard && guard[BCNF_GUARD_HALTED]) return;
   float acc = 0.f;
@@ -217,9 +237,15 @@ __global__ __launch_bounds__(BCNF_WG) void k_clip(TList T, const float* __restri
   const float tot = sqrtf(wg_sum(acc, red));
   const float coef = fminf(max_norm / (tot + 1e-6f), 1.0f);
 #pragma unroll
-  for (int e = 0; e < NE; ++e) {
-    const long long i = (long long)blockIdx.x * G * CHUNK + e * BCNF_WG + threadIdx.x;
-    if (i < total) T.g[t[e]][o[e]] = g[e] * coef;
+  for (int q = 0; q < G; ++q) {
+    if (vec[q]) {
+      *reinterpret_cast<floatx4*>(T.g[t[q][0]] + o[q][0]) =
+          floatx4{g[q][0] * coef, g[q][1] * coef, g[q][2] * coef, g[q][3] * coef};
+    } else {
+#pragma unroll
+      for (int e = 0; e < EPT; ++e)
+        if (i0[q] + e < total) T.g[t[q][e]][o[q][e]] = g[q][e] * coef;
+    }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (norm_out) norm_out[0] = tot;
@@ -597,8 +623,11 @@ int split_rows(long long M) {        // rows per split-K chunk of the weight gra
   return (int)((r + 31) & ~31LL);
 }
 
-// Element groups per thread of k_adam / k_sumsq / k_clip: 4 for large parameter sets (>= 4M), else 1.
-inline int adam_groups(int64_t total_numel) { return total_numel >= (1 << 22) ? 4 : 1; }
+// Element groups per thread of k_adam / k_sumsq / k_clip: BIG_G for large parameter sets (>= 4M), else 1. At
+// FC_large's 48.9M parameters (tools/opt_bench.py, profiles/r05x_opt_bench.txt) Adam takes 297 us at 2 groups, 348 at
+// 4 (the register arrays of 4 groups cost occupancy), 600 at 8; the clip 131 / 124 / 178 us.
+constexpr int BIG_G = 2;
+inline int adam_groups(int64_t total_numel) { return total_numel >= (1 << 22) ? BIG_G : 1; }
 inline int64_t n_partials(int64_t total_numel) {
   const int64_t per = (int64_t)CHUNK * adam_groups(total_numel);
   return total_numel <= 0 ? 1 : (total_numel + per - 1) / per;
@@ -636,8 +665,8 @@ int bcnf_adam_step(int32_t n_tensors, float* const* params, float* const* grads,
     if (!T.p[i] || !T.m[i] || !T.v[i]) return BCNF_ERR_ARG;
   const long long total = T.start[T.n];
   const unsigned nwg = (unsigned)n_partials(total);
-  if (adam_groups(total) == 4)
-    hipLaunchKernelGGL(k_adam<4>, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, step, lr, beta1, beta2, eps,
+  if (adam_groups(total) == BIG_G)
+    hipLaunchKernelGGL(k_adam<BIG_G>, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, step, lr, beta1, beta2, eps,
                        weight_decay, grad_partials, guard, AdamBook{});
   else
     hipLaunchKernelGGL(k_adam<1>, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, step, lr, beta1, beta2, eps,
@@ -663,8 +692,8 @@ int bcnf_adam_step_bookkeep(int32_t n_tensors, float* const* params, float* cons
   const unsigned nwg = (unsigned)n_partials(total);
   const AdamBook bk{step, (long long*)advance_cursor, (long long)cursor_modulo, log_values, log_history,
                     (int*)done_counter};
-  if (adam_groups(total) == 4)
-    hipLaunchKernelGGL(k_adam<4>, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, step, lr, beta1, beta2, eps,
+  if (adam_groups(total) == BIG_G)
+    hipLaunchKernelGGL(k_adam<BIG_G>, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, step, lr, beta1, beta2, eps,
                        weight_decay, (float*)nullptr, guard, bk);
   else
     hipLaunchKernelGGL(k_adam<1>, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, step, lr, beta1, beta2, eps,
@@ -678,8 +707,8 @@ int bcnf_grad_sumsq(int32_t n_tensors, float* const* grads, const int64_t* numel
   if (rc) return rc;
   if (!grad_partials) return BCNF_ERR_ARG;
   const unsigned nwg = (unsigned)n_partials(T.start[T.n]);
-  if (adam_groups(T.start[T.n]) == 4)
-    hipLaunchKernelGGL(k_sumsq<4>, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, grad_partials);
+  if (adam_groups(T.start[T.n]) == BIG_G)
+    hipLaunchKernelGGL(k_sumsq<BIG_G>, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, grad_partials);
   else
     hipLaunchKernelGGL(k_sumsq<1>, dim3(nwg), dim3(BCNF_WG), 0, (hipStream_t)stream, T, grad_partials);
   return launched();
@@ -703,8 +732,8 @@ int bcnf_clip_grad_norm(int32_t n_tensors, float* const* grads, const int64_t* n
     part = grad_partials + np;
     nread = 1;
   }
-  if (adam_groups(T.start[T.n]) == 4)
-    hipLaunchKernelGGL(k_clip<4>, dim3((unsigned)np), dim3(BCNF_WG), 0, (hipStream_t)stream, T, part, nread,
+  if (adam_groups(T.start[T.n]) == BIG_G)
+    hipLaunchKernelGGL(k_clip<BIG_G>, dim3((unsigned)np), dim3(BCNF_WG), 0, (hipStream_t)stream, T, part, nread,
                        max_norm, total_norm, advance_step, (long long*)advance_cursor, (long long)cursor_modulo,
                        log_values, log_history, guard);
   else
