@@ -1179,23 +1179,30 @@ __device__ __forceinline__ void stage4(float* __restrict__ dst, const float* __r
   }
 }
 
-// Two regions staged with every load in flight at once (one memory round trip for up to 16 float4 per thread).
+// Two regions staged with every load in flight at once (one memory round trip for up to 16 float4 per thread). Every
+// workgroup of a link launch stages the SAME weights: the copy starts at a per-workgroup offset (whole 128-B lines,
+// spread over the XCD's 32 concurrent workgroups, b >> 3) so that they do not all request the same L2 lines in the
+// same order.
 __device__ __forceinline__ void stage4x2(float* __restrict__ d1, const float* __restrict__ s1, int n1,
                                          float* __restrict__ d2, const float* __restrict__ s2, int n2) {
   const int n = n1 + n2;
+  const int rot = (int)((blockIdx.x >> 3) * (unsigned)(n >> 5)) & ~7;
   for (int e0 = 0; e0 < n; e0 += 16 * WWG) {
     floatx4 v[16];
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       const int e = e0 + u * WWG + (int)threadIdx.x;
-      if (e < n1) v[u] = ld4(s1 + 4 * e);
-      else if (e < n) v[u] = ld4(s2 + 4 * (e - n1));
+      const int f = e + rot < n ? e + rot : e + rot - n;
+      if (e < n) v[u] = f < n1 ? ld4(s1 + 4 * f) : ld4(s2 + 4 * (f - n1));
     }
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       const int e = e0 + u * WWG + (int)threadIdx.x;
-      if (e < n1) st4(d1 + 4 * e, v[u]);
-      else if (e < n) st4(d2 + 4 * (e - n1), v[u]);
+      const int f = e + rot < n ? e + rot : e + rot - n;
+      if (e < n) {
+        if (f < n1) st4(d1 + 4 * f, v[u]);
+        else st4(d2 + 4 * (f - n1), v[u]);
+      }
     }
   }
 }
