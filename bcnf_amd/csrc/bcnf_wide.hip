@@ -354,6 +354,9 @@ struct GemmArgs {
   //   C + cb(v) + rm_off[side] + n * rm_ld[side] + col
   int rm_hp, rm_h; long long rm_off[2], rm_ld[2];
   int tiling;                   // host-side dispatch only: BcnfStackDesc.gemm_tiling of the call (0 = cost model)
+  // EPI_ACT on tiling W only (wbr_lp_ok): the block's LAST Linear applied to this tile's activations -- lp[row * lp_ld +
+  // 32 tile_x + j] = sum over the tile's columns c of A[row][c] Wl[j][c], j < lp_n (Wl rows of ld HP, lp_w)
+  float* lp; long long lp_ld; const float* lp_w; int lp_n, lp_wld;
 };
 
 __device__ __forceinline__ floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
@@ -435,11 +438,13 @@ __device__ __forceinline__ void epi_pre(const GemmArgs& g, const float* __restri
 
 template <int EPI>
 __device__ __forceinline__ void epi4(const GemmArgs& g, float* __restrict__ Cg, float* __restrict__ Xg, int rbase,
-                                     int col, const float v[4], uint4 rnd, const float pre[4], int rs = 1) {
+                                     int col, const float v[4], uint4 rnd, const float pre[4], int rs = 1,
+                                     float* aout = nullptr) {
   const int M = g.M, N = g.N;
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
     const int row = rbase + rs * rr;
+    if (aout) aout[rr] = 0.f;
     if (row >= M || col >= N) continue;
     if (EPI == EPI_STORE) {
       Cg[(long long)row * g.ldc + col] = v[rr];
@@ -462,6 +467,7 @@ __device__ __forceinline__ void epi4(const GemmArgs& g, float* __restrict__ Cg, 
       }
       Cg[(long long)row * g.ldc + col] = a;
       if (Xg) Xg[(long long)row * g.ldaux + col] = gd;
+      if (aout) aout[rr] = a;
     } else if (EPI == EPI_GRAD) {
       Cg[(long long)row * g.ldc + col] = v[rr] * pre[rr];
     } else if (EPI == EPI_LINGRAD) {
@@ -970,8 +976,14 @@ struct WbCfg {
   static constexpr int KMAX = WB_KMAX;
   __host__ __device__ static constexpr int stride(int K) { return ((K + CK - 1) / CK) * CK + 4; }
   __host__ __device__ static constexpr int band_floats(int K) { return (BN * stride(K) + 255) & ~255; }
+  // after the K loop the band is dead: KS-merge partials at 0, then (EPI_ACT with lp) a [16][17] transpose tile per
+  // wave and the owner waves' last-Linear partials [NT][KS][2][64 lanes][4]
+  // and the tile's slice of the last Linear's weights [32 rows][52] (row stride 52: the B-operand reads of 16 rows x 4
+  // columns hit 64 distinct banks)
+  static constexpr int LP_T = NT * NF * KS * 256, LP_M = LP_T + NW * 272, LP_W = LP_M + NT * KS * 2 * 256,
+                       LP_END = LP_W + 32 * 52;
   __host__ __device__ static constexpr int lds_floats(int K) {
-    return band_floats(K) > NT * NF * KS * 256 ? band_floats(K) : NT * NF * KS * 256;
+    return band_floats(K) > LP_END ? band_floats(K) : LP_END;
   }
 };
 
@@ -1034,6 +1046,15 @@ __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const
 #pragma unroll
   for (int f = 0; f < T::NF; ++f)
     if (mine(f)) epi_pre<EPI>(g, e.X, am0 + 16 * (f / T::TJ) + 4 * qq, n0 + 16 * (f % T::TJ) + c16, pre[f]);
+  // the last Linear's weights for the epilogue (EPI_ACT with lp, the block's last hidden layer): the tile's slice
+  // Wl[j][n0 .. n0 + 47], j < 32, one coalesced float4 per thread (in flight with the band, stored to LDS at the merge)
+  floatx4 wl4 = {0.f, 0.f, 0.f, 0.f};
+  const int wlr = threadIdx.x / 12, wlc = 4 * (threadIdx.x % 12);
+  if constexpr (EPI == EPI_ACT) {
+    static_assert(TI == 1 && KS > 1, "last-Linear partials: one 16-row tile per wave, a KS merge");
+    static_assert(64 * T::NW >= 32 * 12, "one float4 of the weight slice per thread");
+    if (g.lp && wlr < g.lp_n && n0 + wlc < g.N) wl4 = ld4(g.lp_w + (long long)wlr * g.lp_wld + n0 + wlc);
+  }
   // 2. the B band: piece p (1 KB) = LDS floats [256 p, 256 p + 256); lane l's float4 is column f / S, k = f % S
   //    (k >= K: padding, any valid source). (col, k) advance by a constant step per piece: one division per lane,
   //    not one per piece (r05)
@@ -1113,6 +1134,8 @@ __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const
 #pragma unroll
     for (int f = 0; f < T::NF; ++f)
       if (!mine(f)) st4(part + (f * KS + kh) * 256, acc[f]);
+    if constexpr (EPI == EPI_ACT)
+      if (g.lp && wlr < 32) st4(lds + T::LP_W + wlr * 52 + wlc, wl4);
     __syncthreads();
 #pragma unroll
     for (int f = 0; f < T::NF; ++f)
@@ -1128,13 +1151,62 @@ __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const
   }
   WBR_ST(4);
   epi_rng<EPI>(g, e);
+  float act[T::NF][4];
 #pragma unroll
   for (int f = 0; f < T::NF; ++f)
     if (mine(f)) {
       const float v[4] = {acc[f][0], acc[f][1], acc[f][2], acc[f][3]};
       const int rb = am0 + 16 * (f / T::TJ) + 4 * qq, col = n0 + 16 * (f % T::TJ) + c16;
-      epi4<EPI>(g, e.C, e.X, rb, col, v, epi_rnd<EPI>(g, e, rb, col), pre[f]);
+      epi4<EPI>(g, e.C, e.X, rb, col, v, epi_rnd<EPI>(g, e, rb, col), pre[f], 1, act[f]);
     }
+  if constexpr (EPI == EPI_ACT && KS > 1) {
+    if (g.lp) {
+      // the block's last Linear over this tile's 48 columns on the matrix cores: each owner wave transposes its
+      // sub-tiles' activations through LDS into A operands (A[m = lane & 15][k = lane >> 4]) and accumulates
+      // rows x (32 outputs); the owner waves of a row strip are then summed in K-slice order, and one partial per
+      // (row, column tile) goes out -- the link sums the column tiles' partials in order instead of 528-long dots
+      float* Tt = lds + T::LP_T + wave * 272;
+      floatx4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int f = 0; f < T::NF; ++f)
+        if (mine(f)) {
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) Tt[(4 * qq + rr) * 17 + c16] = act[f][rr];
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            // A[m = lane & 15][k = lane >> 4] = activation (row m, column 16 f + 4 s + k);
+            // B[k][n = lane & 15] = Wl[16 h + n][16 f + 4 s + k]
+            const float a = Tt[c16 * 17 + 4 * s4 + qq];
+            const float* wb = lds + T::LP_W + c16 * 52 + 16 * f + 4 * s4 + qq;
+            d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, wb[0], d0, 0, 0, 0);
+            d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, wb[16 * 52], d1, 0, 0, 0);
+          }
+        }
+      float* Mm = lds + T::LP_M + (wm * KS + kh) * 512 + lane * 4;
+      st4(Mm, d0);
+      st4(Mm + 256, d1);
+      __syncthreads();
+      if (kh == 0) {
+        const float* M0 = lds + T::LP_M + wm * KS * 512 + lane * 4;
+        floatx4 s0 = ld4(M0), s1 = ld4(M0 + 256);
+#pragma unroll
+        for (int h = 1; h < KS; ++h) {
+          const floatx4 p0 = ld4(M0 + h * 512), p1 = ld4(M0 + h * 512 + 256);
+          s0 = floatx4{s0[0] + p0[0], s0[1] + p0[1], s0[2] + p0[2], s0[3] + p0[3]};
+          s1 = floatx4{s1[0] + p1[0], s1[1] + p1[1], s1[2] + p1[2], s1[3] + p1[3]};
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = am0 + 4 * qq + i;
+          if (row < g.M) {
+            float* o = g.lp + (long long)row * g.lp_ld + 32 * tl.x;
+            o[c16] = s0[i];
+            o[16 + c16] = s1[i];
+          }
+        }
+      }
+    }
+  }
 #ifdef BCNF_PHASE_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   WBR_ST(5);
@@ -1160,6 +1232,7 @@ __global__ __launch_bounds__(64 * WGM * KS, (WGM * KS + 3) / 4) void k_wbr(const
 // ------------------------------------------------------------------------------------------------
 constexpr int LR = 8;          // samples per link workgroup
 constexpr int MQ = 5;          // float4 chunks per lane prefetched into registers (rows of up to 640 floats)
+constexpr int LP_MAX = 16;     // column-tile partials of the last Linear (tiling W: ceil(HP / 48) <= 16 at K <= 768)
 
 // Global -> LDS copy of n4 float4 by the whole workgroup with 8 loads in flight per thread (a plain copy loop
 // serialises one L2 round trip per iteration).
@@ -1222,6 +1295,8 @@ struct LinkArgs {
   const float* pk;              // packed
   // tail
   const float* Alast;           // [B][HP] last hidden activation of block vt
+  const float* Opart;           // nullable: the last Linear's per-column-tile partials of block vt (GemmArgs.lp),
+  long long ldo; int nop;       //   Opart[row * ldo + 32 p + j], p < nop -- replaces the dot products over Alast
   const float* Xt;              // block vt's saved input rows (forward: pre-ActNorm x or mid-coupling state; inverse: v)
   float* S;                     // forward save: tanh(s) of block vt [B][SP] (nullable)
   float* z;                     // last block: z / inverse output y [B][D] (ld D)
@@ -1303,16 +1378,23 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
   // The sample's HBM rows (last activation of block vt, projection row of block vh, saved input) are requested
   // first, so their latency overlaps the weight staging instead of serialising inside the dot-product loops.
   floatx4 ach[MQ], pch[MQ];
-  const float* arow = vt >= 0 ? a.Alast + row * HP : nullptr;
+  const bool dots = vt >= 0 && !a.Opart;          // the last Linear here (else its partials come with the tail)
+  const float* arow = dots ? a.Alast + row * HP : nullptr;
   const float* Pr = nullptr;
   if (vh >= 0) Pr = a.P + (a.cidx && valid ? a.cidx[row] : row) * a.ldP + (long long)vh * HP;
 #pragma unroll
   for (int t = 0; t < MQ; ++t) {
     const int q = ln + 32 * t;
     if (valid && q < nq) {
-      if (vt >= 0) ach[t] = ld4(arow + 4 * q);
+      if (dots) ach[t] = ld4(arow + 4 * q);
       if (vh >= 0) pch[t] = ld4(Pr + 4 * q);
     }
+  }
+  float opv[LP_MAX];
+  if (vt >= 0 && !dots) {
+#pragma unroll
+    for (int p = 0; p < LP_MAX; ++p)
+      opv[p] = (valid && ln < O2 && p < a.nop) ? a.Opart[row * a.ldo + 32 * p + ln] : 0.f;
   }
   float xpre = 0.f;
   if (lv) xpre = vt >= 0 ? a.Xt[row * L.XP + ln] : a.xin[row * D + ln];
@@ -1347,7 +1429,7 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
     if (vt >= 0) ldj0 = a.ldj[row];
     if (vh >= 0 && L.an && kh < L.nb - 1) ldc_h = a.pk[L.pk_ldc + kh];
   }
-  stage4x2(Wl, a.pk + L.pk_wl + (long long)(vt >= 0 ? vt : 0) * L.WL * HP, vt >= 0 ? O2 * HP / 4 : 0,
+  stage4x2(Wl, a.pk + L.pk_wl + (long long)(vt >= 0 ? vt : 0) * L.WL * HP, dots ? O2 * HP / 4 : 0,
            W0, a.pk + L.pk_w0y + (long long)(vh >= 0 ? vh : 0) * L.WY * HP, vh >= 0 ? nin_h * HP / 4 : 0);
   if (has_q)
 #pragma unroll
@@ -1362,38 +1444,49 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
   }
   float xi = 0.f;                                   // element ln of the sample's D-vector
   // ------------------------------------------------------------ tail of virtual block vt
+  if (vt >= 0 && !dots) {                          // the partials of the chain's last GEMM, summed in column order
+    if (ln < O2) {
+      float sp = opv[0];
+#pragma unroll
+      for (int p = 1; p < LP_MAX; ++p) sp += opv[p];  // zero past nop
+      Os[ln] = sp + blast;
+    }
+    __syncthreads();
+  }
   if (vt >= 0) {
     const int st = vt % L.S;
     float acc[DM];
 #pragma unroll
     for (int j = 0; j < DM; ++j) acc[j] = 0.f;
-    if (valid) {
-      auto chunk = [&](int q, floatx4 av) {
+    if (dots) {
+      if (valid) {
+        auto chunk = [&](int q, floatx4 av) {
 #pragma unroll
-        for (int j = 0; j < DM; ++j) {
-          if (j < O2) {
-            const floatx4 w = ld4(Wl + j * HP + 4 * q);
-            acc[j] = fmaf(av.x, w.x, fmaf(av.y, w.y, fmaf(av.z, w.z, fmaf(av.w, w.w, acc[j]))));
+          for (int j = 0; j < DM; ++j) {
+            if (j < O2) {
+              const floatx4 w = ld4(Wl + j * HP + 4 * q);
+              acc[j] = fmaf(av.x, w.x, fmaf(av.y, w.y, fmaf(av.z, w.z, fmaf(av.w, w.w, acc[j]))));
+            }
           }
-        }
-      };
+        };
 #pragma unroll
-      for (int t = 0; t < MQ; ++t)
-        if (ln + 32 * t < nq) chunk(ln + 32 * t, ach[t]);
-      for (int q = ln + 32 * MQ; q < nq; q += 32) chunk(q, ld4(arow + 4 * q));
+        for (int t = 0; t < MQ; ++t)
+          if (ln + 32 * t < nq) chunk(ln + 32 * t, ach[t]);
+        for (int q = ln + 32 * MQ; q < nq; q += 32) chunk(q, ld4(arow + 4 * q));
+      }
+#pragma unroll
+      for (int j = 0; j < DM; ++j)
+        if (j < O2) part[(r * 32 + ln) * PS + j] = acc[j];
+      LINK_STAMP(2);
+      __syncthreads();
+      if (ln < O2) {
+        float s = 0.f;
+#pragma unroll
+        for (int l = 0; l < 32; ++l) s += part[(r * 32 + l) * PS + ln];
+        Os[ln] = s + blast;
+      }
+      __syncthreads();
     }
-#pragma unroll
-    for (int j = 0; j < DM; ++j)
-      if (j < O2) part[(r * 32 + ln) * PS + j] = acc[j];
-    LINK_STAMP(2);
-    __syncthreads();
-    if (ln < O2) {
-      float s = 0.f;
-#pragma unroll
-      for (int l = 0; l < 32; ++l) s += part[(r * 32 + l) * PS + ln];
-      Os[ln] = s + blast;
-    }
-    __syncthreads();
     LINK_STAMP(3);
     float sj = 0.f;
     const int jt = ln - toff_t;
@@ -2173,8 +2266,11 @@ int lingrad_splitk(const GemmArgs& g, int groups, float* part, long long part_fl
 
 struct WideWs {       // workspace carve-up (floats)
   float *P, *A, *G, *dZ, *dZ0, *X, *S, *U, *O, *DV, *ANP, *nllp, *Hp;
+  float* LP;          // [B][32 * ceil(HP / 48)] last-Linear partials of the current block (tiling W epilogue)
   long long total;
 };
+
+inline int lp_tiles(const WideLayout& L) { return (L.HP + 47) / 48; }
 
 WideWs carve(const WideLayout& L, long long B, bool train, float* base) {
   WideWs w;
@@ -2204,6 +2300,7 @@ WideWs carve(const WideLayout& L, long long B, bool train, float* base) {
     w.X = take(B * (long long)L.XP);
   }
   if (L.Cp != L.C) w.Hp = take(B * (long long)L.Cp);   // h re-laid to rows of Cp floats
+  w.LP = take(B * 32LL * lp_tiles(L));
   w.total = o;
   return w;
 }
@@ -2297,9 +2394,22 @@ int projection(const WideLayout& L, const float* pk, const float* hp, long long 
   return gemm<true, true, EPI_STORE>(g, 1, st);
 }
 
-// hidden Linear l (1..NH-1) of virtual block v: A_l = dropout(GELU(A_{l-1} W_l^T + b_l)), G_l
+// Does gemm<true, true, EPI_ACT> run this GEMM on tiling W (k_wbr, whose epilogue can apply the block's last Linear)?
+// Mirrors the dispatch of gemm() / gemm_gl() for K-contiguous operands.
+bool wbr_lp_ok(const GemmArgs& g, int groups) {
+  if (g.K < 4 || g.K > WB_KMAX || g.M <= 0 || (g.N + 47) / 48 > LP_MAX) return false;
+  const int forced = g.tiling - 1;
+  if (forced == 9 || forced == 10) return true;
+  if (forced >= 0) return false;
+  const long long t128 = (long long)((g.M + 127) / 128) * ((g.N + 127) / 128) * groups;
+  return t128 < 2 * N_CU;
+}
+
+// hidden Linear l (1..NH-1) of virtual block v: A_l = dropout(GELU(A_{l-1} W_l^T + b_l)), G_l. With `lp` and the
+// last hidden layer on tiling W, the epilogue also writes the block's last-Linear partials (returned through *lp_on).
 int hidden_fwd(const WideLayout& L, const float* prm, const float* pk, int v, int l, long long B, const float* Ain,
-               float* Aout, float* Gout, const uint64_t* rng, hipStream_t st) {
+               float* Aout, float* Gout, const uint64_t* rng, hipStream_t st, float* lp = nullptr,
+               bool* lp_on = nullptr) {
   GemmArgs g = gemm_args(L.tiling, (int)B, L.HP, L.HP, Ain, L.HP, pk + L.pk_hid + ((long long)v * (L.NH - 1) + (l - 1)) * L.HP * L.HP,
                          L.HP, Aout, L.HP);
   g.bias = prm + vbase(L, v) + L.lin_b[v % L.S][l];
@@ -2310,6 +2420,16 @@ int hidden_fwd(const WideLayout& L, const float* prm, const float* pk, int v, in
   g.thresh = L.thresh;
   g.keep_scale = L.keep_scale;
   g.tag = (uint32_t)v * 16u + (uint32_t)l;
+  if (lp_on) *lp_on = false;
+  if (lp && l == L.NH - 1 && wbr_lp_ok(g, 1)) {
+    const int sd = v % L.S;
+    g.lp = lp;
+    g.lp_ld = 32LL * lp_tiles(L);
+    g.lp_w = pk + L.pk_wl + (long long)v * L.WL * L.HP;
+    g.lp_wld = L.HP;
+    g.lp_n = 2 * L.nout[sd];
+    if (lp_on) *lp_on = true;
+  }
   return gemm<true, true, EPI_ACT>(g, 1, st);
 }
 
@@ -2353,11 +2473,18 @@ int wide_forward(const WideLayout& L, const float* prm, const float* pk, const f
   auto Aptr = [&](int v, int l) -> float* { return save ? w.A + ((long long)v * L.NH + l) * slab : w.A + (l & 1) * slab; };
   auto Gptr = [&](int v, int l) -> float* { return save ? w.G + ((long long)v * L.NH + l) * slab : nullptr; };
   for (int v = -1; v < L.nv; ++v) {
+    bool lp_on = false;
     if (v >= 0)
       for (int l = 1; l < L.NH; ++l)
-        WCHK(hidden_fwd(L, prm, pk, v, l, B, Aptr(v, l - 1), Aptr(v, l), Gptr(v, l), drop ? rng : nullptr, st));
+        WCHK(hidden_fwd(L, prm, pk, v, l, B, Aptr(v, l - 1), Aptr(v, l), Gptr(v, l), drop ? rng : nullptr, st, w.LP,
+                        &lp_on));
     LinkArgs a;
     memset(&a, 0, sizeof(a));
+    if (lp_on) {
+      a.Opart = w.LP;
+      a.ldo = 32LL * lp_tiles(L);
+      a.nop = lp_tiles(L);
+    }
     a.B = B;
     a.vt = v;
     a.vh = (v + 1 < L.nv) ? v + 1 : -1;
