@@ -147,7 +147,8 @@ def test_wide_family_routing_and_layout_queries():
     ws = N.query_i64(lib.bcnf_wide_workspace_bytes, ctypes.byref(big), ctypes.c_int64(B), ctypes.c_int32(1))
     slab = B * HP
     regions = [B * nb * HP, B, nb * NH * slab, nb * NH * slab, nb * (NH - 1) * slab, B * nb * HP, (nb + 1) * B * 20,
-               nb * B * 12, nb * B * 12, nb * B * 20, B * 20, nb * B * 40]
+               nb * B * 12, nb * B * 12, nb * B * 20, B * 20, nb * B * 40,
+               B * 32 * 11]                   # last-Linear partials: 32 floats x ceil(528 / 48) column tiles per row
     assert ws == 4 * sum(r4(n) + 64 for n in regions)
     # the small family keeps FC_small
     small = N.make_desc(19, [16] * 7, 32, 80, 0.383, True)

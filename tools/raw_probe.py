@@ -33,6 +33,8 @@ def main():
               " helper at barrier0 / barrier1", buf[15] & 0xffffffff, buf[15] >> 32)
         print("  compute: x/Wf landed", buf[16], " helper: table landed", buf[20], "gathers landed", buf[21],
               "records written", buf[22])
+        print("  bwd compute prologue/chain/barrier-wait", buf[0], buf[1], buf[2],
+              " helper barrier-wait/load-issue/grad-jobs/prep-store", buf[4], buf[5], buf[6], buf[7])
         if buf[25]:
             print(f"  compute wave: {buf[24]} cycles in {buf[25] * 10 / 1e3:.2f} us -> {buf[24] / buf[25] / 10:.3f} GHz;"
                   f" helper wave: {buf[26]} cycles in {buf[27] * 10 / 1e3:.2f} us")
