@@ -174,6 +174,17 @@ __device__ __forceinline__ int coupling_base(const BcnfLayout& L, int k) {
   return k * L.blk_stride + ((k < L.nb - 1) ? L.an_size : 0);
 }
 
+// 16-B store written through to memory (sc1): nothing of it stays dirty in the XCD's L2 for the kernel boundary's
+// write-back. Inline asm: the wait pass does not count it, which only makes the compiler's own vmcnt waits stricter;
+// the trailing s_nop 1 is the store-data hazard of a > 8-byte store (a VALU must not overwrite its data VGPRs in the
+// next cycles), which the compiler's hazard pass covers for its own stores only (cdna_hip_programming.md §5.7).
+__device__ __forceinline__ void st4_wt(void* p, floatx4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v));
+}
+__device__ __forceinline__ void st1_wt(void* p, float v) {
+  asm volatile("global_store_dword %0, %1, off sc1" : : "v"(p), "v"(v));
+}
+
 // ---------------------------------------------------------------------------------------------
 // Rotation dot product over a 16-lane row: acc + sum_r x[(j-r)&15] * w[r].
 // The 15 DPP steps sit in ONE asm statement: the leading `s_nop 1` covers the VALU-write -> DPP-read

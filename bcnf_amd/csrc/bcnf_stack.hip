@@ -1947,9 +1947,11 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
       float ar[AR::AR];                                   // activation record of this block (SAVE)
       ar[AR::YA] = ya;
       ar[AR::YB] = yb;
-      // each float4 of the record is stored as soon as it is complete (coalesced across the wave)
+      // each float4 of the record is stored as soon as it is complete (coalesced across the wave), written through
+      // (sc1): the 132 MB of records never sit dirty in the L2s, whose write-back the kernel's end would otherwise
+      // wait for (r05: k_forward 55.3 -> 51.5 us, step -1.7 %, profiles/r05zl_ab_write_through_records.txt)
       auto emit = [&](int q) {
-        if (SAVE) d4[q * BCNF_WG] = floatx4{ar[4 * q], ar[4 * q + 1], ar[4 * q + 2], ar[4 * q + 3]};
+        if (SAVE) st4_wt(d4 + q * BCNF_WG, floatx4{ar[4 * q], ar[4 * q + 1], ar[4 * q + 2], ar[4 * q + 3]});
       };
       mlp_forward_s<NH, SAVE, DROP>(rr, rec + cur * RING + j * L.RF, xa, hpk, msk, T, Sp, ar, emit);
       const float Sv = tanh_bf(Sp);                      // cnf.py:107
@@ -1961,7 +1963,7 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
         for (int q = 0; q < AR::AR4; ++q)
           if (AR::ready_layer(q) == NH + 1) emit(q);
 #pragma unroll
-        for (int i = 0; i < AR::AR1; ++i) d1p[i * BCNF_WG] = ar[4 * AR::AR4 + i];
+        for (int i = 0; i < AR::AR1; ++i) st1_wt(d1p + i * BCNF_WG, ar[4 * AR::AR4 + i]);
         d4 += d4s;
         d1p += d1s;
       }
@@ -2384,7 +2386,8 @@ __device__ __forceinline__ float sum_rows4(float v) {
 //            holds D[4(l>>4) + r][l & 15], r = 0..3, stored as ONE float4 at [c][l] (1 KB per wave, coalesced)
 //            (Linear 1: only its y-part columns; the condition part is the split-K GEMM of the tail)
 //   sum job c: 16 column sums at SUM_OFF + 16 c (lanes 0..15)
-// The slab layout is decoded by slab_to_canonical.
+// The slab layout is decoded by slab_to_canonical. The MFMA tiles are written through (sc1), like the forward's
+// records: k_red_gx reads them from memory anyway.
 template <int NH>
 __device__ __forceinline__ void bwd_grad_jobs(const float* __restrict__ Td, const float* __restrict__ Ta,
                                               float* __restrict__ out, int hw) {
@@ -2418,7 +2421,7 @@ __device__ __forceinline__ void bwd_grad_jobs(const float* __restrict__ Td, cons
   }
 #pragma unroll
   for (int u = 0; u < UW; ++u)
-    if (hw + 4 * u < J::NW) reinterpret_cast<floatx4*>(out + 256 * (hw + 4 * u))[l64] = acc[u];
+    if (hw + 4 * u < J::NW) st4_wt(reinterpret_cast<floatx4*>(out + 256 * (hw + 4 * u)) + l64, acc[u]);
 }
 
 // Whole-stack backward, one launch, 512 threads = two roles per SIMD (waves w and w + 4 share a SIMD):
