@@ -449,6 +449,10 @@ __device__ __forceinline__ void epi4(const GemmArgs& g, float* __restrict__ Cg, 
     if (EPI == EPI_STORE) {
       Cg[(long long)row * g.ldc + col] = v[rr];
     } else if (EPI == EPI_ACT) {
+      // the chain's activations / derivative factors (and EPI_GRAD's dZ, the links' A0 / G0 / dZ) are written through
+      // (sc1): nothing stays dirty in the L2s for the kernel boundary (r05: FC_large 7.59 -> 7.43 ms per step,
+      // profiles/r05zo_ab_wide_write_through.txt); the Linear-gradient / store / row-map epilogues keep write-back
+      // stores (write-through there cost the backward ~80 us)
       float a = 0.f, gd = 0.f;
       if (col < g.n_real) {
         float ge, dg;
@@ -465,11 +469,11 @@ __device__ __forceinline__ void epi4(const GemmArgs& g, float* __restrict__ Cg, 
       } else if (col == g.n_real) {
         a = 1.f;
       }
-      Cg[(long long)row * g.ldc + col] = a;
-      if (Xg) Xg[(long long)row * g.ldaux + col] = gd;
+      st1_wt(Cg + (long long)row * g.ldc + col, a);
+      if (Xg) st1_wt(Xg + (long long)row * g.ldaux + col, gd);
       if (aout) aout[rr] = a;
     } else if (EPI == EPI_GRAD) {
-      Cg[(long long)row * g.ldc + col] = v[rr] * pre[rr];
+      st1_wt(Cg + (long long)row * g.ldc + col, v[rr] * pre[rr]);
     } else if (EPI == EPI_LINGRAD) {
       if (col < g.wcols) Cg[(long long)row * g.ldc + col] = v[rr];
       else if (col == g.wcols) Cg[g.boff + row] = v[rr];
@@ -1597,8 +1601,8 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
           av[e] = c == H ? 1.f : ge * m;
           gv[e] = dg * m;
         }
-        st4(a.A0 + row * HP + n, floatx4{av[0], av[1], av[2], av[3]});
-        if (a.G0) st4(a.G0 + row * HP + n, floatx4{gv[0], gv[1], gv[2], gv[3]});
+        st4_wt(a.A0 + row * HP + n, floatx4{av[0], av[1], av[2], av[3]});
+        if (a.G0) st4_wt(a.G0 + row * HP + n, floatx4{gv[0], gv[1], gv[2], gv[3]});
       };
 #pragma unroll
       for (int t = 0; t < MQ; ++t)
@@ -1797,7 +1801,7 @@ __global__ __launch_bounds__(WWG) void k_wlink_bwd(const WideLayout L, const Lin
             s4.w = fmaf(dO[j], w.w, s4.w);
           }
         }
-        st4(out + n, s4 * gv);
+        st4_wt(out + n, s4 * gv);
       };
 #pragma unroll
       for (int t = 0; t < MQ; ++t)
