@@ -488,6 +488,17 @@ __device__ __forceinline__ void epi4(const GemmArgs& g, float* __restrict__ Cg, 
   }
 }
 
+// EPI_ROWMAP's destination row (see GemmArgs): the flat-gradient row of output row `row`, nullptr when the row is past
+// M or a padding row (n >= rm_h)
+__device__ __forceinline__ float* rowmap_ptr(const GemmArgs& g, float* Cg, int row) {
+  if (row >= g.M) return nullptr;
+  const int vr = row / g.rm_hp, n = row - vr * g.rm_hp, vb = vr + g.cb_v0;
+  if (n >= g.rm_h) return nullptr;
+  const int blk = vb / g.cb_S, sd = vb - blk * g.cb_S;
+  return Cg + (long long)blk * g.cb_stride + ((blk < g.cb_nb - 1) ? g.cb_an : 0) + sd * g.cb_side +
+         (sd ? g.rm_off[1] : g.rm_off[0]) + (long long)n * (sd ? g.rm_ld[1] : g.rm_ld[0]);
+}
+
 struct EpiCtx {
   float* C;
   float* X;
@@ -945,6 +956,25 @@ __global__ __launch_bounds__(64 * WGM * WGN * KS, (S * (BM + BN) * 64 * 4 <= 80 
           const floatx4 p = ld4(part + (i * T::TJ + j) * 256);
           acc[i][j] = floatx4{acc[i][j][0] + p[0], acc[i][j][1] + p[1], acc[i][j][2] + p[2], acc[i][j][3] + p[3]};
         }
+  }
+  if constexpr (EPI == EPI_ROWMAP) {
+    // the row map once per output row of the lane (16 rows x TJ columns share it), not once per element: epi4's
+    // per-element divisions and selects made this epilogue ~5k instructions (r05: the condition-gradient GEMM ran
+    // 183 us against 126 us for the same GEMM with plain stores; backward -8 to -20 us, profiles/r05zv_*)
+#pragma unroll
+    for (int i = 0; i < T::TI; ++i) {
+      float* rowp[4];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) rowp[rr] = rowmap_ptr(g, e.C, rbase(i) + RS * rr);
+#pragma unroll
+      for (int j = 0; j < T::TJ; ++j)
+        if (mine(i * T::TJ + j) && colof(j) < g.N) {
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr)
+            if (rowp[rr]) rowp[rr][colof(j)] = acc[i][j][rr];
+        }
+    }
+    return;
   }
 #pragma unroll
   for (int i = 0; i < T::TI; ++i)
