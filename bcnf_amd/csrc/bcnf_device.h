@@ -178,6 +178,8 @@ __device__ __forceinline__ int coupling_base(const BcnfLayout& L, int k) {
 // write-back. Inline asm: the wait pass does not count it, which only makes the compiler's own vmcnt waits stricter;
 // the trailing s_nop 1 is the store-data hazard of a > 8-byte store (a VALU must not overwrite its data VGPRs in the
 // next cycles), which the compiler's hazard pass covers for its own stores only (cdna_hip_programming.md §5.7).
+// Only for data that later launches read: the asm carries no memory clobber, so the compiler may move this launch's
+// own loads across it (every call site stores records / activations / partials its kernel never reads back).
 __device__ __forceinline__ void st4_wt(void* p, floatx4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v));
 }
