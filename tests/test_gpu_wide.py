@@ -441,3 +441,70 @@ def test_wide_two_way_model_matches_reference():
         assert ok, (name, err)
         n += 1
     assert n == len([k for k in sd if not k.endswith("orthonormal_matrix")])
+
+
+def test_weight_pack_layout_is_the_parameter_relayout():
+    """k_wpack_all (bcnf_wide_pack, one launch): every packed region equals the re-layout of the model's own
+    parameters -- W0's condition columns as W0h rows, each hidden W row-major AND transposed, W0's y columns
+    transposed, the last Linear, Q, the Linear-1 biases (bit-exact copies, zero padding) and the ActNorm log-det
+    constants (within 1e-6). Layout: WideLayout in bcnf_wide.hip."""
+    from bcnf_amd import CondRealNVP_v2
+    H, C, nb, NH, D = 40, 12, 3, 3, 19
+    cfg = {"global": {"parameter_selection": [f"p{i}" for i in range(D)]},
+           "model": {"kwargs": {"size": D, "nested_sizes": [H] * NH, "n_conditions": C, "n_blocks": nb,
+                                "dropout": 0.0, "act_norm": True}},
+           "feature_networks": [{"type": "ConcatenateCondition", "kwargs": {"input_size": None, "output_size": C}}]}
+    torch.manual_seed(3)
+    m = CondRealNVP_v2.from_config(cfg)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if n.endswith("scale"):
+                p.copy_(0.5 + torch.rand_like(p))
+    m.to(DEV)
+    pk = m.fused.packed().cpu()
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    Da, Db = (D + 1) // 2, D // 2
+    r4 = lambda n: (n + 3) // 4 * 4  # noqa: E731
+    HP, Cp, nv, WY, WL = r4(H + 1), r4(C), nb, Da, 2 * Db
+    o_w0h = 0
+    o_hid = o_w0h + r4(nv * HP * Cp)
+    o_hidT = o_hid + r4(nv * (NH - 1) * HP * HP)
+    o_w0y = o_hidT + r4(nv * (NH - 1) * HP * HP)
+    o_wl = o_w0y + r4(nv * WY * HP)
+    o_q = o_wl + r4(nv * WL * HP)
+    o_ldc = o_q + r4((nb - 1) * D * D)
+    o_b0 = o_ldc + r4(nb)
+    assert pk.numel() == o_b0 + nv * HP
+    coup = [i for i in range(3 * nb) if any(k.startswith(f"layers.{i}.nn_a.") for k in sd)]
+    an = [i for i in range(3 * nb) if f"layers.{i}.scale" in sd]
+    qs = [i for i in range(3 * nb) if f"layers.{i}.orthonormal_matrix" in sd]
+    assert len(coup) == nb and len(an) == nb - 1 and len(qs) == nb - 1
+    for v, li in enumerate(coup):
+        wk = sorted((k for k in sd if k.startswith(f"layers.{li}.nn_a.nn.") and k.endswith(".weight")),
+                    key=lambda k: int(k.split(".")[-2]))
+        assert len(wk) == NH + 1
+        W = [sd[k] for k in wk]
+        b0 = sd[wk[0][:-len("weight")] + "bias"]
+        want = torch.zeros(HP, Cp)
+        want[:H, :C] = W[0][:, Da:]
+        assert torch.equal(pk[o_w0h + v * HP * Cp: o_w0h + (v + 1) * HP * Cp].view(HP, Cp), want), ("w0h", v)
+        for l in range(1, NH):
+            base = (v * (NH - 1) + l - 1) * HP * HP
+            want = torch.zeros(HP, HP)
+            want[:H, :H] = W[l]
+            assert torch.equal(pk[o_hid + base: o_hid + base + HP * HP].view(HP, HP), want), ("hid", v, l)
+            assert torch.equal(pk[o_hidT + base: o_hidT + base + HP * HP].view(HP, HP), want.t()), ("hidT", v, l)
+        want = torch.zeros(WY, HP)
+        want[:Da, :H] = W[0][:, :Da].t()
+        assert torch.equal(pk[o_w0y + v * WY * HP: o_w0y + (v + 1) * WY * HP].view(WY, HP), want), ("w0y", v)
+        want = torch.zeros(WL, HP)
+        want[:2 * Db, :H] = W[NH]
+        assert torch.equal(pk[o_wl + v * WL * HP: o_wl + (v + 1) * WL * HP].view(WL, HP), want), ("wl", v)
+        want = torch.zeros(HP)
+        want[:H] = b0
+        assert torch.equal(pk[o_b0 + v * HP: o_b0 + (v + 1) * HP], want), ("b0", v)
+    for k, li in enumerate(qs):
+        assert torch.equal(pk[o_q + k * D * D: o_q + (k + 1) * D * D].view(D, D), sd[f"layers.{li}.orthonormal_matrix"])
+    for k in range(nb):
+        want = float(torch.log(sd[f"layers.{an[k]}.scale"].abs()).sum()) if k < nb - 1 else 0.0
+        assert abs(float(pk[o_ldc + k]) - want) <= 1e-6 * max(1.0, abs(want)), ("ldc", k)
