@@ -625,7 +625,8 @@ int split_rows(long long M) {        // rows per split-K chunk of the weight gra
 
 // Element groups per thread of k_adam / k_sumsq / k_clip: BIG_G for large parameter sets (>= 4M), else 1. At
 // FC_large's 48.9M parameters (tools/opt_bench.py, profiles/r05x_opt_bench.txt) Adam takes 297 us at 2 groups, 348 at
-// 4 (the register arrays of 4 groups cost occupancy), 600 at 8; the clip 131 / 124 / 178 us.
+// 4 (the register arrays of 4 groups cost occupancy), 600 at 8; the clip 131 / 124 / 178 us (103 us at 2 groups once
+// k_sum_partials stopped being a serial chain, r05zz3).
 constexpr int BIG_G = 2;
 inline int adam_groups(int64_t total_numel) { return total_numel >= (1 << 22) ? BIG_G : 1; }
 inline int64_t n_partials(int64_t total_numel) {
@@ -634,16 +635,42 @@ inline int64_t n_partials(int64_t total_numel) {
 }
 
 // Sum of many partials by one workgroup (fixed order), so that every clip workgroup then reads one value
-// instead of re-reducing all partials (quadratic in the parameter count otherwise).
+// instead of re-reducing all partials (quadratic in the parameter count otherwise). 1024 threads, 16-B loads, eight in
+// flight per thread: FC_large's 23.9k partials are ~6 loads per thread, not a 94-deep chain of dependent ones (the
+// 256-thread scalar loop took 18 us at 12k partials, r04zz2).
 constexpr int CLIP_DIRECT_PARTIALS = 2048;
-__global__ __launch_bounds__(BCNF_WG) void k_sum_partials(const float* __restrict__ part, int nparts,
-                                                          float* __restrict__ out, const int32_t* __restrict__ guard) {
-  __shared__ float red[BCNF_WG];
+constexpr int SP_WG = 1024;
+constexpr int SP_U = 8;
+__global__ __launch_bounds__(SP_WG) void k_sum_partials(const float* __restrict__ part, int nparts,
+                                                       float* __restrict__ out, const int32_t* __restrict__ guard) {
+  __shared__ float red[SP_WG / 64];
   if (guard && guard[BCNF_GUARD_HALTED]) return;
-  float acc = 0.f;
-  for (int i = threadIdx.x; i < nparts; i += BCNF_WG) acc += part[i];
-  const float s = wg_sum(acc, red);
-  if (threadIdx.x == 0) out[0] = s;
+  const int n4 = (reinterpret_cast<uintptr_t>(part) & 15) ? 0 : nparts >> 2;    // scalar loop if unaligned
+  const floatx4* __restrict__ p4 = reinterpret_cast<const floatx4*>(part);
+  float acc[SP_U];
+#pragma unroll
+  for (int u = 0; u < SP_U; ++u) acc[u] = 0.f;
+  for (int b = threadIdx.x; b < n4; b += SP_WG * SP_U) {
+    floatx4 v[SP_U];
+#pragma unroll
+    for (int u = 0; u < SP_U; ++u) v[u] = b + u * SP_WG < n4 ? p4[b + u * SP_WG] : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < SP_U; ++u) acc[u] += (v[u][0] + v[u][1]) + (v[u][2] + v[u][3]);
+  }
+  float a = 0.f;
+#pragma unroll
+  for (int u = 0; u < SP_U; ++u) a += acc[u];
+  for (int i = 4 * n4 + threadIdx.x; i < nparts; i += SP_WG) a += part[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < SP_WG / 64; ++w) s += red[w];
+    out[0] = s;
+  }
 }
 
 }  // namespace
@@ -727,7 +754,7 @@ int bcnf_clip_grad_norm(int32_t n_tensors, float* const* grads, const int64_t* n
   const float* part = grad_partials;
   int nread = (int)np;
   if (np > CLIP_DIRECT_PARTIALS) {      // pre-reduce into the extra slot
-    hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(BCNF_WG), 0, (hipStream_t)stream, grad_partials, (int)np,
+    hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(SP_WG), 0, (hipStream_t)stream, grad_partials, (int)np,
                        const_cast<float*>(grad_partials) + np, guard);
     part = grad_partials + np;
     nread = 1;

@@ -375,3 +375,25 @@ def test_clip_grad_norm_over_more_tensors_than_one_launch_matches_torch():
     assert abs(n_ours.item() - n_ref.item()) <= 1e-6 * n_ref.item()
     for a, b in zip(ours, ref):
         assert torch.allclose(a.grad, b.grad, rtol=1e-6, atol=1e-9)
+
+
+def test_clip_after_step_over_a_pre_reduced_partial_set_matches_fp64():
+    """A 5.3M-parameter set (> CLIP_DIRECT_PARTIALS workgroup partials: k_sum_partials pre-reduces them, one
+    1024-thread workgroup) plus ragged tensors: clip-after-step norm and scaled grads against the fp64 clip
+    (torch.nn.utils.clip_grad_norm_'s formula) within 1e-5 relative. fp64, not torch's fp32 CPU norm: at 5.3M terms
+    that one's own rounding is ~1e-4 relative."""
+    from bcnf_amd.optim import FusedAdam
+    gen = torch.Generator().manual_seed(11)
+    shapes = [(5_300_001,), (37, 3), (1,)]
+    grads = [torch.randn(s, generator=gen) for s in shapes]
+    ours = [torch.zeros(s, device=DEV).requires_grad_() for s in shapes]
+    for q, g in zip(ours, grads):
+        q.grad = g.to(DEV)
+    opt = FusedAdam(ours, lr=1e-3)
+    opt.step()
+    n_ours = opt.clip_grad_norm_after_step(1.0)
+    n_ref = float(sum((g.double() ** 2).sum() for g in grads)) ** 0.5
+    coef = min(1.0 / (n_ref + 1e-6), 1.0)
+    assert abs(n_ours.item() - n_ref) <= 1e-5 * n_ref
+    for a, g in zip(ours, grads):
+        assert torch.allclose(a.grad.cpu().double(), g.double() * coef, rtol=1e-5, atol=1e-12)
