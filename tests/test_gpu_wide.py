@@ -443,16 +443,18 @@ def test_wide_two_way_model_matches_reference():
     assert n == len([k for k in sd if not k.endswith("orthonormal_matrix")])
 
 
-def test_weight_pack_layout_is_the_parameter_relayout():
+@pytest.mark.parametrize("two_way", [False, True], ids=["one_way", "two_way"])
+def test_weight_pack_layout_is_the_parameter_relayout(two_way):
     """k_wpack_all (bcnf_wide_pack, one launch): every packed region equals the re-layout of the model's own
     parameters -- W0's condition columns as W0h rows, each hidden W row-major AND transposed, W0's y columns
     transposed, the last Linear, Q, the Linear-1 biases (bit-exact copies, zero padding) and the ActNorm log-det
-    constants (within 1e-6). Layout: WideLayout in bcnf_wide.hip."""
+    constants (within 1e-6). Two-way blocks are two virtual blocks (nn_a, then nn_b). Layout: WideLayout in
+    bcnf_wide.hip."""
     from bcnf_amd import CondRealNVP_v2
     H, C, nb, NH, D = 40, 12, 3, 3, 19
     cfg = {"global": {"parameter_selection": [f"p{i}" for i in range(D)]},
            "model": {"kwargs": {"size": D, "nested_sizes": [H] * NH, "n_conditions": C, "n_blocks": nb,
-                                "dropout": 0.0, "act_norm": True}},
+                                "dropout": 0.0, "act_norm": True, "two_way": two_way}},
            "feature_networks": [{"type": "ConcatenateCondition", "kwargs": {"input_size": None, "output_size": C}}]}
     torch.manual_seed(3)
     m = CondRealNVP_v2.from_config(cfg)
@@ -464,8 +466,10 @@ def test_weight_pack_layout_is_the_parameter_relayout():
     pk = m.fused.packed().cpu()
     sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
     Da, Db = (D + 1) // 2, D // 2
+    S = 2 if two_way else 1
+    nin, nout = [Da, Db], [Db, Da]
     r4 = lambda n: (n + 3) // 4 * 4  # noqa: E731
-    HP, Cp, nv, WY, WL = r4(H + 1), r4(C), nb, Da, 2 * Db
+    HP, Cp, nv, WY, WL = r4(H + 1), r4(C), nb * S, Da, 2 * (Da if two_way else Db)
     o_w0h = 0
     o_hid = o_w0h + r4(nv * HP * Cp)
     o_hidT = o_hid + r4(nv * (NH - 1) * HP * HP)
@@ -479,14 +483,16 @@ def test_weight_pack_layout_is_the_parameter_relayout():
     an = [i for i in range(3 * nb) if f"layers.{i}.scale" in sd]
     qs = [i for i in range(3 * nb) if f"layers.{i}.orthonormal_matrix" in sd]
     assert len(coup) == nb and len(an) == nb - 1 and len(qs) == nb - 1
-    for v, li in enumerate(coup):
-        wk = sorted((k for k in sd if k.startswith(f"layers.{li}.nn_a.nn.") and k.endswith(".weight")),
-                    key=lambda k: int(k.split(".")[-2]))
+    for v in range(nv):
+        li, side = coup[v // S], v % S
+        pre = f"layers.{li}.nn_{'ab'[side]}.nn."
+        wk = sorted((k for k in sd if k.startswith(pre) and k.endswith(".weight")), key=lambda k: int(k.split(".")[-2]))
         assert len(wk) == NH + 1
         W = [sd[k] for k in wk]
         b0 = sd[wk[0][:-len("weight")] + "bias"]
+        ni, no = nin[side], nout[side]
         want = torch.zeros(HP, Cp)
-        want[:H, :C] = W[0][:, Da:]
+        want[:H, :C] = W[0][:, ni:]
         assert torch.equal(pk[o_w0h + v * HP * Cp: o_w0h + (v + 1) * HP * Cp].view(HP, Cp), want), ("w0h", v)
         for l in range(1, NH):
             base = (v * (NH - 1) + l - 1) * HP * HP
@@ -495,10 +501,10 @@ def test_weight_pack_layout_is_the_parameter_relayout():
             assert torch.equal(pk[o_hid + base: o_hid + base + HP * HP].view(HP, HP), want), ("hid", v, l)
             assert torch.equal(pk[o_hidT + base: o_hidT + base + HP * HP].view(HP, HP), want.t()), ("hidT", v, l)
         want = torch.zeros(WY, HP)
-        want[:Da, :H] = W[0][:, :Da].t()
+        want[:ni, :H] = W[0][:, :ni].t()
         assert torch.equal(pk[o_w0y + v * WY * HP: o_w0y + (v + 1) * WY * HP].view(WY, HP), want), ("w0y", v)
         want = torch.zeros(WL, HP)
-        want[:2 * Db, :H] = W[NH]
+        want[:2 * no, :H] = W[NH]
         assert torch.equal(pk[o_wl + v * WL * HP: o_wl + (v + 1) * WL * HP].view(WL, HP), want), ("wl", v)
         want = torch.zeros(HP)
         want[:H] = b0
