@@ -719,18 +719,43 @@ __global__ __launch_bounds__(64 * NW, (wg16_occ<BM, BN, BK, AKC, BKC, NW>())) vo
 #pragma unroll
     for (int kc = 0; kc < BK / 16; ++kc) {
       const int kb = 16 * kc + 4 * qq;
-      floatx4 af[TI], bf[TJ];
+      if constexpr (TI == 1) {
+        // one 16-row strip per wave (the 176 x 176 Linear-gradient tile): B columns two at a time, the four k steps of
+        // each pair interleaved over the pair's two independent accumulators. With every fragment read first (the
+        // order below) hipcc, at its 168-VGPR cap, re-serialised the tile to ds_read2 -> wait -> 2 MFMAs; this order
+        // lets it keep several reads in flight: 1180 -> 1153-1162 us per FC_large step
+        // (profiles/r05zz7_ab_lingrad_pairs.txt). Same k order per accumulator: bit-identical
+        const floatx4 a0 = IO::template frag<BM, AKC>(As, wave * WM + c16, kb);
 #pragma unroll
-      for (int i = 0; i < TI; ++i) af[i] = IO::template frag<BM, AKC>(As, wave * WM + 16 * i + c16, kb);
+        for (int j = 0; j < TJ; j += 2) {
+          const floatx4 b0 = IO::template frag<BN, BKC>(Bs, 16 * j + c16, kb);
+          if (j + 1 < TJ) {
+            const floatx4 b1 = IO::template frag<BN, BKC>(Bs, 16 * (j + 1) + c16, kb);
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) bf[j] = IO::template frag<BN, BKC>(Bs, 16 * j + c16, kb);
+            for (int s = 0; s < 4; ++s) {
+              acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s], b0[s], acc[0][j], 0, 0, 0);
+              acc[0][j + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s], b1[s], acc[0][j + 1], 0, 0, 0);
+            }
+          } else {
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+            for (int s = 0; s < 4; ++s)
+              acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s], b0[s], acc[0][j], 0, 0, 0);
+          }
+        }
+      } else {
+        floatx4 af[TI], bf[TJ];
 #pragma unroll
-        for (int i = 0; i < TI; ++i)
+        for (int i = 0; i < TI; ++i) af[i] = IO::template frag<BM, AKC>(As, wave * WM + 16 * i + c16, kb);
 #pragma unroll
-          for (int j = 0; j < TJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TJ; ++j) bf[j] = IO::template frag<BN, BKC>(Bs, 16 * j + c16, kb);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+      }
     }
   };
   k_loop<IO>(g, A, B, m0, n0, lds, tile);
