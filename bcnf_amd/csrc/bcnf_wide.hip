@@ -363,8 +363,10 @@ __device__ __forceinline__ floatx4 ld4(const float* p) { return *reinterpret_cas
 __device__ __forceinline__ void st4(float* p, floatx4 v) { *reinterpret_cast<floatx4*>(p) = v; }
 
 // Global -> register -> LDS staging of one BM x BK (A) and BK x BN (B) tile pair by NT threads, shared by both MFMA
-// tilings.
-template <int BM, int BN, int BK, bool AKC, bool BKC, int NT = WWG>
+// tilings. FULL: the host has checked that every load of the grid lies inside its operand (K % BK == 0 and the tile
+// grid's row / column extent within each leading dimension), so the loads carry no predicates -- no zeroing moves and
+// no exec-mask branches in the K loop.
+template <int BM, int BN, int BK, bool AKC, bool BKC, int NT = WWG, bool FULL = false>
 struct TileIO {
   static constexpr int BKT = BK;
   static constexpr int ASZ = AKC ? BM * (BK + 4) : BK * (BM + 4);
@@ -376,24 +378,25 @@ struct TileIO {
   __device__ __forceinline__ static floatx4 fetch(const float* __restrict__ X, long long ld, int e, int mn0, int k0,
                                                   int MN, int K) {
     floatx4 v = {0.f, 0.f, 0.f, 0.f};
-    if (e >= ROWS * BK / 4) return v;
+    // e = threadIdx.x + NT i over i < AV / BV: in range by construction when NT divides the tile's float4 count
+    if ((ROWS * BK / 4) % NT != 0 && e >= ROWS * BK / 4) return v;
     if (KC) {
       const int row = e / (BK / 4), kq = e % (BK / 4);
       const int gm = mn0 + row, gk = k0 + 4 * kq;
-      if (gm < MN && gk < K) v = ld4(X + (long long)gm * ld + gk);
+      if (FULL || (gm < MN && gk < K)) v = ld4(X + (long long)gm * ld + gk);
     } else {
       // a whole float4 whenever gm < MN: a [K][MN] operand's rows are readable up to roundup4(MN) <= ld (ld % 4 == 0,
       // host-checked), and the values past MN only reach output rows / columns that are never stored. The row offset
       // splits into a loop-invariant part and k0 ld, so the K loop carries no 64-bit multiply and no edge branches.
       const int kr = e / (ROWS / 4), mq = e % (ROWS / 4);
       const int gk = k0 + kr, gm = mn0 + 4 * mq;
-      if (gk < K && gm < MN) v = ld4(X + ((long long)kr * ld + gm) + (long long)k0 * ld);
+      if (FULL || (gk < K && gm < MN)) v = ld4(X + ((long long)kr * ld + gm) + (long long)k0 * ld);
     }
     return v;
   }
   template <int ROWS, bool KC>
   __device__ __forceinline__ static void put(float* S, int e, floatx4 v) {
-    if (e >= ROWS * BK / 4) return;
+    if ((ROWS * BK / 4) % NT != 0 && e >= ROWS * BK / 4) return;
     if (KC) st4(S + (e / (BK / 4)) * (BK + 4) + 4 * (e % (BK / 4)), v);
     else st4(S + (e / (ROWS / 4)) * (ROWS + 4) + 4 * (e % (ROWS / 4)), v);
   }
@@ -690,9 +693,9 @@ constexpr int wg16_occ() {
   using IO = TileIO<BM, BN, BK, AKC, BKC, 64 * NW>;
   return (NW == 4 && 2 * (IO::ASZ + IO::BSZ) * 4 <= 80 * 1024) ? 2 : 1;
 }
-template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI, int NW = 4>
+template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI, int NW = 4, bool FULL = false>
 __global__ __launch_bounds__(64 * NW, (wg16_occ<BM, BN, BK, AKC, BKC, NW>())) void k_wgemm16(const GemmArgs g) {
-  using IO = TileIO<BM, BN, BK, AKC, BKC, 64 * NW>;
+  using IO = TileIO<BM, BN, BK, AKC, BKC, 64 * NW, FULL>;
   constexpr int WM = BM / NW;
   constexpr int TI = WM / 16, TJ = BN / 16;
   __shared__ __attribute__((aligned(16))) float lds[2 * (IO::ASZ + IO::BSZ)];
@@ -1980,10 +1983,10 @@ int launch_cfg(const GemmArgs& g, int groups, hipStream_t st) {
   return bcnf_rt::launched();
 }
 
-template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI, int NW = 4>
+template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI, int NW = 4, bool FULL = false>
 int launch_cfg16(const GemmArgs& g, int groups, hipStream_t st) {
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, groups);
-  hipLaunchKernelGGL((k_wgemm16<BM, BN, BK, AKC, BKC, EPI, NW>), grid, dim3(64 * NW), 0, st, g);
+  hipLaunchKernelGGL((k_wgemm16<BM, BN, BK, AKC, BKC, EPI, NW, FULL>), grid, dim3(64 * NW), 0, st, g);
   return bcnf_rt::launched();
 }
 
@@ -2069,8 +2072,13 @@ int gemm(const GemmArgs& g, int groups, hipStream_t st) {
   // exactly (the 64 x 64 / 128 x 128 grids compute 1.19x / 1.47x the area) and re-read each operand 3 times instead
   // of 9; 11 waves of 16 x 176
   if constexpr (!AKC && !BKC) {
-    if (pick == 8 || (pick < 0 && g.M > 352 && g.M <= 528 && g.N > 352 && g.N <= 528))
-      return launch_cfg16<176, 176, 32, AKC, BKC, EPI, 11>(g, groups, st);
+    if (pick == 8 || (pick < 0 && g.M > 352 && g.M <= 528 && g.N > 352 && g.N <= 528)) {
+      // unpredicated loads when no load of the grid can leave its operand: whole K tiles, and the tile grid's M / N
+      // extent within the [K][M] / [K][N] rows (the Linear gradients: M = 526, N = 527 in rows of HP = 528)
+      const bool full = g.K % 32 == 0 && (g.M + 175) / 176 * 176 <= g.lda && (g.N + 175) / 176 * 176 <= g.ldb;
+      return full ? launch_cfg16<176, 176, 32, AKC, BKC, EPI, 11, true>(g, groups, st)
+                  : launch_cfg16<176, 176, 32, AKC, BKC, EPI, 11>(g, groups, st);
+    }
   }
   if (pick == 8) pick = -1;
   if (pick < 0) {
