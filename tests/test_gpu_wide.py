@@ -29,11 +29,15 @@ def _lib():
 @pytest.mark.parametrize("tiling", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
 @pytest.mark.parametrize("layout", [0, 1, 2, 3])
 @pytest.mark.parametrize("mnk", [(64, 64, 32), (100, 70, 36), (2048, 528, 528), (18, 527, 300), (1030, 1360, 64),
-                                 (3, 5, 4), (300, 200, 2052)])
+                                 (3, 5, 4), (300, 200, 2052),
+                                 # 176 x 176 with unpredicated staging loads (whole K tiles, grid inside the padded rows):
+                                 # an exact 2 x 2 grid, and the hidden-Linear gradient's own shape (M = H, N = H + 1, K = B)
+                                 (352, 352, 64), (526, 527, 2048)])
 def test_wide_gemm_layouts_vs_fp64(layout, mnk, tiling):
     """C = A B through the MFMA tile machinery (tiling 0 = the dispatcher's choice, 1 = 128x128 32x32-MFMA,
     2 = 64x64, 3 = 128x48 16x16-MFMA, 4 = the same on 8 waves, 5 = 96x48 on 6 waves, 6 = LDS-DMA tiling C,
-    7 = tiling C large tiles, 8 = tiling C 48 x 48, 9 = 176 x 176 on 11 waves (strided x strided only), 10 / 11 =
+    7 = tiling C large tiles, 8 = tiling C 48 x 48, 9 = 176 x 176 on 11 waves (strided x strided only; layout 2 at the
+    last two shapes takes its unpredicated-load instance), 10 / 11 =
     tiling W 96 x 48 / 48 x 48 (LDS-resident B band, K-contiguous x K-contiguous with K <= 768 only); every operand
     layout; ragged M / N / K tails) vs fp64."""
     import ctypes
