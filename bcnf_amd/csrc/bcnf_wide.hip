@@ -665,7 +665,12 @@ __global__ __launch_bounds__(WWG, 2) void k_wgemm(const GemmArgs g) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
     }
   };
-  k_loop<IO>(g, A, B, m0, n0, lds, tile);
+  // interior tiles (whole K tiles, the tile inside M x N: most of any large grid) stage without load predicates; the
+  // edge tiles keep them (a workgroup-uniform branch)
+  if (g.K % BK == 0 && m0 + BM <= g.M && n0 + BN <= g.N)
+    k_loop<TileIO<BM, BN, BK, AKC, BKC, WWG, true>>(g, A, B, m0, n0, lds, tile);
+  else
+    k_loop<IO>(g, A, B, m0, n0, lds, tile);
   // accumulator element r of lane (c32, hh): row = (r & 3) + 8 (r >> 2) + 4 hh, col = c32
 #pragma unroll
   for (int i = 0; i < TI; ++i)
