@@ -39,7 +39,7 @@ EXPORTS = (
     "bcnf_wide_pack", "bcnf_wide_forward", "bcnf_wide_nll_finalize", "bcnf_wide_backward", "bcnf_wide_inverse",
     "bcnf_wide_fold_prepare", "bcnf_wide_fold_forward", "bcnf_wide_fold_backward", "bcnf_wide_proj_rows",
     "bcnf_wide_fold_backward_range", "bcnf_wide_fold_backward_phase", "bcnf_wide_block_offset",
-    "bcnf_wide_gemm_test", "bcnf_rank_count", "bcnf_resimulate",
+    "bcnf_wide_gemm_test", "bcnf_wide_backward_plan", "bcnf_rank_count", "bcnf_resimulate",
     "bcnf_guard_check_global", "bcnf_abi_version",
 )
 ABI_VERSION = 2          # include/bcnf_amd.h BCNF_AMD_ABI_VERSION (the struct layouts below)
@@ -196,6 +196,7 @@ def _bind(lib):
         "bcnf_resimulate": (_i32, [_vp, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _i32, ctypes.c_double, _i32,
                                    ctypes.c_double, ctypes.c_double, _i32, _vp, _vp, _vp, _vp]),
         "bcnf_wide_gemm_test": (_i32, [_i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp]),
+        "bcnf_wide_backward_plan": (_i32, [_pdesc, _i64, _i32, _i32, _i32, _i32, _i32, _pi64]),
         "bcnf_status_string": (ctypes.c_char_p, [_i32]),
         "bcnf_abi_version": (_i32, []),
     }

@@ -156,7 +156,7 @@ struct BcnfLayout {
   int sblk;             // floats per block of a workgroup's gradient slab (slab_blk_floats: MFMA tiles + column sums)
   int n_trainable;
   float p, keep_scale;
-  uint32_t thresh16;    // drop if u16 < thresh16
+  uint32_t thr_hi, thr_lo;   // thresh32 = round(p 2^32) = thr_hi 2^16 + thr_lo: drop if a unit's u32 < thresh32
   int RF, RB;           // per-lane record floats (forward/inverse, backward)
   int PMB;              // floats per block of the matrix-core inverse's operand-ordered record (k_inverse_mfma)
   // record offsets (floats, per lane)
@@ -351,23 +351,55 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
   return c;
 }
 
-// 8 keep-bits (bit l = keep decision for hidden layer l+1) for (sample, block, lane).
+// Keep bits (bit l = keep decision for hidden layer l+1) for (sample, block, lane) of a stack with NU <= 8 hidden
+// layers. Unit i keeps iff its 32-bit uniform u_i >= thresh32 = round(p 2^32): nn.Dropout's p to 2^-32, the rule of
+// the wide family and k_lin (round 5 compared 16-bit draws with round(p 2^16): p = 0.383 ran as 0.38299561, and any
+// p < 2^-17 as no dropout at all). u_i = (high half: one 16-bit half of a Philox4x32-10 draw, low half L):
+//  * NU < 8 (FC_small: 7): L is the draw's unused eighth half, shared by the units of one call -- each u_i is then
+//    exactly uniform on 32 bits (so each unit drops with probability thresh32 / 2^32), and two units of one call
+//    are dependent only through ties of BOTH high halves with thr_hi (probability < 2^-32 per call). One
+//    v_lshl_or / v_and_or + one compare per unit: the cost of the 16-bit rule;
+//  * NU == 8: each unit's own L from a second draw of the same counter with tag bit 29, which a wave runs only when
+//    one of its lanes ties (probability 2^-16 per unit) and thr_lo != 0.
+template <int NU>
 __device__ __forceinline__ uint32_t dropout_bits(const BcnfLayout& L, uint64_t seed, uint64_t offset,
                                                  long long sample, int block, int lane, uint32_t tag) {
-  uint4 ctr = make_uint4((uint32_t)sample, (uint32_t)((unsigned long long)sample >> 32) ^ ((uint32_t)block << 8) ^ tag,
-                         (uint32_t)lane, (uint32_t)offset);
-  uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32) ^ (uint32_t)(offset >> 32));
-  uint4 r = philox4x32_10(ctr, key);
-  const uint32_t t = L.thresh16;
+  static_assert(NU >= 1 && NU <= 8, "8 units per draw");
+  const uint4 ctr = make_uint4((uint32_t)sample,
+                               (uint32_t)((unsigned long long)sample >> 32) ^ ((uint32_t)block << 8) ^ tag,
+                               (uint32_t)lane, (uint32_t)offset);
+  const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32) ^ (uint32_t)(offset >> 32));
+  const uint4 r = philox4x32_10(ctr, key);
   uint32_t bits = 0;
-  bits |= ((r.x & 0xffffu) >= t) ? 1u : 0u;
-  bits |= ((r.x >> 16) >= t) ? 2u : 0u;
-  bits |= ((r.y & 0xffffu) >= t) ? 4u : 0u;
-  bits |= ((r.y >> 16) >= t) ? 8u : 0u;
-  bits |= ((r.z & 0xffffu) >= t) ? 16u : 0u;
-  bits |= ((r.z >> 16) >= t) ? 32u : 0u;
-  bits |= ((r.w & 0xffffu) >= t) ? 64u : 0u;
-  bits |= ((r.w >> 16) >= t) ? 128u : 0u;
+  if constexpr (NU < 8) {
+    const uint32_t t = (L.thr_hi << 16) | L.thr_lo, lo = r.w >> 16;
+    const uint32_t u[7] = {(r.x << 16) | lo, (r.x & 0xffff0000u) | lo, (r.y << 16) | lo, (r.y & 0xffff0000u) | lo,
+                           (r.z << 16) | lo, (r.z & 0xffff0000u) | lo, (r.w << 16) | lo};
+#pragma unroll
+    for (int i = 0; i < NU; ++i) bits |= (u[i] >= t ? 1u : 0u) << i;
+  } else {
+    const uint32_t th = L.thr_hi;
+    const uint32_t h[8] = {r.x & 0xffffu, r.x >> 16, r.y & 0xffffu, r.y >> 16,
+                           r.z & 0xffffu, r.z >> 16, r.w & 0xffffu, r.w >> 16};
+    uint32_t tie = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      bits |= (h[i] > th ? 1u : 0u) << i;
+      tie |= (h[i] == th ? 1u : 0u) << i;
+    }
+    if (tie) {
+      const uint32_t tl = L.thr_lo;
+      if (tl == 0) {
+        bits |= tie;
+      } else {
+        const uint4 r2 = philox4x32_10(make_uint4(ctr.x, ctr.y ^ 0x20000000u, ctr.z, ctr.w), key);
+        const uint32_t lo[8] = {r2.x & 0xffffu, r2.x >> 16, r2.y & 0xffffu, r2.y >> 16,
+                                r2.z & 0xffffu, r2.z >> 16, r2.w & 0xffffu, r2.w >> 16};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) bits |= (((tie >> i) & 1u) && lo[i] >= tl ? 1u : 0u) << i;
+      }
+    }
+  }
   return bits;
 }
 

@@ -105,8 +105,9 @@ int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
   L->sblk = slab_blk_floats(L->NH);
   L->p = d->dropout;
   L->keep_scale = (d->dropout > 0.f) ? (1.0f / (1.0f - d->dropout)) : 1.0f;
-  double t = (double)d->dropout * 65536.0;
-  L->thresh16 = (uint32_t)llround(t);
+  const double t32 = std::min(4294967295.0, floor((double)d->dropout * 4294967296.0 + 0.5));   // dropout_bits
+  L->thr_hi = (uint32_t)t32 >> 16;
+  L->thr_lo = (uint32_t)t32 & 0xffffu;
   // forward/inverse record: [sa ba sb bb][b1 pad pad pad][W1y:16][hidden l: 16+1 ...][T:16+1][S:16+1][Q:64]
   L->rf_b1 = 4;
   L->rf_w1 = 8;
@@ -1570,7 +1571,7 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
       // projection partial
       auto finish_rec = [&](int k, int sl, const Pre& g) {
         if (DROP) {
-          const uint32_t bits = dropout_bits(L, seed, off, bc, k, j, 0u);
+          const uint32_t bits = dropout_bits<NH>(L, seed, off, bc, k, j, 0u);
           float m[8];
 #pragma unroll
           for (int i = 0; i < 8; ++i) m[i] = ((bits >> i) & 1u) ? L.keep_scale : 0.f;
@@ -1726,7 +1727,7 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
 #pragma unroll
       for (int t = 0; t < HP_SMAX; ++t) wb[t] = (t < S) ? wcol[(long long)4 * t * P.NKp + 16 * k] : 0.f;
       if (DROP) {
-        const uint32_t bits = dropout_bits(L, seed, off, bc, k, j, 0u);
+        const uint32_t bits = dropout_bits<NH>(L, seed, off, bc, k, j, 0u);
         float m[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) m[i] = ((bits >> i) & 1u) ? L.keep_scale : 0.f;
@@ -1758,6 +1759,9 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
     }
   } else {
     const int tid = t8;
+    // the compute waves issue ahead of the helper wave on their SIMD whenever both are ready (r06: k_forward
+    // -1.1 us same box, profiles/r06b_rawab.txt; the helpers have slack at every block's barrier)
+    __builtin_amdgcn_s_setprio(3);
     const int D = L.D, Da = L.Da, Db = L.Db;
     float ya, yb, ldc = 0.f;
     if constexpr (RAW) {
@@ -2100,7 +2104,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse(BcnfLayout L, const float* 
     float za, zb;
     mix(rr + RecF<NH>::Q, ya, yb, za, zb);             // z @ Q^T (cnf.py:339); identity for the last block
     uint32_t bits = 0xffu;
-    if (DROP) bits = dropout_bits(L, seed, off, bc, k, j, 0x40000000u);
+    if (DROP) bits = dropout_bits<NH>(L, seed, off, bc, k, j, 0x40000000u);
     float T, Sp;
     mlp_forward<NH, false>(L, rr, za, hpk, bits, DROP, T, Sp, nullptr, nullptr);
     const float S = tanh_bf(Sp);
@@ -2556,6 +2560,9 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
     bwd_grad_jobs<NH>(dT, aT, slab, hw);                     // block 0 (tiles of the last interval)
   } else {
     const int tid = t8;
+#ifdef BCNF_BWD_PRIO
+    __builtin_amdgcn_s_setprio(BCNF_BWD_PRIO);
+#endif
     const long long b = (long long)blockIdx.x * 16 + s;
     const bool valid = b < B;
     const long long bc = valid ? b : B - 1;

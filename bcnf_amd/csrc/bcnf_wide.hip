@@ -1326,7 +1326,9 @@ __device__ __forceinline__ void stage4(float* __restrict__ dst, const float* __r
 __device__ __forceinline__ void stage4x2(float* __restrict__ d1, const float* __restrict__ s1, int n1,
                                          float* __restrict__ d2, const float* __restrict__ s2, int n2) {
   const int n = n1 + n2;
-  const int rot = (int)((blockIdx.x >> 3) * (unsigned)(n >> 5)) & ~7;
+  // (b >> 3) & 31 < 32, so rot <= 31 * (n >> 5) < n at any grid size (a launch of more than 256 workgroups, B > 2048
+  // rows, wraps back to offset 0 instead of stepping past the end of the staged regions).
+  const int rot = (int)(((blockIdx.x >> 3) & 31u) * (unsigned)(n >> 5)) & ~7;
   for (int e0 = 0; e0 < n; e0 += 16 * WWG) {
     floatx4 v[16];
 #pragma unroll
@@ -2340,6 +2342,7 @@ struct WideWs {       // workspace carve-up (floats)
   float *P, *A, *G, *dZ, *dZ0, *X, *S, *U, *O, *DV, *ANP, *nllp, *Hp;
   float* LP;          // [B][32 * ceil(HP / 48)] last-Linear partials of the current block (tiling W epilogue)
   long long total;
+  long long g_off;    // offset of G (floats; bcnf_wide_backward_plan)
 };
 
 inline int lp_tiles(const WideLayout& L) { return (L.HP + 47) / 48; }
@@ -2358,6 +2361,7 @@ WideWs carve(const WideLayout& L, long long B, bool train, float* base) {
   w.nllp = take(B);
   if (train) {
     w.A = take((long long)L.nv * L.NH * slab);
+    w.g_off = o;
     w.G = take((long long)L.nv * L.NH * slab);
     w.dZ = take((long long)L.nv * (L.NH - 1) * slab);
     w.dZ0 = take(B * (long long)L.nv * L.HP);
@@ -2585,6 +2589,29 @@ int wide_forward(const WideLayout& L, const float* prm, const float* pk, const f
   return BCNF_OK;
 }
 
+// The G region's split-K scratch plan of one wide_backward call (host arithmetic only; bcnf_wide_backward_plan
+// exposes it to the CPU tests and the ASan run, tools/asan_host.sh). The G region holds nv * NH slabs of B * HP
+// floats. The last range's dL/dx and [dWf | dbf] put their split-K partials at its END (`tail` floats), the parameter
+// gradients of the range use the range's own G slots from its head (`gsc_off`, `gsc_floats`), so phase 1 and phase 2
+// may run on two streams. A need larger than the whole region reserves nothing (that GEMM runs unsplit), and the
+// head region is clamped to what the tail leaves.
+struct GPlan {
+  long long gfl_all, dx_need, dwfb_need, tail, gsc_off, gsc_floats;
+};
+GPlan g_plan(const WideLayout& L, long long B, bool dx, bool dwfb, int Xp, int blo, int bhi) {
+  GPlan p;
+  p.gfl_all = (long long)L.nv * L.NH * B * L.HP;
+  p.dx_need = (dx && blo == 0) ? (long long)L.nv * B * ((Xp + 3) & ~3) : 0;
+  p.dwfb_need = (dwfb && blo == 0) ? (long long)L.nv * L.C * ((Xp + 3) & ~3) : 0;
+  if (p.dx_need > p.gfl_all) p.dx_need = 0;
+  if (p.dwfb_need > p.gfl_all) p.dwfb_need = 0;
+  p.tail = std::max(p.dx_need, p.dwfb_need);
+  const int vlo = blo * L.S, nvr = (bhi - blo) * L.S;
+  p.gsc_off = (long long)vlo * L.NH * B * L.HP;
+  p.gsc_floats = std::max(0LL, std::min((long long)nvr * L.NH * B * L.HP, p.gfl_all - p.tail - p.gsc_off));
+  return p;
+}
+
 // Real blocks [blo, bhi) of the backward: the chain iterations that complete them, then their parameter gradients
 // (canonical flat, every element written exactly once). The whole backward is [0, nb). A data-parallel caller may
 // split it into descending contiguous ranges, the first with bhi = nb, and reduce each range's gradient slice while
@@ -2606,15 +2633,8 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
   if (blo < 0 || bhi > L.nb || blo >= bhi) return BCNF_ERR_ARG;
   ensure_lds_attrs();
   const WideWs w = carve(L, B, true, ws);
-  // the last range's dL/dx and [dWf | dbf] put their split-K partials at the END of the G region, the parameter
-  // gradients at its head, so phase 1 and phase 2 may run on two streams
-  const long long gfl_all = (long long)L.nv * L.NH * B * L.HP;
-  // (a need larger than the whole region reserves nothing: that GEMM runs unsplit, as it always did)
-  long long dx_need = (fold && fold->dx && blo == 0) ? (long long)L.nv * B * ((fold->Xp + 3) & ~3) : 0;
-  long long dwfb_need = (fold && fold->dwfb && blo == 0) ? (long long)L.nv * L.C * ((fold->Xp + 3) & ~3) : 0;
-  if (dx_need > gfl_all) dx_need = 0;
-  if (dwfb_need > gfl_all) dwfb_need = 0;
-  const long long tail = std::max(dx_need, dwfb_need);
+  const GPlan gp = g_plan(L, B, fold && fold->dx, fold && fold->dwfb, fold ? fold->Xp : 0, blo, bhi);
+  const long long gfl_all = gp.gfl_all, tail = gp.tail;
   const long long slab = B * L.HP;
   const long long ld0 = (long long)L.nv * L.HP;
   const int vlo = blo * L.S, vhi = bhi * L.S, nvr = vhi - vlo;
@@ -2697,8 +2717,8 @@ int wide_backward(const WideLayout& L, const float* prm, const float* pk, const 
   int rc = BCNF_OK;
   const float* hp = fold ? nullptr : padded_h(L, h, B, w.Hp, st, &rc);
   WCHK(rc);
-  float* const gsc = Gptr(vlo, 0);                  // the range's G slots: split-K scratch once its chain has run
-  const long long gsc_floats = std::min((long long)nvr * L.NH * slab, gfl_all - tail);
+  float* const gsc = w.G + gp.gsc_off;               // the range's G slots: split-K scratch once its chain has run
+  const long long gsc_floats = gp.gsc_floats;
   // ---- parameter gradients of the range (canonical flat, every element written exactly once) ----
   if (dprm) {
     auto flat_groups = [&](GemmArgs& g) {   // group g1 = virtual block (or real block with S = 1 semantics)
@@ -2995,6 +3015,24 @@ int bcnf_wide_fold_backward_range(const BcnfStackDesc* desc, const float* params
   WideFold f = {x1, wfb, wcb, gx_scratch, dwfb, dx, (int)xp};
   return wide_backward(L, params, (const float*)packed, nullptr, z, nullptr, nullptr, dloss, 1, batch,
                        (float*)workspace, nullptr, nullptr, dparams, (hipStream_t)stream, &f, block_lo, block_hi);
+}
+
+int bcnf_wide_backward_plan(const BcnfStackDesc* desc, int64_t batch, int32_t xp, int32_t want_dx, int32_t want_dwfb,
+                            int32_t block_lo, int32_t block_hi, int64_t* out) {
+  WideLayout L;
+  WCHK(wide_layout(desc, &L));
+  if (!out || batch < 0 || block_lo < 0 || block_hi > L.nb || block_lo >= block_hi || xp < 0) return BCNF_ERR_ARG;
+  const WideWs w = carve(L, batch, true, nullptr);
+  const GPlan p = g_plan(L, batch, want_dx != 0, want_dwfb != 0, (int)xp, block_lo, block_hi);
+  out[0] = w.total;
+  out[1] = w.g_off;
+  out[2] = p.gfl_all;
+  out[3] = p.tail;
+  out[4] = p.gsc_off;
+  out[5] = p.gsc_floats;
+  out[6] = p.dx_need;
+  out[7] = p.dwfb_need;
+  return BCNF_OK;
 }
 
 int bcnf_wide_block_offset(const BcnfStackDesc* desc, int32_t block, int64_t* offset) {

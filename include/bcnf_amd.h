@@ -477,6 +477,14 @@ int bcnf_lds_fill(float value, void* stream);
  * floats for them (a tight (K - 1) * ld + M buffer is read out of bounds). */
 int bcnf_wide_gemm_test(int32_t layout, int32_t M, int32_t N, int32_t K, const float* A, int64_t lda, const float* B,
                         int64_t ldb, float* C, int64_t ldc, void* stream);
+/* Test hook (host arithmetic only, no launch): the workspace / G-region plan of one folded wide backward call
+ * (bcnf_wide_fold_backward_range) at `batch` rows over blocks [block_lo, block_hi), dL/dx and [dWf | dbf] wanted or
+ * not: out[0] = training workspace floats, out[1] = offset of the G region in it, out[2] = G region floats, out[3] =
+ * the feature-side split-K partials at the region's end, out[4] / out[5] = offset (within G) / floats of the range's
+ * parameter-gradient split-K scratch, out[6] / out[7] = the dL/dx / [dWf | dbf] partial needs. Checked by
+ * tests/test_native_abi.py and under AddressSanitizer (tools/asan_host.sh). */
+int bcnf_wide_backward_plan(const BcnfStackDesc* desc, int64_t batch, int32_t xp, int32_t want_dx, int32_t want_dwfb,
+                            int32_t block_lo, int32_t block_hi, int64_t* out);
 
 #ifdef __cplusplus
 }

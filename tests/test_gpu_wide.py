@@ -133,9 +133,21 @@ def tiling(request):
 def test_wide_shapes_vs_oracle(shape, B, tiling):
     """Forward / log-det / inverse / eval gradients of the wide family vs the oracle (fp64 for gradients), with every
     GEMM tiling (all epilogues: activation, gradient, Linear-gradient, row-mapped, plain)."""
-    from bcnf_amd import inn_nll_loss
     if tiling >= 0 and B == 1:
         pytest.skip("B = 1 covered by the auto tiling")
+    _check_vs_oracle(shape, B, tiling)
+
+
+@pytest.mark.parametrize("shape", [WIDE_SHAPES[0], WIDE_SHAPES[4]], ids=["wide40", "fc_large"])
+def test_wide_link_grids_past_256_workgroups(shape):
+    """B = 4100 rows: every link launch (forward, inverse, backward) has 513 workgroups, past the 256 at which the
+    per-workgroup rotation of the links' weight staging (stage4x2) once stepped beyond the staged regions (ADVICE r05);
+    the rotation only reorders the copy, so the results must match the oracle as at small B."""
+    _check_vs_oracle(shape, 4100, -1)
+
+
+def _check_vs_oracle(shape, B, tiling):
+    from bcnf_amd import inn_nll_loss
     m = _model(shape)
     m.fused.desc.gemm_tiling = tiling + 1
     _perturb(m)
