@@ -179,9 +179,16 @@ __device__ __forceinline__ int coupling_base(const BcnfLayout& L, int k) {
 // the trailing s_nop 1 is the store-data hazard of a > 8-byte store (a VALU must not overwrite its data VGPRs in the
 // next cycles), which the compiler's hazard pass covers for its own stores only (cdna_hip_programming.md §5.7).
 // Only for data that later launches read: the asm carries no memory clobber, so the compiler may move this launch's
-// own loads across it (every call site stores records / activations / partials its kernel never reads back).
+// own loads across it (every st4_wt / st1_wt call site stores records / activations / partials its kernel never
+// reads back; where it may, st4_wt_ordered).
 __device__ __forceinline__ void st4_wt(void* p, floatx4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v));
+}
+// The same with a "memory" clobber, for a destination the launch may also have read: k_wlink's A0 rows are the
+// slab its dots path read as Alast in a non-save forward with NH odd (eval ping-pong), so no load of Alast may move
+// below the store.
+__device__ __forceinline__ void st4_wt_ordered(void* p, floatx4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
 }
 __device__ __forceinline__ void st1_wt(void* p, float v) {
   asm volatile("global_store_dword %0, %1, off sc1" : : "v"(p), "v"(v));

@@ -1666,7 +1666,7 @@ __global__ __launch_bounds__(WWG) void k_wlink(const WideLayout L, const LinkArg
           av[e] = c == H ? 1.f : ge * m;
           gv[e] = dg * m;
         }
-        st4_wt(a.A0 + row * HP + n, floatx4{av[0], av[1], av[2], av[3]});
+        st4_wt_ordered(a.A0 + row * HP + n, floatx4{av[0], av[1], av[2], av[3]});   // may alias Alast (eval, NH odd)
         if (a.G0) st4_wt(a.G0 + row * HP + n, floatx4{gv[0], gv[1], gv[2], gv[3]});
       };
 #pragma unroll
@@ -2013,9 +2013,14 @@ int launch_gl(const GemmArgs& g, int groups, hipStream_t st) {
   return bcnf_rt::launched();
 }
 
+// Set by launch_wb when an EPI_ACT launch on tiling W carries GemmArgs.lp (only tiling W's epilogue writes the
+// last-Linear partials): hidden_fwd reports the partials as written from this, not from a copy of the dispatch rule.
+thread_local bool g_lp_written = false;
+
 template <int WGM, int KS, int P, int KQ, int EPI, int TI = 1>
 int launch_wb(const GemmArgs& g, int groups, hipStream_t st) {
   using T = WbCfg<WGM, KS, P, KQ, TI>;
+  if (EPI == EPI_ACT && g.lp) g_lp_written = true;
   const int bytes = T::lds_floats(g.K) * 4;
   static bool attr = false;
   if (!attr) {
@@ -2470,8 +2475,9 @@ int projection(const WideLayout& L, const float* pk, const float* hp, long long 
   return gemm<true, true, EPI_STORE>(g, 1, st);
 }
 
-// Does gemm<true, true, EPI_ACT> run this GEMM on tiling W (k_wbr, whose epilogue can apply the block's last Linear)?
-// Mirrors the dispatch of gemm() / gemm_gl() for K-contiguous operands.
+// Can gemm<true, true, EPI_ACT> run this GEMM on tiling W (k_wbr, whose epilogue can apply the block's last Linear)?
+// A pre-filter only (the partials' column-tile count fits LP_MAX, K in tiling W's range): whether the partials were
+// written is what launch_wb reports (g_lp_written), so a dispatch change cannot leave the link summing stale ones.
 bool wbr_lp_ok(const GemmArgs& g, int groups) {
   if (g.K < 4 || g.K > WB_KMAX || g.M <= 0 || (g.N + 47) / 48 > LP_MAX) return false;
   const int forced = g.tiling - 1;
@@ -2504,9 +2510,11 @@ int hidden_fwd(const WideLayout& L, const float* prm, const float* pk, int v, in
     g.lp_w = pk + L.pk_wl + (long long)v * L.WL * L.HP;
     g.lp_wld = L.HP;
     g.lp_n = 2 * L.nout[sd];
-    if (lp_on) *lp_on = true;
   }
-  return gemm<true, true, EPI_ACT>(g, 1, st);
+  g_lp_written = false;
+  const int rc = gemm<true, true, EPI_ACT>(g, 1, st);
+  if (lp_on) *lp_on = rc == BCNF_OK && g.lp && g_lp_written;
+  return rc;
 }
 
 // Folded last feature Linear (h = x Wf^T + bf, the wide analogue of bcnf_stack.hip's FC_small fold): with

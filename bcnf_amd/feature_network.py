@@ -167,23 +167,29 @@ class FullyConnectedFeatureNetwork(FeatureNetwork):
     # another model -- CondRealNVP_v2 re-binds its copies), so one device offset serves the feature and the coupling
     # dropout and `model.fused.set_seed` / TrainStep's snapshot cover both; else this module's own state.
     # Advancing: the owner's coupling launch bumps the shared offset once per training step when the coupling itself
-    # drops out; otherwise (coupling dropout 0, the owner in eval mode or elsewhere, no owner) run() bumps it after
-    # the network's last fused dropout layer -- a device-side add, replay-safe in HIP graphs -- so every training
-    # step draws fresh feature masks.
+    # drops out (and a feature draw that no coupling launch followed -- this network run on its own -- is advanced
+    # at the next draw, FusedStack.feature_rng_state); otherwise (coupling dropout 0, the owner in eval mode or
+    # elsewhere, no owner) run() bumps it after the network's last fused dropout layer -- a device-side add,
+    # replay-safe in HIP graphs -- so every training step draws fresh feature masks.
     _own_rng = None
 
     def rng_state(self, device) -> torch.Tensor:
-        return self._rng(device)[0]
+        return self._rng(device, draw=False)[0]
 
-    def _rng(self, device) -> tuple[torch.Tensor, bool]:
-        """(device (seed, offset) state, whether the owner's coupling launch advances it this step)."""
+    def _rng(self, device, draw: bool = True) -> tuple[torch.Tensor, bool]:
+        """(device (seed, offset) state, whether the owner's coupling launch advances it this step); draw: the
+        caller draws from it now (marks the draw on the owner's stack, see FusedStack.feature_rng_state)."""
         ref = _RNG_OWNERS.get(self)
         owner = ref() if ref is not None else None
         fused = owner.__dict__.get("_fused") if owner is not None else None
         if fused is not None and hasattr(fused, "rng_state") and getattr(fused, "flat", None) is not None \
                 and fused.flat.device == device:
             cfg = getattr(fused, "cfg", None)
-            return fused.rng_state(), bool(owner.training and cfg is not None and cfg.dropout > 0.0)
+            if not draw:
+                return fused._rng_tensor(), False
+            if owner.training and cfg is not None and cfg.dropout > 0.0:
+                return fused.feature_rng_state(), True
+            return fused._rng_tensor(), False
         if self._own_rng is None or self._own_rng.device != device:
             seed = (torch.cuda.initial_seed() * 0x9E3779B97F4A7C15 + 0xFEA7) & ((1 << 62) - 1)
             self._own_rng = torch.tensor([seed, 0], dtype=torch.int64, device=device)
@@ -196,6 +202,7 @@ class FullyConnectedFeatureNetwork(FeatureNetwork):
         mods = list(self.nn)[:upto]
         i = 0
         bump = None                       # the state to advance after the last fused dropout layer, if run() must
+        rng = None                        # one state lookup per call (the owner's feature_rng_state marks one draw)
         while i < len(mods):
             m = mods[i]
             act = mods[i + 1] if i + 1 < len(mods) else None
@@ -203,13 +210,12 @@ class FullyConnectedFeatureNetwork(FeatureNetwork):
                     and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and m.weight.dtype == torch.float32:
                 drop = mods[i + 2] if i + 2 < len(mods) and isinstance(mods[i + 2], nn.Dropout) else None
                 p = drop.p if (drop is not None and drop.training) else 0.0
-                rng = None
-                if p > 0.0:
+                if p > 0.0 and rng is None:
                     rng, owner_bumps = self._rng(x.device)
                     bump = None if owner_bumps else rng
                 need_g = torch.is_grad_enabled() and (x.requires_grad or m.weight.requires_grad or
                                                       (m.bias is not None and m.bias.requires_grad))
-                x = _LinearGeluFn.apply(x.contiguous(), m.weight, m.bias, p, rng, i, need_g)
+                x = _LinearGeluFn.apply(x.contiguous(), m.weight, m.bias, p, rng if p > 0.0 else None, i, need_g)
                 i += 3 if drop is not None else 2
                 continue
             x = m(x)

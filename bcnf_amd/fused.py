@@ -181,9 +181,28 @@ class FusedStack:
         """Pack once and reuse it for every launch inside the block (e.g. all chunks of sample())."""
         return FusedStack._Reuse(self)
 
+    # A feature network bound to this stack draws its dropout from the same (seed, offset) and leaves the advance to
+    # the coupling launch that follows in the step (feature_network.py). True between such a feature draw and the
+    # next coupling launch: a second feature draw before any coupling launch (the feature network run on its own)
+    # advances the offset itself first (feature_rng_state), so repeated standalone calls draw fresh masks.
+    _feature_pending = False
+
     def rng_state(self):
         """Device-resident (seed, offset) for the in-kernel Philox dropout; the offset is bumped by a
         device-side add after every training forward, so HIP-graph replays draw fresh masks."""
+        self._feature_pending = False          # a coupling launch takes this step's offset
+        return self._rng_tensor()
+
+    def feature_rng_state(self):
+        """The state a bound feature network's fused dropout draws from, when the coupling launch of the step will
+        advance it (a feature draw not followed by a coupling launch advances it at the next one)."""
+        t = self._rng_tensor()
+        if self._feature_pending:
+            t[1:2].add_(1)
+        self._feature_pending = True
+        return t
+
+    def _rng_tensor(self):
         if self._rng_state is None:
             seed = self.seed
             if seed is None:

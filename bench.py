@@ -82,6 +82,26 @@ WIDE_FWD_FLOP_PER_SAMPLE = 2 * 47_765_617
 WIDE_TRAIN_FLOP_PER_SAMPLE = 3 * WIDE_FWD_FLOP_PER_SAMPLE
 # SURVEY §8d per-block minimum for the training step, nb = 26, D = 19, C = 1360: nb * 4 * (5D + 4C + 2)
 WIDE_ALG_BYTES_PER_SAMPLE = 26 * 4 * (5 * 19 + 4 * 1360 + 2)
+# The FLOPs the wide training step EXECUTES, against the reference count above: the folded last feature
+# Linear (x1 = [x | 1 | 0], Xp = round_up(X + 1, 4): FC_large X = 310 -> 312, LSTM_large X = 280 -> 284) replaces the
+# 1360-wide condition GEMMs per sample by Xp-wide ones plus three per-step GEMMs of nb H C Xp MACs (Wcb = W0h wfb,
+# dW0h = Gx wfb^T, [dWf | dbf] = W0h^T Gx). Per sample, MACs (nin = 10, nout = 18, H = 526):
+#   forward  nb (nin H + Xp H + 4 H^2 + H nout) + (nb - 1) D^2
+#   backward nb (4 H^2 + nout H + nin H          [dX of the hidden, last and Linear-1 y-part]
+#                + 4 H (H + 1) + nout (H + 1) + H (nin + 1))   [dW / db]
+#            + 2 nb H Xp (dL/dx = dZ0 Wcb, Gx = dZ0^T x1) + (nb - 1) D^2
+WIDE_FOLD_X = {"fc_large": 310, "lstm_large": 280}
+
+
+def wide_executed_flop(workload, B):
+    nb, H, C, D, nin, nout = 26, 526, 1360, 19, 10, 18
+    Xp = (WIDE_FOLD_X[workload] + 1 + 3) // 4 * 4
+    fwd = nb * (nin * H + Xp * H + 4 * H * H + H * nout) + (nb - 1) * D * D
+    bwd = nb * (4 * H * H + nout * H + nin * H + 4 * H * (H + 1) + nout * (H + 1) + H * (nin + 1)) \
+        + 2 * nb * H * Xp + (nb - 1) * D * D
+    return 2 * ((fwd + bwd) * B + 3 * nb * H * C * Xp)
+
+
 WIDE_NAMES = {"fc_large": "trajectory_FC_large", "lstm_large": "trajectory_LSTM_large"}
 WORKLOADS = {"fc_small": (FC_SMALL, 4096), "fc_large": (FC_LARGE, 2048), "lstm_large": (LSTM_LARGE, 1024),
              "sample": (FC_SMALL, 1024), "resimulate": (None, 1024)}
@@ -771,6 +791,7 @@ def run_wide(workload, batch, steps, warmup, world, rank, device, graph=True, ke
     fb_us = kern.get("forward", float("nan")) + kern.get("backward", float("nan"))
     ach_fb = flop_step / (fb_us * 1e-6) / 1e12
     alg = WIDE_ALG_BYTES_PER_SAMPLE * B
+    flop_exec = wide_executed_flop(workload, B)
     kw = cfg["model"]["kwargs"]
     line = {
         "metric": f"NLL-training samples/sec, {WIDE_NAMES[workload]}",
@@ -787,13 +808,17 @@ def run_wide(workload, batch, steps, warmup, world, rank, device, graph=True, ke
         "last_loss": vals[-1][0] if vals else None,
         "roofline": {"bound": "mfma", "kernel": "coupling stack forward + backward launches (fp32 MFMA GEMM chain + "
                                                 "link kernels; HIP events over each launch sequence)",
+                     "frac_executed": round(flop_exec / (fb_us * 1e-6) / 1e12 / PEAK_FP32_TFLOPS, 4),
+                     "flop_executed_per_step": flop_exec,
                      "achieved": round(ach_fb, 3), "achieved_whole_step": round(achieved, 3),
                      "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(ach_fb / PEAK_FP32_TFLOPS, 4),
                      "frac_whole_step": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
                      "avg_us": round(fb_us, 2), "flop_per_step": flop_step, "algorithmic_bytes": alg,
                      "alg_hbm_frac": round(alg / (fb_us * 1e3) / PEAK_HBM_GBS, 4),
-                     "note": "flop = SURVEY §8d reference count (3 x forward flow, feature net excluded); the fold "
-                             "of the last feature Linear executes fewer condition-GEMM FLOPs than it counts"},
+                     "note": "frac_executed = the FLOPs the folded step executes (bench.py wide_executed_flop, "
+                             "DESIGN §3d) / launch time / peak: the figure to read against mfma_busy; achieved / frac "
+                             "= SURVEY §8d reference count (3 x forward flow with 1360-wide condition GEMMs, feature "
+                             "net excluded), which the fold does not execute"},
         "kernels_us": {k: round(v, 2) for k, v in kern.items()},
     }
     mb = wide_mfma_busy(workload)

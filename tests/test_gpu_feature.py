@@ -171,3 +171,28 @@ def test_deepcopy_feature_dropout_follows_the_copy():
     assert torch.equal(m.fused.rng_state(), m_state)              # the original's offset never moved
     import pickle
     pickle.loads(pickle.dumps(fc))                                  # no weakref inside the module's state
+
+
+def test_standalone_feature_calls_of_a_training_owner_draw_fresh_masks():
+    """with the owner training and coupling dropout on, the feature network leaves the offset
+    advance to the coupling launch of the step. Called on its own twice (no coupling launch in between) it must still
+    draw fresh masks, and a normal step (feature draw + coupling launch) still advances the offset exactly once."""
+    from bcnf_amd import CondRealNVP_v2
+    cfg = copy.deepcopy(FC_LARGE_CFG)
+    cfg["model"]["kwargs"]["n_blocks"] = 2
+    torch.manual_seed(6)
+    m = CondRealNVP_v2.from_config(cfg).to(DEV).train()
+    fn = m.feature_network_stack.feature_networks[1]
+    x = torch.randn(256, 30, 3, device=DEV)
+    y = torch.randn(256, 19, device=DEV)
+    m.nll_loss(y, x)                                            # a step: feature draw, then the coupling's
+    off0 = int(fn.rng_state(x.device)[1].item())
+    a1 = fn(x).detach().clone()
+    a2 = fn(x).detach().clone()                                 # no coupling launch since a1's draw
+    assert not torch.equal(a1, a2)
+    assert int(fn.rng_state(x.device)[1].item()) == off0 + 1    # advanced once, at a2's draw
+    for _ in range(2):                                          # steps: exactly one advance each
+        o = int(fn.rng_state(x.device)[1].item())
+        m.nll_loss(y, x)
+        torch.cuda.synchronize()
+        assert int(fn.rng_state(x.device)[1].item()) == o + 1 + (1 if _ == 0 else 0)

@@ -22,7 +22,7 @@ for s in $STEPS; do
       timeout -k 10 420 python bench.py > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || { tail -20 gpurun_out/${T}_bench.err; exit 1; }
       python tools/show_bench.py gpurun_out/${T}_bench.json ;;
     rawab)
-      for i in 1 2 3; do
+      for i in $(seq 1 ${NALT:-3}); do
         timeout -k 10 120 python tools/raw_probe.py
         for lib in ${AB_LIBS:-build_exp/libhead.so}; do BCNF_AMD_LIB=$lib timeout -k 10 120 python tools/raw_probe.py; done
       done 2>&1 | grep -v amdgpu.ids | tee gpurun_out/${T}_rawab.txt ;;
