@@ -1010,7 +1010,8 @@ __device__ __forceinline__ void gx_reduce_body(long long total, const float* __r
 // k-slices are summed in a fixed order through LDS.
 __device__ __forceinline__ int c0_of_finish(int bx, int nct) { return (bx % nct) * 16; }
 
-constexpr int FIN_KC = 256;                           // K chunk (role a: Xp <= 256 fits one)
+constexpr int FIN_KC = 512;                           // K chunk: role a (Xp <= 256) and role b at nb <= 32
+                                                      // (K = 16 nb) each load their operands in ONE round trip
 constexpr int FIN_SMEM = 2 * FIN_KC * 16;             // As + Bs; the 16 x 256 reduction aliases them
 
 __device__ __forceinline__ void tile16_accum(const float* __restrict__ As, const float* __restrict__ Bs, int kn,
@@ -1047,7 +1048,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_fold_finish(BcnfLayout L, const flo
                                                          const float* __restrict__ bf, int X,
                                                          float* __restrict__ dparams, float* __restrict__ dwf,
                                                          float* __restrict__ dbf, FoldAdamArgs A) {
-  __shared__ __attribute__((aligned(16))) float smem[FIN_SMEM];
+  extern __shared__ __attribute__((aligned(16))) float smem[];   // FIN_SMEM floats (64 KB: dynamic)
   __shared__ float sc[2];
   float* As = smem;
   float* Bs = smem + FIN_KC * 16;
@@ -3364,7 +3365,9 @@ int bcnf_fold_backward_tail(const BcnfStackDesc* desc, const void* packed, const
                      (int)splits, gx, n_gx, (const float*)slab, S, nwg, dparams, A);
   if ((rc = check_launch())) return rc;
   const int n_fin = (L.nb + (F.Cp >> 4)) * (L.Cp >> 4);
-  hipLaunchKernelGGL(k_fold_finish, dim3((unsigned)n_fin), dim3(BCNF_WG), 0, st, L, (const float*)packed,
+  size_t fin_lds = sizeof(float) * FIN_SMEM;
+  if ((rc = launch_lds(k_fold_finish, fin_lds))) return rc;
+  hipLaunchKernelGGL(k_fold_finish, dim3((unsigned)n_fin), dim3(BCNF_WG), fin_lds, st, L, (const float*)packed,
                      (const float*)gx, feat_weight, feat_bias, (int)in_features, dparams, dfeat_weight, dfeat_bias, A);
   return check_launch();
 }
