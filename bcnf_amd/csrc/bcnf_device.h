@@ -184,6 +184,14 @@ __device__ __forceinline__ int coupling_base(const BcnfLayout& L, int k) {
 __device__ __forceinline__ void st4_wt(void* p, floatx4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v));
 }
+// st4_wt of an MFMA result: the compiler's hazard pass does not see the asm store read the accumulator, so the
+// XDL-write -> VMEM-read wait states (11 for an 8-pass v_mfma_f32_16x16x4_f32, 19 for 16 passes) are inserted here,
+// tied to the value so the nops sit between the MFMA and the store (r06: a tile stored right behind its last MFMA
+// had element 2 of lanes 0-3 of each row group stale, profiles/r06j_gx_mode.patch.txt).
+__device__ __forceinline__ void st4_wt_mfma(void* p, floatx4 v) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" : "+v"(v));
+  st4_wt(p, v);
+}
 // The same with a "memory" clobber, for a destination the launch may also have read: k_wlink's A0 rows are the
 // slab its dots path read as Alast in a non-save forward with NH odd (eval ping-pong), so no load of Alast may move
 // below the store.

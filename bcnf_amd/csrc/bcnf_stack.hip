@@ -2426,7 +2426,7 @@ __device__ __forceinline__ void bwd_grad_jobs(const float* __restrict__ Td, cons
   }
 #pragma unroll
   for (int u = 0; u < UW; ++u)
-    if (hw + 4 * u < J::NW) st4_wt(reinterpret_cast<floatx4*>(out + 256 * (hw + 4 * u)) + l64, acc[u]);
+    if (hw + 4 * u < J::NW) st4_wt_mfma(reinterpret_cast<floatx4*>(out + 256 * (hw + 4 * u)) + l64, acc[u]);
 }
 
 // Whole-stack backward, one launch, 512 threads = two roles per SIMD (waves w and w + 4 share a SIMD):
