@@ -6,7 +6,8 @@ TAG=${1:-r02y}
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-bash tools/profile_round.sh $TAG
+[ -n "$SKIP_FC_SMALL" ] || bash tools/profile_round.sh $TAG   # SKIP_FC_SMALL=1: its passes ran already
+mkdir -p gpurun_out/prof_$TAG
 for w in fc_large lstm_large sample resimulate; do
   timeout -k 10 300 python bench.py --workload $w > gpurun_out/${TAG}_${w}_bench.json 2> gpurun_out/${TAG}_${w}_bench.err
   echo ${w}_ok
