@@ -372,8 +372,8 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
 // p < 2^-17 as no dropout at all). u_i = (high half: one 16-bit half of a Philox4x32-10 draw, low half L):
 //  * NU < 8 (FC_small: 7): L is the draw's unused eighth half, shared by the units of one call -- each u_i is then
 //    exactly uniform on 32 bits (so each unit drops with probability thresh32 / 2^32), and two units of one call
-//    are dependent only through ties of BOTH high halves with thr_hi (probability < 2^-32 per call). One
-//    v_lshl_or / v_and_or + one compare per unit: the cost of the 16-bit rule;
+//    are dependent only through ties of BOTH high halves with thr_hi (probability < 2^-32 per call). As L is shared,
+//    u_i >= thresh32 <=> h_i >= thr_hi + [L < thr_lo]: one compare per unit, the cost of the 16-bit rule;
 //  * NU == 8: each unit's own L from a second draw of the same counter with tag bit 29, which a wave runs only when
 //    one of its lanes ties (probability 2^-16 per unit) and thr_lo != 0.
 template <int NU>
@@ -387,11 +387,12 @@ __device__ __forceinline__ uint32_t dropout_bits(const BcnfLayout& L, uint64_t s
   const uint4 r = philox4x32_10(ctr, key);
   uint32_t bits = 0;
   if constexpr (NU < 8) {
-    const uint32_t t = (L.thr_hi << 16) | L.thr_lo, lo = r.w >> 16;
-    const uint32_t u[7] = {(r.x << 16) | lo, (r.x & 0xffff0000u) | lo, (r.y << 16) | lo, (r.y & 0xffff0000u) | lo,
-                           (r.z << 16) | lo, (r.z & 0xffff0000u) | lo, (r.w << 16) | lo};
+    // u_i = (h_i, L) >= (thr_hi, thr_lo)  <=>  h_i >= thr_hi + [L < thr_lo]: with L shared, one 16-bit threshold per
+    // call, and each unit costs the one compare of a 16-bit rule (a compare of a word half)
+    const uint32_t t = L.thr_hi + ((r.w >> 16) < L.thr_lo ? 1u : 0u);
+    const uint32_t h[7] = {r.x & 0xffffu, r.x >> 16, r.y & 0xffffu, r.y >> 16, r.z & 0xffffu, r.z >> 16, r.w & 0xffffu};
 #pragma unroll
-    for (int i = 0; i < NU; ++i) bits |= (u[i] >= t ? 1u : 0u) << i;
+    for (int i = 0; i < NU; ++i) bits |= (h[i] >= t ? 1u : 0u) << i;
   } else {
     const uint32_t th = L.thr_hi;
     const uint32_t h[8] = {r.x & 0xffffu, r.x >> 16, r.y & 0xffffu, r.y >> 16,
