@@ -155,6 +155,9 @@ struct BcnfLayout {
   int blk_pad;          // cblk rounded up to 4
   int sblk;             // floats per block of a workgroup's gradient slab (slab_blk_floats: MFMA tiles + column sums)
   int n_trainable;
+  int qbc;              // 1 (Da = 9, Db = 10: every D = 19 stack): the mix, Linear 1's y-part and the backward's T / S
+                        // heads are in broadcast form (record entry c of lane j = weight of input c to output j; bc9,
+                        // mix_bc, bc10x2), else in rotation form (entry r of lane j = weight of input (j - r) & 15)
   float p, keep_scale;
   uint32_t thr_hi, thr_lo;   // thresh32 = round(p 2^32) = thr_hi 2^16 + thr_lo: drop if a unit's u32 < thresh32
   int RF, RB;           // per-lane record floats (forward/inverse, backward)
@@ -254,6 +257,71 @@ __device__ __forceinline__ void rot16x2(float x0, const float* __restrict__ w0, 
         "v"(w0[9]), "v"(w0[10]), "v"(w0[11]), "v"(w0[12]), "v"(w0[13]), "v"(w0[14]), "v"(w0[15]),
         "v"(w1[1]), "v"(w1[2]), "v"(w1[3]), "v"(w1[4]), "v"(w1[5]), "v"(w1[6]), "v"(w1[7]), "v"(w1[8]),
         "v"(w1[9]), "v"(w1[10]), "v"(w1[11]), "v"(w1[12]), "v"(w1[13]), "v"(w1[14]), "v"(w1[15]));
+}
+
+// Broadcast forms (round 6) for the D = 19 stacks' half-vectors (Da = 10, Db = 9 inputs in lanes 0 .. 9 / 0 .. 8):
+// `row_newbcast:c` reads lane c of the lane's own 16-lane row, so acc_j + sum_{c < N} x[c] w_j[c] costs N DPP FMAs
+// where a rotation matvec costs 16 (record entry c of lane j = the weight from input c to output j). Two interleaved
+// accumulators hide the fmac latency; the leading s_nop 1 covers a VALU write of x right before (as in rot16).
+#define BCNF_BC(C, A, X, W) "v_fmac_f32_dpp " A ", " X ", " W " row_newbcast:" #C " row_mask:0xf bank_mask:0xf\n\t"
+#define BCNF_BCM(C, A, X, W) "v_mul_f32_dpp " A ", " X ", " W " row_newbcast:" #C " row_mask:0xf bank_mask:0xf\n\t"
+
+// acc + sum_{c < 10} x[c] w[c]  (Linear 1's y-part: Da = 10 inputs -> 16 hidden)
+__device__ __forceinline__ float bc10(float x, const float* __restrict__ w, float acc) {
+  float acc1;
+  asm("s_nop 1\n\t"
+      BCNF_BC(0, "%0", "%2", "%3") BCNF_BCM(1, "%1", "%2", "%4") BCNF_BC(2, "%0", "%2", "%5")
+      BCNF_BC(3, "%1", "%2", "%6") BCNF_BC(4, "%0", "%2", "%7") BCNF_BC(5, "%1", "%2", "%8")
+      BCNF_BC(6, "%0", "%2", "%9") BCNF_BC(7, "%1", "%2", "%10") BCNF_BC(8, "%0", "%2", "%11")
+      BCNF_BC(9, "%1", "%2", "%12")
+      : "+v"(acc), "=&v"(acc1)
+      : "v"(x), "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]), "v"(w[6]), "v"(w[7]), "v"(w[8]), "v"(w[9]));
+  return acc + acc1;
+}
+
+// (a0, a1) = (sum_{c < 9} x0[c] w0[c], sum_{c < 9} x1[c] w1[c])  (the backward's T / S heads: Db = 9 inputs each)
+__device__ __forceinline__ void bc9x2(float x0, const float* __restrict__ w0, float& a0,
+                                      float x1, const float* __restrict__ w1, float& a1) {
+  asm("s_nop 1\n\t"
+      BCNF_BCM(0, "%0", "%2", "%4") BCNF_BCM(0, "%1", "%3", "%13")
+      BCNF_BC(1, "%0", "%2", "%5") BCNF_BC(1, "%1", "%3", "%14")
+      BCNF_BC(2, "%0", "%2", "%6") BCNF_BC(2, "%1", "%3", "%15")
+      BCNF_BC(3, "%0", "%2", "%7") BCNF_BC(3, "%1", "%3", "%16")
+      BCNF_BC(4, "%0", "%2", "%8") BCNF_BC(4, "%1", "%3", "%17")
+      BCNF_BC(5, "%0", "%2", "%9") BCNF_BC(5, "%1", "%3", "%18")
+      BCNF_BC(6, "%0", "%2", "%10") BCNF_BC(6, "%1", "%3", "%19")
+      BCNF_BC(7, "%0", "%2", "%11") BCNF_BC(7, "%1", "%3", "%20")
+      BCNF_BC(8, "%0", "%2", "%12") BCNF_BC(8, "%1", "%3", "%21")
+      : "=&v"(a0), "=&v"(a1)
+      : "v"(x0), "v"(x1), "v"(w0[0]), "v"(w0[1]), "v"(w0[2]), "v"(w0[3]), "v"(w0[4]), "v"(w0[5]), "v"(w0[6]), "v"(w0[7]), "v"(w0[8]),
+        "v"(w1[0]), "v"(w1[1]), "v"(w1[2]), "v"(w1[3]), "v"(w1[4]), "v"(w1[5]), "v"(w1[6]), "v"(w1[7]), "v"(w1[8]));
+}
+
+// The orthonormal mix of a D = 19 state (a: 10 lanes, b: 9 lanes) in broadcast form: na = sum_c a[c] rq[c] +
+// sum_c b[c] rq[10 + c], nb = sum_c a[c] rq[19 + c] + sum_c b[c] rq[29 + c]: 38 DPP FMAs instead of 4 rotations (64).
+__device__ __forceinline__ void mix_bc(const float* __restrict__ rq, float a, float b, float& na, float& nbv) {
+  asm("s_nop 1\n\t"
+      BCNF_BCM(0, "%0", "%2", "%4") BCNF_BCM(0, "%1", "%2", "%23")
+      BCNF_BC(1, "%0", "%2", "%5") BCNF_BC(1, "%1", "%2", "%24")
+      BCNF_BC(2, "%0", "%2", "%6") BCNF_BC(2, "%1", "%2", "%25")
+      BCNF_BC(3, "%0", "%2", "%7") BCNF_BC(3, "%1", "%2", "%26")
+      BCNF_BC(4, "%0", "%2", "%8") BCNF_BC(4, "%1", "%2", "%27")
+      BCNF_BC(5, "%0", "%2", "%9") BCNF_BC(5, "%1", "%2", "%28")
+      BCNF_BC(6, "%0", "%2", "%10") BCNF_BC(6, "%1", "%2", "%29")
+      BCNF_BC(7, "%0", "%2", "%11") BCNF_BC(7, "%1", "%2", "%30")
+      BCNF_BC(8, "%0", "%2", "%12") BCNF_BC(8, "%1", "%2", "%31")
+      BCNF_BC(9, "%0", "%2", "%13") BCNF_BC(9, "%1", "%2", "%32")
+      BCNF_BC(0, "%0", "%3", "%14") BCNF_BC(0, "%1", "%3", "%33")
+      BCNF_BC(1, "%0", "%3", "%15") BCNF_BC(1, "%1", "%3", "%34")
+      BCNF_BC(2, "%0", "%3", "%16") BCNF_BC(2, "%1", "%3", "%35")
+      BCNF_BC(3, "%0", "%3", "%17") BCNF_BC(3, "%1", "%3", "%36")
+      BCNF_BC(4, "%0", "%3", "%18") BCNF_BC(4, "%1", "%3", "%37")
+      BCNF_BC(5, "%0", "%3", "%19") BCNF_BC(5, "%1", "%3", "%38")
+      BCNF_BC(6, "%0", "%3", "%20") BCNF_BC(6, "%1", "%3", "%39")
+      BCNF_BC(7, "%0", "%3", "%21") BCNF_BC(7, "%1", "%3", "%40")
+      BCNF_BC(8, "%0", "%3", "%22") BCNF_BC(8, "%1", "%3", "%41")
+      : "=&v"(na), "=&v"(nbv)
+      : "v"(a), "v"(b), "v"(rq[0]), "v"(rq[1]), "v"(rq[2]), "v"(rq[3]), "v"(rq[4]), "v"(rq[5]), "v"(rq[6]), "v"(rq[7]), "v"(rq[8]), "v"(rq[9]), "v"(rq[10]), "v"(rq[11]), "v"(rq[12]), "v"(rq[13]), "v"(rq[14]), "v"(rq[15]), "v"(rq[16]), "v"(rq[17]), "v"(rq[18]), "v"(rq[19]), "v"(rq[20]), "v"(rq[21]), "v"(rq[22]), "v"(rq[23]), "v"(rq[24]), "v"(rq[25]), "v"(rq[26]), "v"(rq[27]), "v"(rq[28]), "v"(rq[29]), "v"(rq[30]), "v"(rq[31]), "v"(rq[32]), "v"(rq[33]), "v"(rq[34]), "v"(rq[35]), "v"(rq[36]), "v"(rq[37]));
 }
 
 // Sum over the 16 lanes of a row, result in every lane of the row.

@@ -67,6 +67,13 @@ int round_rec(int n) {            // multiple of 4 floats with odd quotient (con
   return n;
 }
 
+// Broadcast-form sections (row_newbcast DPP, D_a = 10 / D_b = 9 stacks only): QBC_W1 Linear 1 (forward), QBC_MIX
+// the mix Q / Q^T (forward, inverse, backward), QBC_HEAD the T / S heads' transposes (backward).
+#ifndef BCNF_QBC_MASK
+#define BCNF_QBC_MASK 7
+#endif
+constexpr int QBC_W1 = 1, QBC_MIX = 2, QBC_HEAD = 4;
+
 int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
   if (!d || !L) return BCNF_ERR_ARG;
   memset(L, 0, sizeof(*L));
@@ -103,6 +110,7 @@ int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
   L->cblk = L->blk_stride - L->H[1] * L->C;
   L->blk_pad = (L->cblk + 3) & ~3;
   L->sblk = slab_blk_floats(L->NH);
+  L->qbc = (L->Da == 10 && L->Db == 9) ? BCNF_QBC_MASK : 0;
   L->p = d->dropout;
   L->keep_scale = (d->dropout > 0.f) ? (1.0f / (1.0f - d->dropout)) : 1.0f;
   const double t32 = std::min(4294967295.0, floor((double)d->dropout * 4294967296.0 + 0.5));   // dropout_bits
@@ -178,6 +186,42 @@ __device__ __forceinline__ float cB(const BcnfLayout& L, const float* P, int k, 
   return P[coupling_base(L, k) + L.lin_b[l] + row];
 }
 
+// Input index of record entry r of lane j in a matvec section: rotation form (r-th rotation: input (j - r) & 15) or,
+// with L.qbc's bit for the section (QBC_*), broadcast form (entry r = input r; bc10 / bc9x2 / mix_bc).
+__host__ __device__ inline int rec_src(const BcnfLayout& L, int j, int r, int bit) {
+  return (L.qbc & bit) ? r : ((j - r) & 15);
+}
+
+// Entry c (0..63) of lane j of a mix section -> (quadrant qi: 0 a->a, 1 b->a, 2 a->b, 3 b->b, input src of the
+// quadrant's input half); false: a padding entry. Rotation form: 16 entries per quadrant; broadcast form (mix_bc):
+// entries [0, D) feed output half a, [D, 2D) half b, each over the D inputs (a's Da first, then b's Db).
+__host__ __device__ inline bool q_entry(const BcnfLayout& L, int j, int c, int* qi, int* src) {
+  if (!(L.qbc & QBC_MIX)) {
+    *qi = c / 16;
+    *src = (j - c % 16) & 15;
+    return true;
+  }
+  const int D = L.D;
+  if (c >= 2 * D) return false;
+  const int oh = c / D, gi = c % D;
+  *qi = 2 * oh + (gi < L.Da ? 0 : 1);
+  *src = gi < L.Da ? gi : gi - L.Da;
+  return true;
+}
+
+// The mix weight of quadrant qi from input src (of its input half) to output lane j (of its output half) in block k:
+// y_new = y @ Q (cnf.py:335) or, inverse, z_prev = y @ Q^T (cnf.py:339); the identity after the last block (no mix),
+// so the kernels need no branch.
+__device__ float q_quad(const BcnfLayout& L, const float* Q, int k, int j, int qi, int src, bool inverse) {
+  const int Da = L.Da, Db = L.Db, D = L.D;
+  const int no = (qi < 2) ? Da : Db, ni = (qi & 1) ? Db : Da;   // output / input half widths
+  if (j >= no || src >= ni) return 0.f;
+  if (k >= L.nb - 1) return ((qi == 0 || qi == 3) && src == j) ? 1.f : 0.f;
+  const float* q = Q + (long long)k * D * D;
+  const int gi = (qi & 1) ? Da + src : src, go = (qi < 2) ? j : Da + j;   // global input / output index
+  return inverse ? q[go * D + gi] : q[gi * D + go];
+}
+
 // PF (inverse=false) / PI (inverse=true) record entry e of lane j in block k.
 __device__ float rec_f(const BcnfLayout& L, const float* P, const float* Q, int k, int j, int e, bool inverse) {
   const int Da = L.Da, Db = L.Db, D = L.D, NH = L.NH;
@@ -193,7 +237,7 @@ __device__ float rec_f(const BcnfLayout& L, const float* P, const float* Q, int 
   }
   if (e == L.rf_b1) return (j < L.H[1]) ? cB(L, P, k, 1, j) : 0.f;
   if (e >= L.rf_w1 && e < L.rf_w1 + 16) {
-    const int src = (j - (e - L.rf_w1)) & 15;
+    const int src = rec_src(L, j, e - L.rf_w1, QBC_W1);
     return (j < L.H[1] && src < Da) ? cW(L, P, k, 1, j, src) : 0.f;
   }
   if (e >= L.rf_hid && e < L.rf_t) {
@@ -209,27 +253,9 @@ __device__ float rec_f(const BcnfLayout& L, const float* P, const float* Q, int 
     return (j < Db && src < L.H[NH]) ? cW(L, P, k, NH + 1, half * Db + j, src) : 0.f;
   }
   if (e >= L.rf_q && e < L.rf_q + 64) {
-    const int qi = (e - L.rf_q) / 16, r = (e - L.rf_q) % 16, src = (j - r) & 15;
-    if (k >= L.nb - 1) {   // last block has no mix: identity, so the kernels need no branch
-      if (r != 0) return 0.f;
-      return (qi == 0 && j < Da) || (qi == 3 && j < Db) ? 1.f : 0.f;
-    }
-    const float* q = Q + (long long)k * D * D;
-    if (!inverse) {  // y_new = y @ Q   (cnf.py:335): [q0 QAA | q1 QBA | q2 QAB | q3 QBB]
-      switch (qi) {
-        case 0: return (j < Da && src < Da) ? q[src * D + j] : 0.f;
-        case 1: return (j < Da && src < Db) ? q[(Da + src) * D + j] : 0.f;
-        case 2: return (j < Db && src < Da) ? q[src * D + Da + j] : 0.f;
-        default: return (j < Db && src < Db) ? q[(Da + src) * D + Da + j] : 0.f;
-      }
-    } else {         // z_prev = y @ Q^T (cnf.py:339): [q0 over a->a | q1 over b->a | q2 over a->b | q3 over b->b]
-      switch (qi) {
-        case 0: return (j < Da && src < Da) ? q[j * D + src] : 0.f;
-        case 1: return (j < Da && src < Db) ? q[j * D + Da + src] : 0.f;
-        case 2: return (j < Db && src < Da) ? q[(Da + j) * D + src] : 0.f;
-        default: return (j < Db && src < Db) ? q[(Da + j) * D + Da + src] : 0.f;
-      }
-    }
+    int qi, src;
+    if (!q_entry(L, j, e - L.rf_q, &qi, &src)) return 0.f;
+    return q_quad(L, Q, k, j, qi, src, inverse);
   }
   return 0.f;
 }
@@ -246,7 +272,7 @@ __device__ float rec_b(const BcnfLayout& L, const float* P, const float* Q, int 
     return (j < L.H[l - 1] && src < L.H[l]) ? cW(L, P, k, l, src, j) : 0.f;
   }
   if (e >= L.rb_tt && e < L.rb_tt + 32) {
-    const int half = (e - L.rb_tt) / 16, r = (e - L.rb_tt) % 16, src = (j - r) & 15;
+    const int half = (e - L.rb_tt) / 16, src = rec_src(L, j, (e - L.rb_tt) % 16, QBC_HEAD);
     return (j < L.H[NH] && src < Db) ? cW(L, P, k, NH + 1, half * Db + src, j) : 0.f;
   }
   if (e >= L.rb_qt && e < L.rb_qt + 64) return rec_f(L, P, Q, k, j, L.rf_q + (e - L.rb_qt), true);
@@ -271,12 +297,11 @@ __device__ float rec_pm(const BcnfLayout& L, const float* P, const float* Q, int
     const int ch = perm ? 3 * q + t : 4 * q + t, cu = 4 * q + t;
     if (m < 4) {                                                           // mix quadrant qi = m
       if (perm && t == 3) return 0.f;
-      const int off = L.rf_q + 16 * m;
-      return none ? rec_f(L, P, Q, k, 15, off, true) : rec_f(L, P, Q, k, fo, off + ((fo - ch) & 15), true);
+      return none ? 0.f : q_quad(L, Q, k, fo, m, ch, true);
     }
     if (m == 4) {                                                          // Linear 1, y-part
       if (perm && t == 3) return 0.f;
-      return rec_f(L, P, Q, k, s, L.rf_w1 + ((s - ch) & 15), true);
+      return (s < L.H[1] && ch < L.Da) ? cW(L, P, k, 1, s, ch) : 0.f;
     }
     if (m < NH + 4) return rec_f(L, P, Q, k, s, L.rf_hid + 17 * (m - 5) + ((s - cu) & 15), true);
     const int off = (m == NH + 4) ? L.rf_t : L.rf_s;
@@ -317,6 +342,18 @@ constexpr int RAW_SRC_MAX = 1 << 20;
 // A table entry: destination float of the ring slot (j * RF + e, < 4096) | source offset << 12.
 __host__ __device__ constexpr uint32_t raw_entry(int dst, int src) { return (uint32_t)dst | ((uint32_t)src << 12); }
 
+// Source of mix-section entry c of lane j (q_entry / q_quad): kind 2 (qmats at k * D * D + off) or 0 (zero).
+int q_quad_source(const BcnfLayout& L, int j, int c, bool inverse, int* off) {
+  int qi, src;
+  if (!q_entry(L, j, c, &qi, &src)) return 0;
+  const int Da = L.Da, Db = L.Db, D = L.D;
+  const int no = (qi < 2) ? Da : Db, ni = (qi & 1) ? Db : Da;
+  if (j >= no || src >= ni) return 0;
+  const int gi = (qi & 1) ? Da + src : src, go = (qi < 2) ? j : Da + j;
+  *off = inverse ? go * D + gi : gi * D + go;
+  return 2;
+}
+
 // Source of forward-record entry e of lane j for a block k < nb - 1: kind 0 = structurally zero, 1 = params at
 // k * blk_stride + off, 2 = qmats at k * D * D + off; -1 = a constant the table cannot express (no ActNorm: 1.0).
 // Mirrors rec_f (inverse = false) entry by entry.
@@ -335,7 +372,7 @@ int rec_f_source(const BcnfLayout& L, int j, int e, int* off) {
   }
   if (e == L.rf_b1) return j < L.H[1] ? (*off = an + L.lin_b[1] + j, 1) : 0;
   if (e >= L.rf_w1 && e < L.rf_w1 + 16) {
-    const int src = (j - (e - L.rf_w1)) & 15;
+    const int src = rec_src(L, j, e - L.rf_w1, QBC_W1);
     return (j < L.H[1] && src < Da) ? (*off = lin_w(1, j, src), 1) : 0;
   }
   if (e >= L.rf_hid && e < L.rf_t) {
@@ -350,15 +387,7 @@ int rec_f_source(const BcnfLayout& L, int j, int e, int* off) {
     const int src = (j - r) & 15;
     return (j < Db && src < L.H[NH]) ? (*off = lin_w(NH + 1, half * Db + j, src), 1) : 0;
   }
-  if (e >= L.rf_q && e < L.rf_q + 64) {
-    const int qi = (e - L.rf_q) / 16, r = (e - L.rf_q) % 16, src = (j - r) & 15;
-    switch (qi) {
-      case 0: return (j < Da && src < Da) ? (*off = src * D + j, 2) : 0;
-      case 1: return (j < Da && src < Db) ? (*off = (Da + src) * D + j, 2) : 0;
-      case 2: return (j < Db && src < Da) ? (*off = src * D + Da + j, 2) : 0;
-      default: return (j < Db && src < Db) ? (*off = (Da + src) * D + Da + j, 2) : 0;
-    }
-  }
+  if (e >= L.rf_q && e < L.rf_q + 64) return q_quad_source(L, j, e - L.rf_q, false, off);
   return 0;
 }
 
@@ -376,18 +405,10 @@ int rec_b_source(const BcnfLayout& L, int j, int e, int* off) {
     return (j < L.H[l - 1] && src < L.H[l]) ? (*off = lin_w(l, src, j), 1) : 0;
   }
   if (e >= L.rb_tt && e < L.rb_tt + 32) {
-    const int half = (e - L.rb_tt) / 16, r = (e - L.rb_tt) % 16, src = (j - r) & 15;
+    const int half = (e - L.rb_tt) / 16, src = rec_src(L, j, (e - L.rb_tt) % 16, QBC_HEAD);
     return (j < L.H[NH] && src < Db) ? (*off = lin_w(NH + 1, half * Db + src, j), 1) : 0;
   }
-  if (e >= L.rb_qt && e < L.rb_qt + 64) {                 // rec_f(inverse = true) of the mix: Q^T
-    const int qi = (e - L.rb_qt) / 16, r = (e - L.rb_qt) % 16, src = (j - r) & 15;
-    switch (qi) {
-      case 0: return (j < Da && src < Da) ? (*off = j * D + src, 2) : 0;
-      case 1: return (j < Da && src < Db) ? (*off = j * D + Da + src, 2) : 0;
-      case 2: return (j < Db && src < Da) ? (*off = (Da + j) * D + src, 2) : 0;
-      default: return (j < Db && src < Db) ? (*off = (Da + j) * D + Da + src, 2) : 0;
-    }
-  }
+  if (e >= L.rb_qt && e < L.rb_qt + 64) return q_quad_source(L, j, e - L.rb_qt, true, off);   // Q^T
   if (e >= L.rb_an && e < L.rb_an + 4) return rec_f_source(L, j, e - L.rb_an, off);
   return 0;
 }
@@ -1239,7 +1260,7 @@ __device__ __forceinline__ void mlp_forward(const BcnfLayout& L, const float* __
   for (int l = 1; l <= NH; ++l) {
     const float* w = (l == 1) ? rr + F::W1 : rr + F::HID + 17 * (l - 2);
     const float bias = (l == 1) ? hp : w[16];            // hp = h W1h^T + b1 (k_hp)
-    const float pre = rot16(a, w, bias);
+    const float pre = (l == 1 && (L.qbc & QBC_W1)) ? bc10(a, w, bias) : rot16(a, w, bias);   // (uniform)
     const float m = drop ? (((bits >> (l - 1)) & 1u) ? L.keep_scale : 0.f) : 1.f;
     if (KEEP) {
       float g, dg;
@@ -1320,7 +1341,7 @@ __device__ __forceinline__ void rf_issue(float* __restrict__ rr, const float* __
 template <int NH, bool KEEP, bool DROP, typename Emit>
 __device__ __forceinline__ void mlp_forward_s(float* __restrict__ rr, const float* __restrict__ R, float x, float hp,
                                               const float* __restrict__ msk, float& T, float& Sp, float* ar,
-                                              Emit&& emit) {
+                                              Emit&& emit, bool qbc) {
   static_assert(RecF<NH>::HID == 24, "stage 1 reads only the prefetched head (FWD_HEAD = 24)");
   using F = RecF<NH>;
   using AR = ActRec<NH>;
@@ -1329,7 +1350,7 @@ __device__ __forceinline__ void mlp_forward_s(float* __restrict__ rr, const floa
   for (int l = 1; l <= NH; ++l) {
     rf_issue<NH>(rr, R, l);
     const float* w = (l == 1) ? rr + F::W1 : rr + F::HID + 17 * (l - 2);
-    const float pre = rot16(a, w, (l == 1) ? hp : w[16]);
+    const float pre = (l == 1 && qbc) ? bc10(a, w, hp) : rot16(a, w, (l == 1) ? hp : w[16]);   // (uniform)
     if (KEEP) {
       float g, dg;
       gelu_fg(pre, g, dg);
@@ -1958,7 +1979,7 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
       auto emit = [&](int q) {
         if (SAVE) st4_wt(d4 + q * BCNF_WG, floatx4{ar[4 * q], ar[4 * q + 1], ar[4 * q + 2], ar[4 * q + 3]});
       };
-      mlp_forward_s<NH, SAVE, DROP>(rr, rec + cur * RING + j * L.RF, xa, hpk, msk, T, Sp, ar, emit);
+      mlp_forward_s<NH, SAVE, DROP>(rr, rec + cur * RING + j * L.RF, xa, hpk, msk, T, Sp, ar, emit, (L.qbc & QBC_W1) != 0);
       const float Sv = tanh_bf(Sp);                      // cnf.py:107
       const float zb = fmaf(exp_fast(Sv), xb, T);        // cnf.py:179
       ldj += Sv;                                         // cnf.py:190
@@ -1974,7 +1995,8 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
       }
       fetch_head(nxt);     // slot nxt is complete since the previous barrier (after the last block: unused, no
                            // branch); the reads land while the mix runs
-      mix(rr + RecF<NH>::Q, xa, zb, ya, yb);             // y @ Q (cnf.py:335); identity after the last block
+      if (L.qbc & QBC_MIX) mix_bc(rr + RecF<NH>::Q, xa, zb, ya, yb);   // y @ Q (cnf.py:335); identity after the last block
+      else mix(rr + RecF<NH>::Q, xa, zb, ya, yb);
       cur = nxt;
       PHF(1)
       // a bare barrier: the head reads stay in flight across it (nobody writes slot nxt in the next interval; the
@@ -2103,7 +2125,8 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse(BcnfLayout L, const float* 
     float rr[RecF<NH>::USED];
     ld_rec<0, RecF<NH>::USED>(rr, rec + cur * RING + j * L.RF);
     float za, zb;
-    mix(rr + RecF<NH>::Q, ya, yb, za, zb);             // z @ Q^T (cnf.py:339); identity for the last block
+    if (L.qbc & QBC_MIX) mix_bc(rr + RecF<NH>::Q, ya, yb, za, zb);   // z @ Q^T (cnf.py:339); identity for the last block
+    else mix(rr + RecF<NH>::Q, ya, yb, za, zb);
     uint32_t bits = 0xffu;
     if (DROP) bits = dropout_bits<NH>(L, seed, off, bc, k, j, 0x40000000u);
     float T, Sp;
@@ -2617,7 +2640,8 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
       const float xb = fmaf(an_sb, yb, an_bb);
       const float e = exp_fast(S);
       float gza, gzb;
-      mix(rb + RBk::QT, gya, gyb, gza, gzb);            // g @ Q^T (identity for the last block)
+      if (L.qbc & QBC_MIX) mix_bc(rb + RBk::QT, gya, gyb, gza, gzb);   // g @ Q^T (identity for the last block)
+      else mix(rb + RBk::QT, gya, gyb, gza, gzb);
       ld16(rb + RBk::HID, R + RBk::HID);                 // hidden layer NH
       __builtin_amdgcn_sched_barrier(0);
       const float dT_ = gzb;                             // z_b = exp(s) y_b + t
@@ -2627,7 +2651,8 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
       Tt[NH * TILE] = dT_;
       Tt[(NH + 1) * TILE] = dSp;
       float da = 0.f, da2 = 0.f;
-      rot16x2(dT_, rb + RBk::TT, da, dSp, rb + RBk::ST, da2);
+      if (L.qbc & QBC_HEAD) bc9x2(dT_, rb + RBk::TT, da, dSp, rb + RBk::ST, da2);   // (uniform)
+      else rot16x2(dT_, rb + RBk::TT, da, dSp, rb + RBk::ST, da2);
       da += da2;
 #pragma unroll
       for (int l = NH; l >= 2; --l) {

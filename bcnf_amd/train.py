@@ -74,7 +74,7 @@ class TrainStep:
         self._graphs = None
         self._static = None
         self._pool = None
-        self._multi = None      # (graph, steps, grads): run_epoch's multi-step graph (world 1)
+        self._multi = {}        # steps -> (graph, steps, grads): run_epoch's multi-step graphs (world 1)
         self._single_grads = None
         self._rebind = False    # .grad currently points at buffers other than the single-step graph's
         self._book = None       # Adam's finished-workgroup counter (bcnf_adam_step_bookkeep)
@@ -644,13 +644,16 @@ class TrainStep:
         if check_divergence:        # data parallel: judged on the all-reduced loss, the same on every rank
             self._guard[GUARD_CHECK if self.world == 1 else GUARD_CHECK_GLOBAL] = 1
         i = 0
-        if self.world == 1 and self.epoch_unroll > 1 and n >= self.epoch_unroll:
-            g, k, grads = self._multi_graph()
-            while n - i >= k:
-                g.replay()
-                i += k
-            self._bind(grads)
-            self._rebind = True
+        if self.world == 1 and self.epoch_unroll > 1:
+            for k in self._unroll_sizes():
+                if n - i < k:
+                    continue
+                g, _, grads = self._multi_graph(k)
+                while n - i >= k:
+                    g.replay()
+                    i += k
+                self._bind(grads)
+                self._rebind = True
         if self.world > 1 and self._g21 is not None and n >= 2:
             g1, g2, _ = self._graphs          # g1, then (all-reduce, g21) per later step, then the last update
             g1.replay()
@@ -676,16 +679,24 @@ class TrainStep:
 
     # Steps per captured graph in run_epoch: a graph boundary costs ~9 us of idle GPU between two replays
     # (measured, r01j), so run_epoch replays `epoch_unroll` device-driven steps (cursor, RNG offset, Adam step,
-    # history row all advance on the device) per launch and the remainder one by one.
+    # history row all advance on the device) per launch and the remainder in graphs of epoch_unroll / 2, / 4, ...
+    # steps (20 steps: 8 + 8 + 4, three launches instead of six) and a last single step.
     epoch_unroll = 8
+
+    def _unroll_sizes(self):
+        k, out = self.epoch_unroll, []
+        while k > 1:
+            out.append(k)
+            k //= 2
+        return out
     # The captured step runs the batch gather inside the folded path's pack launch (one launch fewer).
     fuse_gather = True
     # Inside a multi-step graph only the last step's clip-after-step is observable (see _update).
     skip_hidden_clips = True
 
-    def _multi_graph(self):
-        if self._multi is None or self._multi[1] != self.epoch_unroll:
-            k = self.epoch_unroll
+    def _multi_graph(self, k: int):
+        if k not in self._multi:
+            self._bind(self._single_grads)         # every multi-step graph is captured from the same .grad state
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 slots = self._fold_adam_slots()
@@ -698,10 +709,10 @@ class TrainStep:
                         continue
                     vals = self._forward_backward(sy, st, spec)
                     self._update(vals, clip=not (hidden and self.opt.can_bookkeep()))
-            self._multi = (g, k, [p.grad for p in self.params])
+            self._multi[k] = (g, k, [p.grad for p in self.params])
             self._bind(self._single_grads)
             self._rebind = False
-        return self._multi
+        return self._multi[k]
 
     # Hidden steps of a folded model update their parameters inside the backward tail (no Adam launch).
     fuse_adam = True
@@ -743,8 +754,12 @@ class TrainStep:
         if self._epoch is None or not self.capture or not self.fused_loss:
             return
         self._ensure_epoch_graphs()
-        if self.world == 1 and self.epoch_unroll > 1 and n_steps >= self.epoch_unroll:
-            self._multi_graph()
+        if self.world == 1 and self.epoch_unroll > 1:
+            i = 0
+            for k in self._unroll_sizes():
+                if n_steps - i >= k:
+                    self._multi_graph(k)
+                    i += k * ((n_steps - i) // k)
 
     def _replay(self, hidden: bool = False):
         if self._rebind:

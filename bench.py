@@ -129,6 +129,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=12)
     ap.add_argument("--kernel-iters", type=int, default=20)
+    ap.add_argument("--spinup-ms", type=float, default=150.0,
+                    help="device spin-up before the warmup steps: the step's own kernels back to back for this long "
+                         "(untimed, no parameter update), so the timed steps do not run inside the GPU's clock ramp "
+                         "(the first ~40 ms of continuous work after idle run ~10 %% slower, DESIGN 3k); 0 = off")
     ap.add_argument("--indexed", action="store_true", help="per-step index copy instead of the device epoch cursor")
     ap.add_argument("--per-step-sync", action="store_true",
                     help="one host sync + logged-value read per step (the Trainer loop shape) instead of run_epoch")
@@ -390,6 +394,19 @@ def cpu_baseline(args):
                       f"{threads} threads, {med * 1e3:.1f} ms/step"}
 
 
+def spinup(fn, ms):
+    """Run fn back to back until `ms` of wall time have passed (untimed device spin-up, --spinup-ms); returns the
+    milliseconds spent. Nothing it runs touches the parameters or the optimizer state."""
+    if ms <= 0:
+        return 0.0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        fn()
+    torch.cuda.synchronize()
+    return round((time.perf_counter() - t0) * 1e3, 1)
+
+
 def kernel_timing(model, data, args):
     """Average device time (us) of each launch of the NLL training pass on one batch, measured with HIP
     events on the launch stream around back-to-back launches (FusedStack.time_kernels)."""
@@ -462,9 +479,15 @@ def main():
             vals = step.run_epoch(b - a)
             return vals[-1] if vals else None
 
+    if not (args.indexed or args.per_step_sync):
+        # graph captures (host work, the GPU idle) before the spin-up and the warmup steps, so the timed steps follow
+        # device work without an idle gap
+        step.prepare_epoch(max(args.steps, args.warmup))
+    spin = argparse.Namespace(**{**vars(args), "kernel_iters": 4})
+    spun = spinup(lambda: kernel_timing(model, data, spin), args.spinup_ms)
     run_range(0, args.warmup)
     if not (args.indexed or args.per_step_sync):
-        step.prepare_epoch(args.steps)      # graph captures (host work) stay out of the timed region at any --warmup
+        step.prepare_epoch(args.steps)      # (captured above: no capture lands in the timed region at any --warmup)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -491,7 +514,8 @@ def main():
         dom = max(per_kernel, key=lambda k: per_kernel[k]["avg_us"])   # the longest single launch, measured
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "samples/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "ranks_seen": seen,
+            "steps": args.steps, "warmup": args.warmup, "device_spinup_ms": spun, "ms_per_step": round(ms_per_step, 4),
+            "ranks_seen": seen,
             **({"shared_devices": True} if SHARED_DEVICES else {}),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic ballistic trajectories (bcnf_amd/data.py RK4 restatement of physics.py), device-resident",
@@ -543,16 +567,16 @@ def run_sublines(args, world, rank, device, dry=False):
             if dry:
                 res = run_dry(wl, steps, world, rank, device)
             elif wl == "resimulate":
-                res = run_resim(WORKLOADS[wl][1], steps, 2, world, rank, device, cpu=cpu)
+                res = run_resim(WORKLOADS[wl][1], steps, 2, world, rank, device, cpu=cpu, spinup_ms=args.spinup_ms)
             elif wl == "sample":
                 # 10 warm-up draws (~20 ms): the first launches after the FC_large / LSTM_large sub-lines
                 # run while the clocks settle (k_inverse_mfma 1.81 -> 1.57 ms over 13 launches, r03i trace)
-                res = run_sample(WORKLOADS[wl][1], steps, 10, world, rank, device, cpu=cpu)
+                res = run_sample(WORKLOADS[wl][1], steps, 10, world, rank, device, cpu=cpu, spinup_ms=args.spinup_ms)
             else:
                 res = run_wide(wl, WORKLOADS[wl][1], steps, 3, world, rank, device, graph=not args.no_graph,
                                kernel_iters=3, cpu=cpu, cpu_batch=256 if wl == "fc_large" else 128, cpu_steps=2,
                                overlap_ranges=(args.overlap_ranges if args.overlap_ranges is not None
-                                               else OVERLAP_RANGES) if world > 1 else 0)
+                                               else OVERLAP_RANGES) if world > 1 else 0, spinup_ms=args.spinup_ms)
         except Exception as e:           # a sub-line never takes the headline down with it
             res = {"error": f"{type(e).__name__}: {e}"}
         if rank == 0:
@@ -741,7 +765,7 @@ def wide_mfma_busy(workload):
 
 
 def run_wide(workload, batch, steps, warmup, world, rank, device, graph=True, kernel_iters=20, cpu=True,
-             cpu_batch=256, cpu_steps=4, overlap_ranges=0):
+             cpu_batch=256, cpu_steps=4, overlap_ranges=0, spinup_ms=150.0):
     """NLL-training samples/s of a wide workload (trajectory_FC_large = configs[2], trajectory_LSTM_large =
     configs[3]) per GPU, same step definition and timing contract as main(). Returns rank 0's JSON object."""
     from bcnf_amd import CondRealNVP_v2
@@ -760,6 +784,13 @@ def run_wide(workload, batch, steps, warmup, world, rank, device, graph=True, ke
     step.set_pool(data.y, data.traj)
     batches = [data.next_indices() for _ in range(warmup + steps)]
     step.set_epoch(torch.cat(batches), batch)
+
+    class _A:                           # kernel_timing's argument shape
+        pass
+    ka = _A()
+    ka.kernel_iters = 2
+    step.prepare_epoch(max(steps, warmup))      # captures first, then spin-up and warmup without an idle gap
+    spun = spinup(lambda: kernel_timing(model, data, ka), spinup_ms)
     step.run_epoch(warmup)
     step.prepare_epoch(steps)          # no graph capture inside the timed region
     if world > 1:
@@ -779,10 +810,6 @@ def run_wide(workload, batch, steps, warmup, world, rank, device, graph=True, ke
     seen = ranks_seen(world, device)
     if rank != 0:
         return None
-
-    class _A:                           # kernel_timing's argument shape
-        pass
-    ka = _A()
     ka.kernel_iters = kernel_iters
     kern = kernel_timing(model, data, ka)
     B = batch
@@ -796,7 +823,7 @@ def run_wide(workload, batch, steps, warmup, world, rank, device, graph=True, ke
     line = {
         "metric": f"NLL-training samples/sec, {WIDE_NAMES[workload]}",
         "value": round(value, 1), "unit": "samples/s", "n_gpus": world, "steps": steps,
-        "warmup": warmup, "ms_per_step": round(dt / steps * 1e3, 4), "ranks_seen": seen,
+        "warmup": warmup, "device_spinup_ms": spun, "ms_per_step": round(dt / steps * 1e3, 4), "ranks_seen": seen,
         **({"shared_devices": True} if SHARED_DEVICES else {}),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic ballistic trajectories (bcnf_amd/data.py), device-resident",
@@ -842,7 +869,8 @@ def main_wide(args):
     torch.cuda.set_device(device)
     ov = args.overlap_ranges if args.overlap_ranges is not None else (OVERLAP_RANGES if world > 1 else 0)
     line = run_wide(args.workload, args.batch, args.steps, args.warmup, world, rank, device, graph=not args.no_graph,
-                    kernel_iters=args.kernel_iters, cpu=not args.no_cpu_baseline, overlap_ranges=ov)
+                    kernel_iters=args.kernel_iters, cpu=not args.no_cpu_baseline, overlap_ranges=ov,
+                    spinup_ms=args.spinup_ms)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -850,7 +878,7 @@ def main_wide(args):
         dist.destroy_process_group()
 
 
-def run_sample(n_cond, steps, warmup, world, rank, device, n_draws=500, cpu=True, cpu_conds=1024):
+def run_sample(n_cond, steps, warmup, world, rank, device, n_draws=500, cpu=True, cpu_conds=1024, spinup_ms=150.0):
     """Posterior draws/s (BASELINE configs[4]): 500 draws for each of `n_cond` conditions with trajectory_FC_small,
     the conditions sharded over the ranks (strong scaling of a fixed job; bcnf_amd/sampling.py), gathered at the end.
     One step = draw_sharded(500, all conditions) incl. feature net, device z draw, inverse, all-gather."""
@@ -864,6 +892,7 @@ def run_sample(n_cond, steps, warmup, world, rank, device, n_draws=500, cpu=True
     traj = ((traj - traj.mean((0, 1))) / (traj.std((0, 1)) + 1e-6)).to(device)
     gen = torch.Generator(device=device).manual_seed(17 + rank)
     with model.fused.reuse_pack():
+        spun = spinup(lambda: draw_sharded(model, n_draws, traj, generator=gen), spinup_ms)
         for _ in range(warmup):
             draw_sharded(model, n_draws, traj, generator=gen)
         if world > 1:
@@ -910,6 +939,7 @@ def run_sample(n_cond, steps, warmup, world, rank, device, n_draws=500, cpu=True
     line = {
         "metric": "posterior draws/sec (inverse sampling, 500 draws x 1024 conditions), trajectory_FC_small",
         "value": round(value, 1), "unit": "draws/s", "n_gpus": world, "steps": steps, "warmup": warmup,
+        "device_spinup_ms": spun,
         "ms_per_step": round(dt / steps * 1e3, 4), "ranks_seen": seen, "higher_is_better": True,
         **({"shared_devices": True} if SHARED_DEVICES else {}),
         "scaling": "strong",
@@ -971,7 +1001,7 @@ def main_sample(args, n_draws=500):
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     line = run_sample(args.batch, args.steps, args.warmup, world, rank, device, n_draws=n_draws,
-                      cpu=not args.no_cpu_baseline)
+                      cpu=not args.no_cpu_baseline, spinup_ms=args.spinup_ms)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -1010,7 +1040,7 @@ def resim_draws(n_traj, n_draws, seed=2024_03_25):
     return yh.astype(np.float32), data_dict
 
 
-def run_resim(n_traj, steps, warmup, world, rank, device, n_draws=1000, cpu=True, T=2.0, dt=1 / 15):
+def run_resim(n_traj, steps, warmup, world, rank, device, n_draws=1000, cpu=True, T=2.0, dt=1 / 15, spinup_ms=150.0):
     """Re-simulated trajectories/s (resimulate with y_hat given, resimulation.py:21-59; notebooks/resimulation.ipynb
     sizes): n_draws x n_traj trajectories, the trajectories sharded over the ranks (independent, no collective).
     One step = bcnf_resimulate over this rank's draws, y_hat resident in HBM, (N, M, 30, 3) float64 written."""
@@ -1023,6 +1053,7 @@ def run_resim(n_traj, steps, warmup, world, rank, device, n_draws=1000, cpu=True
     dd = {k: v[a:b] for k, v in data_dict.items()}
     y = torch.from_numpy(yh[:, a:b]).to(device).contiguous()
     st = torch.cuda.current_stream(device)
+    spun = spinup(lambda: resimulate_device(y, T, dt, dd, pim, break_on_impact=True, device=device), spinup_ms)
     for _ in range(warmup):
         out = resimulate_device(y, T, dt, dd, pim, break_on_impact=True, device=device)
     if world > 1:
@@ -1085,6 +1116,7 @@ def run_resim(n_traj, steps, warmup, world, rank, device, n_draws=1000, cpu=True
         "metric": "re-simulated trajectories/sec, device-resident (resimulate_device: y_hat in HBM, positions left "
                   "in HBM; 1000 draws x 1024 trajectories, T=2, dt=1/15, break_on_impact)",
         "value": round(value, 1), "unit": "trajectories/s", "n_gpus": world, "steps": steps, "warmup": warmup,
+        "device_spinup_ms": spun,
         "ms_per_step": round(el / steps * 1e3, 4), "ranks_seen": seen, "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic draws: bcnf_amd/data.py priors jittered 5% per draw, device-resident",
@@ -1113,7 +1145,8 @@ def main_resim(args):
     world, rank, local = init_dist(args)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
-    line = run_resim(args.batch, args.steps, args.warmup, world, rank, device, cpu=not args.no_cpu_baseline)
+    line = run_resim(args.batch, args.steps, args.warmup, world, rank, device, cpu=not args.no_cpu_baseline,
+                     spinup_ms=args.spinup_ms)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
