@@ -142,7 +142,21 @@ struct FoldAdamArgs {
   int* done;
   const int* guard;
   int on;
+  float* asc;                   // [step_size, bc2s] of this step, written by an earlier launch of the tail
 };
+
+// The folded tail's Adam scalars, once per step: one thread of the tail's first launch derives step_size and bc2s
+// exactly as adam_scalars does (double, rounded once) and stores them; the later launches load the two floats with
+// their other operands instead of a step-count round trip, two double pows and a barrier per workgroup.
+__device__ __forceinline__ void adam_scalars_publish(const FoldAdamArgs& A) {
+  const double t = (double)(A.step[0] + 1.0f);
+  A.asc[0] = (float)(A.lr / (1.0 - pow(A.b1, t)));
+  A.asc[1] = (float)sqrt(1.0 - pow(A.b2, t));
+}
+__device__ __forceinline__ AdamScalars adam_scalars_of(const FoldAdamArgs& A, float step_size, float bc2s) {
+  return AdamScalars{step_size, bc2s, (float)(1.0 - A.b1), (float)(1.0 - A.b2), (float)A.b2, (float)A.eps,
+                     (float)A.wd};
+}
 
 // Host-computed layout of one stack (passed by value to every kernel).
 struct BcnfLayout {

@@ -977,8 +977,13 @@ size_t dw1h_lds_bytes(const BcnfLayout& L, int bpw = 4) {
 template <bool VEC>
 __global__ __launch_bounds__(BCNF_WG) void k_fold_splitk(BcnfLayout F, const float* __restrict__ d1,
                                                          const float* __restrict__ x, long long B, int rows_per_split,
-                                                         float* __restrict__ work, int gx_dw, int ones) {
+                                                         float* __restrict__ work, int gx_dw, int ones,
+                                                         FoldAdamArgs A) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  if (A.on && blockIdx.x == gridDim.x - 1) {       // one extra workgroup: the Adam scalars for k_red_gx / finish
+    if (threadIdx.x == 0) adam_scalars_publish(A);
+    return;
+  }
   dw1h_body<VEC, 2>(F, d1, x, B, rows_per_split, work, blockIdx.x % gx_dw, blockIdx.x / gx_dw, smem, ones);
 }
 
@@ -1070,7 +1075,6 @@ __global__ __launch_bounds__(BCNF_WG) void k_fold_finish(BcnfLayout L, const flo
                                                          float* __restrict__ dparams, float* __restrict__ dwf,
                                                          float* __restrict__ dbf, FoldAdamArgs A) {
   extern __shared__ __attribute__((aligned(16))) float smem[];   // FIN_SMEM floats (64 KB: dynamic)
-  __shared__ float sc[2];
   float* As = smem;
   float* Bs = smem + FIN_KC * 16;
   const int Xp = fold_xp(X), tid = threadIdx.x, nct = L.Cp >> 4;
@@ -1080,11 +1084,27 @@ __global__ __launch_bounds__(BCNF_WG) void k_fold_finish(BcnfLayout L, const flo
   // fused Adam (FoldAdamArgs): this thread's output is one parameter whose gradient it computes; its parameter and
   // moments are fetched now, the update follows the tile product. The launch's last workgroup does the step's
   // bookkeeping (bcnf_adam_step_bookkeep semantics), workgroup 0 stores the logged values.
+  // The scalars come from k_fold_splitk (adam_scalars_publish); workgroup 0's log row index is loaded now and its
+  // system-scope stores issued once the operands are staged, their fence at the end (no round trip up front).
   const bool adam = A.on && !(A.guard && A.guard[BCNF_GUARD_HALTED]);
   AdamScalars as{};
+  // Workgroup 0's thread 0 keeps the step's books (bcnf_adam_step_bookkeep semantics): it alone reads the step count
+  // and the cursor in this launch (the scalars came from k_fold_splitk), so it advances both itself at its end --
+  // no arrival counter, no last-workgroup round trip.
+  const bool keeper = adam && blockIdx.x == 0 && tid == 0;
+  const bool logger = keeper && A.log_values && A.log_history;
+  long long log_row = 0;
+  float step0 = 0.f, log_v[3];
   if (adam) {
-    if (blockIdx.x == 0 && tid == 0) store_log(A.log_values, A.log_history, A.cursor);
-    as = adam_scalars(A.step[0] + 1.0f, A.lr, A.b1, A.b2, A.eps, A.wd, sc);
+    as = adam_scalars_of(A, A.asc[0], A.asc[1]);
+    if (keeper) {
+      log_row = A.cursor ? A.cursor[0] : 0LL;
+      step0 = A.step[0];
+    }
+    if (logger) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) log_v[i] = A.log_values[i];
+    }
   }
   int slot = -1;                                       // which parameter tensor / element this thread updates
   long long idx = 0;
@@ -1120,11 +1140,12 @@ __global__ __launch_bounds__(BCNF_WG) void k_fold_finish(BcnfLayout L, const flo
     A.v[slot][idx] = av;
   };
   auto arrive = [&]() {
-    if (!adam || tid != 0) return;
-    // every thread of this workgroup read the step count before this point (adam_scalars synchronised)
-    if (__hip_atomic_fetch_add(A.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
-      advance_counters(A.step, A.cursor, A.n_batches);
-      __hip_atomic_store(A.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!keeper) return;
+    if (logger) __threadfence_system();                // the log row's stores (system scope)
+    A.step[0] = step0 + 1.0f;                          // advance_counters on the values read at the start
+    if (A.cursor) {
+      const long long c = log_row + 1;
+      A.cursor[0] = c < A.n_batches ? c : 0;
     }
   };
   if ((int)blockIdx.x < L.nb * nct) {
@@ -1151,6 +1172,11 @@ __global__ __launch_bounds__(BCNF_WG) void k_fold_finish(BcnfLayout L, const flo
       }
     }
     __syncthreads();
+    if (logger) {                                     // the step's logged values -> history row of this batch
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        __hip_atomic_store(A.log_history + 3 * log_row + i, log_v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     tile16_accum(As, Bs, Xp, acc);
     const float v = tile16_reduce(smem, acc);
     const int j = tid >> 4, c = c0 + (tid & 15);
@@ -2819,14 +2845,13 @@ __global__ __launch_bounds__(BCNF_WG) void k_red_gx(BcnfLayout L, long long tota
                                                     const float* __restrict__ slab, long long stride, int nwg,
                                                     float* __restrict__ dparams, FoldAdamArgs A) {
   __shared__ __attribute__((aligned(16))) float smem[RED_G * RED_O4 * 4];
-  __shared__ float sc[2];
   const int bx = blockIdx.x;
   if (bx < n_gx) {
     gx_reduce_body(total, work, splits, gx, (long long)bx * BCNF_WG + threadIdx.x);
     return;
   }
   if (A.on && !(A.guard && A.guard[BCNF_GUARD_HALTED])) {      // (a halted step updates nothing)
-    const AdamScalars as = adam_scalars(A.step[0] + 1.0f, A.lr, A.b1, A.b2, A.eps, A.wd, sc);
+    const AdamScalars as = adam_scalars_of(A, A.asc[0], A.asc[1]);   // (k_fold_splitk published them)
     reduce_body(L, slab, stride, nwg, dparams, bx - n_gx, smem, &A, &as);
     return;
   }
@@ -3215,7 +3240,7 @@ int bcnf_fold_slab_bytes(const BcnfStackDesc* desc, int32_t in_features, int64_t
   if (!bytes || batch < 0) return BCNF_ERR_ARG;
   const BcnfLayout F = fold_layout(L, in_features, in_features);
   *bytes = ((int64_t)((batch + 15) / 16) * slab_stride_of(L) + w1h_work_floats(F, batch) +
-            (int64_t)L.nb * 16 * F.Cp) * 4;
+            (int64_t)L.nb * 16 * F.Cp + 4) * 4;                // + the fused Adam's two scalars (FoldAdamArgs::asc)
   return BCNF_OK;
 }
 
@@ -3368,20 +3393,21 @@ int bcnf_fold_backward_tail(const BcnfStackDesc* desc, const void* packed, const
   const float* d1 = (const float*)workspace + ws_d1_off(L, batch, drop);
   float* work = (float*)slab + (long long)nwg * S;
   float* gx = work + w1h_work_floats(F, batch);
+  A.asc = gx + (long long)L.nb * 16 * F.Cp;
   const int rps = w1h_rows_per_split(batch);
   const long long splits = w1h_splits(batch);
   const int n_red = (int)((S / 4 + RED_O4 - 1) / RED_O4);
   const int gx_dw = (L.nb + 1) / 2;
-  const dim3 grid((unsigned)((long long)gx_dw * splits));
+  const dim3 grid((unsigned)((long long)gx_dw * splits + (A.on ? 1 : 0)));
   size_t lds = dw1h_lds_bytes(F, 2);
   if (vec_rows(F, x)) {
     if ((rc = launch_lds(k_fold_splitk<true>, lds))) return rc;
     hipLaunchKernelGGL(k_fold_splitk<true>, grid, dim3(BCNF_WG), lds, st, F, d1, x, (long long)batch, rps, work, gx_dw,
-                       (int)in_features);
+                       (int)in_features, A);
   } else {
     if ((rc = launch_lds(k_fold_splitk<false>, lds))) return rc;
     hipLaunchKernelGGL(k_fold_splitk<false>, grid, dim3(BCNF_WG), lds, st, F, d1, x, (long long)batch, rps, work, gx_dw,
-                       (int)in_features);
+                       (int)in_features, A);
   }
   if ((rc = check_launch())) return rc;
   const long long total = (long long)L.nb * 16 * F.Cp;

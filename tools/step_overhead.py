@@ -2,7 +2,7 @@
 each n in STEPS, the host wall time of run_epoch(n) bracketed by synchronize() as bench.py brackets it, the GPU time
 between events recorded right before and after it, and the host time until the first graph launch returned.
 A fit wall = a + b n separates the per-step time b from the fixed cost a. PREWARM=matmul MS=200 runs unrelated GEMMs
-first; WARM = the run_epoch steps before the measurements (16)."""
+first; WARM = the run_epoch steps before the measurements (16); LR; FUSE_ADAM=0 keeps Adam out of the tail."""
 import os
 import sys
 import time
@@ -24,6 +24,7 @@ model = CondRealNVP_v2.from_config(FC_SMALL).to(dev)
 model.train()
 data = DeviceBatches(65536, B, dev, seed=2024_03_25)
 step = TrainStep(model, lr=float(os.environ.get("LR", "2e-4")), capture=True)
+step.fuse_adam = os.environ.get("FUSE_ADAM", "1") == "1"     # 0: Adam in its own launch every step
 step.set_pool(data.y, data.traj)
 WARM = int(os.environ.get("WARM", "16"))
 total = WARM + 3 * sum(STEPS) + 32
