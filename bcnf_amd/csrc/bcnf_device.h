@@ -169,9 +169,9 @@ struct BcnfLayout {
   int blk_pad;          // cblk rounded up to 4
   int sblk;             // floats per block of a workgroup's gradient slab (slab_blk_floats: MFMA tiles + column sums)
   int n_trainable;
-  int qbc;              // 1 (Da = 9, Db = 10: every D = 19 stack): the mix, Linear 1's y-part and the backward's T / S
-                        // heads are in broadcast form (record entry c of lane j = weight of input c to output j; bc9,
-                        // mix_bc, bc10x2), else in rotation form (entry r of lane j = weight of input (j - r) & 15)
+  int qbc;              // QBC_* bits (Da = 10, Db = 9: every D = 19 stack): Linear 1's y-part, the mix and the
+                        // backward's T / S head transposes in broadcast form (record entry c of lane j = weight of
+                        // input c to output j; bc10, mix_bc, bc9x2), else rotation form (input (j - r) & 15)
   float p, keep_scale;
   uint32_t thr_hi, thr_lo;   // thresh32 = round(p 2^32) = thr_hi 2^16 + thr_lo: drop if a unit's u32 < thresh32
   int RF, RB;           // per-lane record floats (forward/inverse, backward)

@@ -22,7 +22,7 @@ dev = torch.device("cuda", 0)
 torch.manual_seed(2024_03_25)
 model = CondRealNVP_v2.from_config(FC_SMALL).to(dev)
 model.train()
-data = DeviceBatches(65536, B, dev, seed=2024_03_25)
+data = DeviceBatches(int(os.environ.get("POOL", "65536")), B, dev, seed=2024_03_25)
 step = TrainStep(model, lr=float(os.environ.get("LR", "2e-4")), capture=True)
 step.fuse_adam = os.environ.get("FUSE_ADAM", "1") == "1"     # 0: Adam in its own launch every step
 step.set_pool(data.y, data.traj)
