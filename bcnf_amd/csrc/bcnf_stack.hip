@@ -73,6 +73,12 @@ int round_rec(int n) {            // multiple of 4 floats with odd quotient (con
 #define BCNF_QBC_MASK 7
 #endif
 constexpr int QBC_W1 = 1, QBC_MIX = 2, QBC_HEAD = 4;
+// the kernels' test of a section's form (BCNF_QBC_CONST: a compile-time answer, for layout-specific A/B builds)
+#ifdef BCNF_QBC_CONST
+#define QBC_DEV(L, bit) (BCNF_QBC_CONST != 0)
+#else
+#define QBC_DEV(L, bit) (((L).qbc & (bit)) != 0)
+#endif
 
 int make_layout(const BcnfStackDesc* d, BcnfLayout* L) {
   if (!d || !L) return BCNF_ERR_ARG;
@@ -1286,7 +1292,7 @@ __device__ __forceinline__ void mlp_forward(const BcnfLayout& L, const float* __
   for (int l = 1; l <= NH; ++l) {
     const float* w = (l == 1) ? rr + F::W1 : rr + F::HID + 17 * (l - 2);
     const float bias = (l == 1) ? hp : w[16];            // hp = h W1h^T + b1 (k_hp)
-    const float pre = (l == 1 && (L.qbc & QBC_W1)) ? bc10(a, w, bias) : rot16(a, w, bias);   // (uniform)
+    const float pre = (l == 1 && QBC_DEV(L, QBC_W1)) ? bc10(a, w, bias) : rot16(a, w, bias);   // (uniform)
     const float m = drop ? (((bits >> (l - 1)) & 1u) ? L.keep_scale : 0.f) : 1.f;
     if (KEEP) {
       float g, dg;
@@ -2005,7 +2011,7 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
       auto emit = [&](int q) {
         if (SAVE) st4_wt(d4 + q * BCNF_WG, floatx4{ar[4 * q], ar[4 * q + 1], ar[4 * q + 2], ar[4 * q + 3]});
       };
-      mlp_forward_s<NH, SAVE, DROP>(rr, rec + cur * RING + j * L.RF, xa, hpk, msk, T, Sp, ar, emit, (L.qbc & QBC_W1) != 0);
+      mlp_forward_s<NH, SAVE, DROP>(rr, rec + cur * RING + j * L.RF, xa, hpk, msk, T, Sp, ar, emit, QBC_DEV(L, QBC_W1));
       const float Sv = tanh_bf(Sp);                      // cnf.py:107
       const float zb = fmaf(exp_fast(Sv), xb, T);        // cnf.py:179
       ldj += Sv;                                         // cnf.py:190
@@ -2021,7 +2027,7 @@ __global__ __launch_bounds__(2 * BCNF_WG) void k_forward(BcnfLayout L, const flo
       }
       fetch_head(nxt);     // slot nxt is complete since the previous barrier (after the last block: unused, no
                            // branch); the reads land while the mix runs
-      if (L.qbc & QBC_MIX) mix_bc(rr + RecF<NH>::Q, xa, zb, ya, yb);   // y @ Q (cnf.py:335); identity after the last block
+      if (QBC_DEV(L, QBC_MIX)) mix_bc(rr + RecF<NH>::Q, xa, zb, ya, yb);   // y @ Q (cnf.py:335); identity after the last block
       else mix(rr + RecF<NH>::Q, xa, zb, ya, yb);
       cur = nxt;
       PHF(1)
@@ -2151,7 +2157,7 @@ __global__ __launch_bounds__(BCNF_WG) void k_inverse(BcnfLayout L, const float* 
     float rr[RecF<NH>::USED];
     ld_rec<0, RecF<NH>::USED>(rr, rec + cur * RING + j * L.RF);
     float za, zb;
-    if (L.qbc & QBC_MIX) mix_bc(rr + RecF<NH>::Q, ya, yb, za, zb);   // z @ Q^T (cnf.py:339); identity for the last block
+    if (QBC_DEV(L, QBC_MIX)) mix_bc(rr + RecF<NH>::Q, ya, yb, za, zb);   // z @ Q^T (cnf.py:339); identity for the last block
     else mix(rr + RecF<NH>::Q, ya, yb, za, zb);
     uint32_t bits = 0xffu;
     if (DROP) bits = dropout_bits<NH>(L, seed, off, bc, k, j, 0x40000000u);
@@ -2666,7 +2672,7 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
       const float xb = fmaf(an_sb, yb, an_bb);
       const float e = exp_fast(S);
       float gza, gzb;
-      if (L.qbc & QBC_MIX) mix_bc(rb + RBk::QT, gya, gyb, gza, gzb);   // g @ Q^T (identity for the last block)
+      if (QBC_DEV(L, QBC_MIX)) mix_bc(rb + RBk::QT, gya, gyb, gza, gzb);   // g @ Q^T (identity for the last block)
       else mix(rb + RBk::QT, gya, gyb, gza, gzb);
       ld16(rb + RBk::HID, R + RBk::HID);                 // hidden layer NH
       __builtin_amdgcn_sched_barrier(0);
@@ -2677,7 +2683,7 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
       Tt[NH * TILE] = dT_;
       Tt[(NH + 1) * TILE] = dSp;
       float da = 0.f, da2 = 0.f;
-      if (L.qbc & QBC_HEAD) bc9x2(dT_, rb + RBk::TT, da, dSp, rb + RBk::ST, da2);   // (uniform)
+      if (QBC_DEV(L, QBC_HEAD)) bc9x2(dT_, rb + RBk::TT, da, dSp, rb + RBk::ST, da2);   // (uniform)
       else rot16x2(dT_, rb + RBk::TT, da, dSp, rb + RBk::ST, da2);
       da += da2;
 #pragma unroll
