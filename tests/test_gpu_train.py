@@ -222,14 +222,16 @@ def _epoch_pool(gen, n=768, blow_up=None):
     return y.to(DEV), traj.to(DEV)
 
 
-@pytest.mark.parametrize("unroll", [8, 2, 3])
-def test_run_epoch_equals_per_step_loop(g1, unroll):
-    """run_epoch (back-to-back replays, one sync; `unroll` steps per captured graph) == step_epoch per step: same
-    logged values, parameters, Adam state, RNG offset, cursor and .grad (the last step's), bit for bit."""
+@pytest.mark.parametrize("unroll,batch", [(8, 192), (2, 192), (3, 192), (8, 48)])
+def test_run_epoch_equals_per_step_loop(g1, unroll, batch):
+    """run_epoch (back-to-back replays, one sync; `unroll` steps per captured graph, the remainder in unroll / 2,
+    / 4 ... step graphs) == step_epoch per step: same logged values, parameters, Adam state, RNG offset, cursor and
+    .grad (the last step's), bit for bit. Batch 48: 16 steps, run as 1 + (8 + 4 + 2 + 1)."""
     from bcnf_amd.train import TrainStep
     gen = torch.Generator().manual_seed(21)
     py, pt = _epoch_pool(gen)
-    order = torch.randperm(768, generator=gen)[:4 * 192].to(DEV)
+    nb = 768 // batch
+    order = torch.randperm(768, generator=gen)[:nb * batch].to(DEV)
     res = []
     for batched in (False, True):
         m = fresh_model(g1, train=True)
@@ -237,16 +239,16 @@ def test_run_epoch_equals_per_step_loop(g1, unroll):
         st = TrainStep(m, lr=2e-4)
         st.epoch_unroll = unroll
         st.set_pool(py, pt)
-        st.set_epoch(order, 192)
+        st.set_epoch(order, batch)
         if batched:
             vals = st.run_epoch(1) + st.run_epoch()          # a partial run, then the rest of the epoch
         else:
-            vals = [st.step_epoch() for _ in range(4)]
+            vals = [st.step_epoch() for _ in range(nb)]
         state = [v.clone() for s in st.opt.state.values() for v in s.values()]
         res.append((vals, [p.detach().clone() for p in m.parameters()], state,
                     m.fused.rng_state().clone(), st._epoch[1].item(), [p.grad.clone() for p in st.params]))
     (v0, p0, s0, r0, c0, g0), (v1, p1, s1, r1, c1, gr1) = res
-    assert v0 == v1 and len(v1) == 4
+    assert v0 == v1 and len(v1) == nb
     assert c0 == c1 == 0 and torch.equal(r0, r1)
     names = [f"param{i}" for i in range(len(p0))] + [f"state{i}" for i in range(len(s0))] + \
         [f"grad{i}" for i in range(len(g0))]
