@@ -396,14 +396,16 @@ def cpu_baseline(args):
 
 def spinup(fn, ms):
     """Run fn back to back until `ms` of wall time have passed (untimed device spin-up, --spinup-ms); returns the
-    milliseconds spent. Nothing it runs touches the parameters or the optimizer state."""
+    milliseconds spent. Nothing it runs touches the parameters or the optimizer state, and fn holds no collective:
+    each rank runs it a different number of times."""
     if ms <= 0:
         return 0.0
-    torch.cuda.synchronize()
+    sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)   # (CPU: the gloo tests)
+    sync()
     t0 = time.perf_counter()
     while (time.perf_counter() - t0) * 1e3 < ms:
         fn()
-    torch.cuda.synchronize()
+    sync()
     return round((time.perf_counter() - t0) * 1e3, 1)
 
 
@@ -892,7 +894,9 @@ def run_sample(n_cond, steps, warmup, world, rank, device, n_draws=500, cpu=True
     traj = ((traj - traj.mean((0, 1))) / (traj.std((0, 1)) + 1e-6)).to(device)
     gen = torch.Generator(device=device).manual_seed(17 + rank)
     with model.fused.reuse_pack():
-        spun = spinup(lambda: draw_sharded(model, n_draws, traj, generator=gen), spinup_ms)
+        # this rank's shard only (gather=False): the spin-up is time-bounded, so ranks run different counts of it,
+        # and a collective inside would pair up across ranks wrongly
+        spun = spinup(lambda: draw_sharded(model, n_draws, traj, generator=gen, gather=False), spinup_ms)
         for _ in range(warmup):
             draw_sharded(model, n_draws, traj, generator=gen)
         if world > 1:

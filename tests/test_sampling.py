@@ -43,7 +43,11 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from bcnf_amd.sampling import draw_sharded
+        import bench
         cond = torch.arange(7 * 30 * 3, dtype=torch.float32).view(7, 30, 3)
+        # bench.py's sampling spin-up shape: time-bounded, so the ranks run it a different number of times -- it must
+        # hold no collective, or the gathered call below would pair up with a spin-up call of another rank
+        bench.spinup(lambda: draw_sharded(None, 3, cond, sampler=_fake_sampler, gather=False), 20 + 40 * rank)
         out = draw_sharded(None, 3, cond, sampler=_fake_sampler)
         local = draw_sharded(None, 3, cond, sampler=_fake_sampler, gather=False)
         q.put((rank, torch.equal(out, _fake_sampler(cond)), tuple(local.shape)))
