@@ -1133,17 +1133,29 @@ __global__ __launch_bounds__(BCNF_WG) void k_fold_finish(BcnfLayout L, const flo
       }
     }
   }
-  if (adam && slot >= 0 && A.p[slot]) {
-    ap = A.p[slot][idx];
-    am = A.m[slot][idx];
-    av = A.v[slot][idx];
+  // the slot's tensors picked with constant indices (scalar argument loads + a per-lane select): indexed by the
+  // per-lane slot they were per-lane loads of the kernel arguments, a round trip in front of the p / m / v loads
+  float *sp = nullptr, *sm = nullptr, *sv = nullptr;
+  if (adam) {
+    if (slot == 0) {
+      sp = A.p[0]; sm = A.m[0]; sv = A.v[0];
+    } else if (slot == 1) {
+      sp = A.p[1]; sm = A.m[1]; sv = A.v[1];
+    } else if (slot == 2) {
+      sp = A.p[2]; sm = A.m[2]; sv = A.v[2];
+    }
+  }
+  if (sp) {
+    ap = sp[idx];
+    am = sm[idx];
+    av = sv[idx];
   }
   auto finish_elem = [&](float gval) {
-    if (!adam || slot < 0 || !A.p[slot]) return;
+    if (!sp) return;
     adam_elem(ap, gval, am, av, as);
-    A.p[slot][idx] = ap;
-    A.m[slot][idx] = am;
-    A.v[slot][idx] = av;
+    sp[idx] = ap;
+    sm[idx] = am;
+    sv[idx] = av;
   };
   auto arrive = [&]() {
     if (!keeper) return;
@@ -2732,6 +2744,16 @@ __global__ __launch_bounds__(BWD_WG) void k_backward(BcnfLayout L, const float* 
 // floats at m * L.sblk) is what the backward's helper waves wrote (BwdJobs): NH + 2 MFMA tiles in lane order, then
 // NH + 6 column sums; this maps each element back to its canonical position, or -1 for tile padding (rows / columns
 // past a Linear's shape, ActNorm sums of the last block). W1's condition columns come from the split-K GEMM.
+// a[i] for a per-lane i through constant indices (scalar argument loads and selects): indexed directly, every such
+// read was a per-lane load of the kernel arguments in front of the reduce's first dependent load
+template <int N>
+__device__ __forceinline__ int lpick(const int (&a)[N], int i) {
+  int r = a[0];
+#pragma unroll
+  for (int t = 1; t < N; ++t) r = (i == t) ? a[t] : r;
+  return r;
+}
+
 __device__ __forceinline__ long long slab_to_canonical(const BcnfLayout& L, int m, int o) {
   const int NH = L.NH, NW = NH + 2;
   const int cb = m * L.blk_stride + ((m < L.nb - 1) ? L.an_size : 0);      // coupling base
@@ -2739,14 +2761,14 @@ __device__ __forceinline__ long long slab_to_canonical(const BcnfLayout& L, int 
     const int c = o >> 8, e = o & 255, lane = e >> 2;
     const int row = 4 * (lane >> 4) + (e & 3), col = lane & 15;
     const int l = c < NH ? c + 1 : NH + 1;
-    const int nrows = c < NH ? L.H[l] : L.Db, ncols = (l == 1) ? L.Da : L.H[l - 1];
+    const int nrows = c < NH ? lpick(L.H, l) : L.Db, ncols = (l == 1) ? L.Da : lpick(L.H, l - 1);
     if (row >= nrows || col >= ncols) return -1;
     const int row0 = (c == NH + 1) ? L.Db : 0;
-    return (long long)cb + L.lin_w[l] + (row0 + row) * L.lin_in[l] + col;
+    return (long long)cb + lpick(L.lin_w, l) + (row0 + row) * lpick(L.lin_in, l) + col;
   }
   const int o2 = o - NW * 256, c = o2 >> 4, r = o2 & 15;
-  if (c < NH) return r < L.H[c + 1] ? (long long)cb + L.lin_b[c + 1] + r : -1;
-  if (c < NH + 2) return r < L.Db ? (long long)cb + L.lin_b[NH + 1] + ((c == NH + 1) ? L.Db : 0) + r : -1;
+  if (c < NH) return r < lpick(L.H, c + 1) ? (long long)cb + lpick(L.lin_b, c + 1) + r : -1;
+  if (c < NH + 2) return r < L.Db ? (long long)cb + lpick(L.lin_b, NH + 1) + ((c == NH + 1) ? L.Db : 0) + r : -1;
   const int a = c - NH - 2;
   if (a >= 4 || !L.act_norm || m >= L.nb - 1 || r >= ((a < 2) ? L.Da : L.Db)) return -1;
   return (long long)m * L.blk_stride + ((a & 1) ? L.D : 0) + ((a < 2) ? 0 : L.Da) + r;
